@@ -1,0 +1,195 @@
+// Fused optimizer kernels over FLAT parameter storage (gfx950).
+//
+// Design (MI355X-first): every trainable parameter of a model lives in one
+// contiguous bf16 buffer (compute copy), with matching contiguous fp32 master /
+// exp_avg / exp_avg_sq buffers and one contiguous bf16 gradient buffer.  An
+// optimizer step is therefore ONE streaming kernel over N elements instead of
+// a multi-tensor launch list: 16 B bf16 loads, 2x16 B fp32 loads per stream,
+// grid capped at 2048 blocks and grid-strided (CDNA guide G11/G13).  Gradient
+// clipping reads the global grad-norm^2 from device memory, so the step never
+// synchronises with the host.
+//
+// Reference parity: the reference payload's Adam (examples/v1/dist-mnist/
+// dist_mnist.py:194,208 ; multi_worker_strategy-with-keras.py:56) -- SURVEY K5.
+#include "toa_common.h"
+
+// ---------------------------------------------------------------------------
+// sum of squares of a bf16 (or fp32) vector, two-pass deterministic reduction
+// ---------------------------------------------------------------------------
+template <bool BF16>
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const void* __restrict__ x, int64_t n,
+                                                            float* __restrict__ partial) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const int64_t n8 = n / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float f[8];
+    if (BF16) {
+      unpack8(ld16((const bf16_t*)x + i * 8), f);
+    } else {
+      f32x4 a = *((const f32x4*)x + 2 * i), b = *((const f32x4*)x + 2 * i + 1);
+      f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+      f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(f[j], f[j], acc);
+  }
+  // tail (n % 8) handled by block 0
+  if (blockIdx.x == 0) {
+    for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += blockDim.x) {
+      float f = BF16 ? bf2f(((const bf16_t*)x)[i]) : ((const float*)x)[i];
+      acc = fmaf(f, f, acc);
+    }
+  }
+  float t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partial, int np,
+                                                           float* __restrict__ out, int accumulate) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) acc += partial[i];
+  float t = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = accumulate ? out[0] + t : t;
+}
+
+// workspace must hold >= 2048 floats
+extern "C" int toa_sumsq(const void* x, int64_t n, int is_bf16, float* workspace, float* out,
+                         int accumulate, hipStream_t stream) {
+  int grid = toa_stream_grid(n / 8 > 0 ? n / 8 : 1, 256);
+  if (is_bf16)
+    hipLaunchKernelGGL(sumsq_partial_kernel<true>, dim3(grid), dim3(256), 0, stream, x, n, workspace);
+  else
+    hipLaunchKernelGGL(sumsq_partial_kernel<false>, dim3(grid), dim3(256), 0, stream, x, n, workspace);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, stream, workspace, grid, out, accumulate);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// AdamW on flat buffers.
+//   g_eff = grad * grad_scale * clip,   clip = min(1, max_norm / (||grad*grad_scale|| + 1e-6))
+//   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2
+//   p = p - lr * ( m/bc1 / (sqrt(v/bc2) + eps) + wd * p )      (decoupled decay)
+//   param_bf16 = bf16(p)
+// grad may be bf16 or fp32.  n must be a multiple of 8 (flat buffers are
+// padded to 64 elements by the Python side).
+// ---------------------------------------------------------------------------
+template <bool GRAD_BF16>
+__global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ master, bf16_t* __restrict__ param,
+                                                         const void* __restrict__ grad, float* __restrict__ m,
+                                                         float* __restrict__ v, int64_t n8, float lr, float b1,
+                                                         float b2, float eps, float wd, float inv_bc1,
+                                                         float inv_sqrt_bc2, float grad_scale,
+                                                         const float* __restrict__ norm_sq, float max_norm) {
+  float scale = grad_scale;
+  if (norm_sq != nullptr && max_norm > 0.f) {
+    float nrm = sqrtf(norm_sq[0]) * grad_scale;
+    float c = max_norm / (nrm + 1e-6f);
+    scale *= (c < 1.f ? c : 1.f);
+  }
+  const float omb1 = 1.f - b1, omb2 = 1.f - b2, lrwd = lr * wd;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float g[8], p[8], mm[8], vv[8];
+    if (GRAD_BF16) {
+      unpack8(ld16((const bf16_t*)grad + i * 8), g);
+    } else {
+      f32x4 a = *((const f32x4*)grad + 2 * i), b = *((const f32x4*)grad + 2 * i + 1);
+      g[0] = a[0]; g[1] = a[1]; g[2] = a[2]; g[3] = a[3];
+      g[4] = b[0]; g[5] = b[1]; g[6] = b[2]; g[7] = b[3];
+    }
+    f32x4* pm = (f32x4*)master + 2 * i;
+    f32x4* mv = (f32x4*)m + 2 * i;
+    f32x4* vvp = (f32x4*)v + 2 * i;
+    f32x4 p0 = pm[0], p1 = pm[1], m0 = mv[0], m1 = mv[1], v0 = vvp[0], v1 = vvp[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p[j] = p0[j]; p[j + 4] = p1[j];
+      mm[j] = m0[j]; mm[j + 4] = m1[j];
+      vv[j] = v0[j]; vv[j + 4] = v1[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float gj = g[j] * scale;
+      mm[j] = fmaf(b1, mm[j], omb1 * gj);
+      vv[j] = fmaf(b2, vv[j], omb2 * gj * gj);
+      float denom = sqrtf(vv[j]) * inv_sqrt_bc2 + eps;
+      p[j] = p[j] - lr * (mm[j] * inv_bc1) / denom - lrwd * p[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p0[j] = p[j]; p1[j] = p[j + 4];
+      m0[j] = mm[j]; m1[j] = mm[j + 4];
+      v0[j] = vv[j]; v1[j] = vv[j + 4];
+    }
+    pm[0] = p0; pm[1] = p1; mv[0] = m0; mv[1] = m1; vvp[0] = v0; vvp[1] = v1;
+    if (param != nullptr) st16(param + i * 8, pack8(p));
+  }
+}
+
+extern "C" int toa_adamw_flat(float* master, bf16_t* param, const void* grad, int grad_is_bf16, float* m,
+                              float* v, int64_t n, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, int step, float grad_scale, const float* norm_sq,
+                              float max_norm, hipStream_t stream) {
+  if (n % 8 != 0) return (int)hipErrorInvalidValue;
+  const int64_t n8 = n / 8;
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2 = 1.f - powf(beta2, (float)step);
+  const float inv_bc1 = 1.f / bc1, inv_sqrt_bc2 = 1.f / sqrtf(bc2);
+  int grid = toa_stream_grid(n8, 256);
+  if (grad_is_bf16)
+    hipLaunchKernelGGL(adamw_flat_kernel<true>, dim3(grid), dim3(256), 0, stream, master, param, grad, m, v, n8,
+                       lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
+                       max_norm);
+  else
+    hipLaunchKernelGGL(adamw_flat_kernel<false>, dim3(grid), dim3(256), 0, stream, master, param, grad, m, v, n8,
+                       lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
+                       max_norm);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Plain SGD with momentum over flat fp32 params (the estimator example's
+// optimizer) -- fp32 params, fp32 grads.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ buf, int64_t n, float lr,
+                                                       float momentum, float wd) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] + wd * p[i];
+    if (buf != nullptr) {
+      float b = momentum * buf[i] + gi;
+      buf[i] = b;
+      gi = b;
+    }
+    p[i] -= lr * gi;
+  }
+}
+
+extern "C" int toa_sgd_flat(float* p, const float* g, float* momentum_buf, int64_t n, float lr, float momentum,
+                            float weight_decay, hipStream_t stream) {
+  int grid = toa_stream_grid(n, 256);
+  hipLaunchKernelGGL(sgd_flat_kernel, dim3(grid), dim3(256), 0, stream, p, g, momentum_buf, n, lr, momentum,
+                     weight_decay);
+  return (int)hipGetLastError();
+}
+
+// bf16 <-> fp32 flat casts (used to (re)materialise the compute copy after a
+// checkpoint load and to zero/scale gradient buckets).
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                            int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 a = *((const f32x4*)x + 2 * i), b = *((const f32x4*)x + 2 * i + 1);
+    float f[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    st16(y + i * 8, pack8(f));
+  }
+}
+
+extern "C" int toa_cast_f32_to_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t stream) {
+  if (n % 8 != 0) return (int)hipErrorInvalidValue;
+  int grid = toa_stream_grid(n / 8, 256);
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid), dim3(256), 0, stream, x, y, n / 8);
+  return (int)hipGetLastError();
+}

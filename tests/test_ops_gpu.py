@@ -1,0 +1,191 @@
+"""Numerics of every HIP kernel vs a plain PyTorch fp32 reference (MI355X)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _lib():
+    from tf_operator_amd.ops import _lib
+
+    assert _lib.available(), _lib.load_error()
+    return _lib
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.mark.parametrize("cols", [4096, 1024, 200, 8192])
+@pytest.mark.parametrize("res", [False, True])
+def test_rmsnorm_fwd_bwd(cols, res):
+    _lib()
+    from tf_operator_amd.ops.norm import _ref_norm, _ref_norm_bwd, add_rms_norm, rms_norm
+
+    torch.manual_seed(0)
+    rows = 777
+    x = torch.randn(rows, cols, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(rows, cols, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(cols, device=DEV)).to(torch.bfloat16).requires_grad_()
+    if res:
+        h, y = add_rms_norm(x, r, w, 1e-5)
+        href = (x.float() + r.float())
+        assert rel(h, href) < 1e-2
+    else:
+        y = rms_norm(x, w, 1e-5)
+        href = x.float()
+    yref = href * torch.rsqrt(href.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    assert rel(y, yref) < 1e-2
+    dy = torch.randn_like(y)
+    if res:
+        dh = torch.randn_like(y)
+        torch.autograd.backward([h, y], [dh, dy])
+    else:
+        y.backward(dy)
+    hr = href.detach().clone().requires_grad_()
+    wr = w.detach().float().clone().requires_grad_()
+    yr = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    yr.backward(dy.float())
+    dx_ref = hr.grad + (dh.float() if res else 0)
+    assert rel(x.grad, dx_ref) < 2e-2
+    assert rel(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("cols", [4096, 512])
+def test_layernorm_fwd_bwd(cols):
+    _lib()
+    from tf_operator_amd.ops.norm import layer_norm
+
+    torch.manual_seed(1)
+    for dt in (torch.bfloat16, torch.float32):
+        x = torch.randn(300, cols, device=DEV, dtype=dt, requires_grad=True)
+        w = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
+        b = torch.randn(cols, device=DEV, dtype=dt, requires_grad=True)
+        y = layer_norm(x, w, b, 1e-5)
+        xr, wr, br = [t.detach().float().clone().requires_grad_() for t in (x, w, b)]
+        yr = torch.nn.functional.layer_norm(xr, (cols,), wr, br, 1e-5)
+        tol = 1e-2 if dt == torch.bfloat16 else 1e-5
+        assert rel(y, yr) < tol
+        dy = torch.randn_like(yr)
+        y.backward(dy.to(dt))
+        yr.backward(dy)
+        assert rel(x.grad, xr.grad) < 2 * tol + 1e-5
+        assert rel(w.grad, wr.grad) < 2 * tol + 1e-5
+        assert rel(b.grad, br.grad) < 2 * tol + 1e-5
+
+
+def test_rope_qkv_roundtrip():
+    _lib()
+    from tf_operator_amd.ops import llm
+
+    torch.manual_seed(2)
+    B, S, Hq, Hkv, D = 2, 64, 8, 2, 128
+    cos, sin = llm.rope_tables(S, D, device=DEV)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    for rep in (Hq // Hkv, 1):
+        q, k, v = llm.rope_qkv(qkv, cos, sin, B, S, Hq, Hkv, D, rep)
+        qc = qkv.detach().cpu().requires_grad_()
+        qr, kr, vr = llm.rope_qkv(qc, cos.cpu(), sin.cpu(), B, S, Hq, Hkv, D, rep)
+        assert rel(q.cpu(), qr) < 1e-2 and rel(k.cpu(), kr) < 1e-2 and rel(v.cpu(), vr) < 1e-3
+        gq, gk, gv = torch.randn_like(q), torch.randn_like(k), torch.randn_like(v)
+        (g,) = torch.autograd.grad([q, k, v], [qkv], [gq, gk, gv])
+        (gr,) = torch.autograd.grad([qr, kr, vr], [qc], [gq.cpu(), gk.cpu(), gv.cpu()])
+        assert rel(g.cpu(), gr) < 1e-2
+
+
+def test_swiglu():
+    _lib()
+    from tf_operator_amd.ops import llm
+
+    torch.manual_seed(3)
+    gu = torch.randn(333, 2 * 1024, device=DEV, dtype=torch.bfloat16)
+    out = llm.swiglu(gu)
+    ref = torch.nn.functional.silu(gu[:, :1024].float()) * gu[:, 1024:].float()
+    assert rel(out, ref) < 1e-2
+    d = torch.randn(333, 1024, device=DEV, dtype=torch.bfloat16)
+    dgu = llm.swiglu_bwd(d, gu)
+    g = gu.float().requires_grad_()
+    (torch.nn.functional.silu(g[:, :1024]) * g[:, 1024:]).backward(d.float())
+    assert rel(dgu, g.grad) < 1e-2
+
+
+@pytest.mark.parametrize("V", [128256, 1000, 10])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_cross_entropy(V, dt):
+    _lib()
+    from tf_operator_amd.ops.llm import cross_entropy
+
+    torch.manual_seed(4)
+    rows = 65
+    x = (3 * torch.randn(rows, V, device=DEV)).to(dt).requires_grad_()
+    t = torch.randint(0, V, (rows,), device=DEV)
+    t[5] = -100
+    loss = cross_entropy(x, t)
+    xr = x.detach().float().requires_grad_()
+    lr = torch.nn.functional.cross_entropy(xr, t, ignore_index=-100)
+    assert abs(float(loss) - float(lr)) < 1e-3 * max(1, abs(float(lr)))
+    loss.backward()
+    lr.backward()
+    assert rel(x.grad, xr.grad) < 1e-2
+
+
+def test_adamw_flat_matches_reference():
+    _lib()
+    from tf_operator_amd.ops.optim import adamw_reference, grad_norm_sq
+    from tf_operator_amd.ops import _lib as L
+
+    torch.manual_seed(5)
+    n = 1 << 20
+    master = torch.randn(n, device=DEV)
+    param = master.to(torch.bfloat16)
+    grad = torch.randn(n, device=DEV).to(torch.bfloat16)
+    m = torch.randn(n, device=DEV).abs() * 0.01
+    v = torch.rand(n, device=DEV) * 0.01
+    ref = [t.clone() for t in (master, m, v)]
+    nsq = grad_norm_sq(grad)
+    assert abs(float(nsq) - float(grad.float().pow(2).sum())) < 1e-3 * float(nsq)
+    L.call("toa_adamw_flat", L.ptr(master), L.ptr(param), L.ptr(grad), 1, L.ptr(m), L.ptr(v), n, 1e-3, 0.9,
+           0.95, 1e-8, 0.1, 3, 0.5, L.ptr(nsq), 1.0, L.stream(master))
+    adamw_reference(ref[0], grad, ref[1], ref[2], lr=1e-3, beta1=0.9, beta2=0.95, eps=1e-8, weight_decay=0.1,
+                    step=3, grad_scale=0.5, norm_sq=nsq, max_norm=1.0)
+    torch.cuda.synchronize()
+    assert rel(master, ref[0]) < 1e-6
+    assert rel(m, ref[1]) < 1e-6 and rel(v, ref[2]) < 1e-6
+    assert rel(param, ref[0]) < 1e-2
+
+
+def test_llama_tiny_gpu_matches_cpu_reference():
+    _lib()
+    from tf_operator_amd.models.llama import PRESETS, Llama
+
+    torch.manual_seed(6)
+    cfg = PRESETS["llama-tiny"]
+    m_gpu = Llama(cfg, device=DEV)
+    m_gpu.init_weights(0)
+    m_cpu = Llama(cfg, device="cpu")
+    m_cpu.load_state_dict({k: v.cpu() for k, v in m_gpu.state_dict().items()})
+    tok = torch.randint(0, cfg.vocab_size, (2, 64))
+    tgt = torch.randint(0, cfg.vocab_size, (2, 64))
+    lg = m_gpu(tok.to(DEV), tgt.to(DEV))
+    lc = m_cpu(tok, tgt)
+    assert abs(float(lg) - float(lc)) < 2e-2
+    lg.backward()
+    lc.backward()
+    for (n, pg), (_, pc) in zip(m_gpu.named_parameters(), m_cpu.named_parameters()):
+        assert rel(pg.grad.cpu(), pc.grad) < 5e-2, n
+
+
+def test_trainer_tiny_loss_decreases():
+    _lib()
+    from tf_operator_amd.models.llama import PRESETS
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device(DEV), micro_batch=2, seq_len=128, lr=1e-3)
+    b = tr.synthetic_batch()
+    losses = [float(tr.step([b])) for _ in range(5)]
+    assert losses[-1] < losses[0]

@@ -1,0 +1,140 @@
+"""Loader for the in-tree gfx950 HIP kernel library (``libtoa_hip.so``).
+
+The kernels are plain ``extern "C"`` launchers compiled by ``hipcc
+--offload-arch=gfx950`` (see :mod:`tf_operator_amd._build`); they are bound
+with :mod:`ctypes` and launched on PyTorch's *current* HIP stream, so they
+compose with hipBLASLt GEMMs, RCCL collectives and HIP-graph capture exactly
+like native torch ops.
+
+Policy: on a GPU tensor the HIP path is the only path.  If the library is
+missing or fails to load, every op raises -- there is no silent eager
+fallback on the GPU (CPU tensors use the PyTorch reference implementations
+that the numerics tests compare against).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtoa_hip.so")
+
+_lock = threading.Lock()
+_lib = None
+_err = None
+
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_f = ctypes.c_float
+c_p = ctypes.c_void_p
+
+# name -> argtypes (restype is always int = hipError_t)
+_SIGS = {
+    "toa_sumsq": [c_p, c_i64, c_int, c_p, c_p, c_int, c_p],
+    "toa_adamw_flat": [c_p, c_p, c_p, c_int, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_int, c_f, c_p, c_f, c_p],
+    "toa_sgd_flat": [c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_p],
+    "toa_cast_f32_to_bf16": [c_p, c_p, c_i64, c_p],
+    "toa_rmsnorm_fwd": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_f, c_p],
+    "toa_rmsnorm_bwd": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p],
+    "toa_layernorm_fwd": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_f, c_p],
+    "toa_layernorm_bwd": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_int, c_int, c_int, c_int,
+                          c_p],
+    "toa_norm_bwd_blocks": [c_int, c_int],
+    "toa_rope_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
+    "toa_rope_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
+    "toa_swiglu_fwd": [c_p, c_p, c_i64, c_int, c_p],
+    "toa_swiglu_bwd": [c_p, c_p, c_p, c_i64, c_int, c_p],
+    "toa_xent_fwd": [c_int, c_p, c_p, c_p, c_p, c_i64, c_int, c_i64, c_int, c_p],
+    "toa_xent_bwd": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_i64, c_int, c_p],
+    "toa_gemm_bias_act": [c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
+    "toa_softmax_xent_small": [c_p, c_p, c_p, c_p, c_int, c_int, c_f, c_p],
+    "toa_dropout_fwd": [c_int, c_p, c_p, c_p, c_i64, c_f, ctypes.c_uint64, ctypes.c_uint64, c_p],
+    "toa_accuracy": [c_p, c_p, c_p, c_int, c_int, c_p],
+    "toa_bias_act_bwd": [c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p],
+    "toa_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_p],
+    "toa_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                     c_f, c_p],
+    "toa_allreduce_oneshot": [c_p, c_p, c_int, c_int, c_i64, c_int, c_p],
+}
+
+
+def _load():
+    global _lib, _err
+    with _lock:
+        if _lib is not None or _err is not None:
+            return
+        if not os.path.exists(LIB_PATH):
+            _err = f"HIP kernel library not built: {LIB_PATH} (run `python -m tf_operator_amd._build`)"
+            return
+        try:
+            lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover - depends on the box
+            _err = f"failed to load {LIB_PATH}: {e}"
+            return
+        for name, argt in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argt
+            fn.restype = c_int
+        _lib = lib
+
+
+def available() -> bool:
+    _load()
+    return _lib is not None
+
+
+def load_error():
+    _load()
+    return _err
+
+
+def lib():
+    _load()
+    if _lib is None:
+        raise RuntimeError(_err)
+    return _lib
+
+
+def has(name: str) -> bool:
+    return available() and hasattr(_lib, name)
+
+
+def call(name: str, *args):
+    """Invoke launcher `name`; raise on a non-zero hipError_t."""
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with hipError {rc}")
+    return rc
+
+
+def stream(t: torch.Tensor | None = None):
+    dev = t.device if t is not None else None
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def use_hip(*tensors) -> bool:
+    """True when the op must run on the HIP path (any tensor on the GPU)."""
+    on_gpu = any(t is not None and t.is_cuda for t in tensors)
+    if on_gpu and not available():
+        raise RuntimeError(f"tf_operator_amd: GPU tensor but HIP kernels unavailable: {load_error()}")
+    return on_gpu
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return 0
+    if t.dtype == torch.float32:
+        return 1
+    raise TypeError(f"unsupported dtype {t.dtype} (bf16/fp32 only)")

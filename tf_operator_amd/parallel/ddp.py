@@ -1,0 +1,97 @@
+"""Bucketed, backward-overlapped gradient all-reduce on the flat gradient buffer.
+
+The flat gradient buffer (:class:`FlatParams`) is cut into buckets on
+parameter boundaries.  Each parameter's ready-hook (fired by the fused op
+that accumulated its gradient) decrements its bucket's pending count; when a
+bucket completes, an async ``all_reduce`` is issued on that slice of the
+flat buffer -- no copy into/out of bucket staging (zero-copy, unlike a
+generic DDP wrapper).
+
+Bucket sizing for MI355X xGMI: RCCL's ring/tree collectives on an 8-GPU
+xGMI node are per-link bound (~153 GB/s per link, 7 links per GPU), so
+buckets are large (default 512 MB) to stay in the bandwidth regime; at
+Llama-3-8B one decoder layer's gradients are ~436 MB, i.e. roughly one
+all-reduce per layer, each hidden under the backward of the next layers.
+
+Reference parity: SURVEY P3 / K16 (MultiWorkerMirroredStrategy NCCL
+all-reduce, multi_worker_strategy-with-keras.py:76-77) -- here RCCL.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from .flat import FlatParams, _round_up
+
+
+class GradBucketer:
+    def __init__(self, flat: FlatParams, bucket_bytes=None, group=None, average=True, enabled=None):
+        self.flat = flat
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.enabled = (self.world > 1) if enabled is None else enabled
+        self.average = average
+        mb = float(os.environ.get("TOA_BUCKET_MB", "512"))
+        self.bucket_bytes = int(bucket_bytes or mb * (1 << 20))
+        esz = flat.grad.element_size()
+        self.buckets = []  # [start, end, expected_uses]
+        cur = None
+        for s in flat.segments:
+            end = s.offset + _round_up(s.numel)
+            uses = getattr(s.param, "_toa_uses", 1)
+            if cur is None or (cur[1] - cur[0]) * esz >= self.bucket_bytes:
+                cur = [s.offset, end, 0]
+                self.buckets.append(cur)
+            cur[1] = end
+            cur[2] += uses
+            s.param._toa_bucket = len(self.buckets) - 1
+            if self.enabled:
+                s.param._toa_ready = self._ready
+        if self.buckets:
+            self.buckets[-1][1] = flat.numel
+        self.pending = [b[2] for b in self.buckets]
+        self.works = []
+        self.launched = [False] * len(self.buckets)
+
+    def _ready(self, param):
+        b = param._toa_bucket
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch(b)
+
+    def _launch(self, b):
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        s, e, _ = self.buckets[b]
+        view = self.flat.grad[s:e]
+        self.works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def finish(self):
+        """Launch any bucket not yet reduced (unused params), wait for all."""
+        if not self.enabled:
+            return
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for w in self.works:
+            w.wait()
+        self.works = []
+        self.pending = [b[2] for b in self.buckets]
+        self.launched = [False] * len(self.buckets)
+
+    @property
+    def grad_scale(self):
+        """Factor the optimizer applies to the summed gradients."""
+        return 1.0 / self.world if (self.enabled and self.average) else 1.0
+
+
+def broadcast_params(flat: FlatParams, src=0, group=None):
+    """Make every rank start from rank `src`'s weights (and master copy)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    dist.broadcast(flat.param, src, group=group)
+    if flat.master is not None:
+        flat.master.copy_(flat.param.float())

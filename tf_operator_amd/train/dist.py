@@ -1,0 +1,88 @@
+"""Process-group bootstrap from the operator's env contract.
+
+The operator (C++ core, ``torchenv`` / ``tfconfig`` generators) injects
+``MASTER_ADDR``, ``MASTER_PORT``, ``WORLD_SIZE``, ``RANK``, ``LOCAL_RANK``,
+``LOCAL_WORLD_SIZE`` (and ``TF_CONFIG`` for TFJob parity) into every replica;
+``torchrun`` sets the same variables.  One process per GPU; backend
+``nccl`` is RCCL on ROCm (xGMI inside a node), ``gloo`` for CPU plumbing.
+
+Reference parity: SURVEY D7 (pytorch.go:13-68 env contract), P4.
+"""
+from __future__ import annotations
+
+import dataclasses
+import datetime
+import json
+import os
+
+import torch
+import torch.distributed as dist
+
+
+@dataclasses.dataclass
+class DistInfo:
+    rank: int
+    world: int
+    local_rank: int
+    device: torch.device
+    backend: str | None
+
+
+def env_rank_world():
+    if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+        return int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    tf = os.environ.get("TF_CONFIG")
+    if tf:  # TF_CONFIG-only replica: chief/master first, then workers
+        cfg = json.loads(tf)
+        cluster, task = cfg.get("cluster", {}), cfg.get("task", {})
+        order = [t for t in ("chief", "master", "worker") if t in cluster]
+        rank, world = 0, 0
+        for t in order:
+            if t == task.get("type"):
+                rank = world + int(task.get("index", 0))
+            world += len(cluster[t])
+        if task.get("type") in order:
+            return rank, max(world, 1)
+    return 0, 1
+
+
+def init(backend=None, timeout_s=1800) -> DistInfo:
+    rank, world = env_rank_world()
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+        device = torch.device("cuda", torch.cuda.current_device())
+    else:
+        device = torch.device("cpu")
+    backend = backend or ("nccl" if use_cuda else "gloo")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = {}
+        if use_cuda and backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return DistInfo(rank, world, local_rank, device, backend if world > 1 else None)
+
+
+def barrier():
+    if dist.is_initialized():
+        if torch.cuda.is_available() and dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_max(x: float, device) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown():
+    if dist.is_initialized():
+        dist.destroy_process_group()

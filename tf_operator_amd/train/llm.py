@@ -1,0 +1,72 @@
+"""Data-parallel Llama trainer step (the flagship MI355X training path).
+
+One process per GPU.  Per step: forward (fused HIP ops + hipBLASLt GEMMs),
+backward writing weight gradients straight into the flat bf16 gradient
+buffer, bucketed RCCL all-reduce overlapped with backward, one fused AdamW
+over the flat fp32 master/m/v (device-side grad clipping, no host sync).
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..models.llama import PRESETS, Llama, LlamaConfig
+from ..ops.optim import FlatAdamW
+from ..parallel.ddp import GradBucketer, broadcast_params
+from ..parallel.flat import FlatParams
+
+
+class LlamaTrainer:
+    def __init__(self, cfg: LlamaConfig | str, device, micro_batch=1, seq_len=4096, grad_accum=1, lr=3e-4,
+                 seed=0, bucket_mb=None):
+        if isinstance(cfg, str):
+            cfg = PRESETS[cfg]
+        self.cfg = cfg
+        self.device = device
+        self.micro_batch = micro_batch
+        self.seq_len = seq_len
+        self.grad_accum = grad_accum
+        with torch.device(device):
+            model = Llama(cfg, device=device)
+        model.init_weights(seed)
+        self.model = model
+        names = {id(p): n for n, p in model.named_parameters()}
+        self.flat = FlatParams(model.params_backward_order(), names=names, no_decay=model.no_decay)
+        broadcast_params(self.flat)
+        self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20))
+        self.opt = FlatAdamW(self.flat, lr=lr)
+        self.step_idx = 0
+
+    def synthetic_batch(self, seed=1234):
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed)
+        tok = torch.randint(0, self.cfg.vocab_size, (self.micro_batch, self.seq_len + 1), device=self.device,
+                            generator=g)
+        return tok[:, :-1].contiguous(), tok[:, 1:].contiguous()
+
+    def step(self, batches):
+        """batches: list (len grad_accum) of (tokens, targets)."""
+        self.flat.zero_grad()
+        loss_sum = None
+        for i, (tok, tgt) in enumerate(batches):
+            loss = self.model(tok, tgt)
+            (loss / len(batches)).backward()
+            loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
+        self.bucketer.finish()
+        self.opt.step(grad_scale=self.bucketer.grad_scale)
+        self.step_idx += 1
+        return loss_sum / len(batches)
+
+    def tokens_per_step(self, world=1):
+        return self.micro_batch * self.seq_len * self.grad_accum * world
+
+
+def timed_steps(trainer: LlamaTrainer, batches, n, sync=True):
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(n):
+        loss = trainer.step(batches)
+    if sync and torch.cuda.is_available():
+        torch.cuda.synchronize()
+    return time.perf_counter() - t0, loss
