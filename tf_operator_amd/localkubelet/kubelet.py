@@ -1,0 +1,455 @@
+"""Local kubelet + scheduler simulator: runs Pods as local processes.
+
+Lets the whole operator stack run end-to-end on one machine (SURVEY 7.1
+item 2; replaces the reference's EKS-based E2E):
+
+* **scheduling**: a pod is bound when its ``amd.com/gpu`` request fits the
+  node's free GPUs (each pod gets exclusive device indices, exported as
+  ``HIP_VISIBLE_DEVICES`` -- the role the AMD device plugin plays on a real
+  node); ``schedulerName: volcano`` pods are gang-admitted only when their
+  PodGroup's ``minMember`` pods all fit at once (Volcano semantics);
+* **networking**: every per-replica headless Service name gets a unique
+  localhost port; MASTER_ADDR/PORT and DMLC_PS_ROOT_* are rewritten to
+  ``127.0.0.1:<port>``, cluster-spec strings (TF_CONFIG, TOA_PS_HOSTS) stay
+  byte-identical and their endpoints are mapped in ``TOA_ENDPOINT_MAP``; the
+  replica learns its own port from ``PORT``;
+* **lifecycle**: phase Pending -> Running -> Succeeded / Failed with
+  containerStatuses (exit code, restartCount, start times); restartPolicy
+  Always / OnFailure restart the container IN PLACE (restartCount++, as the
+  real kubelet does -- E2E replica_restart_policy_tests.py:27-156 checks
+  start times), Never leaves the pod terminal; pod deletion -> SIGTERM, then
+  SIGKILL after the grace period;
+* logs per container, served by the fake API server (``/log``).
+"""
+from __future__ import annotations
+
+import asyncio
+import copy
+import logging
+import os
+import re
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+from .. import core
+from ..operator.kube import ApiError, KubeClient
+
+log = logging.getLogger("tf_operator_amd.kubelet")
+
+SVC_RE = re.compile(r"([a-z0-9]([-a-z0-9]*[a-z0-9])?)\.([a-z0-9]([-a-z0-9]*[a-z0-9])?)\.svc(\.[a-z0-9.-]+)?:(\d+)")
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _quantity_int(v):
+    if v is None:
+        return 0
+    try:
+        return int(float(str(v)))
+    except ValueError:
+        return 0
+
+
+def pod_gpus(pod, resource="amd.com/gpu"):
+    n = 0
+    for c in pod.get("spec", {}).get("containers", []):
+        res = c.get("resources") or {}
+        n += _quantity_int((res.get("limits") or {}).get(resource) or (res.get("requests") or {}).get(resource))
+    return n
+
+
+class _Proc:
+    def __init__(self, pod, container, gpus):
+        self.pod = pod
+        self.container = container
+        self.gpus = gpus
+        self.proc: asyncio.subprocess.Process | None = None
+        self.restart_count = 0
+        self.started_at = None
+        self.finished_at = None
+        self.exit_code = None
+        self.deleting = False
+
+
+class LocalKubelet:
+    def __init__(self, kube: KubeClient, api=None, node_name="mi355x-node-0", gpus=0, workdir="/tmp/toa-kubelet",
+                 python=sys.executable, grace_seconds=3.0, restart_backoff=0.2, gpu_resource="amd.com/gpu"):
+        self.kube = kube
+        self.api = api
+        if api is not None:
+            api.kubelet = self
+        self.node = node_name
+        self.total_gpus = gpus
+        self.free_gpus = list(range(gpus))
+        self.workdir = workdir
+        self.python = python
+        self.grace = grace_seconds
+        self.restart_backoff = restart_backoff
+        self.gpu_resource = gpu_resource
+        self.ports: dict[tuple, int] = {}
+        self.running: dict[tuple, dict] = {}  # (ns, pod) -> {"procs": [...], "task": Task, "gpus": [...]}
+        self.pending: dict[tuple, dict] = {}
+        self._stop = asyncio.Event()
+        self._tasks = []
+        self.start_times: dict[tuple, list] = {}
+
+    # ---------------------------------------------------------------- service registry
+    def service_port(self, ns, name):
+        k = (ns, name)
+        if k not in self.ports:
+            self.ports[k] = _free_port()
+        return self.ports[k]
+
+    def service_address(self, ns, name, port=None):
+        return ("127.0.0.1", self.service_port(ns, name))
+
+    def log_path(self, ns, name, container=None):
+        d = os.path.join(self.workdir, ns, name)
+        if not os.path.isdir(d):
+            return None
+        if container is None:
+            logs = sorted(f for f in os.listdir(d) if f.endswith(".log"))
+            if not logs:
+                return None
+            return os.path.join(d, logs[0])
+        p = os.path.join(d, f"{container}.log")
+        return p if os.path.exists(p) else None
+
+    def is_running(self, ns, name):
+        r = self.running.get((ns, name))
+        return bool(r and any(p.proc is not None and p.proc.returncode is None for p in r["procs"]))
+
+    # ---------------------------------------------------------------- env rewriting
+    def _rewrite_env(self, pod, env: dict) -> dict:
+        ns = pod["metadata"].get("namespace", "default")
+        me = pod["metadata"]["name"]
+
+        # Cluster-spec strings (TF_CONFIG, TOA_PS_HOSTS, ...) stay byte-identical
+        # to what the operator injected; every service endpoint they mention is
+        # published in TOA_ENDPOINT_MAP ("svc.ns.svc:port" -> "127.0.0.1:port")
+        # and resolved by tf_operator_amd.train.dist.resolve_endpoint().
+        out = dict(env)
+        emap = {}
+        for v in env.values():
+            if isinstance(v, str):
+                for m in SVC_RE.finditer(v):
+                    emap[m.group(0)] = f"127.0.0.1:{self.service_port(m.group(3), m.group(1))}"
+        if emap:
+            import json as _json
+
+            out["TOA_ENDPOINT_MAP"] = _json.dumps(emap, separators=(",", ":"))
+
+        def host_to_port(host):
+            if host in ("localhost", "127.0.0.1"):
+                return self.service_port(ns, me)
+            parts = host.split(".")
+            hns = parts[1] if len(parts) > 2 and parts[2] == "svc" else ns
+            return self.service_port(hns, parts[0])
+
+        if "MASTER_ADDR" in env:
+            out["MASTER_PORT"] = str(host_to_port(env["MASTER_ADDR"]))
+            out["MASTER_ADDR"] = "127.0.0.1"
+        if env.get("DMLC_PS_ROOT_URI"):
+            out["DMLC_PS_ROOT_PORT"] = str(host_to_port(env["DMLC_PS_ROOT_URI"]))
+            out["DMLC_PS_ROOT_URI"] = "127.0.0.1"
+        return out
+
+    # ---------------------------------------------------------------- status
+    async def _put_status(self, pod_key, mutate):
+        ns, name = pod_key
+        for _ in range(5):
+            try:
+                cur = await self.kube.get("pods", ns, name)
+            except ApiError:
+                return
+            st = copy.deepcopy(cur.get("status") or {})
+            mutate(st)
+            cur["status"] = st
+            try:
+                await self.kube.update_status("pods", ns, cur)
+                return
+            except ApiError as e:
+                if e.status != 409:
+                    return
+
+    def _container_statuses(self, procs):
+        out = []
+        for p in procs:
+            s = {"name": p.container["name"], "restartCount": p.restart_count, "image": p.container.get("image", ""),
+                 "ready": p.exit_code is None and p.proc is not None}
+            if p.exit_code is None and p.proc is not None:
+                s["state"] = {"running": {"startedAt": core.rfc3339(p.started_at)}}
+            elif p.exit_code is not None:
+                s["state"] = {"terminated": {"exitCode": p.exit_code,
+                                             "reason": "Completed" if p.exit_code == 0 else "Error",
+                                             "startedAt": core.rfc3339(p.started_at),
+                                             "finishedAt": core.rfc3339(p.finished_at or time.time())}}
+            else:
+                s["state"] = {"waiting": {"reason": "ContainerCreating"}}
+            out.append(s)
+        return out
+
+    # ---------------------------------------------------------------- scheduling
+    def _gang_ready(self, pod):
+        """Volcano admission: all minMember pods of the group fit together."""
+        ann = pod["metadata"].get("annotations") or {}
+        group = ann.get("scheduling.k8s.io/group-name")
+        if not group or pod.get("spec", {}).get("schedulerName") != "volcano" or self.api is None:
+            return True, [pod]
+        ns = pod["metadata"].get("namespace", "default")
+        pg = self.api.get("scheduling.volcano.sh/podgroups", ns, group)
+        if pg is None:
+            return False, []
+        min_member = int(pg.get("spec", {}).get("minMember", 1))
+        members = [p for (pns, _), p in ((k, v["pod"]) for k, v in self.pending.items())
+                   if pns == ns and (p["metadata"].get("annotations") or {}).get("scheduling.k8s.io/group-name") == group]
+        if len(members) < min_member:
+            return False, []
+        need = sum(pod_gpus(p, self.gpu_resource) for p in members)
+        if need > len(self.free_gpus):
+            return False, []
+        pg_status = dict(pg.get("status") or {})
+        pg_status.update({"phase": "Running", "running": len(members)})
+        self.api.put_status("scheduling.volcano.sh/podgroups", ns, group, pg_status)
+        return True, members
+
+    async def _try_schedule(self):
+        for key in list(self.pending):
+            if key not in self.pending:
+                continue
+            pod = self.pending[key]["pod"]
+            ok, members = self._gang_ready(pod)
+            if not ok:
+                continue
+            if len(members) == 1:
+                need = pod_gpus(pod, self.gpu_resource)
+                if need > len(self.free_gpus):
+                    if not self.pending[key].get("unsched_reported"):
+                        self.pending[key]["unsched_reported"] = True
+                        await self._put_status(key, lambda st: st.update({
+                            "phase": "Pending", "conditions": [{"type": "PodScheduled", "status": "False",
+                                                                "reason": "Unschedulable",
+                                                                "message": f"0/1 nodes are available: 1 Insufficient "
+                                                                           f"{self.gpu_resource}."}]}))
+                    continue
+            for m in members:
+                mk = (m["metadata"].get("namespace", "default"), m["metadata"]["name"])
+                if mk not in self.pending:
+                    continue
+                p = self.pending.pop(mk)["pod"]
+                need = pod_gpus(p, self.gpu_resource)
+                gpus = [self.free_gpus.pop(0) for _ in range(need)]
+                self._start_pod(p, gpus)
+
+    # ---------------------------------------------------------------- running
+    def _start_pod(self, pod, gpus):
+        key = (pod["metadata"].get("namespace", "default"), pod["metadata"]["name"])
+        procs = [_Proc(pod, c, gpus) for c in pod.get("spec", {}).get("containers", [])]
+        rec = {"procs": procs, "gpus": gpus, "pod": pod}
+        self.running[key] = rec
+        rec["task"] = asyncio.create_task(self._run_pod(key, rec))
+
+    def _build_env(self, pod, container, gpus):
+        env = {}
+        for e in container.get("env") or []:
+            if "value" in e:
+                env[e["name"]] = str(e["value"])
+        env = self._rewrite_env(pod, env)
+        ns = pod["metadata"].get("namespace", "default")
+        base = dict(os.environ)
+        base.update(env)
+        base["HOSTNAME"] = pod["metadata"]["name"]
+        base["PORT"] = str(self.service_port(ns, pod["metadata"]["name"]))
+        base["TOA_POD_NAME"] = pod["metadata"]["name"]
+        base["TOA_POD_NAMESPACE"] = ns
+        base["TOA_NODE_NAME"] = self.node
+        base["PYTHONPATH"] = REPO_ROOT + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
+        if gpus:
+            base["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpus)
+        else:
+            base.pop("HIP_VISIBLE_DEVICES", None)
+            base["TOA_NO_GPU"] = "1"
+        return base
+
+    def _argv(self, container):
+        cmd = list(container.get("command") or []) + [str(a) for a in container.get("args") or []]
+        if cmd and cmd[0] in ("python", "python3"):
+            cmd[0] = self.python
+        return cmd
+
+    async def _run_container(self, key, rec, p: _Proc):
+        pod = rec["pod"]
+        rp = pod.get("spec", {}).get("restartPolicy", "Always")
+        d = os.path.join(self.workdir, key[0], key[1])
+        os.makedirs(d, exist_ok=True)
+        logf = os.path.join(d, f"{p.container['name']}.log")
+        while True:
+            argv = self._argv(p.container)
+            env = self._build_env(pod, p.container, rec["gpus"])
+            with open(logf, "ab") as lf:
+                p.started_at = time.time()
+                self.start_times.setdefault(key, []).append(p.started_at)
+                p.exit_code = None
+                try:
+                    p.proc = await asyncio.create_subprocess_exec(*argv, stdout=lf, stderr=subprocess.STDOUT,
+                                                                  env=env, cwd=d, start_new_session=True)
+                except (FileNotFoundError, PermissionError, IndexError) as e:
+                    lf.write(f"failed to start container: {e}\n".encode())
+                    p.proc = None
+                    p.exit_code = 127
+                    p.finished_at = time.time()
+                await self._sync_status(key, rec)
+                if p.proc is not None:
+                    code = await p.proc.wait()
+                    p.exit_code = code if code >= 0 else 128 - code  # signal N -> 128+N
+                    p.finished_at = time.time()
+            if p.deleting or self._stop.is_set():
+                return
+            restart = rp == "Always" or (rp == "OnFailure" and p.exit_code != 0)
+            if not restart:
+                await self._sync_status(key, rec)
+                return
+            p.restart_count += 1
+            await self._sync_status(key, rec)
+            await asyncio.sleep(min(5.0, self.restart_backoff * (2 ** min(p.restart_count - 1, 5))))
+            if p.deleting or self._stop.is_set():
+                return
+
+    async def _sync_status(self, key, rec):
+        procs = rec["procs"]
+        done = all(p.exit_code is not None and (p.proc is None or p.proc.returncode is not None) for p in procs)
+        rp = rec["pod"].get("spec", {}).get("restartPolicy", "Always")
+        if done and (rp == "Never" or (rp == "OnFailure" and all(p.exit_code == 0 for p in procs))):
+            phase = "Succeeded" if all(p.exit_code == 0 for p in procs) else "Failed"
+        else:
+            phase = "Running"
+        cs = self._container_statuses(procs)
+
+        def mutate(st):
+            st["phase"] = phase
+            st["podIP"] = "127.0.0.1"
+            st["hostIP"] = "127.0.0.1"
+            st.setdefault("startTime", core.rfc3339())
+            st["containerStatuses"] = cs
+            st["conditions"] = [{"type": "PodScheduled", "status": "True"},
+                                {"type": "Ready", "status": "True" if phase == "Running" else "False"}]
+
+        await self._put_status(key, mutate)
+
+    async def _run_pod(self, key, rec):
+        try:
+            await asyncio.gather(*(self._run_container(key, rec, p) for p in rec["procs"]))
+        finally:
+            if not any(p.deleting for p in rec["procs"]):
+                await self._sync_status(key, rec)
+            self._release(key)
+
+    def _release(self, key):
+        rec = self.running.get(key)
+        if rec is None:
+            return
+        if all(p.proc is None or p.proc.returncode is not None for p in rec["procs"]):
+            self.free_gpus.extend(rec["gpus"])
+            self.free_gpus.sort()
+            rec["gpus"] = []
+            self.running.pop(key, None)
+
+    async def _kill(self, key):
+        rec = self.running.get(key)
+        if rec is None:
+            return
+        for p in rec["procs"]:
+            p.deleting = True
+            if p.proc is not None and p.proc.returncode is None:
+                try:
+                    os.killpg(p.proc.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        deadline = time.monotonic() + self.grace
+        for p in rec["procs"]:
+            if p.proc is None:
+                continue
+            try:
+                await asyncio.wait_for(p.proc.wait(), timeout=max(0.0, deadline - time.monotonic()))
+            except asyncio.TimeoutError:
+                try:
+                    os.killpg(p.proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                await p.proc.wait()
+        self._release(key)
+
+    # ---------------------------------------------------------------- watch loop
+    async def _loop(self):
+        while not self._stop.is_set():
+            try:
+                lst = await self.kube.list("pods")
+                for pod in lst.get("items", []):
+                    await self._on_pod("ADDED", pod)
+                async for et, pod in self.kube.watch("pods", None, None, lst["metadata"]["resourceVersion"]):
+                    if self._stop.is_set():
+                        return
+                    if et in ("BOOKMARK", "ERROR"):
+                        if et == "ERROR":
+                            break
+                        continue
+                    await self._on_pod(et, pod)
+            except asyncio.CancelledError:
+                return
+            except Exception as e:
+                if self._stop.is_set():
+                    return
+                log.warning("kubelet watch: %s", e)
+                await asyncio.sleep(0.3)
+
+    async def _on_pod(self, et, pod):
+        key = (pod["metadata"].get("namespace", "default"), pod["metadata"]["name"])
+        if et == "DELETED":
+            self.pending.pop(key, None)
+            if key in self.running:
+                await self._kill(key)
+            return
+        if pod.get("metadata", {}).get("deletionTimestamp"):
+            if key in self.running:
+                await self._kill(key)
+            return
+        if key in self.running or key in self.pending:
+            return
+        if (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
+            return
+        if (pod.get("status") or {}).get("phase") == "Running":
+            return  # owned by a previous kubelet incarnation
+        self.pending[key] = {"pod": pod}
+        await self._try_schedule()
+
+    async def _scheduler(self):
+        while not self._stop.is_set():
+            await asyncio.sleep(0.1)
+            if self.pending:
+                await self._try_schedule()
+
+    async def start(self):
+        os.makedirs(self.workdir, exist_ok=True)
+        self._tasks = [asyncio.create_task(self._loop()), asyncio.create_task(self._scheduler())]
+
+    async def stop(self):
+        self._stop.set()
+        for key in list(self.running):
+            await self._kill(key)
+        for t in self._tasks:
+            t.cancel()
+        for t in self._tasks:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass

@@ -1,0 +1,376 @@
+"""The operator's asyncio I/O shell around the pure C++ reconcile engine.
+
+Replaces both reference control planes (controller-runtime
+`TFJobReconciler` and the legacy informer/workqueue `TFController`) with one:
+
+* informers: list+watch of every enabled job kind and of pods / services
+  labelled ``group-name=kubeflow.org``, cached in the native
+  :class:`~tf_operator_amd.core.Store`, with resync-dropping and
+  expectation bookkeeping on dependent create/delete
+  (pkg/common/util/reconciler.go:38-157);
+* a native rate-limited :class:`~tf_operator_amd.core.WorkQueue` with REAL
+  delayed requeue (fixes the new binary's no-op FakeWorkQueue,
+  tfjob_controller.go:90);
+* N sync workers: job -> ``core.reconcile`` -> execute the action list
+  (pod / service / PodGroup create & delete, job TTL deletion), write status
+  through the status subresource, emit Events, bump metrics, requeue.
+
+Reference call stacks: SURVEY CS2 / CS3 / CS4.
+"""
+from __future__ import annotations
+
+import asyncio
+import dataclasses
+import logging
+import time
+
+from .. import core
+from ..utils.k8s import controller_ref, format_selector
+from .kube import ApiError, KubeClient, plural_key
+from .metrics import OperatorMetrics
+
+log = logging.getLogger("tf_operator_amd.controller")
+
+KIND_PLURAL = {"TFJob": "tfjobs", "PyTorchJob": "pytorchjobs", "MXJob": "mxjobs", "XGBoostJob": "xgboostjobs"}
+PLURAL_KIND = {v: k for k, v in KIND_PLURAL.items()}
+
+
+@dataclasses.dataclass
+class ControllerOptions:
+    namespace: str | None = None          # None = all namespaces (--namespace)
+    threadiness: int = 1                  # --threadiness
+    enable_gang_scheduling: bool = False  # --enable-gang-scheduling
+    gang_scheduler_name: str = "volcano"
+    inject_rocm_env: bool = True
+    cluster_domain: str = ""              # CUSTOM_CLUSTER_DOMAIN
+    nccl_env: dict = dataclasses.field(default_factory=dict)
+    resync_period: float = 12 * 3600.0    # --resyc-period (12h)
+    report_url: str | None = None         # injected as TOA_REPORT_URL
+
+
+class JobController:
+    def __init__(self, kube: KubeClient, kinds=("TFJob", "PyTorchJob", "MXJob", "XGBoostJob"),
+                 options: ControllerOptions | None = None, metrics: OperatorMetrics | None = None):
+        self.kube = kube
+        self.kinds = [k for k in kinds]
+        self.opt = options or ControllerOptions()
+        self.metrics = metrics or OperatorMetrics()
+        self.queue = core.WorkQueue()
+        self.expectations = core.Expectations()
+        self.jobs = {KIND_PLURAL[k]: core.Store() for k in self.kinds}
+        self.pods = core.Store()
+        self.services = core.Store()
+        self._synced = {}
+        self._tasks = []
+        self._stop = asyncio.Event()
+        self._emitted = {}  # job uid -> set of (reason, message) already recorded
+        self._first_step_seen = set()
+        self.sync_count = 0
+
+    # ------------------------------------------------------------------ informers
+    async def _informer(self, key, store, on_event, label_selector=None):
+        name = key
+        while not self._stop.is_set():
+            try:
+                lst = await self.kube.list(key, self.opt.namespace, label_selector=label_selector)
+                seen = set()
+                for o in lst.get("items", []):
+                    k = core.Store.key_of(o)
+                    seen.add(k)
+                    changed = store.upsert(o)
+                    await on_event("ADDED" if changed else "SYNC", o)
+                for k in store.keys():
+                    if k not in seen:
+                        old = store.get(k)
+                        store.remove(k)
+                        await on_event("DELETED", old)
+                self._synced[name] = True
+                rv = lst.get("metadata", {}).get("resourceVersion")
+                async for et, o in self.kube.watch(key, self.opt.namespace, label_selector, rv):
+                    if self._stop.is_set():
+                        return
+                    if et == "BOOKMARK":
+                        continue
+                    if et == "ERROR":
+                        break  # 410 Gone -> relist
+                    if et == "DELETED":
+                        store.remove(core.Store.key_of(o))
+                        await on_event("DELETED", o)
+                    else:
+                        changed = store.upsert(o)
+                        await on_event(et if changed else "SYNC", o)
+            except asyncio.CancelledError:
+                return
+            except Exception as e:  # connection loss: back off and relist
+                if self._stop.is_set():
+                    return
+                log.warning("informer %s: %s; relisting", name, e)
+                await asyncio.sleep(0.5)
+
+    def _job_key(self, plural, ns, name):
+        return f"{plural}/{ns}/{name}"
+
+    async def _on_job(self, plural, et, job):
+        md = job.get("metadata", {})
+        key = self._job_key(plural, md.get("namespace", "default"), md.get("name"))
+        if et == "DELETED":
+            self.metrics.deleted.labels(md.get("namespace", "default")).inc()
+            for rt in (job.get("spec", {}).get(core.kind_info(PLURAL_KIND[plural])["specs_field"]) or {}):
+                jk = f"{md.get('namespace', 'default')}/{md.get('name')}"
+                self.expectations.delete_key(core.native().expectation_pods_key(jk, rt.lower()))
+                self.expectations.delete_key(core.native().expectation_services_key(jk, rt.lower()))
+            self._emitted.pop(md.get("uid"), None)
+            return
+        if et == "ADDED" and not (job.get("status") or {}).get("conditions"):
+            self.metrics.created.labels(md.get("namespace", "default")).inc()
+        if et != "SYNC":
+            self.queue.add(key)
+
+    async def _on_dependent(self, kind, et, obj):
+        ref = controller_ref(obj)
+        if not ref or ref.get("apiVersion", "").split("/")[0] != "kubeflow.org":
+            return
+        plural = KIND_PLURAL.get(ref.get("kind"))
+        if plural not in self.jobs:
+            return
+        md = obj.get("metadata", {})
+        ns = md.get("namespace", "default")
+        rt = (md.get("labels") or {}).get("replica-type", "")
+        jk = f"{ns}/{ref.get('name')}"
+        ek = (core.native().expectation_pods_key(jk, rt) if kind == "pods"
+              else core.native().expectation_services_key(jk, rt))
+        if et == "ADDED":
+            self.expectations.creation_observed(ek)
+        elif et == "DELETED":
+            self.expectations.deletion_observed(ek)
+        if et != "SYNC":
+            self.queue.add(self._job_key(plural, ns, ref.get("name")))
+
+    # ------------------------------------------------------------------ sync
+    def _satisfied(self, job, kind):
+        md = job["metadata"]
+        jk = f"{md.get('namespace', 'default')}/{md['name']}"
+        specs = job.get("spec", {}).get(core.kind_info(kind)["specs_field"]) or {}
+        now = time.time()
+        n = core.native()
+        for rt in specs:
+            if not self.expectations.satisfied(n.expectation_pods_key(jk, rt.lower()), now):
+                return False
+            if not self.expectations.satisfied(n.expectation_services_key(jk, rt.lower()), now):
+                return False
+        return True
+
+    def _options(self, key):
+        o = {"cluster_domain": self.opt.cluster_domain, "enable_gang_scheduling": self.opt.enable_gang_scheduling,
+             "gang_scheduler_name": self.opt.gang_scheduler_name, "inject_rocm_env": self.opt.inject_rocm_env,
+             "previous_retry": self.queue.num_requeues(key)}
+        env = dict(self.opt.nccl_env)
+        if self.opt.report_url:
+            env["TOA_REPORT_URL"] = self.opt.report_url
+        if env:
+            o["nccl_env"] = env
+        return o
+
+    async def sync(self, key):
+        plural, ns, name = key.split("/", 2)
+        kind = PLURAL_KIND[plural]
+        job = self.jobs[plural].get(f"{ns}/{name}")
+        if job is None:
+            return None
+        self.sync_count += 1
+        t0 = time.perf_counter()
+        res_key = plural_key(plural)
+        orig_status = job.get("status") or {}
+        if not orig_status.get("conditions"):
+            job = core.on_job_created(job)
+        dynamic = bool(job.get("spec", {}).get("enableDynamicWorker"))
+        if not dynamic and not self._satisfied(job, kind):
+            return None
+        uid = job["metadata"].get("uid")
+        sel = format_selector({"group-name": "kubeflow.org", "job-name": name.replace("/", "-")})
+
+        def owned(objs):
+            out = []
+            for o in objs:
+                ref = controller_ref(o)
+                if ref is None or ref.get("uid") == uid:
+                    out.append(o)
+            return out
+
+        pods = owned(self.pods.list(ns, {"group-name": "kubeflow.org", "job-name": name.replace("/", "-")}))
+        svcs = owned(self.services.list(ns, {"group-name": "kubeflow.org", "job-name": name.replace("/", "-")}))
+        del sel
+        now = time.time()
+        res = core.reconcile(job, pods, svcs, now=now, options=self._options(key))
+        for e in res.get("expect", []):
+            self.expectations.expect_creations(e["key"], int(e["add"]), now)
+        await self._execute(res, job, res_key)
+        status = res["status"]
+        if res.get("status_changed") or status != orig_status:
+            body = dict(job)
+            body["status"] = status
+            try:
+                await self.kube.update_status(res_key, ns, body)
+            except ApiError as e:
+                if e.status == 409:
+                    self.queue.add_rate_limited(key)
+                elif e.status != 404:
+                    raise
+        await self._emit_events(job, res.get("events", []), kind)
+        m = res.get("metrics", {})
+        if m.get("succeeded"):
+            self.metrics.successful.labels(ns).inc(m["succeeded"])
+        if m.get("failed"):
+            self.metrics.failed.labels(ns).inc(m["failed"])
+        if m.get("restarted"):
+            self.metrics.restarted.labels(ns).inc(m["restarted"])
+        if res.get("requeue_after") is not None:
+            self.queue.add_after(key, max(0.05, float(res["requeue_after"])))
+        self.metrics.reconcile_seconds.labels(kind).observe(time.perf_counter() - t0)
+        return res
+
+    async def _execute(self, res, job, res_key):
+        ns = job["metadata"].get("namespace", "default")
+
+        async def do(a):
+            op = a["op"]
+            try:
+                if op == "create_pod":
+                    await self.kube.create("pods", ns, a["pod"])
+                elif op == "create_service":
+                    await self.kube.create("services", ns, a["service"])
+                elif op == "delete_pod":
+                    await self.kube.delete("pods", a["namespace"], a["name"])
+                elif op == "delete_service":
+                    await self.kube.delete("services", a["namespace"], a["name"])
+                elif op == "sync_podgroup":
+                    pg = a["podgroup"]
+                    try:
+                        cur = await self.kube.get("scheduling.volcano.sh/podgroups", ns, pg["metadata"]["name"])
+                        if cur.get("spec") != pg["spec"]:
+                            cur["spec"] = pg["spec"]
+                            await self.kube.update("scheduling.volcano.sh/podgroups", ns, cur)
+                    except ApiError as e:
+                        if e.status != 404:
+                            raise
+                        await self.kube.create("scheduling.volcano.sh/podgroups", ns, pg)
+                elif op == "delete_podgroup":
+                    await self.kube.delete("scheduling.volcano.sh/podgroups", a["namespace"], a["name"])
+                elif op == "delete_job":
+                    await self.kube.delete(res_key, a["namespace"], a["name"])
+                    await self._record_event(job, "Normal", "SuccessfulDeleteJob",
+                                             f"Deleted job: {a['name']}")
+            except ApiError as e:
+                if op.startswith("create") and e.status != 409 and a.get("expectation_key"):
+                    # failed creation: lower the expectation (createNewPod, pod.go:248-256)
+                    self.expectations.creation_observed(a["expectation_key"])
+                if e.status in (404, 409):
+                    return
+                if op == "delete_job":
+                    await self._record_event(job, "Warning", "FailedDeleteJob", str(e))
+                log.warning("action %s failed: %s", op, e)
+
+        creates = [a for a in res["actions"] if a["op"].startswith("create")]
+        others = [a for a in res["actions"] if not a["op"].startswith("create")]
+        for a in others:
+            await do(a)
+        if creates:
+            await asyncio.gather(*(do(a) for a in creates))
+
+    async def _record_event(self, job, etype, reason, message):
+        md = job["metadata"]
+        ev = {"apiVersion": "v1", "kind": "Event",
+              "metadata": {"generateName": md["name"] + ".", "namespace": md.get("namespace", "default")},
+              "involvedObject": {"apiVersion": job.get("apiVersion", "kubeflow.org/v1"), "kind": job.get("kind"),
+                                 "name": md["name"], "namespace": md.get("namespace", "default"),
+                                 "uid": md.get("uid")},
+              "type": etype, "reason": reason, "message": message, "count": 1,
+              "firstTimestamp": core.rfc3339(), "lastTimestamp": core.rfc3339(),
+              "source": {"component": "tf-operator-amd"}}
+        try:
+            await self.kube.create("events", md.get("namespace", "default"), ev)
+        except Exception as e:  # events are best effort
+            log.debug("event: %s", e)
+
+    async def _emit_events(self, job, events, kind):
+        seen = self._emitted.setdefault(job["metadata"].get("uid"), set())
+        for e in events:
+            k = (e["reason"], e["message"])
+            if k in seen:
+                continue  # k8s would aggregate repeats into one Event with count++
+            seen.add(k)
+            await self._record_event(job, e["type"], e["reason"], e["message"])
+
+    # ------------------------------------------------------------------ first-step reports
+    def report(self, payload: dict):
+        """POST /report from a trainer's rank 0: first-step time + throughput."""
+        ns, name = payload.get("namespace", "default"), payload.get("job")
+        kind = payload.get("kind", "TFJob")
+        job = None
+        plural = KIND_PLURAL.get(kind, "tfjobs")
+        if plural in self.jobs:
+            job = self.jobs[plural].get(f"{ns}/{name}")
+        if payload.get("first_step_time") and (ns, name) not in self._first_step_seen and job is not None:
+            created = core.parse_rfc3339(job["metadata"].get("creationTimestamp", ""))
+            if created == created:  # not NaN
+                self.metrics.first_step.labels(ns, kind).observe(max(0.0, float(payload["first_step_time"]) - created))
+                self._first_step_seen.add((ns, name))
+        if payload.get("samples_per_sec") is not None:
+            self.metrics.samples_per_sec.labels(ns, name).set(float(payload["samples_per_sec"]))
+
+    # ------------------------------------------------------------------ run
+    async def _worker(self):
+        loop = asyncio.get_running_loop()
+        while not self._stop.is_set():
+            key = await loop.run_in_executor(None, self.queue.get, 0.2)
+            if key is None:
+                if self.queue.shutting_down():
+                    return
+                continue
+            try:
+                await self.sync(key)
+                self.queue.forget(key)
+            except Exception as e:
+                log.exception("sync %s failed: %s", key, e)
+                self.queue.add_rate_limited(key)
+            finally:
+                self.queue.done(key)
+
+    async def _resync(self):
+        while not self._stop.is_set():
+            try:
+                await asyncio.wait_for(self._stop.wait(), timeout=self.opt.resync_period)
+            except asyncio.TimeoutError:
+                for plural, store in self.jobs.items():
+                    for k in store.keys():
+                        self.queue.add(f"{plural}/{k}")
+
+    async def start(self):
+        lbl = "group-name=kubeflow.org"
+        for plural in self.jobs:
+            store = self.jobs[plural]
+            self._tasks.append(asyncio.create_task(self._informer(
+                plural_key(plural), store, lambda et, o, p=plural: self._on_job(p, et, o))))
+        self._tasks.append(asyncio.create_task(self._informer(
+            "pods", self.pods, lambda et, o: self._on_dependent("pods", et, o), lbl)))
+        self._tasks.append(asyncio.create_task(self._informer(
+            "services", self.services, lambda et, o: self._on_dependent("services", et, o), lbl)))
+        # WaitForCacheSync
+        want = len(self.jobs) + 2
+        while len(self._synced) < want and not self._stop.is_set():
+            await asyncio.sleep(0.01)
+        for _ in range(max(1, self.opt.threadiness)):
+            self._tasks.append(asyncio.create_task(self._worker()))
+        self._tasks.append(asyncio.create_task(self._resync()))
+
+    async def stop(self):
+        self._stop.set()
+        self.queue.shutdown()
+        for t in self._tasks:
+            t.cancel()
+        for t in self._tasks:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass
+        self._tasks = []

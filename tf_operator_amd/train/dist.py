@@ -86,3 +86,18 @@ def all_max(x: float, device) -> float:
 def shutdown():
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def resolve_endpoint(addr: str) -> tuple[str, int]:
+    """'svc.ns.svc[.domain]:port' -> (host, port).  On a real cluster DNS
+    resolves the service name; under the local kubelet TOA_ENDPOINT_MAP maps
+    it to 127.0.0.1:<allocated port>."""
+    m = json.loads(os.environ.get("TOA_ENDPOINT_MAP", "{}") or "{}")
+    addr = m.get(addr, addr)
+    host, _, port = addr.rpartition(":")
+    return host, int(port)
+
+
+def own_port(default: int) -> int:
+    """Port this replica should listen on (local kubelet sets PORT)."""
+    return int(os.environ.get("PORT", default))
