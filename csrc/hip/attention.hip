@@ -1,0 +1,564 @@
+// Causal flash attention for gfx950 (bf16 in/out, fp32 accumulate), with
+// native GQA (K/V stay packed per kv-head; no repeat_interleave copies).
+//
+// Layouts: q/o [B, H, S, D], k/v [B, Hk, S, D], lse [B, H, S] (natural log),
+// D = 128 (or 64).  One workgroup = 4 waves = a 128-row query block of one
+// (batch, head); wave w owns 32 query rows.  K/V tiles of 64 keys are staged
+// global -> registers -> LDS (double buffered, loads of tile t+1 in flight
+// while tile t is computed -- guide T14), K in a 16-way XOR-swizzled
+// row-major image read with ds_read_b128 (conflict-free for the 32x32 MFMA
+// operand pattern, guide T2), V row-major with a 4-row XOR swizzle read by
+// ds_read_b64_tr_b16 (hardware transpose for the PV operand, guide T10).
+//
+// MFMA orientation (guide §3 "accumulator tile as next operand"):
+//   S^T[key][q] = K . Q^T      v_mfma_f32_32x32x16_bf16, A = K frag, B = Q frag
+//   -> each lane owns ONE query row (column q = lane&31) and 16 of the 64 key
+//      scores (its partner lane l^32 owns the other 16 of each 32-key half), so
+//      the online softmax row max/sum is lane-local + one cross-half shuffle;
+//   O^T[d][q] += V^T . P^T     the S^T accumulator registers, converted to
+//      bf16, ARE the B operand (k permutation handled by the V^T read order).
+// Softmax in the exp2 domain with the scale folded in; causal tiles beyond a
+// wave's last row are skipped wave-uniformly; blocks are launched
+// heaviest-first for load balance.
+//
+// Backward = three kernels: preprocess (delta = rowsum(dO*O)), dK/dV
+// (workgroup per 128-key block, sweeping the GQA group's query heads), dQ
+// (workgroup per 128-query block).  No float atomics: deterministic.
+#include "toa_common.h"
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+#define LOG2E 1.4426950408889634f
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// LDS tile geometry: 64 keys x 128 d bf16 = 16 KB, rows of 256 B = 16 chunks of 16 B.
+#define TK 64
+#define ROWB 256
+
+// K image: chunk c of row `key` stored at chunk position c ^ (key & 15)
+__device__ __forceinline__ int k_off(int key, int chunk) { return key * ROWB + ((chunk ^ (key & 15)) << 4); }
+// V image: chunk c of row `key` stored at chunk position c ^ ((key & 3) << 2)
+__device__ __forceinline__ int v_off(int key, int chunk) { return key * ROWB + ((chunk ^ ((key & 3) << 2)) << 4); }
+
+typedef short __attribute__((ext_vector_type(4))) s16x4;
+__device__ __forceinline__ bf16x4 tr_read(const char* lds_base, int byte_off) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  lds_s16x4* p = (lds_s16x4*)(lds_base + byte_off);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+                                                          const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+                                                          float* __restrict__ LSE, int H, int Hk, int S,
+                                                          float scale_log2) {
+  static_assert(D == 128, "D=128 path");
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16KB + V 16KB)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = S / 128;
+  const int qb = nqb - 1 - blockIdx.x;  // heaviest (most keys) first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (H / Hk);
+  const int64_t qoff = ((int64_t)(b * H + h) * S) * D;
+  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
+  const int q0 = qb * 128 + wave * 32;  // first row of this wave
+  const int myq = q0 + r;               // the query row this lane owns
+
+  // Q fragments: Q[myq][16s + 8hh .. +7], s = 0..7
+  bf16x8 qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = as_bf16x8(ld16(Q + qoff + (int64_t)myq * D + 16 * s + 8 * hh));
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int ntiles = (qb * 128 + 127) / TK + 1;  // causal: keys < (qb+1)*128
+  // staging: each thread moves 4 x 16 B of K and of V per tile
+  u32x4 stk[4], stv[4];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;  // 16-B element index in the 64x16 tile
+      const int key = e >> 4, c = e & 15;
+      const int64_t g = koff + (int64_t)(t * TK + key) * D + c * 8;
+      stk[i] = ld16(K + g);
+      stv[i] = ld16(V + g);
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* kb = smem + buf * 32768;
+    char* vb = kb + 16384;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int key = e >> 4, c = e & 15;
+      *(u32x4*)(kb + k_off(key, c)) = stk[i];
+      *(u32x4*)(vb + v_off(key, c)) = stv[i];
+    }
+  };
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    const int kbase = t * TK;
+    const bool active = kbase <= q0 + 31;  // wave-uniform: some row of this wave sees this tile
+    if (active) {
+      const char* kb = smem + (t & 1) * 32768;
+      const char* vb = kb + 16384;
+      // ---- S^T = K Q^T : two 32-key halves
+      f32x16 sc[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sc[n][j] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 kf = as_bf16x8(*(const u32x4*)(kb + k_off(32 * n + r, 2 * s + hh)));
+          sc[n] = mfma32(kf, qf[s], sc[n]);
+        }
+      }
+      // ---- online softmax (exp2 domain), causal mask on the diagonal tiles
+      const bool diag = kbase + TK - 1 > q0;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          float v = sc[n][j] * scale_log2;
+          if (diag) {
+            const int key = kbase + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
+            if (key > myq) v = -INFINITY;
+          }
+          sc[n][j] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = (m_run == -INFINITY) ? 0.f : exp2f(m_run - m_new);
+      float ls = 0.f;
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const float p = (sc[n][j] == -INFINITY) ? 0.f : exp2f(sc[n][j] - m_new);
+          sc[n][j] = p;
+          ls += p;
+        }
+      l_run = l_run * alpha + ls;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+      // ---- O^T += V^T P^T
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          u32x4 pw;
+          pw[0] = pack2(sc[n][8 * s + 0], sc[n][8 * s + 1]);
+          pw[1] = pack2(sc[n][8 * s + 2], sc[n][8 * s + 3]);
+          pw[2] = pack2(sc[n][8 * s + 4], sc[n][8 * s + 5]);
+          pw[3] = pack2(sc[n][8 * s + 6], sc[n][8 * s + 7]);
+          const bf16x8 pf = as_bf16x8(pw);
+          // V^T fragment rows: keys 32n + 16s + 4hh + (0..3) and +8
+          const int g = lane >> 4, i16 = lane & 15;
+          const int qq = i16 >> 2, pp = i16 & 3;  // this lane supplies row qq, cols 4pp..4pp+3
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) {
+            const int col = 32 * dt + 16 * (g & 1) + 4 * pp;  // d column of the block this lane addresses
+            const int key_a = 32 * n + 16 * s + 4 * hh + qq;
+            const int key_b = key_a + 8;
+            const int ca = col >> 3, wa = (col & 7) * 2;  // 16-B chunk, byte within chunk
+            const bf16x4 va = tr_read(vb, v_off(key_a, ca) + wa);
+            const bf16x4 vbv = tr_read(vb, v_off(key_b, ca) + wa);
+            bf16x8 vf;
+            vf[0] = va[0]; vf[1] = va[1]; vf[2] = va[2]; vf[3] = va[3];
+            vf[4] = vbv[0]; vf[5] = vbv[1]; vf[6] = vbv[2]; vf[7] = vbv[3];
+            acc[dt] = mfma32(vf, pf, acc[dt]);
+          }
+        }
+      }
+    }
+    if (t + 1 < ntiles) swrite((t + 1) & 1);
+    __syncthreads();
+  }
+  // ---- epilogue: O = O^T / l  (lane owns query row myq; d rows from the C map)
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  bf16_t* orow = O + qoff + (int64_t)myq * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * dt + 8 * g + 4 * hh;
+      uint2 w;
+      w.x = pack2(acc[dt][4 * g + 0] * inv, acc[dt][4 * g + 1] * inv);
+      w.y = pack2(acc[dt][4 * g + 2] * inv, acc[dt][4 * g + 3] * inv);
+      *(uint2*)(orow + d) = w;
+    }
+  if (hh == 0) LSE[(int64_t)(b * H + h) * S + myq] = (m_run + log2f(l_tot)) * 0.6931471805599453f;
+}
+
+// ---------------------------------------------------------------------------
+// backward preprocess: delta[b,h,q] = sum_d dO * O
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                           float* __restrict__ delta, int64_t rows, int D) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float acc = 0.f;
+  for (int c = lane; c < D / 8; c += 64) {
+    float a[8], g[8];
+    unpack8(ld16(O + row * D + c * 8), a);
+    unpack8(ld16(dO + row * D + c * 8), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(a[j], g[j], acc);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) delta[row] = acc;
+}
+
+// One image for row reads (ds_read_b128, 32x32x16 A/B operand) AND
+// transposed reads (ds_read_b64_tr_b16): guide T10 layout (b),
+// chunk' = chunk ^ (((row & 3) << 2) | ((row >> 2) & 3)).
+__device__ __forceinline__ int rt_off(int row, int chunk) {
+  return row * ROWB + ((chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+
+// A-operand fragment of X^T . Y where X is a row-major [rows][128] bf16 LDS
+// image read transposed: lane (r, hh) gets X[rows rb + 4hh + (0..3)][32dt + r]
+// and X[rows rb + 8 + 4hh + (0..3)][32dt + r]  (the permuted k order that
+// matches a C-layout accumulator used as the B operand).
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int rb, int dt, int lane) {
+  const int g = lane >> 4, i16 = lane & 15, hh = lane >> 5;
+  const int qq = i16 >> 2, pp = i16 & 3;
+  const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
+  const int ra = rb + 4 * hh + qq;
+  const bf16x4 a = tr_read(img, rt_off(ra, col >> 3) + (col & 7) * 2);
+  const bf16x4 b = tr_read(img, rt_off(ra + 8, col >> 3) + (col & 7) * 2);
+  bf16x8 f;
+  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+  return f;
+}
+
+__device__ __forceinline__ bf16x8 pack_frag(const f32x16& x, int s) {
+  u32x4 w;
+  w[0] = pack2(x[8 * s + 0], x[8 * s + 1]);
+  w[1] = pack2(x[8 * s + 2], x[8 * s + 3]);
+  w[2] = pack2(x[8 * s + 4], x[8 * s + 5]);
+  w[3] = pack2(x[8 * s + 6], x[8 * s + 7]);
+  return as_bf16x8(w);
+}
+
+// ---------------------------------------------------------------------------
+// dK / dV: workgroup = 128 keys of one (batch, kv head); wave w owns keys
+// kb*128 + 32w .. +31 and keeps their K/V operand fragments and the dK^T /
+// dV^T accumulators in registers while the workgroup sweeps every query head
+// of the GQA group and every causal 64-row query tile (Q and dO tiles staged
+// through LDS, double buffered).  Orientation: key on the MFMA lane, so
+//   S = Q K^T, dP = dO V^T        (A = Q / dO row reads, B = K / V registers)
+//   dV^T += dO^T P, dK^T += Q^T dS (A = transposed reads, B = the accumulators)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int Hk, int S, float scale, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (Q 16K + dO 16K + lse 256 + delta 256)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int rep = H / Hk;
+  const int kw = kb * 128 + wave * 32;  // first key of this wave
+  const int mykey = kw + r;
+  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * 128;
+  constexpr int BUF = 32768 + 512;
+
+  bf16x8 kf[8], vf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    kf[s] = as_bf16x8(ld16(K + koff + (int64_t)mykey * 128 + 16 * s + 8 * hh));
+    vf[s] = as_bf16x8(ld16(V + koff + (int64_t)mykey * 128 + 16 * s + 8 * hh));
+  }
+  f32x16 dk[4], dv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { dk[i][j] = 0.f; dv[i][j] = 0.f; }
+
+  const int qt0 = (kb * 128) / 64;       // first causal 64-row query tile
+  const int nqt = S / 64 - qt0;          // tiles per head
+  const int total = nqt * rep;
+  u32x4 sq[4], sdo[4];
+  float slse = 0.f, sdel = 0.f;
+  auto gload = [&](int it) {
+    const int hq = hk * rep + it / nqt;
+    const int qt = qt0 + it % nqt;
+    const int64_t qoff = ((int64_t)(b * H + hq) * S) * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int row = e >> 4, c = e & 15;
+      const int64_t g = qoff + (int64_t)(qt * 64 + row) * 128 + c * 8;
+      sq[i] = ld16(Q + g);
+      sdo[i] = ld16(dO + g);
+    }
+    if (tid < 64) {
+      const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + tid;
+      slse = LSE[li] * LOG2E;
+      sdel = DELTA[li];
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* qb_ = smem + buf * BUF;
+    char* ob = qb_ + 16384;
+    float* lb = (float*)(qb_ + 32768);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int row = e >> 4, c = e & 15;
+      *(u32x4*)(qb_ + rt_off(row, c)) = sq[i];
+      *(u32x4*)(ob + rt_off(row, c)) = sdo[i];
+    }
+    if (tid < 64) {
+      lb[tid] = slse;
+      lb[64 + tid] = sdel;
+    }
+  };
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    if (it + 1 < total) gload(it + 1);
+    const int qt = qt0 + it % nqt;
+    const char* qi = smem + (it & 1) * BUF;
+    const char* oi = qi + 16384;
+    const float* lb = (const float*)(qi + 32768);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int qs = qt * 64 + 32 * m;
+      if (qs + 31 < kw) continue;  // whole sub-tile above the diagonal for this wave
+      f32x16 sc, dp;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) { sc[j] = 0.f; dp[j] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8 qa = as_bf16x8(*(const u32x4*)(qi + rt_off(32 * m + r, 2 * s + hh)));
+        sc = mfma32(qa, kf[s], sc);
+        const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rt_off(32 * m + r, 2 * s + hh)));
+        dp = mfma32(oa, vf[s], dp);
+      }
+      // P and dS; C rows = q (16 per lane), column = mykey
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int ql = 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        const int q = qt * 64 + ql;
+        float p = exp2f(sc[j] * scale_log2 - lb[ql]);
+        if (q < mykey) p = 0.f;
+        sc[j] = p;
+        dp[j] = p * (dp[j] - lb[64 + ql]);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack_frag(sc, s);
+        const bf16x8 sb = pack_frag(dp, s);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[dt] = mfma32(tr_frag(oi, 32 * m + 16 * s, dt, lane), pb, dv[dt]);
+          dk[dt] = mfma32(tr_frag(qi, 32 * m + 16 * s, dt, lane), sb, dk[dt]);
+        }
+      }
+    }
+    if (it + 1 < total) swrite((it + 1) & 1);
+    __syncthreads();
+  }
+  // store: lane owns key `mykey`, d rows 32dt + 8g + 4hh + (0..3)
+  bf16_t* dkr = dK + koff + (int64_t)mykey * 128;
+  bf16_t* dvr = dV + koff + (int64_t)mykey * 128;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * dt + 8 * g + 4 * hh;
+      uint2 a, c;
+      a.x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
+      a.y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+      c.x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
+      c.y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+      *(uint2*)(dkr + d) = a;
+      *(uint2*)(dvr + d) = c;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// dQ: workgroup = 128 query rows of one (batch, head), the forward's
+// orientation (query on the lane):
+//   S^T = K Q^T, dP^T = V dO^T  (A = K / V row reads, B = Q / dO registers)
+//   dQ^T += K^T dS^T            (A = transposed K reads, B = dS^T accumulator)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16_t* __restrict__ dQ, int H, int Hk, int S, float scale, float scale_log2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16K + V 16K)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = S / 128;
+  const int qb = nqb - 1 - blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (H / Hk);
+  const int64_t qoff = ((int64_t)(b * H + h) * S) * 128;
+  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * 128;
+  const int q0 = qb * 128 + wave * 32;
+  const int myq = q0 + r;
+
+  bf16x8 qf[8], of[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    qf[s] = as_bf16x8(ld16(Q + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh));
+    of[s] = as_bf16x8(ld16(dO + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh));
+  }
+  const float lse2 = LSE[(int64_t)(b * H + h) * S + myq] * LOG2E;
+  const float del = DELTA[(int64_t)(b * H + h) * S + myq];
+  f32x16 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+
+  const int ntiles = (qb * 128 + 127) / TK + 1;
+  u32x4 stk[4], stv[4];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int key = e >> 4, c = e & 15;
+      const int64_t g = koff + (int64_t)(t * TK + key) * 128 + c * 8;
+      stk[i] = ld16(K + g);
+      stv[i] = ld16(V + g);
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* kb = smem + buf * 32768;
+    char* vb = kb + 16384;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int key = e >> 4, c = e & 15;
+      *(u32x4*)(kb + rt_off(key, c)) = stk[i];
+      *(u32x4*)(vb + k_off(key, c)) = stv[i];
+    }
+  };
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    const int kbase = t * TK;
+    if (kbase <= q0 + 31) {
+      const char* kb = smem + (t & 1) * 32768;
+      const char* vb = kb + 16384;
+      const bool diag = kbase + TK - 1 > q0;
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        f32x16 sc, dp;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) { sc[j] = 0.f; dp[j] = 0.f; }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 ka = as_bf16x8(*(const u32x4*)(kb + rt_off(32 * n + r, 2 * s + hh)));
+          sc = mfma32(ka, qf[s], sc);
+          const bf16x8 va = as_bf16x8(*(const u32x4*)(vb + k_off(32 * n + r, 2 * s + hh)));
+          dp = mfma32(va, of[s], dp);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int key = kbase + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          float p = exp2f(sc[j] * scale_log2 - lse2);
+          if (diag && key > myq) p = 0.f;
+          dp[j] = p * (dp[j] - del);
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 sb = pack_frag(dp, s);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma32(tr_frag(kb, 32 * n + 16 * s, dt, lane), sb, acc[dt]);
+        }
+      }
+    }
+    if (t + 1 < ntiles) swrite((t + 1) & 1);
+    __syncthreads();
+  }
+  bf16_t* qrow = dQ + qoff + (int64_t)myq * 128;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = 32 * dt + 8 * g + 4 * hh;
+      uint2 w;
+      w.x = pack2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
+      w.y = pack2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
+      *(uint2*)(qrow + d) = w;
+    }
+}
+
+static void attn_set_lds_limits() {
+  static bool done = false;
+  if (done) return;
+  hipFuncSetAttribute((const void*)attn_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      2 * (32768 + 512));
+  hipFuncSetAttribute((const void*)attn_bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  done = true;
+}
+
+extern "C" int toa_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int H,
+                            int Hk, int S, int D, int causal, float scale, hipStream_t stream) {
+  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !causal) return (int)hipErrorInvalidValue;
+  attn_set_lds_limits();
+  dim3 grid(S / 128, H, B);
+  hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 65536, stream, q, k, v, o, lse, H, Hk, S,
+                     scale * LOG2E);
+  return (int)hipGetLastError();
+}
+
+// dq_acc is unused (kept in the ABI for an atomic-dQ variant); dq/dk/dv bf16.
+extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                            const float* lse, float* delta, float* dq_acc, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B,
+                            int H, int Hk, int S, int D, int causal, float scale, hipStream_t stream) {
+  (void)dq_acc;
+  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !causal) return (int)hipErrorInvalidValue;
+  attn_set_lds_limits();
+  const int64_t rows = (int64_t)B * H * S;
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, o, dout, delta,
+                     rows, D);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 128, Hk, B), dim3(256), 2 * (32768 + 512), stream, q, k, v,
+                     dout, lse, delta, dk, dv, H, Hk, S, scale, scale * LOG2E);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 128, H, B), dim3(256), 65536, stream, q, k, v, dout, lse, delta,
+                     dq, H, Hk, S, scale, scale * LOG2E);
+  return (int)hipGetLastError();
+}

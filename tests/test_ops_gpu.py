@@ -189,3 +189,67 @@ def test_trainer_tiny_loss_decreases():
     b = tr.synthetic_batch()
     losses = [float(tr.step([b])) for _ in range(5)]
     assert losses[-1] < losses[0]
+
+
+def _attn_ref(q, k, v, scale):
+    rep = q.shape[1] // k.shape[1]
+    kf = k.float().repeat_interleave(rep, 1)
+    vf = v.float().repeat_interleave(rep, 1)
+    s = torch.matmul(q.float(), kf.transpose(-1, -2)) * scale
+    S = q.shape[2]
+    mask = torch.triu(torch.ones(S, S, dtype=torch.bool, device=q.device), 1)
+    s = s.masked_fill(mask, float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    return torch.matmul(torch.softmax(s, -1), vf), lse
+
+
+@pytest.mark.parametrize("B,H,Hk,S", [(1, 2, 2, 128), (2, 4, 2, 384), (1, 8, 2, 1024)])
+def test_flash_attention_fwd_bwd(B, H, Hk, S):
+    L = _lib()
+    from tf_operator_amd.ops import llm
+
+    torch.manual_seed(7)
+    D = 128
+    scale = 1.0 / math.sqrt(D)
+    q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = llm._FlashAttn.apply(q, k, v, scale)
+    qr, kr, vr = [t.detach().float().requires_grad_() for t in (q, k, v)]
+    orf, lse_ref = _attn_ref(qr, kr, vr, scale)
+    assert rel(o, orf) < 2e-2, rel(o, orf)
+    # lse from a direct forward call
+    o2 = torch.empty_like(q)
+    lse = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
+    L.call("toa_attn_fwd", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o2), L.ptr(lse), B, H, Hk, S, D, 1, scale,
+           L.stream(q))
+    torch.cuda.synchronize()
+    assert float((lse - lse_ref).abs().max()) < 2e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    assert rel(q.grad, qr.grad) < 3e-2, rel(q.grad, qr.grad)
+    assert rel(k.grad, kr.grad) < 3e-2, rel(k.grad, kr.grad)
+    assert rel(v.grad, vr.grad) < 3e-2, rel(v.grad, vr.grad)
+
+
+def test_flash_attention_in_llama_layer():
+    """A D=128 Llama block through the packed-GQA HIP attention path vs CPU fp32."""
+    _lib()
+    from tf_operator_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(8)
+    cfg = LlamaConfig(vocab_size=256, hidden=512, layers=1, heads=4, kv_heads=2, ffn=1024, max_seq=256)
+    m_gpu = Llama(cfg, device=DEV)
+    m_gpu.init_weights(0)
+    m_cpu = Llama(cfg, device="cpu")
+    m_cpu.load_state_dict({k: v.cpu() for k, v in m_gpu.state_dict().items()})
+    tok = torch.randint(0, cfg.vocab_size, (2, 256))
+    tgt = torch.randint(0, cfg.vocab_size, (2, 256))
+    lg = m_gpu(tok.to(DEV), tgt.to(DEV))
+    lc = m_cpu(tok, tgt)
+    assert abs(float(lg) - float(lc)) < 2e-2
+    lg.backward()
+    lc.backward()
+    for (n, pg), (_, pc) in zip(m_gpu.named_parameters(), m_cpu.named_parameters()):
+        assert rel(pg.grad.cpu(), pc.grad) < 5e-2, n

@@ -213,7 +213,8 @@ _ATTN_IMPL = os.environ.get("TOA_ATTN", "auto")  # auto | hip | sdpa
 
 
 def _attn_hip_ok(q):
-    return q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (64, 128) and _lib.has("toa_attn_fwd")
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == 128 and _lib.has("toa_attn_fwd")
+            and _lib.has("toa_attn_bwd"))
 
 
 class _FlashAttn(torch.autograd.Function):
@@ -238,10 +239,9 @@ class _FlashAttn(torch.autograd.Function):
         dq = torch.empty_like(q)
         dk = torch.empty_like(k)
         dv = torch.empty_like(v)
-        dq_acc = torch.zeros(B, H, S, D, device=q.device, dtype=torch.float32)
         delta = torch.empty(B, H, S, device=q.device, dtype=torch.float32)
         _lib.call("toa_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do), _lib.ptr(lse),
-                  _lib.ptr(delta), _lib.ptr(dq_acc), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D, 1,
+                  _lib.ptr(delta), None, _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D, 1,
                   float(ctx.scale), _lib.stream(q))
         return dq, dk, dv, None
 
@@ -250,7 +250,7 @@ def causal_attention(q, k, v, scale=None):
     """q [B,H,S,D], k/v [B,Hk,S,D] (Hk == H unless the HIP kernel is used)."""
     scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
     impl = _ATTN_IMPL
-    if impl in ("auto", "hip") and _attn_hip_ok(q):
+    if impl in ("auto", "hip") and _attn_hip_ok(q) and q.shape[2] % 128 == 0:
         return _FlashAttn.apply(q.contiguous(), k.contiguous(), v.contiguous(), scale)
     if impl == "hip" and q.is_cuda:
         raise RuntimeError("TOA_ATTN=hip but the HIP attention kernel is unavailable")
