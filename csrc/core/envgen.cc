@@ -118,6 +118,7 @@ static void rocm_block(const Json& job, const std::string& rtype, int index, con
   const Json& md = job.get("metadata");
   const std::string name = md.get("name").str();
   add_env(out, container, "TOA_JOB_NAME", name);
+  add_env(out, container, "TOA_JOB_KIND", job_kind(job));
   add_env(out, container, "TOA_JOB_NAMESPACE", md.get("namespace").str("default"));
   add_env(out, container, "TOA_REPLICA_TYPE", lower(rtype));
   add_env(out, container, "TOA_REPLICA_INDEX", std::to_string(index));

@@ -31,6 +31,8 @@ typedef __attribute__((ext_vector_type(4))) short bf16x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 #define LOG2E 1.4426950408889634f
+#define EXP2(x) __builtin_amdgcn_exp2f(x)
+#define RESCALE_THR 8.0f  // guide T13: defer the O rescale while the row max grows < 2^8
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -154,23 +156,28 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
           mx = fmaxf(mx, v);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = (m_run == -INFINITY) ? 0.f : exp2f(m_run - m_new);
+      // T13: rescale O / l only when some row's max grew by more than THR
+      // (both lanes of a row see the same max, so they decide alike).
+      if (__any(mx > m_run + RESCALE_THR)) {
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = (m_run == -INFINITY) ? 0.f : EXP2(m_run - m_new);
+        l_run *= alpha;
+        m_run = m_new;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+      }
       float ls = 0.f;
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float p = (sc[n][j] == -INFINITY) ? 0.f : exp2f(sc[n][j] - m_new);
+          const float p = EXP2(sc[n][j] - m_run);  // exp2(-inf) = 0 for masked keys
           sc[n][j] = p;
           ls += p;
         }
-      l_run = l_run * alpha + ls;
-      m_run = m_new;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+      l_run += ls;
       // ---- O^T += V^T P^T
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
@@ -372,15 +379,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
         const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rt_off(32 * m + r, 2 * s + hh)));
         dp = mfma32(oa, vf[s], dp);
       }
-      // P and dS; C rows = q (16 per lane), column = mykey
+      // P and dS; C rows = q (16 per lane: 4 runs of 4 consecutive rows), column = mykey
+      f32x4 lse4[4], del4[4];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        lse4[g4] = *(const f32x4*)(lb + 32 * m + 8 * g4 + 4 * hh);
+        del4[g4] = *(const f32x4*)(lb + 64 + 32 * m + 8 * g4 + 4 * hh);
+      }
+      const bool need_mask = qs < kw + 31;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int ql = 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        const int q = qt * 64 + ql;
-        float p = exp2f(sc[j] * scale_log2 - lb[ql]);
-        if (q < mykey) p = 0.f;
+        float p = EXP2(sc[j] * scale_log2 - lse4[j >> 2][j & 3]);
+        if (need_mask && qt * 64 + ql < mykey) p = 0.f;
         sc[j] = p;
-        dp[j] = p * (dp[j] - lb[64 + ql]);
+        dp[j] = p * (dp[j] - del4[j >> 2][j & 3]);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -498,7 +511,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int key = kbase + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
-          float p = exp2f(sc[j] * scale_log2 - lse2);
+          float p = EXP2(sc[j] * scale_log2 - lse2);
           if (diag && key > myq) p = 0.f;
           dp[j] = p * (dp[j] - del);
         }
@@ -529,10 +542,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
 static void attn_set_lds_limits() {
   static bool done = false;
   if (done) return;
-  hipFuncSetAttribute((const void*)attn_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-  hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                       2 * (32768 + 512));
-  hipFuncSetAttribute((const void*)attn_bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
   done = true;
 }
 

@@ -203,8 +203,9 @@ def _attn_ref(q, k, v, scale):
     return torch.matmul(torch.softmax(s, -1), vf), lse
 
 
-@pytest.mark.parametrize("B,H,Hk,S", [(1, 2, 2, 128), (2, 4, 2, 384), (1, 8, 2, 1024)])
-def test_flash_attention_fwd_bwd(B, H, Hk, S):
+@pytest.mark.parametrize("B,H,Hk,S,spike", [(1, 2, 2, 128, False), (2, 4, 2, 384, False), (1, 8, 2, 1024, False),
+                                             (1, 2, 1, 1024, True)])
+def test_flash_attention_fwd_bwd(B, H, Hk, S, spike):
     L = _lib()
     from tf_operator_amd.ops import llm
 
@@ -214,6 +215,10 @@ def test_flash_attention_fwd_bwd(B, H, Hk, S):
     q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    if spike:  # force the deferred-rescale branch (guide rule 26): late keys dominate
+        with torch.no_grad():
+            k[:, :, 600:] *= 6.0
+            k[:, :, 900] = 4.0 * q[0, 0, 950].to(k.dtype)
     o = llm._FlashAttn.apply(q, k, v, scale)
     qr, kr, vr = [t.detach().float().requires_grad_() for t in (q, k, v)]
     orf, lse_ref = _attn_ref(qr, kr, vr, scale)

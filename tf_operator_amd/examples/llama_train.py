@@ -1,0 +1,69 @@
+"""Llama-family DP training payload (BASELINE configs #3 / #4 / #5):
+TFJob/PyTorchJob Worker=N, one GPU per worker, RCCL all-reduce over xGMI,
+fused HIP kernels, AdamW.  Checkpoints every `--checkpoint-every` steps and on
+SIGTERM (preemption) to TOA_CHECKPOINT_DIR, resumes from it on restart --
+with ANY world size, which is what the elastic policy relies on."""
+from __future__ import annotations
+
+import argparse
+import time
+
+import torch
+
+from tf_operator_amd.examples.common import pick_device
+from tf_operator_amd.train import checkpoint as ckpt
+from tf_operator_amd.train.llm import LlamaTrainer, load_trainer_state, trainer_state
+from tf_operator_amd.train.runtime import Runtime
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="llama-tiny")
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--seq-len", type=int, default=128)
+    p.add_argument("--micro-batch", type=int, default=2)
+    p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--checkpoint-every", type=int, default=0)
+    p.add_argument("--step-sleep", type=float, default=0.0, help="testing: slow steps down")
+    a = p.parse_args(argv)
+    rt = Runtime()
+    rt.install_preemption_handler()
+    info = rt.init_dist()
+    dev = pick_device() if info.backend != "gloo" else torch.device("cpu")
+    tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr)
+    payload = ckpt.load_latest(rt.ckpt_dir)
+    if payload is not None:
+        load_trainer_state(tr, payload["state"])
+        rt.log(f"resumed at step {tr.step_idx} (world {rt.world})")
+    batch = [tr.synthetic_batch(seed=100 + rt.rank)]
+    t0, n0 = time.perf_counter(), tr.step_idx
+    while tr.step_idx < a.steps:
+        loss = tr.step(batch)
+        if tr.step_idx == n0 + 1:
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            rt.first_step_done()
+        if tr.step_idx % 5 == 0 or tr.step_idx == a.steps:
+            rt.log(f"step {tr.step_idx} loss {float(loss):.4f}")
+        if a.checkpoint_every and tr.step_idx % a.checkpoint_every == 0 and rt.is_chief:
+            ckpt.save(rt.ckpt_dir, tr.step_idx, trainer_state(tr))
+        if rt.preempted.is_set():
+            if rt.is_chief and rt.ckpt_dir:
+                ckpt.save(rt.ckpt_dir, tr.step_idx, trainer_state(tr))
+            rt.log(f"preempted at step {tr.step_idx}")
+            raise SystemExit(143)
+        if a.step_sleep:
+            time.sleep(a.step_sleep)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    done = tr.step_idx - n0
+    if done:
+        rt.report(samples_per_sec=a.micro_batch * rt.world * done / dt)
+    if rt.is_chief and rt.ckpt_dir:
+        ckpt.save(rt.ckpt_dir, tr.step_idx, trainer_state(tr))
+    rt.log(f"done: {tr.step_idx} steps")
+
+
+if __name__ == "__main__":
+    main()

@@ -49,11 +49,13 @@ _SIGS = {
     "toa_swiglu_bwd": [c_p, c_p, c_p, c_i64, c_int, c_p],
     "toa_xent_fwd": [c_int, c_p, c_p, c_p, c_p, c_i64, c_int, c_i64, c_int, c_p],
     "toa_xent_bwd": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_i64, c_int, c_p],
-    "toa_gemm_bias_act": [c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
-    "toa_softmax_xent_small": [c_p, c_p, c_p, c_p, c_int, c_int, c_f, c_p],
-    "toa_dropout_fwd": [c_int, c_p, c_p, c_p, c_i64, c_f, ctypes.c_uint64, ctypes.c_uint64, c_p],
-    "toa_accuracy": [c_p, c_p, c_p, c_int, c_int, c_p],
+    "toa_gemm_bias_act": [c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
+    "toa_gemm_bias_act_dropout": [c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_f,
+                                  ctypes.c_uint64, c_p],
     "toa_bias_act_bwd": [c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p],
+    "toa_bias_act_dropout_bwd": [c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_f, ctypes.c_uint64, c_p],
+    "toa_dropout_fwd": [c_int, c_p, c_p, c_p, c_i64, c_f, ctypes.c_uint64, ctypes.c_uint64, c_p],
+    "toa_accuracy": [c_int, c_p, c_p, c_p, c_int, c_int, c_p],
     "toa_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_p],
     "toa_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_f, c_p],

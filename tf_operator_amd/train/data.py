@@ -1,0 +1,63 @@
+"""Synthetic datasets of the reference payloads' shapes (no network, no
+downloads): MNIST-shaped images with a learnable labelling (labels = argmax
+of a fixed random projection, so accuracy actually rises), CIFAR/ImageNet
+shaped tensors for the CNN/ResNet benchmarks, and token streams for Llama.
+Every rank draws a disjoint shard (seeded by rank), like a DistributedSampler.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class SyntheticMNIST:
+    def __init__(self, batch, rank=0, world=1, seed=0, device="cpu", image=False, dtype=torch.float32):
+        g = torch.Generator().manual_seed(1234)
+        self.proj = torch.randn(784, 10, generator=g)
+        self.batch = batch
+        self.gen = torch.Generator().manual_seed(seed * 1000003 + rank)
+        self.device = device
+        self.image = image
+        self.dtype = dtype
+
+    def next(self):
+        x = torch.rand(self.batch, 784, generator=self.gen)
+        y = (x @ self.proj).argmax(-1)
+        if self.image:
+            x = x.view(-1, 1, 28, 28)
+        return x.to(self.device, self.dtype), y.to(self.device)
+
+    def __iter__(self):
+        while True:
+            yield self.next()
+
+
+class SyntheticImages:
+    """ImageNet-shaped (3x224x224) random batches with random labels."""
+
+    def __init__(self, batch, shape=(3, 224, 224), classes=1000, rank=0, device="cpu", dtype=torch.bfloat16,
+                 channels_last=True):
+        g = torch.Generator(device=device).manual_seed(77 + rank)
+        self.x = torch.randn(batch, *shape, generator=g, device=device).to(dtype)
+        if channels_last:
+            self.x = self.x.contiguous(memory_format=torch.channels_last)
+        self.y = torch.randint(0, classes, (batch,), generator=g, device=device)
+
+    def next(self):
+        return self.x, self.y
+
+
+class SyntheticBinary:
+    """keras_model_to_estimator.py:26-33: 1024 x 10 random features, 0/1 labels."""
+
+    def __init__(self, n=1024, batch=32, rank=0, device="cpu"):
+        g = torch.Generator().manual_seed(5 + rank)
+        self.x = torch.rand(n, 10, generator=g)
+        w = torch.randn(10, generator=torch.Generator().manual_seed(9))
+        self.y = ((self.x - 0.5) @ w > 0).float()
+        self.batch, self.i, self.device = batch, 0, device
+
+    def next(self):
+        n = self.x.shape[0]
+        idx = torch.arange(self.i, self.i + self.batch) % n
+        self.i = (self.i + self.batch) % n
+        return self.x[idx].to(self.device), self.y[idx].to(self.device)

@@ -70,3 +70,14 @@ def timed_steps(trainer: LlamaTrainer, batches, n, sync=True):
     if sync and torch.cuda.is_available():
         torch.cuda.synchronize()
     return time.perf_counter() - t0, loss
+
+
+def trainer_state(tr: LlamaTrainer):
+    return {"flat": tr.flat.state_dict(), "opt": tr.opt.state_dict(), "step": tr.step_idx}
+
+
+def load_trainer_state(tr: LlamaTrainer, st):
+    dev = tr.flat.device
+    tr.flat.load_state_dict({k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in st["flat"].items()})
+    tr.opt.load_state_dict(st["opt"])
+    tr.step_idx = int(st["step"])

@@ -1,0 +1,134 @@
+"""Data-parallel trainer for the small bundled models (MNIST MLP, Keras CNN,
+estimator DNN, ResNet-50): flat parameters, backward-overlapped bucketed
+RCCL/gloo all-reduce, fused HIP Adam/SGD, checkpoint/resume, first-step
+reporting.  The Llama path has its own trainer (:mod:`.llm`)."""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..ops.optim import FlatAdamW, FlatSGD
+from ..parallel.ddp import GradBucketer, broadcast_params
+from ..parallel.flat import FlatParams
+from . import checkpoint as ckpt
+
+
+def attach_autograd_hooks(flat: FlatParams):
+    """Params whose gradients come from plain autograd ops (convs, BN) get a
+    post-accumulate hook that folds .grad into the flat buffer and fires the
+    bucket hook, so their all-reduce also overlaps backward."""
+    for s in flat.segments:
+        p = s.param
+
+        def hook(param):
+            if param.grad is None:
+                return
+            param.main_grad.add_(param.grad.view_as(param.main_grad).to(param.main_grad.dtype))
+            param.grad = None
+            h = getattr(param, "_toa_ready", None)
+            if h is not None:
+                h(param)
+
+        p.register_post_accumulate_grad_hook(hook)
+
+
+class DPTrainer:
+    def __init__(self, model, loss_fn, runtime, lr=1e-3, optimizer="adam", weight_decay=0.0, bucket_mb=None,
+                 max_grad_norm=0.0, grad_dtype=torch.float32):
+        self.model = model
+        self.loss_fn = loss_fn
+        self.rt = runtime
+        params = [p for p in model.parameters() if p.requires_grad]
+        names = {id(p): n for n, p in model.named_parameters()}
+        # backward order ~ reverse registration order
+        self.flat = FlatParams(list(reversed(params)), names=names, grad_dtype=grad_dtype)
+        attach_autograd_hooks(self.flat)
+        broadcast_params(self.flat)
+        self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20))
+        if optimizer == "adam":
+            self.opt = FlatAdamW(self.flat, lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay,
+                                 max_grad_norm=max_grad_norm)
+        else:
+            self.opt = FlatSGD(self.flat, lr=lr, weight_decay=weight_decay)
+        self.step_idx = 0
+
+    def step(self, x, y):
+        self.flat.zero_grad()
+        out = self.model(x)
+        loss = self.loss_fn(out, y)
+        loss.backward()
+        self.bucketer.finish()
+        self.opt.step(grad_scale=self.bucketer.grad_scale)
+        self.step_idx += 1
+        if self.step_idx == 1:
+            if torch.cuda.is_available() and x.is_cuda:
+                torch.cuda.synchronize()
+            self.rt.first_step_done()
+        return loss.detach(), out.detach()
+
+    # ------------------------------------------------------------------ checkpoint
+    def state(self):
+        st = {"flat": self.flat.state_dict(), "step": self.step_idx}
+        if isinstance(self.opt, FlatAdamW):
+            st["opt"] = self.opt.state_dict()
+        buffers = {n: b for n, b in self.model.named_buffers()}
+        if buffers:
+            st["buffers"] = buffers
+        return st
+
+    def save(self, ckpt_dir, keep=2):
+        if ckpt_dir and self.rt.is_chief:
+            ckpt.save(ckpt_dir, self.step_idx, self.state(), keep)
+
+    def maybe_resume(self, ckpt_dir):
+        payload = ckpt.load_latest(ckpt_dir)
+        if payload is None:
+            return 0
+        st = payload["state"]
+        dev = self.flat.device
+        self.flat.load_state_dict({k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in st["flat"].items()})
+        if "opt" in st and isinstance(self.opt, FlatAdamW):
+            self.opt.load_state_dict(st["opt"])
+        for n, b in (st.get("buffers") or {}).items():
+            dict(self.model.named_buffers())[n].copy_(b.to(dev))
+        self.step_idx = int(payload["step"])
+        return self.step_idx
+
+
+def run(trainer: DPTrainer, data, steps, log_every=50, ckpt_dir=None, ckpt_every=0, metric_fn=None,
+        samples_per_step=None):
+    rt = trainer.rt
+    start = trainer.maybe_resume(ckpt_dir)
+    if start:
+        rt.log(f"resumed from checkpoint at step {start}")
+    t0 = time.perf_counter()
+    n0 = trainer.step_idx
+    last = None
+    while trainer.step_idx < steps:
+        x, y = data.next()
+        loss, out = trainer.step(x, y)
+        last = (loss, out, y)
+        s = trainer.step_idx
+        if log_every and (s % log_every == 0 or s == steps):
+            msg = f"step {s} loss {float(loss):.4f}"
+            if metric_fn is not None:
+                msg += f" acc {float(metric_fn(out, y)):.3f}"
+            rt.log(msg)
+        if ckpt_dir and ckpt_every and s % ckpt_every == 0:
+            trainer.save(ckpt_dir)
+        if rt.preempted.is_set():
+            trainer.save(ckpt_dir)
+            rt.log(f"preempted at step {s}; checkpoint written")
+            raise SystemExit(143)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    done = trainer.step_idx - n0
+    if samples_per_step and done:
+        sps = samples_per_step * done / max(dt, 1e-9)
+        rt.report(samples_per_sec=sps)
+        rt.log(f"throughput {sps:.1f} samples/s over {done} steps")
+    if ckpt_dir:
+        trainer.save(ckpt_dir)
+    return last
