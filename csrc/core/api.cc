@@ -9,6 +9,8 @@
 #include <cctype>
 #include <stdexcept>
 
+#include <cstdint>
+
 #include "core.h"
 
 namespace toa {
@@ -266,8 +268,19 @@ std::string validate(const Json& job) {
   const Json& spec = job.get("spec");
   if (!spec.is_object()) return ki->kind + "Spec is not valid";
   const Json& specs = spec.get(ki->specs_field);
-  if (ki->kind == "TFJob" || ki->kind == "MXJob") return validate_tf_mx(*ki, specs);
-  return validate_master_worker(*ki, specs);
+  const std::string err =
+      (ki->kind == "TFJob" || ki->kind == "MXJob") ? validate_tf_mx(*ki, specs) : validate_master_worker(*ki, specs);
+  if (!err.empty()) return err;
+  // elasticPolicy (P9 extension): a Worker group with 1 <= min <= max
+  const Json& ep = spec.get("elasticPolicy");
+  if (ep.is_null()) return "";
+  if (!ep.is_object()) return ki->kind + "Spec is not valid: elasticPolicy must be an object";
+  if (!specs.has("Worker")) return ki->kind + "Spec is not valid: elasticPolicy requires a Worker replica spec";
+  const int64_t mn = ep.get("minReplicas").as_int(1), mx = ep.get("maxReplicas").as_int(INT64_MAX);
+  if (mn < 1) return ki->kind + "Spec is not valid: elasticPolicy.minReplicas must be >= 1";
+  if (mx < mn) return ki->kind + "Spec is not valid: elasticPolicy.maxReplicas must be >= minReplicas";
+  if (ep.get("maxRestarts").as_int(0) < 0) return ki->kind + "Spec is not valid: elasticPolicy.maxRestarts must be >= 0";
+  return "";
 }
 
 }  // namespace toa

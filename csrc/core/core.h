@@ -16,6 +16,7 @@
 //   expectations.cc [EXT] controller expectations (client-go semantics)
 //   podgroup.cc   [EXT] Volcano PodGroup sync
 #pragma once
+#include <cmath>
 #include <map>
 #include <mutex>
 #include <string>
@@ -105,6 +106,7 @@ struct Options {
   int previous_retry = 0;               // workqueue NumRequeues(job)
   Json nccl_env = Json::object();       // extra NCCL_*/RCCL_* knobs
   std::string gpu_resource = "amd.com/gpu";
+  int64_t elastic_free_gpus = -1;       // free GPUs for an elastic job (own pods count as free); -1 unknown
 };
 Options options_from_json(const Json& o);
 
@@ -158,6 +160,27 @@ std::string expectation_services_key(const std::string& job_key, const std::stri
 // gang scheduling (C7)
 // ---------------------------------------------------------------------------
 Json gen_podgroup(const Json& job, const Options& opt);
+// per-pod request (limits when no request) of `resource` in a replica spec
+double pod_resource_request(const Json& replica_spec, const std::string& resource);
+
+// ---------------------------------------------------------------------------
+// elastic worker groups (P9 extension, elastic.cc)
+// ---------------------------------------------------------------------------
+extern const char* kLabelElasticGeneration;  // training.amd.com/elastic-generation
+struct ElasticPlan {
+  bool enabled = false;
+  bool draining = false;   // old-generation pods still exist: delete them, create nothing
+  bool restarted = false;  // a new generation started in this pass
+  bool give_up = false;    // maxRestarts exceeded: fail the job
+  std::string message;
+  Json actions = Json::array();
+  Json pods;                      // the current generation's pods
+  double requeue_after = NAN;
+};
+bool is_elastic(const Json& job);
+// mutates the defaulted job copy (Worker replicas, generation label/env,
+// restartPolicy) and status.elasticStatus
+ElasticPlan elastic_prepass(Json& job, const Json& pods, Json& status, double now, const Options& opt);
 
 // ---------------------------------------------------------------------------
 // reconcile engine (C1, C2, C4, C6, D1-D3)

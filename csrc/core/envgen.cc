@@ -29,6 +29,7 @@ Options options_from_json(const Json& o) {
   opt.previous_retry = (int)o.get("previous_retry").as_int(0);
   if (o.get("nccl_env").is_object()) opt.nccl_env = o.get("nccl_env");
   opt.gpu_resource = o.get("gpu_resource").str("amd.com/gpu");
+  opt.elastic_free_gpus = o.get("elastic_free_gpus").as_int(-1);
   return opt;
 }
 

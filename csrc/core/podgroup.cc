@@ -55,6 +55,16 @@ static std::string format_quantity(const std::string& res, double v) {
   return buf;
 }
 
+double pod_resource_request(const Json& replica_spec, const std::string& resource) {
+  double total = 0;
+  for (const auto& c : replica_spec.path({"template", "spec", "containers"}).items()) {
+    const Json* q = c.path({"resources", "requests"}).find(resource);
+    if (q == nullptr) q = c.path({"resources", "limits"}).find(resource);
+    if (q != nullptr) total += parse_quantity(q->is_string() ? q->str() : q->dump());
+  }
+  return total;
+}
+
 Json gen_podgroup(const Json& job, const Options& opt) {
   const Json& md = job.get("metadata");
   const Json& sp = job.get("spec").get("runPolicy").get("schedulingPolicy");

@@ -215,7 +215,7 @@ Json on_job_created(const Json& job_in, double now) {
   return job;
 }
 
-Json reconcile(const Json& job_in, const Json& pods, const Json& services, double now, const Options& opt) {
+Json reconcile(const Json& job_in, const Json& pods_all, const Json& services, double now, const Options& opt) {
   Json res = Json::object();
   Json actions = Json::array();
   Json events = Json::array();
@@ -238,16 +238,13 @@ Json reconcile(const Json& job_in, const Json& pods, const Json& services, doubl
 
   Json job = set_defaults(job_in);
   const KindInfo& ki = kind_info(job_kind(job));
-  const Json& md = job.get("metadata");
-  const std::string name = md.get("name").str();
-  const std::string ns = md.get("namespace").str("default");
+  const std::string name = job.path({"metadata", "name"}).str();
+  const std::string ns = job.path({"metadata", "namespace"}).str("default");
   const std::string job_key = ns + "/" + name;
   const Json old_status = job_in.get("status").is_object() ? job_in.get("status") : Json::object();
   Json status = old_status;
   if (!status.get("conditions").is_array()) status.set("conditions", Json::array());
   if (!status.get("replicaStatuses").is_object()) status.set("replicaStatuses", Json::object());
-  const Json& rp = job.get("spec").get("runPolicy");
-  const Json& specs = replica_specs(job);
   double requeue = NAN;
 
   auto finish = [&](void) {
@@ -275,6 +272,34 @@ Json reconcile(const Json& job_in, const Json& pods, const Json& services, doubl
     }
     return finish();
   }
+
+  // ---- elastic worker group (elastic.cc): may resize the job copy, restart
+  // the group, and narrows the observed pods to the current generation
+  ElasticPlan eplan = elastic_prepass(job, pods_all, status, now, opt);
+  const Json& pods = eplan.enabled ? eplan.pods : pods_all;
+  for (const auto& a : eplan.actions.items()) actions.push_back(a);
+  if (eplan.give_up) {
+    add_event(events, "Warning", ki.reason_prefix + "Failed", eplan.message);
+    update_job_conditions(status, "Failed", ki.reason_prefix + "Failed", eplan.message, now);
+    if (status.get("completionTime").is_null()) status.set("completionTime", rfc3339(now));
+    metrics.set("failed", (int64_t)1);
+    requeue = 0.0;
+    return finish();
+  }
+  if (eplan.restarted) {
+    if (update_job_conditions(status, "Restarting", ki.reason_prefix + "Restarting", eplan.message, now))
+      add_event(events, "Warning", ki.reason_prefix + "Restarting", eplan.message);
+    else
+      add_event(events, "Normal", "ElasticResize", eplan.message);
+    m_restarted++;
+  }
+  if (eplan.draining) {
+    requeue = 0.5;  // recreate as soon as the old generation is gone
+    return finish();
+  }
+  if (!std::isnan(eplan.requeue_after)) requeue = eplan.requeue_after;
+  const Json& rp = job.get("spec").get("runPolicy");
+  const Json& specs = replica_specs(job);
 
   // ---- limits ----
   int64_t active = 0, failed = 0, total = 0, prev_failed = 0;
@@ -482,7 +507,7 @@ Json reconcile(const Json& job_in, const Json& pods, const Json& services, doubl
   if (!ads.is_null() && !is_succeeded(status) && !is_failed(status)) {
     const double st = parse_rfc3339(status.get("startTime").str());
     const double left = st + (double)ads.as_int() - now;
-    if (!had_start || left > 0) requeue = std::max(0.0, left);
+    if (!had_start || left > 0) requeue = std::isnan(requeue) ? std::max(0.0, left) : std::min(requeue, std::max(0.0, left));
   }
   // a freshly terminal job needs one more pass for cleanup / TTL
   if ((is_succeeded(status) || is_failed(status)) && !(is_succeeded(old_status) || is_failed(old_status))) {

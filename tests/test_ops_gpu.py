@@ -258,3 +258,47 @@ def test_flash_attention_in_llama_layer():
     lc.backward()
     for (n, pg), (_, pc) in zip(m_gpu.named_parameters(), m_cpu.named_parameters()):
         assert rel(pg.grad.cpu(), pc.grad) < 5e-2, n
+
+
+@pytest.mark.parametrize("M,K,N,act,keep", [(100, 784, 128, "relu", 1.0), (64, 100, 10, "none", 1.0),
+                                            (256, 512, 300, "relu", 0.9), (33, 64, 96, "gelu", 0.75)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_dense_bias_act_dropout(M, K, N, act, keep, dt):
+    """Fused MFMA dense (csrc/hip/mlp.hip) vs the fp32 CPU reference, same
+    counter-hash dropout mask (exact mask parity)."""
+    _lib()
+    from tf_operator_amd.ops.mlp import linear_bias_act
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, dtype=dt)
+    w = (torch.randn(N, K) / K ** 0.5).to(dt)
+    b = (torch.randn(N) * 0.1).to(dt)
+    dy = torch.randn(M, N, dtype=dt)
+    outs = []
+    for dev in ("cpu", DEV):
+        xx = x.detach().to(dev).requires_grad_()
+        ww = w.detach().to(dev).requires_grad_()
+        bb = b.detach().to(dev).requires_grad_()
+        y = linear_bias_act(xx, ww, bb, act, keep, seed=1234)
+        y.backward(dy.to(dev))
+        g = [t.grad for t in (xx, ww, bb)]
+        outs.append([y.detach().cpu()] + [t.detach().cpu() for t in g])
+    # the GEMM runs on bf16 MFMA (fp32 accumulate) for fp32 inputs too
+    tol = 2e-2 if dt == torch.bfloat16 else 6e-3
+    for a, r, name in zip(outs[1], outs[0], ["y", "dx", "dw", "db"]):
+        assert rel(a, r) < tol, (name, rel(a, r))
+
+
+@pytest.mark.parametrize("C", [10, 1000])
+def test_accuracy_kernel(C):
+    _lib()
+    from tf_operator_amd.ops.mlp import accuracy
+
+    torch.manual_seed(1)
+    lg = torch.randn(517, C)
+    lab = torch.randint(0, C, (517,))
+    lab[:200] = lg[:200].argmax(-1)
+    ref = float((lg.argmax(-1) == lab).float().mean())
+    got = float(accuracy(lg.to(DEV, torch.bfloat16), lab.to(DEV)))
+    ref_bf = float((lg.to(torch.bfloat16).float().argmax(-1) == lab).float().mean())
+    assert abs(got - ref_bf) < 1e-6 and abs(ref_bf - ref) < 0.05

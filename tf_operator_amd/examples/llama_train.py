@@ -29,6 +29,11 @@ def main(argv=None):
     rt = Runtime()
     rt.install_preemption_handler()
     info = rt.init_dist()
+    with rt.guard():
+        _train(a, rt, info)
+
+
+def _train(a, rt, info):
     dev = pick_device() if info.backend != "gloo" else torch.device("cpu")
     tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr)
     payload = ckpt.load_latest(rt.ckpt_dir)

@@ -44,6 +44,7 @@ RESOURCES = {
     "services": ("Service", True, False),
     "events": ("Event", True, False),
     "namespaces": ("Namespace", False, False),
+    "nodes": ("Node", False, True),
     "configmaps": ("ConfigMap", True, False),
     "scheduling.volcano.sh/podgroups": ("PodGroup", True, True),
     "coordination.k8s.io/leases": ("Lease", True, False),
@@ -53,7 +54,7 @@ for _plural, (_kind, _f) in KUBEFLOW_KINDS.items():
     RESOURCES["kubeflow.org/" + _plural] = (_kind, True, True)
 
 API_VERSIONS = {
-    "pods": "v1", "services": "v1", "events": "v1", "namespaces": "v1", "configmaps": "v1",
+    "pods": "v1", "services": "v1", "events": "v1", "namespaces": "v1", "configmaps": "v1", "nodes": "v1",
     "scheduling.volcano.sh/podgroups": "scheduling.volcano.sh/v1beta1",
     "coordination.k8s.io/leases": "coordination.k8s.io/v1",
     "apiextensions.k8s.io/customresourcedefinitions": "apiextensions.k8s.io/v1",
@@ -109,6 +110,9 @@ class FakeAPIServer:
             self._add_resource(core, res, res)
         r.add_route("*", core + "/namespaces", self._bind(self.h_collection, "namespaces", None))
         r.add_route("*", core + "/namespaces/{name}", self._bind(self.h_item, "namespaces", None))
+        r.add_route("*", core + "/nodes", self._bind(self.h_collection, "nodes", None))
+        r.add_route("*", core + "/nodes/{name}", self._bind(self.h_item, "nodes", None))
+        r.add_route("*", core + "/nodes/{name}/status", self._bind(self.h_status, "nodes", None))
         for key in RESOURCES:
             if "/" in key:
                 group, plural = key.split("/")

@@ -102,6 +102,7 @@ class LocalKubelet:
         self._stop = asyncio.Event()
         self._tasks = []
         self.start_times: dict[tuple, list] = {}
+        self.terminating: dict[tuple, asyncio.Task] = {}  # pods being killed (a same-named successor waits)
 
     # ---------------------------------------------------------------- service registry
     def service_port(self, ns, name):
@@ -211,8 +212,8 @@ class LocalKubelet:
         if pg is None:
             return False, []
         min_member = int(pg.get("spec", {}).get("minMember", 1))
-        members = [p for (pns, _), p in ((k, v["pod"]) for k, v in self.pending.items())
-                   if pns == ns and (p["metadata"].get("annotations") or {}).get("scheduling.k8s.io/group-name") == group]
+        members = [p for (pns, pname), p in ((k, v["pod"]) for k, v in self.pending.items())
+                   if pns == ns and (pns, pname) not in self.terminating and (p["metadata"].get("annotations") or {}).get("scheduling.k8s.io/group-name") == group]
         if len(members) < min_member:
             return False, []
         need = sum(pod_gpus(p, self.gpu_resource) for p in members)
@@ -226,6 +227,8 @@ class LocalKubelet:
     async def _try_schedule(self):
         for key in list(self.pending):
             if key not in self.pending:
+                continue
+            if key in self.terminating:
                 continue
             pod = self.pending[key]["pod"]
             ok, members = self._gang_ready(pod)
@@ -359,7 +362,7 @@ class LocalKubelet:
         if rec is None:
             return
         if all(p.proc is None or p.proc.returncode is not None for p in rec["procs"]):
-            self.free_gpus.extend(rec["gpus"])
+            self.free_gpus.extend(g for g in rec["gpus"] if g < self.total_gpus)
             self.free_gpus.sort()
             rec["gpus"] = []
             self.running.pop(key, None)
@@ -414,16 +417,19 @@ class LocalKubelet:
 
     async def _on_pod(self, et, pod):
         key = (pod["metadata"].get("namespace", "default"), pod["metadata"]["name"])
-        if et == "DELETED":
-            self.pending.pop(key, None)
-            if key in self.running:
-                await self._kill(key)
+        if et == "DELETED" or pod.get("metadata", {}).get("deletionTimestamp"):
+            if et == "DELETED":
+                self.pending.pop(key, None)
+            if key in self.running and key not in self.terminating:
+                # kill concurrently: deleting a whole elastic generation must
+                # not serialise N grace periods
+                t = asyncio.create_task(self._kill(key))
+                self.terminating[key] = t
+                t.add_done_callback(lambda _t, k=key: self.terminating.pop(k, None))
             return
-        if pod.get("metadata", {}).get("deletionTimestamp"):
-            if key in self.running:
-                await self._kill(key)
+        if key in self.pending:
             return
-        if key in self.running or key in self.pending:
+        if key in self.running and key not in self.terminating:
             return
         if (pod.get("status") or {}).get("phase") in ("Succeeded", "Failed"):
             return
@@ -438,8 +444,40 @@ class LocalKubelet:
             if self.pending:
                 await self._try_schedule()
 
+    # ---------------------------------------------------------------- node object
+    def node_object(self):
+        q = str(self.total_gpus)
+        res = {self.gpu_resource: q, "cpu": str(os.cpu_count() or 1)}
+        return {"apiVersion": "v1", "kind": "Node",
+                "metadata": {"name": self.node, "labels": {"kubernetes.io/hostname": self.node,
+                                                           "amd.com/gpu.product-name": "MI355X"}},
+                "status": {"capacity": dict(res), "allocatable": dict(res),
+                           "conditions": [{"type": "Ready", "status": "True"}]}}
+
+    async def _register_node(self):
+        body = self.node_object()
+        try:
+            cur = await self.kube.get("nodes", None, self.node)
+            cur["status"] = body["status"]
+            await self.kube.update_status("nodes", None, cur)
+        except ApiError:
+            try:
+                await self.kube.create("nodes", None, body)
+            except ApiError:
+                pass
+
+    async def set_capacity(self, gpus: int):
+        """Change the node's allocatable GPUs (fault injection: a device or
+        node slice lost / returned).  Devices >= `gpus` are not handed out
+        again; pods already holding them keep running until they end."""
+        self.total_gpus = int(gpus)
+        used = {g for rec in self.running.values() for g in rec["gpus"]}
+        self.free_gpus = sorted(g for g in range(self.total_gpus) if g not in used)
+        await self._register_node()
+
     async def start(self):
         os.makedirs(self.workdir, exist_ok=True)
+        await self._register_node()
         self._tasks = [asyncio.create_task(self._loop()), asyncio.create_task(self._scheduler())]
 
     async def stop(self):

@@ -46,6 +46,7 @@ class ControllerOptions:
     nccl_env: dict = dataclasses.field(default_factory=dict)
     resync_period: float = 12 * 3600.0    # --resyc-period (12h)
     report_url: str | None = None         # injected as TOA_REPORT_URL
+    gpu_resource: str = "amd.com/gpu"
 
 
 class JobController:
@@ -65,6 +66,7 @@ class JobController:
         self._stop = asyncio.Event()
         self._emitted = {}  # job uid -> set of (reason, message) already recorded
         self._first_step_seen = set()
+        self._first_seen: dict[str, float] = {}
         self.sync_count = 0
 
     # ------------------------------------------------------------------ informers
@@ -123,6 +125,8 @@ class JobController:
             return
         if et == "ADDED" and not (job.get("status") or {}).get("conditions"):
             self.metrics.created.labels(md.get("namespace", "default")).inc()
+            # creationTimestamp has 1 s resolution; remember when we saw it
+            self._first_seen.setdefault(md.get("uid"), time.time())
         if et != "SYNC":
             self.queue.add(key)
 
@@ -163,13 +167,46 @@ class JobController:
     def _options(self, key):
         o = {"cluster_domain": self.opt.cluster_domain, "enable_gang_scheduling": self.opt.enable_gang_scheduling,
              "gang_scheduler_name": self.opt.gang_scheduler_name, "inject_rocm_env": self.opt.inject_rocm_env,
-             "previous_retry": self.queue.num_requeues(key)}
+             "gpu_resource": self.opt.gpu_resource, "previous_retry": self.queue.num_requeues(key)}
         env = dict(self.opt.nccl_env)
         if self.opt.report_url:
             env["TOA_REPORT_URL"] = self.opt.report_url
         if env:
             o["nccl_env"] = env
         return o
+
+    async def _elastic_free_gpus(self, uid):
+        """GPUs an elastic job may use: node allocatable minus what other
+        operator-managed pods hold (this job's own pods count as free).
+        None when the cluster exposes no GPU nodes."""
+        try:
+            nodes = (await self.kube.list("nodes")).get("items") or []
+        except ApiError:
+            return None
+        res = self.opt.gpu_resource
+        total = 0
+        for n in nodes:
+            q = ((n.get("status") or {}).get("allocatable") or {}).get(res)
+            if q is not None:
+                total += int(float(str(q)))
+        if not nodes:
+            return None
+        used = 0
+        for p in self.pods.list(""):
+            ref = controller_ref(p)
+            if ref is not None and ref.get("uid") == uid:
+                continue
+            st = p.get("status") or {}
+            ph = st.get("phase")
+            scheduled = any(c.get("type") == "PodScheduled" and c.get("status") == "True"
+                            for c in st.get("conditions") or [])
+            if ph == "Running" or (ph == "Pending" and scheduled):
+                for c in (p.get("spec") or {}).get("containers") or []:
+                    r = c.get("resources") or {}
+                    q = (r.get("requests") or {}).get(res, (r.get("limits") or {}).get(res))
+                    if q is not None:
+                        used += int(float(str(q)))
+        return max(0, total - used)
 
     async def sync(self, key):
         plural, ns, name = key.split("/", 2)
@@ -200,8 +237,13 @@ class JobController:
         pods = owned(self.pods.list(ns, {"group-name": "kubeflow.org", "job-name": name.replace("/", "-")}))
         svcs = owned(self.services.list(ns, {"group-name": "kubeflow.org", "job-name": name.replace("/", "-")}))
         del sel
+        opts = self._options(key)
+        if job.get("spec", {}).get("elasticPolicy"):
+            free = await self._elastic_free_gpus(uid)
+            if free is not None:
+                opts["elastic_free_gpus"] = free
         now = time.time()
-        res = core.reconcile(job, pods, svcs, now=now, options=self._options(key))
+        res = core.reconcile(job, pods, svcs, now=now, options=opts)
         for e in res.get("expect", []):
             self.expectations.expect_creations(e["key"], int(e["add"]), now)
         await self._execute(res, job, res_key)
@@ -310,11 +352,20 @@ class JobController:
         plural = KIND_PLURAL.get(kind, "tfjobs")
         if plural in self.jobs:
             job = self.jobs[plural].get(f"{ns}/{name}")
-        if payload.get("first_step_time") and (ns, name) not in self._first_step_seen and job is not None:
-            created = core.parse_rfc3339(job["metadata"].get("creationTimestamp", ""))
-            if created == created:  # not NaN
-                self.metrics.first_step.labels(ns, kind).observe(max(0.0, float(payload["first_step_time"]) - created))
-                self._first_step_seen.add((ns, name))
+        gen = int(payload.get("elastic_generation") or 0)
+        seen_key = (ns, name, gen)
+        if payload.get("first_step_time") and seen_key not in self._first_step_seen and job is not None:
+            t = float(payload["first_step_time"])
+            self._first_step_seen.add(seen_key)
+            es = (job.get("status") or {}).get("elasticStatus") or {}
+            if gen > 0 and es.get("lastRestartUnix") is not None:
+                self.metrics.time_to_resume.labels(ns, kind).observe(max(0.0, t - float(es["lastRestartUnix"])))
+            elif gen == 0:
+                created = self._first_seen.get(job["metadata"].get("uid"))
+                if created is None:
+                    created = core.parse_rfc3339(job["metadata"].get("creationTimestamp", ""))
+                if created == created:  # not NaN
+                    self.metrics.first_step.labels(ns, kind).observe(max(0.0, t - created))
         if payload.get("samples_per_sec") is not None:
             self.metrics.samples_per_sec.labels(ns, name).set(float(payload["samples_per_sec"]))
 

@@ -23,7 +23,7 @@ import aiohttp
 
 GROUP_VERSIONS = {"kubeflow.org": "v1", "scheduling.volcano.sh": "v1beta1", "coordination.k8s.io": "v1",
                   "apiextensions.k8s.io": "v1"}
-CLUSTER_SCOPED = {"namespaces", "apiextensions.k8s.io/customresourcedefinitions"}
+CLUSTER_SCOPED = {"namespaces", "nodes", "apiextensions.k8s.io/customresourcedefinitions"}
 
 
 class ApiError(Exception):

@@ -31,6 +31,9 @@ class OperatorMetrics:
         self.first_step = Histogram("trainop_job_submit_to_first_step_seconds",
                                     "Job creationTimestamp -> first completed training step (rank 0)",
                                     ["job_namespace", "kind"], registry=r, buckets=LATENCY_BUCKETS)
+        self.time_to_resume = Histogram("trainop_elastic_time_to_resume_seconds",
+                                        "Elastic group restart -> first training step of the new generation",
+                                        ["job_namespace", "kind"], registry=r, buckets=LATENCY_BUCKETS)
         self.samples_per_sec = Gauge("trainop_samples_per_second", "Training throughput reported by rank 0",
                                      ["job_namespace", "job_name"], registry=r)
 

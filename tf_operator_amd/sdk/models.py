@@ -122,9 +122,30 @@ class V1ReplicaSpec(_Model):
 
 @dataclasses.dataclass
 class V1ElasticPolicy(_Model):
-    """tf_operator_amd extension (BASELINE config #5; not in the reference)."""
+    """tf_operator_amd extension (BASELINE config #5; not in the reference).
+    Semantics: csrc/core/elastic.cc (group restarts, resize to capacity)."""
     min_replicas: typing.Optional[int] = None
     max_replicas: typing.Optional[int] = None
+    max_restarts: typing.Optional[int] = None
+    scale_up_cooldown_seconds: typing.Optional[float] = None
+    scale_down_delay_seconds: typing.Optional[float] = None
+
+
+@dataclasses.dataclass
+class V1ElasticStatus(_Model):
+    generation: typing.Optional[int] = None
+    current_replicas: typing.Optional[int] = None
+    desired_replicas: typing.Optional[int] = None
+    restarts: typing.Optional[int] = None
+    launched: typing.Optional[bool] = None
+    capacity: typing.Optional[int] = None
+    generation_start_time: typing.Optional[str] = None
+    launch_time: typing.Optional[str] = None
+    last_restart_time: typing.Optional[str] = None
+    last_restart_unix: typing.Optional[float] = None
+    last_scale_time: typing.Optional[str] = None
+    last_transition_reason: typing.Optional[str] = None
+    last_resume_seconds: typing.Optional[float] = None
 
 
 @dataclasses.dataclass
@@ -175,6 +196,7 @@ class V1JobStatus(_Model):
     start_time: typing.Optional[str] = None
     completion_time: typing.Optional[str] = None
     last_reconcile_time: typing.Optional[str] = None
+    elastic_status: typing.Optional[V1ElasticStatus] = None
 
 
 @dataclasses.dataclass

@@ -149,3 +149,24 @@ def with_status(job, status):
     j = copy.deepcopy(job)
     j["status"] = status
     return j
+
+
+def get_condition(job_or_status, ctype):
+    st = job_or_status.get("status", job_or_status)
+    for c in st.get("conditions", []):
+        if c["type"] == ctype:
+            return c
+    return None
+
+
+def new_pytorchjob(master=1, worker=0, name="test-pytorchjob", namespace="default"):
+    """pkg/controller.v1/pytorch/pytorchjob_controller_suite_test.go style job."""
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "metadata": {"name": name, "namespace": namespace,
+                        "uid": str(uuid.uuid5(uuid.NAMESPACE_DNS, name + namespace))},
+           "spec": {"runPolicy": {}, "pytorchReplicaSpecs": {}}}
+    specs = job["spec"]["pytorchReplicaSpecs"]
+    for rt, n in (("Master", master), ("Worker", worker)):
+        if n > 0:
+            specs[rt] = {"replicas": n, "template": replica_template("pytorch", "pytorchjob-port", 23456)}
+    return job

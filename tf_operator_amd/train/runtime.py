@@ -6,6 +6,7 @@ ExitCode / elastic restart policies), and the role of this replica
 (chief/worker/ps/evaluator)."""
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import signal
@@ -14,6 +15,23 @@ import time
 import urllib.request
 
 from . import dist as tdist
+
+# a lost peer (broken collective) exits with a retryable code (>= 128), so
+# ExitCode / elastic policies restart the group instead of failing the job
+PEER_LOST_EXIT = 143
+_PEER_MARKERS = ("Connection closed by peer", "Connection reset by peer", "Broken pipe", "NCCL", "RCCL",
+                 "Socket Timeout", "ProcessGroup", "gloo")
+
+
+def is_peer_failure(e: BaseException) -> bool:
+    try:
+        import torch.distributed as d
+
+        if isinstance(e, d.DistError):
+            return True
+    except Exception:  # pragma: no cover - torch without distributed
+        pass
+    return isinstance(e, (RuntimeError, ConnectionError)) and any(m in str(e) for m in _PEER_MARKERS)
 
 
 class Runtime:
@@ -47,6 +65,19 @@ class Runtime:
     def is_chief(self):
         return self.rank == 0
 
+    @contextlib.contextmanager
+    def guard(self):
+        """Wrap a training loop: a collective that fails because a peer died
+        ends this replica with PEER_LOST_EXIT (no hang in process-group
+        teardown) so the operator restarts the whole group."""
+        try:
+            yield
+        except Exception as e:
+            if self.info is not None and self.info.world > 1 and is_peer_failure(e):
+                self.log(f"lost a peer ({type(e).__name__}: {str(e)[:200]}); exiting {PEER_LOST_EXIT}")
+                os._exit(PEER_LOST_EXIT)
+            raise
+
     # -------------------------------------------------------------- preemption
     def install_preemption_handler(self):
         def _h(signum, frame):
@@ -61,7 +92,8 @@ class Runtime:
     def report(self, **kw):
         if not self.report_url or not self.is_chief:
             return
-        body = {"job": self.job, "namespace": self.namespace, "kind": self.kind, **kw}
+        body = {"job": self.job, "namespace": self.namespace, "kind": self.kind,
+                "elastic_generation": int(os.environ.get("TOA_ELASTIC_GENERATION", "0") or 0), **kw}
         try:
             req = urllib.request.Request(self.report_url, data=json.dumps(body).encode(),
                                          headers={"Content-Type": "application/json"}, method="POST")
