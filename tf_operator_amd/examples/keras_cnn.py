@@ -41,6 +41,8 @@ def main(argv=None):
     tr = simple.DPTrainer(model, lambda o, y: cross_entropy(o.float(), y), rt, lr=decay(0))
     data = SyntheticMNIST(a.batch_per_replica, rt.rank, rt.world, device=dev, image=True, dtype=model_dtype(dev))
     start = tr.maybe_resume(a.saved_model_dir)
+    if start:
+        rt.log(f"resumed from checkpoint at step {start} (epoch {start // a.steps_per_epoch})")
     for epoch in range(start // a.steps_per_epoch, a.epochs):
         tr.opt.lr = decay(epoch)
         for _ in range(a.steps_per_epoch):
