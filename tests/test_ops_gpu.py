@@ -270,8 +270,10 @@ def test_dense_bias_act_dropout(M, K, N, act, keep, dt):
     from tf_operator_amd.ops.mlp import linear_bias_act
 
     torch.manual_seed(0)
-    x = torch.randn(M, K, dtype=dt)
-    w = (torch.randn(N, K) / K ** 0.5).to(dt)
+    # the GEMM runs on bf16 MFMA (fp32 accumulate) for fp32 inputs too: give
+    # both paths bf16-representable operands so ReLU masks agree exactly
+    x = torch.randn(M, K).to(torch.bfloat16).to(dt)
+    w = (torch.randn(N, K) / K ** 0.5).to(torch.bfloat16).to(dt)
     b = (torch.randn(N) * 0.1).to(dt)
     dy = torch.randn(M, N, dtype=dt)
     outs = []
@@ -283,8 +285,7 @@ def test_dense_bias_act_dropout(M, K, N, act, keep, dt):
         y.backward(dy.to(dev))
         g = [t.grad for t in (xx, ww, bb)]
         outs.append([y.detach().cpu()] + [t.detach().cpu() for t in g])
-    # the GEMM runs on bf16 MFMA (fp32 accumulate) for fp32 inputs too
-    tol = 2e-2 if dt == torch.bfloat16 else 6e-3
+    tol = 2e-2 if dt == torch.bfloat16 else 5e-3
     for a, r, name in zip(outs[1], outs[0], ["y", "dx", "dw", "db"]):
         assert rel(a, r) < tol, (name, rel(a, r))
 
