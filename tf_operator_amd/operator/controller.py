@@ -67,6 +67,7 @@ class JobController:
         self._emitted = {}  # job uid -> set of (reason, message) already recorded
         self._first_step_seen = set()
         self._first_seen: dict[str, float] = {}
+        self.reports: dict[tuple, dict] = {}  # (ns, job) -> merged rank-0 reports (first first_step_time kept)
         self.sync_count = 0
 
     # ------------------------------------------------------------------ informers
@@ -352,6 +353,10 @@ class JobController:
         plural = KIND_PLURAL.get(kind, "tfjobs")
         if plural in self.jobs:
             job = self.jobs[plural].get(f"{ns}/{name}")
+        rec = self.reports.setdefault((ns, name), {})
+        for k, v in payload.items():
+            if k not in rec or k != "first_step_time":
+                rec[k] = v
         gen = int(payload.get("elastic_generation") or 0)
         seen_key = (ns, name, gen)
         if payload.get("first_step_time") and seen_key not in self._first_step_seen and job is not None:
