@@ -120,6 +120,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
 
   gload(0);
   swrite(0);
+  // Retire the Q loads HERE.  Left to itself the compiler sinks them past the
+  // barrier; the loop then inherits "Q pending" and, vmcnt being in-order,
+  // its first MFMA waits on the K/V prefetch of the same iteration -- fully
+  // exposing the prefetch latency every tile (measured: 390 TF/s).
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) gload(t + 1);
@@ -335,7 +341,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     }
     if (tid < 64) {
       const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + tid;
-      slse = LSE[li] * LOG2E;
+      slse = LSE[li];  // scaled at swrite: consuming it here would wait on the whole prefetch
       sdel = DELTA[li];
     }
   };
@@ -351,13 +357,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
       *(u32x4*)(ob + rt_off(row, c)) = sdo[i];
     }
     if (tid < 64) {
-      lb[tid] = slse;
+      lb[tid] = slse * LOG2E;
       lb[64 + tid] = sdel;
     }
   };
 
   gload(0);
   swrite(0);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(kf[s]), "v"(vf[s]));  // retire resident loads (see fwd)
   __syncthreads();
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) gload(it + 1);
@@ -488,6 +496,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
   };
   gload(0);
   swrite(0);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]), "v"(of[s]));  // retire resident loads (see fwd)
+  asm volatile("" ::"v"(lse2), "v"(del));
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     if (t + 1 < ntiles) gload(t + 1);

@@ -1,6 +1,7 @@
 """Micro-benchmark: HIP flash attention (packed GQA) vs torch SDPA (aotriton,
 expanded K/V) at the Llama-3-8B training shape.  Prints ms and TFLOP/s."""
 import math
+import os
 import sys
 import time
 
@@ -12,10 +13,12 @@ from tf_operator_amd.ops import llm  # noqa: E402
 B, H, Hk, S, D = 4, 32, 8, 4096, 128
 dev = "cuda"
 torch.manual_seed(0)
-q = torch.randn(B, H, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-k = torch.randn(B, Hk, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-v = torch.randn(B, Hk, S, D, device=dev, dtype=torch.bfloat16, requires_grad=True)
-do = torch.randn(B, H, S, D, device=dev, dtype=torch.bfloat16)
+XS = float(os.environ.get("XS", "1"))    # input scale (q, k, v)
+GS = float(os.environ.get("GS", "1"))    # upstream-gradient scale
+q = (torch.randn(B, H, S, D, device=dev) * XS).to(torch.bfloat16).requires_grad_()
+k = (torch.randn(B, Hk, S, D, device=dev) * XS).to(torch.bfloat16).requires_grad_()
+v = (torch.randn(B, Hk, S, D, device=dev) * XS).to(torch.bfloat16).requires_grad_()
+do = (torch.randn(B, H, S, D, device=dev) * GS).to(torch.bfloat16)
 scale = 1 / math.sqrt(D)
 flops_fwd = 4 * B * H * S * S * D / 2
 
@@ -41,6 +44,7 @@ def timeit(fn, n=10):
     return (time.perf_counter() - t) / n * 1e3
 
 
+print(f"XS={XS} GS={GS}")
 for name, f in (("hip", hip_fwd), ("sdpa", sdpa_fwd)):
     with torch.no_grad():
         tf = timeit(f)
