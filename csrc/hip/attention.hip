@@ -61,30 +61,107 @@ __device__ __forceinline__ bf16x4 tr_read(const char* lds_base, int byte_off) {
 }
 
 // ---------------------------------------------------------------------------
-// forward
+// forward: workgroup = 8 waves = a 256-row query block of one (batch, head);
+// wave w owns rows 32w..32w+31, two waves per SIMD.  One 64-key K/V tile in
+// LDS feeds all 8 waves (half the L2->LDS traffic of two 4-wave blocks).
 // ---------------------------------------------------------------------------
+#define FWD_QB 256
+#define FWD_WAVES 8
+
+__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));  // one v_cvt_pk_bf16_f32
+}
+
+// combine a value with the partner lane's (l ^ 32) by v_permlane32_swap
+// (vdst's upper half <-> vsrc's lower half; with both = v, lane l < 32 ends
+// with {v[l], v[l+32]} and lane l >= 32 with {v[l-32], v[l]}).  Inline asm:
+// the builtin with identical operands gets folded to a single result.
+__device__ __forceinline__ void xhalf_pair(float v, float& a, float& b) {
+  a = v;
+  b = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float xhalf_max(float v) {
+  float a, b;
+  xhalf_pair(v, a, b);
+  return fmaxf(a, b);
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  float a, b;
+  xhalf_pair(v, a, b);
+  return a + b;
+}
+
+// XCD-aware block order: the hardware deals workgroups to the 8 XCDs round
+// robin, so give every XCD whole (batch, kv-head) groups -- their K/V stay
+// in that XCD's L2 across the GQA heads and query blocks -- and walk each
+// XCD's share heaviest (most keys) first.
+__device__ __forceinline__ void fwd_block_coords(int pid, int nqb, int B, int H, int Hk, int* qb, int* h, int* b) {
+  const int rep = H / Hk, G = B * Hk;
+  if ((G & 7) == 0) {
+    const int xcd = pid & 7, slot = pid >> 3, gper = G >> 3;
+    const int per_rank = gper * rep;
+    const int rank = slot / per_rank, w = slot - rank * per_rank;
+    const int gi = w / rep, hr = w - gi * rep;
+    const int grp = xcd * gper + gi;
+    *b = grp / Hk;
+    *h = (grp - *b * Hk) * rep + hr;
+    *qb = nqb - 1 - rank;
+  } else {
+    const int per = H * B, rank = pid / per, w = pid - rank * per;
+    *qb = nqb - 1 - rank;
+    *h = w % H;
+    *b = w / H;
+  }
+}
+
 template <int D>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+__global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
-                                                          float* __restrict__ LSE, int H, int Hk, int S,
+                                                          float* __restrict__ LSE, int B, int H, int Hk, int S,
                                                           float scale_log2) {
   static_assert(D == 128, "D=128 path");
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16KB + V 16KB)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int nqb = S / 128;
-  const int qb = nqb - 1 - blockIdx.x;  // heaviest (most keys) first
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int nqb = (S + FWD_QB - 1) / FWD_QB;
+  int qb, h, b;
+  fwd_block_coords(blockIdx.x, nqb, B, H, Hk, &qb, &h, &b);
   const int hk = h / (H / Hk);
   const int64_t qoff = ((int64_t)(b * H + h) * S) * D;
   const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
-  const int q0 = qb * 128 + wave * 32;  // first row of this wave
-  const int myq = q0 + r;               // the query row this lane owns
+  const int q0 = qb * FWD_QB + wave * 32;  // first row of this wave
+  const bool live = q0 < S;                // S % 128 == 0: a wave is all in or all out
+  const int myq = q0 + r;                  // the query row this lane owns
+  const int kend = min(S, (qb + 1) * FWD_QB);
+  const int ntiles = kend / TK;
+  const int t_diag = live ? (q0 + 31) / TK : -1;  // this wave's last (masked) tile
 
   // Q fragments: Q[myq][16s + 8hh .. +7], s = 0..7
   bf16x8 qf[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) qf[s] = as_bf16x8(ld16(Q + qoff + (int64_t)myq * D + 16 * s + 8 * hh));
+  for (int s = 0; s < 8; ++s)
+    qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq * D + 16 * s + 8 * hh)) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+
+  // lane-constant LDS read offsets (buffer / half / k-step parts are immediates)
+  // K: k_off(32n + r, 2s + hh) = r*256 + ((2s ^ x) << 4) + 8192 n,  x = hh ^ (r & 15)
+  int kro[8];
+  {
+    const int x = hh ^ (r & 15);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) kro[s] = r * ROWB + (((2 * s) ^ x) << 4);
+  }
+  // V^T: key = 32n + 16s' + 4hh + qq (+8), column block 32dt + 16(g&1) + 4pp
+  int vro[4];
+  {
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      vro[dt] = (4 * hh + qq) * ROWB + ((4 * (dt ^ qq) + 2 * (g & 1) + (pp >> 1)) << 4) + (pp & 1) * 8;
+  }
 
   f32x16 acc[4];
 #pragma unroll
@@ -93,132 +170,130 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  const int ntiles = (qb * 128 + 127) / TK + 1;  // causal: keys < (qb+1)*128
-  // staging: each thread moves 4 x 16 B of K and of V per tile
-  u32x4 stk[4], stv[4];
+  // staging: 512 threads x (2 x 16 B of K + 2 x 16 B of V) = one 64-key tile
+  u32x4 stk[2], stv[2];
   auto gload = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;  // 16-B element index in the 64x16 tile
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 512 * i;
       const int key = e >> 4, c = e & 15;
-      const int64_t g = koff + (int64_t)(t * TK + key) * D + c * 8;
-      stk[i] = ld16(K + g);
-      stv[i] = ld16(V + g);
+      const int64_t gidx = koff + (int64_t)(t * TK + key) * D + c * 8;
+      stk[i] = ld16(K + gidx);
+      stv[i] = ld16(V + gidx);
     }
   };
   auto swrite = [&](int buf) {
     char* kb = smem + buf * 32768;
     char* vb = kb + 16384;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 512 * i;
       const int key = e >> 4, c = e & 15;
       *(u32x4*)(kb + k_off(key, c)) = stk[i];
       *(u32x4*)(vb + v_off(key, c)) = stv[i];
     }
   };
 
+  auto compute = [&](int t, int buf, bool mask) {
+    const char* kb = smem + buf * 32768;
+    const char* vb = kb + 16384;
+    // ---- S^T = K Q^T : two 32-key halves (first MFMA of each chain starts from 0)
+    f32x16 sc[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const f32x16 z = {};
+      sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[0] + 8192 * n)), qf[0], z);
+#pragma unroll
+      for (int s = 1; s < 8; ++s)
+        sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[s] + 8192 * n)), qf[s], sc[n]);
+    }
+    // ---- causal mask (diagonal tile only) and row max of the raw scores
+    if (mask) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int key = t * TK + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          if (key > myq) sc[n][j] = -INFINITY;
+        }
+    }
+    float mx = sc[0][0];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sc[n][j]);
+    mx = xhalf_max(mx) * scale_log2;
+    // T13: rescale O / l only when some row's max grew by more than THR
+    if (__any(mx > m_run + RESCALE_THR)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = (m_run == -INFINITY) ? 0.f : EXP2(m_run - m_new);
+      l_run *= alpha;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+    }
+    // ---- P = exp2(s*c - m) packed straight into the PV B operand
+    float ls = 0.f;
+    uint32_t pw[2][8];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        const float p0 = EXP2(fmaf(sc[n][j], scale_log2, -m_run));
+        const float p1 = EXP2(fmaf(sc[n][j + 1], scale_log2, -m_run));
+        ls += p0 + p1;
+        pw[n][j >> 1] = cvt_pk(p0, p1);
+      }
+    l_run += ls;
+    // ---- O^T += V^T P^T (k permutation of the accumulator handled by the V^T read order)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        u32x4 w;
+        w[0] = pw[n][4 * s + 0];
+        w[1] = pw[n][4 * s + 1];
+        w[2] = pw[n][4 * s + 2];
+        w[3] = pw[n][4 * s + 3];
+        const bf16x8 pf = as_bf16x8(w);
+        const int kb0 = (32 * n + 16 * s) * ROWB;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x4 va = tr_read(vb, vro[dt] + kb0);
+          const bf16x4 vbv = tr_read(vb, vro[dt] + kb0 + 8 * ROWB);
+          const bf16x8 vf = __builtin_shufflevector(va, vbv, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[dt] = mfma32(vf, pf, acc[dt]);
+        }
+      }
+  };
+  auto step = [&](int t, int buf) {
+    if (t + 1 < ntiles) gload(t + 1);
+    if (t < t_diag) compute(t, buf, false);
+    else if (t == t_diag) compute(t, buf, true);
+    if (t + 1 < ntiles) swrite(buf ^ 1);
+    __syncthreads();
+  };
+
   gload(0);
   swrite(0);
   // Retire the Q loads HERE.  Left to itself the compiler sinks them past the
   // barrier; the loop then inherits "Q pending" and, vmcnt being in-order,
-  // its first MFMA waits on the K/V prefetch of the same iteration -- fully
-  // exposing the prefetch latency every tile (measured: 390 TF/s).
+  // its first MFMA waits on the K/V prefetch of the same iteration.
 #pragma unroll
   for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) gload(t + 1);
-    const int kbase = t * TK;
-    const bool active = kbase <= q0 + 31;  // wave-uniform: some row of this wave sees this tile
-    if (active) {
-      const char* kb = smem + (t & 1) * 32768;
-      const char* vb = kb + 16384;
-      // ---- S^T = K Q^T : two 32-key halves
-      f32x16 sc[2];
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) sc[n][j] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 kf = as_bf16x8(*(const u32x4*)(kb + k_off(32 * n + r, 2 * s + hh)));
-          sc[n] = mfma32(kf, qf[s], sc[n]);
-        }
-      }
-      // ---- online softmax (exp2 domain), causal mask on the diagonal tiles
-      const bool diag = kbase + TK - 1 > q0;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          float v = sc[n][j] * scale_log2;
-          if (diag) {
-            const int key = kbase + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
-            if (key > myq) v = -INFINITY;
-          }
-          sc[n][j] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      // T13: rescale O / l only when some row's max grew by more than THR
-      // (both lanes of a row see the same max, so they decide alike).
-      if (__any(mx > m_run + RESCALE_THR)) {
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = (m_run == -INFINITY) ? 0.f : EXP2(m_run - m_new);
-        l_run *= alpha;
-        m_run = m_new;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
-      }
-      float ls = 0.f;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const float p = EXP2(sc[n][j] - m_run);  // exp2(-inf) = 0 for masked keys
-          sc[n][j] = p;
-          ls += p;
-        }
-      l_run += ls;
-      // ---- O^T += V^T P^T
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          u32x4 pw;
-          pw[0] = pack2(sc[n][8 * s + 0], sc[n][8 * s + 1]);
-          pw[1] = pack2(sc[n][8 * s + 2], sc[n][8 * s + 3]);
-          pw[2] = pack2(sc[n][8 * s + 4], sc[n][8 * s + 5]);
-          pw[3] = pack2(sc[n][8 * s + 6], sc[n][8 * s + 7]);
-          const bf16x8 pf = as_bf16x8(pw);
-          // V^T fragment rows: keys 32n + 16s + 4hh + (0..3) and +8
-          const int g = lane >> 4, i16 = lane & 15;
-          const int qq = i16 >> 2, pp = i16 & 3;  // this lane supplies row qq, cols 4pp..4pp+3
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) {
-            const int col = 32 * dt + 16 * (g & 1) + 4 * pp;  // d column of the block this lane addresses
-            const int key_a = 32 * n + 16 * s + 4 * hh + qq;
-            const int key_b = key_a + 8;
-            const int ca = col >> 3, wa = (col & 7) * 2;  // 16-B chunk, byte within chunk
-            const bf16x4 va = tr_read(vb, v_off(key_a, ca) + wa);
-            const bf16x4 vbv = tr_read(vb, v_off(key_b, ca) + wa);
-            bf16x8 vf;
-            vf[0] = va[0]; vf[1] = va[1]; vf[2] = va[2]; vf[3] = va[3];
-            vf[4] = vbv[0]; vf[5] = vbv[1]; vf[6] = vbv[2]; vf[7] = vbv[3];
-            acc[dt] = mfma32(vf, pf, acc[dt]);
-          }
-        }
-      }
-    }
-    if (t + 1 < ntiles) swrite((t + 1) & 1);
-    __syncthreads();
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {  // unrolled by 2: buffer offsets become immediates
+    step(t, 0);
+    step(t + 1, 1);
   }
+  if (t < ntiles) step(t, 0);
+
+  if (!live) return;
   // ---- epilogue: O = O^T / l  (lane owns query row myq; d rows from the C map)
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = xhalf_sum(l_run);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
   bf16_t* orow = O + qoff + (int64_t)myq * D;
 #pragma unroll
@@ -227,8 +302,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16_t* __restri
     for (int g = 0; g < 4; ++g) {
       const int d = 32 * dt + 8 * g + 4 * hh;
       uint2 w;
-      w.x = pack2(acc[dt][4 * g + 0] * inv, acc[dt][4 * g + 1] * inv);
-      w.y = pack2(acc[dt][4 * g + 2] * inv, acc[dt][4 * g + 3] * inv);
+      w.x = cvt_pk(acc[dt][4 * g + 0] * inv, acc[dt][4 * g + 1] * inv);
+      w.y = cvt_pk(acc[dt][4 * g + 2] * inv, acc[dt][4 * g + 3] * inv);
       *(uint2*)(orow + d) = w;
     }
   if (hh == 0) LSE[(int64_t)(b * H + h) * S + myq] = (m_run + log2f(l_tot)) * 0.6931471805599453f;
@@ -564,9 +639,9 @@ extern "C" int toa_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, b
                             int Hk, int S, int D, int causal, float scale, hipStream_t stream) {
   if (D != 128 || S % 128 != 0 || H % Hk != 0 || !causal) return (int)hipErrorInvalidValue;
   attn_set_lds_limits();
-  dim3 grid(S / 128, H, B);
-  hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 65536, stream, q, k, v, o, lse, H, Hk, S,
-                     scale * LOG2E);
+  const int nqb = (S + FWD_QB - 1) / FWD_QB;
+  hipLaunchKernelGGL(attn_fwd_kernel<128>, dim3(nqb * H * B), dim3(64 * FWD_WAVES), 65536, stream, q, k, v, o, lse,
+                     B, H, Hk, S, scale * LOG2E);
   return (int)hipGetLastError();
 }
 
