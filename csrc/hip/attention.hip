@@ -41,7 +41,10 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));  // one v_cvt_pk_bf16_f32
 }
 
 // LDS tile geometry: 64 keys x 128 d bf16 = 16 KB, rows of 256 B = 16 chunks of 16 B.
@@ -68,12 +71,7 @@ __device__ __forceinline__ bf16x4 tr_read(const char* lds_base, int byte_off) {
 #define FWD_QB 256
 #define FWD_WAVES 8
 
-__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  const f2 v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));  // one v_cvt_pk_bf16_f32
-}
+__device__ __forceinline__ uint32_t cvt_pk(float a, float b) { return pack2(a, b); }
 
 // combine a value with the partner lane's (l ^ 32) by v_permlane32_swap
 // (vdst's upper half <-> vsrc's lower half; with both = v, lane l < 32 ends
@@ -433,8 +431,94 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     }
     if (tid < 64) {
       lb[tid] = slse * LOG2E;
-      lb[64 + tid] = sdel;
+      lb[64 + tid] = -sdel;
     }
+  };
+
+  // lane-constant LDS offsets of the one-image-two-ways layout (rt_off):
+  //  row reads   rows 32m + r, chunk 2s + hh:  rro[s] + 8192 m
+  //  tr reads    rows rb + 4hh + qq (+8):      tro[dt] (tro8[dt]) + 256 rb
+  int rro[8], tro[4], tro8[4];
+  {
+    const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) rro[s] = r * ROWB + (((2 * s + hh) ^ swz) << 4);
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int lo = 2 * (g & 1) + (pp >> 1);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      tro[dt] = (4 * hh + qq) * ROWB + ((4 * (dt ^ qq) + (lo ^ hh)) << 4) + (pp & 1) * 8;
+      tro8[dt] = (4 * hh + qq + 8) * ROWB + ((4 * (dt ^ qq) + (lo ^ ((hh + 2) & 3))) << 4) + (pp & 1) * 8;
+    }
+  }
+  auto rows = [&](const char* img, int m, bf16x8 (&f)[8]) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) f[s] = as_bf16x8(*(const u32x4*)(img + rro[s] + 8192 * m));
+  };
+  auto trf = [&](const char* img, int rb, int dt) {
+    const bf16x4 a = tr_read(img, tro[dt] + rb * ROWB);
+    const bf16x4 c = tr_read(img, tro8[dt] + rb * ROWB);
+    return (bf16x8)__builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  // S = Q K^T and dP' = dO V^T - delta (the -delta rows are dP's initial accumulator)
+  auto sdp = [&](const char* qi, const char* oi, const float* lb, int m, f32x16& sc, f32x16& dp) {
+    bf16x8 qa[8], oa[8];
+    rows(qi, m, qa);
+    rows(oi, m, oa);
+    f32x16 nd;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 d4 = *(const f32x4*)(lb + 64 + 32 * m + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nd[4 * g4 + j] = d4[j];
+    }
+    const f32x16 z = {};
+    sc = mfma32(qa[0], kf[0], z);
+    dp = mfma32(oa[0], vf[0], nd);
+#pragma unroll
+    for (int s = 1; s < 8; ++s) {
+      sc = mfma32(qa[s], kf[s], sc);
+      dp = mfma32(oa[s], vf[s], dp);
+    }
+  };
+  // P = exp2(S c - lse2) (masked on the diagonal sub-tile), dS = P dP', packed as B operands
+  auto softmax = [&](const float* lb, int m, f32x16& sc, f32x16& dp, bool mask, int qs, bf16x8 (&pb)[2],
+                     bf16x8 (&sb)[2]) {
+    uint32_t pw[8], sw[8];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      const f32x4 l4 = *(const f32x4*)(lb + 32 * m + 8 * (j >> 2) + 4 * hh);
+      float p0 = EXP2(fmaf(sc[j], scale_log2, -l4[j & 3]));
+      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, -l4[(j + 1) & 3]));
+      if (mask) {
+        const int q0_ = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        if (q0_ < mykey) p0 = 0.f;
+        if (q0_ + 1 < mykey) p1 = 0.f;
+      }
+      pw[j >> 1] = cvt_pk(p0, p1);
+      sw[j >> 1] = cvt_pk(p0 * dp[j], p1 * dp[j + 1]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      u32x4 a, c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = pw[4 * s2 + i];
+        c[i] = sw[4 * s2 + i];
+      }
+      pb[s2] = as_bf16x8(a);
+      sb[s2] = as_bf16x8(c);
+    }
+  };
+  // dV^T += dO^T P,  dK^T += Q^T dS
+  auto dkdv = [&](const char* qi, const char* oi, int m, const bf16x8 (&pb)[2], const bf16x8 (&sb)[2]) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma32(trf(oi, 32 * m + 16 * s2, dt), pb[s2], dv[dt]);
+        dk[dt] = mfma32(trf(qi, 32 * m + 16 * s2, dt), sb[s2], dk[dt]);
+      }
   };
 
   gload(0);
@@ -448,45 +532,28 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     const char* qi = smem + (it & 1) * BUF;
     const char* oi = qi + 16384;
     const float* lb = (const float*)(qi + 32768);
+    if (qt >= qt0 + 2) {
+      // below every wave's diagonal: both sub-tiles full, no masks, one
+      // straight-line block so the scheduler can overlap sub-tile 1's
+      // MFMAs with sub-tile 0's softmax and so on
+      f32x16 sc0, dp0, sc1, dp1;
+      bf16x8 pb0[2], sb0[2], pb1[2], sb1[2];
+      sdp(qi, oi, lb, 0, sc0, dp0);
+      sdp(qi, oi, lb, 1, sc1, dp1);
+      softmax(lb, 0, sc0, dp0, false, 0, pb0, sb0);
+      dkdv(qi, oi, 0, pb0, sb0);
+      softmax(lb, 1, sc1, dp1, false, 0, pb1, sb1);
+      dkdv(qi, oi, 1, pb1, sb1);
+    } else {
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int qs = qt * 64 + 32 * m;
-      if (qs + 31 < kw) continue;  // whole sub-tile above the diagonal for this wave
-      f32x16 sc, dp;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) { sc[j] = 0.f; dp[j] = 0.f; }
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const bf16x8 qa = as_bf16x8(*(const u32x4*)(qi + rt_off(32 * m + r, 2 * s + hh)));
-        sc = mfma32(qa, kf[s], sc);
-        const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rt_off(32 * m + r, 2 * s + hh)));
-        dp = mfma32(oa, vf[s], dp);
-      }
-      // P and dS; C rows = q (16 per lane: 4 runs of 4 consecutive rows), column = mykey
-      f32x4 lse4[4], del4[4];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        lse4[g4] = *(const f32x4*)(lb + 32 * m + 8 * g4 + 4 * hh);
-        del4[g4] = *(const f32x4*)(lb + 64 + 32 * m + 8 * g4 + 4 * hh);
-      }
-      const bool need_mask = qs < kw + 31;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int ql = 32 * m + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        float p = EXP2(sc[j] * scale_log2 - lse4[j >> 2][j & 3]);
-        if (need_mask && qt * 64 + ql < mykey) p = 0.f;
-        sc[j] = p;
-        dp[j] = p * (dp[j] - del4[j >> 2][j & 3]);
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 pb = pack_frag(sc, s);
-        const bf16x8 sb = pack_frag(dp, s);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          dv[dt] = mfma32(tr_frag(oi, 32 * m + 16 * s, dt, lane), pb, dv[dt]);
-          dk[dt] = mfma32(tr_frag(qi, 32 * m + 16 * s, dt, lane), sb, dk[dt]);
-        }
+      for (int m = 0; m < 2; ++m) {
+        const int qs = qt * 64 + 32 * m;
+        if (qs + 31 < kw) continue;  // whole sub-tile above the diagonal for this wave
+        f32x16 sc, dp;
+        bf16x8 pb[2], sb[2];
+        sdp(qi, oi, lb, m, sc, dp);
+        softmax(lb, m, sc, dp, qs < kw + 31, qs, pb, sb);
+        dkdv(qi, oi, m, pb, sb);
       }
     }
     if (it + 1 < total) swrite((it + 1) & 1);
@@ -511,107 +578,146 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// dQ: workgroup = 128 query rows of one (batch, head), the forward's
-// orientation (query on the lane):
-//   S^T = K Q^T, dP^T = V dO^T  (A = K / V row reads, B = Q / dO registers)
-//   dQ^T += K^T dS^T            (A = transposed K reads, B = dS^T accumulator)
+// dQ: same geometry as the forward (8 waves x 32 query rows, XCD-aware
+// heaviest-first blocks, 64-key K/V tiles shared by all waves, query on the
+// lane).  Per tile: S^T = K Q^T and dP^T = V dO^T (K, V row reads), then
+// dS^T = P^T (dP^T - delta) feeds dQ^T += K^T dS^T (K transposed reads) as
+// the B operand straight from the accumulator.  K and V share the
+// one-image-two-ways layout (rt_off).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 1) void attn_bwd_dq_kernel(
+__global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16_t* __restrict__ dQ, int H, int Hk, int S, float scale, float scale_log2) {
+    bf16_t* __restrict__ dQ, int B, int H, int Hk, int S, float scale, float scale_log2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16K + V 16K)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int nqb = S / 128;
-  const int qb = nqb - 1 - blockIdx.x;
-  const int h = blockIdx.y, b = blockIdx.z;
+  const int nqb = (S + FWD_QB - 1) / FWD_QB;
+  int qb, h, b;
+  fwd_block_coords(blockIdx.x, nqb, B, H, Hk, &qb, &h, &b);
   const int hk = h / (H / Hk);
   const int64_t qoff = ((int64_t)(b * H + h) * S) * 128;
   const int64_t koff = ((int64_t)(b * Hk + hk) * S) * 128;
-  const int q0 = qb * 128 + wave * 32;
+  const int q0 = qb * FWD_QB + wave * 32;
+  const bool live = q0 < S;
   const int myq = q0 + r;
+  const int kend = min(S, (qb + 1) * FWD_QB);
+  const int ntiles = kend / TK;
+  const int t_diag = live ? (q0 + 31) / TK : -1;
 
   bf16x8 qf[8], of[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
-    qf[s] = as_bf16x8(ld16(Q + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh));
-    of[s] = as_bf16x8(ld16(dO + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh));
+    qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh)) : bf16x8{};
+    of[s] = live ? as_bf16x8(ld16(dO + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh)) : bf16x8{};
   }
-  const float lse2 = LSE[(int64_t)(b * H + h) * S + myq] * LOG2E;
-  const float del = DELTA[(int64_t)(b * H + h) * S + myq];
+  const float lse2 = live ? LSE[(int64_t)(b * H + h) * S + myq] * LOG2E : 0.f;
+  const float del = live ? DELTA[(int64_t)(b * H + h) * S + myq] : 0.f;
   f32x16 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
 
-  const int ntiles = (qb * 128 + 127) / TK + 1;
-  u32x4 stk[4], stv[4];
+  int rro[8], tro[4], tro8[4];
+  {
+    const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) rro[s] = r * ROWB + (((2 * s + hh) ^ swz) << 4);
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+    const int lo = 2 * (g & 1) + (pp >> 1);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      tro[dt] = (4 * hh + qq) * ROWB + ((4 * (dt ^ qq) + (lo ^ hh)) << 4) + (pp & 1) * 8;
+      tro8[dt] = (4 * hh + qq + 8) * ROWB + ((4 * (dt ^ qq) + (lo ^ ((hh + 2) & 3))) << 4) + (pp & 1) * 8;
+    }
+  }
+
+  u32x4 stk[2], stv[2];
   auto gload = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 512 * i;
       const int key = e >> 4, c = e & 15;
-      const int64_t g = koff + (int64_t)(t * TK + key) * 128 + c * 8;
-      stk[i] = ld16(K + g);
-      stv[i] = ld16(V + g);
+      const int64_t gidx = koff + (int64_t)(t * TK + key) * 128 + c * 8;
+      stk[i] = ld16(K + gidx);
+      stv[i] = ld16(V + gidx);
     }
   };
   auto swrite = [&](int buf) {
     char* kb = smem + buf * 32768;
     char* vb = kb + 16384;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 512 * i;
       const int key = e >> 4, c = e & 15;
       *(u32x4*)(kb + rt_off(key, c)) = stk[i];
-      *(u32x4*)(vb + k_off(key, c)) = stv[i];
+      *(u32x4*)(vb + rt_off(key, c)) = stv[i];
     }
   };
+  auto compute = [&](int t, int buf, bool mask) {
+    const char* kb = smem + buf * 32768;
+    const char* vb = kb + 16384;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const f32x16 z = {};
+      f32x16 sc = mfma32(as_bf16x8(*(const u32x4*)(kb + rro[0] + 8192 * n)), qf[0], z);
+      f32x16 dp = mfma32(as_bf16x8(*(const u32x4*)(vb + rro[0] + 8192 * n)), of[0], z);
+#pragma unroll
+      for (int s = 1; s < 8; ++s) {
+        sc = mfma32(as_bf16x8(*(const u32x4*)(kb + rro[s] + 8192 * n)), qf[s], sc);
+        dp = mfma32(as_bf16x8(*(const u32x4*)(vb + rro[s] + 8192 * n)), of[s], dp);
+      }
+      uint32_t sw[8];
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        float p0 = EXP2(fmaf(sc[j], scale_log2, -lse2));
+        float p1 = EXP2(fmaf(sc[j + 1], scale_log2, -lse2));
+        if (mask) {
+          const int key = t * TK + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          if (key > myq) p0 = 0.f;
+          if (key + 1 > myq) p1 = 0.f;
+        }
+        sw[j >> 1] = pack2(p0 * (dp[j] - del), p1 * (dp[j + 1] - del));
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        u32x4 w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = sw[4 * s2 + i];
+        const bf16x8 sb = as_bf16x8(w);
+        const int rb = 32 * n + 16 * s2;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x4 a = tr_read(kb, tro[dt] + rb * ROWB);
+          const bf16x4 c = tr_read(kb, tro8[dt] + rb * ROWB);
+          acc[dt] = mfma32((bf16x8)__builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7), sb, acc[dt]);
+        }
+      }
+    }
+  };
+  auto step = [&](int t, int buf) {
+    if (t + 1 < ntiles) gload(t + 1);
+    if (t < t_diag) compute(t, buf, false);
+    else if (t == t_diag) compute(t, buf, true);
+    if (t + 1 < ntiles) swrite(buf ^ 1);
+    __syncthreads();
+  };
+
   gload(0);
   swrite(0);
 #pragma unroll
   for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]), "v"(of[s]));  // retire resident loads (see fwd)
   asm volatile("" ::"v"(lse2), "v"(del));
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) gload(t + 1);
-    const int kbase = t * TK;
-    if (kbase <= q0 + 31) {
-      const char* kb = smem + (t & 1) * 32768;
-      const char* vb = kb + 16384;
-      const bool diag = kbase + TK - 1 > q0;
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        f32x16 sc, dp;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) { sc[j] = 0.f; dp[j] = 0.f; }
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 ka = as_bf16x8(*(const u32x4*)(kb + rt_off(32 * n + r, 2 * s + hh)));
-          sc = mfma32(ka, qf[s], sc);
-          const bf16x8 va = as_bf16x8(*(const u32x4*)(vb + k_off(32 * n + r, 2 * s + hh)));
-          dp = mfma32(va, of[s], dp);
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int key = kbase + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
-          float p = EXP2(sc[j] * scale_log2 - lse2);
-          if (diag && key > myq) p = 0.f;
-          dp[j] = p * (dp[j] - del);
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const bf16x8 sb = pack_frag(dp, s);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma32(tr_frag(kb, 32 * n + 16 * s, dt, lane), sb, acc[dt]);
-        }
-      }
-    }
-    if (t + 1 < ntiles) swrite((t + 1) & 1);
-    __syncthreads();
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {
+    step(t, 0);
+    step(t + 1, 1);
   }
+  if (t < ntiles) step(t, 0);
+
+  if (!live) return;
   bf16_t* qrow = dQ + qoff + (int64_t)myq * 128;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -657,7 +763,7 @@ extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
                      rows, D);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 128, Hk, B), dim3(256), 2 * (32768 + 512), stream, q, k, v,
                      dout, lse, delta, dk, dv, H, Hk, S, scale, scale * LOG2E);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(S / 128, H, B), dim3(256), 65536, stream, q, k, v, dout, lse, delta,
-                     dq, H, Hk, S, scale, scale * LOG2E);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES), 65536,
+                     stream, q, k, v, dout, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E);
   return (int)hipGetLastError();
 }
