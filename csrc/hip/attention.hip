@@ -361,33 +361,50 @@ __device__ __forceinline__ bf16x8 pack_frag(const f32x16& x, int s) {
 }
 
 // ---------------------------------------------------------------------------
-// dK / dV: workgroup = 128 keys of one (batch, kv head); wave w owns keys
-// kb*128 + 32w .. +31 and keeps their K/V operand fragments and the dK^T /
-// dV^T accumulators in registers while the workgroup sweeps every query head
-// of the GQA group and every causal 64-row query tile (Q and dO tiles staged
-// through LDS, double buffered).  Orientation: key on the MFMA lane, so
-//   S = Q K^T, dP = dO V^T        (A = Q / dO row reads, B = K / V registers)
-//   dV^T += dO^T P, dK^T += Q^T dS (A = transposed reads, B = the accumulators)
+// dK / dV: workgroup = 8 waves = 128 keys of one (batch, kv head).  Wave w
+// owns keys 32(w&3)..+31 of the block (key on the MFMA lane) and query half
+// m = w>>2 of every 64-row query tile, so two waves accumulate partial dK^T /
+// dV^T for the same keys over disjoint query rows; they are summed through
+// LDS at the end.  K/V of the block live in LDS (not registers): the
+// accumulators (128) + one sub-tile's working set fit 256 VGPRs, i.e. two
+// waves per SIMD, which is what hides the LDS and softmax latency.
+//   S = Q K^T, dP = dO V^T - delta   (A = Q / dO row reads, B = K / V row reads)
+//   dV^T += dO^T P, dK^T += Q^T dS   (A = transposed reads, B = the accumulators)
+// The block sweeps every query head of the GQA group and every causal tile.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
+#define DKV_QBUF (32768 + 512)
+#define DKV_LDS (2 * DKV_QBUF + 65536)
+
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int Hk, int S, float scale, float scale_log2) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (Q 16K + dO 16K + lse 256 + delta 256)
+    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int H, int Hk, int S, float scale,
+    float scale_log2) {
+  // [Q/dO/lse/-delta buffer 0][buffer 1][K 32K][V 32K]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem + 2 * DKV_QBUF;
+  char* vimg = kimg + 32768;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int kb = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int kg = wave & 3, m = wave >> 2;
+  // heaviest (most query tiles) key blocks first; (b, hk) fastest
+  const int nkb = S / 128;
+  const int kb = nkb - 1 - (int)(blockIdx.x / (B * Hk));
+  const int bh = blockIdx.x % (B * Hk);
+  const int b = bh / Hk, hk = bh % Hk;
   const int rep = H / Hk;
-  const int kw = kb * 128 + wave * 32;  // first key of this wave
+  const int kw = kb * 128 + kg * 32;  // first key of this wave
   const int mykey = kw + r;
   const int64_t koff = ((int64_t)(b * Hk + hk) * S) * 128;
-  constexpr int BUF = 32768 + 512;
 
-  bf16x8 kf[8], vf[8];
+  // K / V of the block -> LDS (rt_off image: row reads give the B operands)
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    kf[s] = as_bf16x8(ld16(K + koff + (int64_t)mykey * 128 + 16 * s + 8 * hh));
-    vf[s] = as_bf16x8(ld16(V + koff + (int64_t)mykey * 128 + 16 * s + 8 * hh));
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + 512 * i;
+    const int row = e >> 4, c = e & 15;
+    const int64_t g = koff + (int64_t)(kb * 128 + row) * 128 + c * 8;
+    *(u32x4*)(kimg + rt_off(row, c)) = ld16(K + g);
+    *(u32x4*)(vimg + rt_off(row, c)) = ld16(V + g);
   }
   f32x16 dk[4], dv[4];
 #pragma unroll
@@ -395,49 +412,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
     for (int j = 0; j < 16; ++j) { dk[i][j] = 0.f; dv[i][j] = 0.f; }
 
-  const int qt0 = (kb * 128) / 64;       // first causal 64-row query tile
-  const int nqt = S / 64 - qt0;          // tiles per head
-  const int total = nqt * rep;
-  u32x4 sq[4], sdo[4];
-  float slse = 0.f, sdel = 0.f;
-  auto gload = [&](int it) {
-    const int hq = hk * rep + it / nqt;
-    const int qt = qt0 + it % nqt;
-    const int64_t qoff = ((int64_t)(b * H + hq) * S) * 128;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      const int row = e >> 4, c = e & 15;
-      const int64_t g = qoff + (int64_t)(qt * 64 + row) * 128 + c * 8;
-      sq[i] = ld16(Q + g);
-      sdo[i] = ld16(dO + g);
-    }
-    if (tid < 64) {
-      const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + tid;
-      slse = LSE[li];  // scaled at swrite: consuming it here would wait on the whole prefetch
-      sdel = DELTA[li];
-    }
-  };
-  auto swrite = [&](int buf) {
-    char* qb_ = smem + buf * BUF;
-    char* ob = qb_ + 16384;
-    float* lb = (float*)(qb_ + 32768);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      const int row = e >> 4, c = e & 15;
-      *(u32x4*)(qb_ + rt_off(row, c)) = sq[i];
-      *(u32x4*)(ob + rt_off(row, c)) = sdo[i];
-    }
-    if (tid < 64) {
-      lb[tid] = slse * LOG2E;
-      lb[64 + tid] = -sdel;
-    }
-  };
-
-  // lane-constant LDS offsets of the one-image-two-ways layout (rt_off):
-  //  row reads   rows 32m + r, chunk 2s + hh:  rro[s] + 8192 m
-  //  tr reads    rows rb + 4hh + qq (+8):      tro[dt] (tro8[dt]) + 256 rb
   int rro[8], tro[4], tro8[4];
   {
     const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
@@ -451,20 +425,51 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
       tro8[dt] = (4 * hh + qq + 8) * ROWB + ((4 * (dt ^ qq) + (lo ^ ((hh + 2) & 3))) << 4) + (pp & 1) * 8;
     }
   }
-  auto rows = [&](const char* img, int m, bf16x8 (&f)[8]) {
+
+  const int qt0 = (kb * 128) / 64;  // first causal 64-row query tile
+  const int nqt = S / 64 - qt0;
+  const int total = nqt * rep;
+  u32x4 sq[2], sdo[2];
+  float slse = 0.f, sdel = 0.f;
+  auto gload = [&](int it) {
+    const int hq = hk * rep + it / nqt;
+    const int qt = qt0 + it % nqt;
+    const int64_t qoff = ((int64_t)(b * H + hq) * S) * 128;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) f[s] = as_bf16x8(*(const u32x4*)(img + rro[s] + 8192 * m));
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 512 * i;
+      const int row = e >> 4, c = e & 15;
+      const int64_t g = qoff + (int64_t)(qt * 64 + row) * 128 + c * 8;
+      sq[i] = ld16(Q + g);
+      sdo[i] = ld16(dO + g);
+    }
+    if (tid < 64) {
+      const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + tid;
+      slse = LSE[li];  // scaled at swrite: consuming it here would wait on the whole prefetch
+      sdel = DELTA[li];
+    }
   };
-  auto trf = [&](const char* img, int rb, int dt) {
-    const bf16x4 a = tr_read(img, tro[dt] + rb * ROWB);
-    const bf16x4 c = tr_read(img, tro8[dt] + rb * ROWB);
-    return (bf16x8)__builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7);
+  auto swrite = [&](int buf) {
+    char* qb_ = smem + buf * DKV_QBUF;
+    char* ob = qb_ + 16384;
+    float* lb = (float*)(qb_ + 32768);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 512 * i;
+      const int row = e >> 4, c = e & 15;
+      *(u32x4*)(qb_ + rt_off(row, c)) = sq[i];
+      *(u32x4*)(ob + rt_off(row, c)) = sdo[i];
+    }
+    if (tid < 64) {
+      lb[tid] = slse * LOG2E;
+      lb[64 + tid] = -sdel;
+    }
   };
-  // S = Q K^T and dP' = dO V^T - delta (the -delta rows are dP's initial accumulator)
-  auto sdp = [&](const char* qi, const char* oi, const float* lb, int m, f32x16& sc, f32x16& dp) {
-    bf16x8 qa[8], oa[8];
-    rows(qi, m, qa);
-    rows(oi, m, oa);
+
+  auto subtile = [&](int buf, int qs, bool mask) {
+    const char* qi = smem + buf * DKV_QBUF;
+    const char* oi = qi + 16384;
+    const float* lb = (const float*)(qi + 32768);
     f32x16 nd;
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -473,17 +478,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
       for (int j = 0; j < 4; ++j) nd[4 * g4 + j] = d4[j];
     }
     const f32x16 z = {};
-    sc = mfma32(qa[0], kf[0], z);
-    dp = mfma32(oa[0], vf[0], nd);
+    f32x16 sc = z, dp = nd;
 #pragma unroll
-    for (int s = 1; s < 8; ++s) {
-      sc = mfma32(qa[s], kf[s], sc);
-      dp = mfma32(oa[s], vf[s], dp);
+    for (int s = 0; s < 8; ++s) {
+      const bf16x8 qa = as_bf16x8(*(const u32x4*)(qi + rro[s] + 8192 * m));
+      const bf16x8 kf = as_bf16x8(*(const u32x4*)(kimg + rro[s] + 8192 * kg));
+      sc = mfma32(qa, kf, sc);
+      const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rro[s] + 8192 * m));
+      const bf16x8 vf = as_bf16x8(*(const u32x4*)(vimg + rro[s] + 8192 * kg));
+      dp = mfma32(oa, vf, dp);
     }
-  };
-  // P = exp2(S c - lse2) (masked on the diagonal sub-tile), dS = P dP', packed as B operands
-  auto softmax = [&](const float* lb, int m, f32x16& sc, f32x16& dp, bool mask, int qs, bf16x8 (&pb)[2],
-                     bf16x8 (&sb)[2]) {
     uint32_t pw[8], sw[8];
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
@@ -491,12 +495,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
       float p0 = EXP2(fmaf(sc[j], scale_log2, -l4[j & 3]));
       float p1 = EXP2(fmaf(sc[j + 1], scale_log2, -l4[(j + 1) & 3]));
       if (mask) {
-        const int q0_ = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        if (q0_ < mykey) p0 = 0.f;
-        if (q0_ + 1 < mykey) p1 = 0.f;
+        const int q = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        if (q < mykey) p0 = 0.f;
+        if (q + 1 < mykey) p1 = 0.f;
       }
-      pw[j >> 1] = cvt_pk(p0, p1);
-      sw[j >> 1] = cvt_pk(p0 * dp[j], p1 * dp[j + 1]);
+      pw[j >> 1] = pack2(p0, p1);
+      sw[j >> 1] = pack2(p0 * dp[j], p1 * dp[j + 1]);
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -506,59 +510,63 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
         a[i] = pw[4 * s2 + i];
         c[i] = sw[4 * s2 + i];
       }
-      pb[s2] = as_bf16x8(a);
-      sb[s2] = as_bf16x8(c);
-    }
-  };
-  // dV^T += dO^T P,  dK^T += Q^T dS
-  auto dkdv = [&](const char* qi, const char* oi, int m, const bf16x8 (&pb)[2], const bf16x8 (&sb)[2]) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
+      const bf16x8 pb = as_bf16x8(a), sb = as_bf16x8(c);
+      const int rb = (32 * m + 16 * s2) * ROWB;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = mfma32(trf(oi, 32 * m + 16 * s2, dt), pb[s2], dv[dt]);
-        dk[dt] = mfma32(trf(qi, 32 * m + 16 * s2, dt), sb[s2], dk[dt]);
+        const bf16x4 o0 = tr_read(oi, tro[dt] + rb), o1 = tr_read(oi, tro8[dt] + rb);
+        dv[dt] = mfma32((bf16x8)__builtin_shufflevector(o0, o1, 0, 1, 2, 3, 4, 5, 6, 7), pb, dv[dt]);
+        const bf16x4 q0 = tr_read(qi, tro[dt] + rb), q1 = tr_read(qi, tro8[dt] + rb);
+        dk[dt] = mfma32((bf16x8)__builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7), sb, dk[dt]);
       }
+    }
+  };
+  auto step = [&](int it, int buf) {
+    if (it + 1 < total) gload(it + 1);
+    const int qs = (qt0 + it % nqt) * 64 + 32 * m;
+    if (qs > kw) subtile(buf, qs, false);        // strictly below this wave's diagonal
+    else if (qs == kw) subtile(buf, qs, true);  // the diagonal sub-tile
+    if (it + 1 < total) swrite(buf ^ 1);
+    __syncthreads();
   };
 
   gload(0);
   swrite(0);
-#pragma unroll
-  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(kf[s]), "v"(vf[s]));  // retire resident loads (see fwd)
   __syncthreads();
-  for (int it = 0; it < total; ++it) {
-    if (it + 1 < total) gload(it + 1);
-    const int qt = qt0 + it % nqt;
-    const char* qi = smem + (it & 1) * BUF;
-    const char* oi = qi + 16384;
-    const float* lb = (const float*)(qi + 32768);
-    if (qt >= qt0 + 2) {
-      // below every wave's diagonal: both sub-tiles full, no masks, one
-      // straight-line block so the scheduler can overlap sub-tile 1's
-      // MFMAs with sub-tile 0's softmax and so on
-      f32x16 sc0, dp0, sc1, dp1;
-      bf16x8 pb0[2], sb0[2], pb1[2], sb1[2];
-      sdp(qi, oi, lb, 0, sc0, dp0);
-      sdp(qi, oi, lb, 1, sc1, dp1);
-      softmax(lb, 0, sc0, dp0, false, 0, pb0, sb0);
-      dkdv(qi, oi, 0, pb0, sb0);
-      softmax(lb, 1, sc1, dp1, false, 0, pb1, sb1);
-      dkdv(qi, oi, 1, pb1, sb1);
-    } else {
+  int it = 0;
+  for (; it + 1 < total; it += 2) {  // unrolled by 2: buffer offsets become immediates
+    step(it, 0);
+    step(it + 1, 1);
+  }
+  if (it < total) step(it, 0);
+
+  // sum the two query halves' partials: waves m = 1 park theirs in LDS
+  float* red = (float*)smem;  // 4 waves x 2 x 64 lanes x 64 floats = 128 KB, Q/dO/K/V are dead
+  if (m == 1) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const int qs = qt * 64 + 32 * m;
-        if (qs + 31 < kw) continue;  // whole sub-tile above the diagonal for this wave
-        f32x16 sc, dp;
-        bf16x8 pb[2], sb[2];
-        sdp(qi, oi, lb, m, sc, dp);
-        softmax(lb, m, sc, dp, qs < kw + 31, qs, pb, sb);
-        dkdv(qi, oi, m, pb, sb);
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        *(f32x4*)(red + ((kg * 2 + 0) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4) =
+            f32x4{dk[dt][j], dk[dt][j + 1], dk[dt][j + 2], dk[dt][j + 3]};
+        *(f32x4*)(red + ((kg * 2 + 1) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4) =
+            f32x4{dv[dt][j], dv[dt][j + 1], dv[dt][j + 2], dv[dt][j + 3]};
+      }
+  }
+  __syncthreads();
+  if (m == 1) return;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      const f32x4 a = *(const f32x4*)(red + ((kg * 2 + 0) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4);
+      const f32x4 c = *(const f32x4*)(red + ((kg * 2 + 1) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dk[dt][j + i] += a[i];
+        dv[dt][j + i] += c[i];
       }
     }
-    if (it + 1 < total) swrite((it + 1) & 1);
-    __syncthreads();
-  }
   // store: lane owns key `mykey`, d rows 32dt + 8g + 4hh + (0..3)
   bf16_t* dkr = dK + koff + (int64_t)mykey * 128;
   bf16_t* dvr = dV + koff + (int64_t)mykey * 128;
@@ -735,8 +743,7 @@ static void attn_set_lds_limits() {
   static bool done = false;
   if (done) return;
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      2 * (32768 + 512));
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, DKV_LDS);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
   done = true;
 }
@@ -761,8 +768,8 @@ extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   const int64_t rows = (int64_t)B * H * S;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, o, dout, delta,
                      rows, D);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(S / 128, Hk, B), dim3(256), 2 * (32768 + 512), stream, q, k, v,
-                     dout, lse, delta, dk, dv, H, Hk, S, scale, scale * LOG2E);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S / 128) * B * Hk), dim3(512), DKV_LDS, stream, q, k, v, dout, lse,
+                     delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES), 65536,
                      stream, q, k, v, dout, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E);
   return (int)hipGetLastError();
