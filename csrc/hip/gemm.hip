@@ -1,0 +1,237 @@
+// Plain bf16 GEMMs of the training step on hipBLASLt, with per-shape
+// algorithm selection that is MEASURED on the MI355X instead of taken from
+// the library's heuristic.
+//
+// The Llama-3-8B step issues ~15 distinct GEMM forms (5 projections x
+// forward / dgrad / wgrad-accumulate); hipBLASLt's default pick for them runs
+// at 1.0-1.6 PF/s (scripts/gemm_bench.py).  toa_gemm_tune() times every
+// solution hipBLASLt has for a form (getAllAlgos, two passes: 1 rep each,
+// then the best 8 at 10 reps) and records the winner's solution index;
+// tf_operator_amd/ops/gemm.py persists the table (ops/gemm_tuning_gfx950.json)
+// and re-installs it at start-up with toa_gemm_set_algo(), so training never
+// tunes.  Forms without an entry use the library heuristic.
+//
+// Column-major BLAS convention (D = alpha op(A) op(B) + beta C, D m x n).
+// The row-major wrappers in ops/gemm.py map
+//   Y = X W^T  -> D^T = op_T(W) op_N(X)     (m=N, n=M, k=K)
+//   dX = dY W  -> D^T = op_N(W) op_N(dY)    (m=K, n=M, k=N)
+//   dW += dY^T X -> D^T = op_N(X) op_T(dY)  (m=K, n=N, k=M, beta=1)
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
+#include <hipblaslt/hipblaslt.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+namespace {
+
+typedef std::tuple<int, int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int> Key;
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
+  hipblasLtMatmulAlgo_t algo;
+  bool has_algo = false;
+  int index = -1;
+};
+
+struct Ctx {
+  hipblasLtHandle_t h = nullptr;
+  void* ws = nullptr;
+  size_t ws_size = 0;
+  int device = -1;
+  std::map<Key, Plan> plans;
+  std::map<Key, int> wanted;  // installed tuned indices, resolved lazily
+  std::mutex mu;
+};
+
+Ctx& ctx() {
+  static Ctx c;
+  return c;
+}
+
+hipblasOperation_t op_of(int t) { return t ? HIPBLAS_OP_T : HIPBLAS_OP_N; }
+
+int ensure_handle(Ctx& c) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (c.h != nullptr && c.device == dev) return 0;
+  if (hipblasLtCreate(&c.h) != HIPBLAS_STATUS_SUCCESS) return 1;
+  c.ws_size = 256ull << 20;  // 256 MB: stream-K / split-K solutions need room
+  if (hipMalloc(&c.ws, c.ws_size) != hipSuccess) {
+    c.ws = nullptr;
+    c.ws_size = 0;
+  }
+  c.device = dev;
+  return 0;
+}
+
+// out_bf16: D type bf16 (else fp32)
+Plan& plan_for(Ctx& c, const Key& k) {
+  auto it = c.plans.find(k);
+  if (it != c.plans.end()) return it->second;
+  Plan p;
+  const int ta = std::get<0>(k), tb = std::get<1>(k), out_f32 = std::get<9>(k);
+  const int64_t m = std::get<2>(k), n = std::get<3>(k), kk = std::get<4>(k);
+  const int64_t lda = std::get<5>(k), ldb = std::get<6>(k), ldc = std::get<7>(k);
+  hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F);
+  hipblasOperation_t oa = op_of(ta), ob = op_of(tb);
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &oa, sizeof(oa));
+  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &ob, sizeof(ob));
+  hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16BF, ta ? kk : m, ta ? m : kk, lda);
+  hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16BF, tb ? n : kk, tb ? kk : n, ldb);
+  hipblasLtMatrixLayoutCreate(&p.c, out_f32 ? HIP_R_32F : HIP_R_16BF, m, n, ldc);
+  return c.plans.emplace(k, p).first->second;
+}
+
+bool supported(Ctx& c, Plan& p, hipblasLtMatmulAlgo_t& algo, float beta) {
+  const float alpha = 1.f;
+  size_t ws = 0;
+  if (hipblaslt_ext::matmulIsAlgoSupported(c.h, p.desc, &alpha, p.a, p.b, &beta, p.c, p.c, algo, ws) !=
+      HIPBLAS_STATUS_SUCCESS)
+    return false;
+  return ws <= c.ws_size;
+}
+
+int resolve(Ctx& c, const Key& k, Plan& p, float beta) {
+  if (p.has_algo) return 0;
+  auto w = c.wanted.find(k);
+  if (w != c.wanted.end()) {
+    std::vector<int> idx{w->second};
+    std::vector<hipblasLtMatmulHeuristicResult_t> res;
+    if (hipblaslt_ext::getAlgosFromIndex(c.h, idx, res) == HIPBLAS_STATUS_SUCCESS && !res.empty() &&
+        supported(c, p, res[0].algo, beta)) {
+      p.algo = res[0].algo;
+      p.has_algo = true;
+      p.index = w->second;
+      return 0;
+    }
+  }
+  hipblasLtMatmulPreference_t pref;
+  hipblasLtMatmulPreferenceCreate(&pref);
+  uint64_t wsz = c.ws_size;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz));
+  hipblasLtMatmulHeuristicResult_t r[1];
+  int got = 0;
+  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(c.h, p.desc, p.a, p.b, p.c, p.c, pref, 1, r, &got);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || got == 0) return 2;
+  p.algo = r[0].algo;
+  p.has_algo = true;
+  p.index = hipblaslt_ext::getIndexFromAlgo(p.algo);
+  return 0;
+}
+
+int run(Ctx& c, Plan& p, hipblasLtMatmulAlgo_t& algo, const void* A, const void* B, void* C, float beta,
+        hipStream_t s) {
+  const float alpha = 1.f;
+  return hipblasLtMatmul(c.h, p.desc, &alpha, A, p.a, B, p.b, &beta, C, p.c, C, p.c, &algo, c.ws, c.ws_size, s) ==
+                 HIPBLAS_STATUS_SUCCESS
+             ? 0
+             : 3;
+}
+
+}  // namespace
+
+// D (= C) = op(A) op(B) + beta C ; bf16 A/B, bf16 or fp32 C/D, fp32 accumulate.
+extern "C" int toa_gemm(int ta, int tb, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda, const void* B,
+                        int64_t ldb, void* C, int64_t ldc, float beta, int out_f32, hipStream_t stream) {
+  Ctx& c = ctx();
+  std::lock_guard<std::mutex> g(c.mu);
+  if (ensure_handle(c)) return 1;
+  const Key key{ta, tb, m, n, k, lda, ldb, ldc, beta != 0.f, out_f32};
+  Plan& p = plan_for(c, key);
+  if (int e = resolve(c, key, p, beta)) return e;
+  return run(c, p, p.algo, A, B, C, beta, stream);
+}
+
+// Install a tuned solution index for a form (from the persisted table).
+extern "C" int toa_gemm_set_algo(int ta, int tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
+                                 int64_t ldc, int beta_nz, int out_f32, int index) {
+  Ctx& c = ctx();
+  std::lock_guard<std::mutex> g(c.mu);
+  const Key key{ta, tb, m, n, k, lda, ldb, ldc, beta_nz, out_f32};
+  c.wanted[key] = index;
+  auto it = c.plans.find(key);
+  if (it != c.plans.end()) it->second.has_algo = false;
+  return 0;
+}
+
+// Index of the solution a form currently runs (-1 if not resolved yet).
+extern "C" int toa_gemm_current_algo(int ta, int tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
+                                     int64_t ldc, int beta_nz, int out_f32) {
+  Ctx& c = ctx();
+  std::lock_guard<std::mutex> g(c.mu);
+  auto it = c.plans.find(Key{ta, tb, m, n, k, lda, ldb, ldc, beta_nz, out_f32});
+  return (it == c.plans.end() || !it->second.has_algo) ? -1 : it->second.index;
+}
+
+// Time every hipBLASLt solution for a form on the given (scratch) buffers and
+// keep the fastest.  Returns 0 and writes the winner's index / ms, the
+// heuristic default's ms, and the number of candidates timed.
+extern "C" int toa_gemm_tune(int ta, int tb, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
+                             const void* B, int64_t ldb, void* C, int64_t ldc, float beta, int out_f32,
+                             hipStream_t stream, int* best_index, float* best_ms, float* default_ms,
+                             int* n_timed) {
+  Ctx& c = ctx();
+  std::lock_guard<std::mutex> g(c.mu);
+  if (ensure_handle(c)) return 1;
+  const Key key{ta, tb, m, n, k, lda, ldb, ldc, beta != 0.f, out_f32};
+  Plan& p = plan_for(c, key);
+  std::vector<hipblasLtMatmulHeuristicResult_t> all;
+  if (hipblaslt_ext::getAllAlgos(c.h, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, op_of(ta), op_of(tb), HIP_R_16BF,
+                                 HIP_R_16BF, out_f32 ? HIP_R_32F : HIP_R_16BF, out_f32 ? HIP_R_32F : HIP_R_16BF,
+                                 HIPBLAS_COMPUTE_32F, all) != HIPBLAS_STATUS_SUCCESS)
+    return 4;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  auto time_it = [&](hipblasLtMatmulAlgo_t& algo, int reps) -> float {
+    if (run(c, p, algo, A, B, C, beta, stream)) return 1e30f;  // warm-up / launch check
+    (void)hipEventRecord(e0, stream);
+    for (int i = 0; i < reps; ++i) run(c, p, algo, A, B, C, beta, stream);
+    (void)hipEventRecord(e1, stream);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / reps;
+  };
+  // the heuristic default, for the report
+  Plan dflt = p;
+  dflt.has_algo = false;
+  c.wanted.erase(key);
+  float dms = 1e30f;
+  if (resolve(c, key, dflt, beta) == 0) dms = time_it(dflt.algo, 10);
+  std::vector<std::pair<float, size_t>> first;
+  for (size_t i = 0; i < all.size(); ++i) {
+    if (!supported(c, p, all[i].algo, beta)) continue;
+    first.emplace_back(time_it(all[i].algo, 1), i);
+  }
+  std::sort(first.begin(), first.end());
+  float bms = dms;
+  int bidx = dflt.has_algo ? dflt.index : -1;
+  hipblasLtMatmulAlgo_t balgo = dflt.algo;
+  for (size_t j = 0; j < first.size() && j < 8; ++j) {
+    const float ms = time_it(all[first[j].second].algo, 10);
+    if (ms < bms) {
+      bms = ms;
+      balgo = all[first[j].second].algo;
+      bidx = hipblaslt_ext::getIndexFromAlgo(balgo);
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  p.algo = balgo;
+  p.has_algo = bidx >= 0;
+  p.index = bidx;
+  if (bidx >= 0) c.wanted[key] = bidx;
+  *best_index = bidx;
+  *best_ms = bms;
+  *default_ms = dms;
+  *n_timed = (int)first.size();
+  return 0;
+}

@@ -303,3 +303,30 @@ def test_accuracy_kernel(C):
     got = float(accuracy(lg.to(DEV, torch.bfloat16), lab.to(DEV)))
     ref_bf = float((lg.to(torch.bfloat16).float().argmax(-1) == lab).float().mean())
     assert abs(got - ref_bf) < 1e-6 and abs(ref_bf - ref) < 0.05
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 512, 384), (1000, 768, 1024)])
+def test_tuned_gemm_forms(M, K, N):
+    """ops/gemm.py's three hipBLASLt forms vs fp32 torch."""
+    _lib()
+    from tf_operator_amd.ops import gemm
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    assert rel(gemm.linear_fwd(x, w), x.float() @ w.float().t()) < 1e-2
+    assert rel(gemm.linear_dgrad(dy, w), dy.float() @ w.float()) < 1e-2
+    g0 = torch.randn(N, K, device=DEV, dtype=torch.float32)
+    g = g0.clone()
+    gemm.wgrad_acc_(g, dy, x)
+    assert rel(g, g0 + dy.float().t() @ x.float()) < 1e-2
+    gb = g0.to(torch.bfloat16)
+    gemm.wgrad_acc_(gb, dy, x)
+    assert rel(gb, g0 + dy.float().t() @ x.float()) < 2e-2
+    # tuning a small form runs and installs a solution
+    key = (1, 0, N, M, K, K, K, N, 0)
+    idx, best, dflt, n = gemm.tune_form(key)
+    assert n > 0 and best <= dflt * 1.05
+    assert gemm.current_algo(key) == idx
+    assert rel(gemm.linear_fwd(x, w), x.float() @ w.float().t()) < 1e-2

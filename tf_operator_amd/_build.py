@@ -77,7 +77,8 @@ def build_hip(force=False, verbose=False):
             if verbose and out.strip():
                 print(out)
     if force or todo or _stale(HIP_LIB, objs):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", HIP_LIB] + objs)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", HIP_LIB] + objs +
+             ["-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"])
     return HIP_LIB
 
 

@@ -60,6 +60,11 @@ _SIGS = {
     "toa_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_f, c_p],
     "toa_allreduce_oneshot": [c_p, c_p, c_int, c_int, c_i64, c_int, c_p],
+    "toa_gemm": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p],
+    "toa_gemm_set_algo": [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int],
+    "toa_gemm_current_algo": [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int],
+    "toa_gemm_tune": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p, c_p, c_p,
+                      c_p, c_p],
 }
 
 
@@ -113,6 +118,11 @@ def call(name: str, *args):
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")
     return rc
+
+
+def call_ret(name: str, *args) -> int:
+    """Invoke `name` and return its int result (no error check)."""
+    return getattr(lib(), name)(*args)
 
 
 def stream(t: torch.Tensor | None = None):

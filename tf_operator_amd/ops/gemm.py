@@ -1,0 +1,143 @@
+"""Row-major bf16 GEMM entry points of the training step, on the tuned
+hipBLASLt layer (csrc/hip/gemm.hip).
+
+    linear_fwd(x, w)           y  = x w^T            [M,K] x [N,K] -> [M,N]
+    linear_dgrad(dy, w)        dx = dy w             [M,N] x [N,K] -> [M,K]
+    wgrad_acc_(g, dy, x)       g += dy^T x           (beta = 1, in place)
+
+Each maps to one column-major hipBLASLt call (see gemm.hip for the
+transposition algebra).  The per-form solution table measured by
+``scripts/tune_gemm.py`` on an MI355X is stored next to this file
+(``gemm_tuning_gfx950.json``, keyed by the hipBLASLt build it was measured
+with) and installed once per process; untuned forms use the library
+heuristic.  ``TOA_GEMM=torch`` routes everything through torch.matmul.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+
+import torch
+
+from . import _lib
+
+TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning_gfx950.json")
+_MODE = os.environ.get("TOA_GEMM", "auto")
+_installed = False
+
+
+def hipblaslt_build() -> str:
+    """Identity of the hipBLASLt library solution indices belong to."""
+    for d in ("/opt/rocm/lib", os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")):
+        p = os.path.join(d, "libhipblaslt.so")
+        if os.path.exists(p):
+            return os.path.basename(os.path.realpath(p))
+    return "unknown"
+
+
+def _install():
+    global _installed
+    if _installed:
+        return
+    _installed = True
+    if not os.path.exists(TABLE):
+        return
+    with open(TABLE) as f:
+        tab = json.load(f)
+    if tab.get("hipblaslt") != hipblaslt_build():
+        return
+    for e in tab.get("entries", []):
+        if e.get("index", -1) >= 0:
+            _lib.call("toa_gemm_set_algo", e["ta"], e["tb"], e["m"], e["n"], e["k"], e["lda"], e["ldb"], e["ldc"],
+                      e["beta_nz"], e.get("out_f32", 0), e["index"])
+
+
+def _ok(*ts):
+    if _MODE == "torch" or not _lib.has("toa_gemm"):
+        return False
+    for t in ts:
+        if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
+            return False
+    return _lib.use_hip(ts[0])
+
+
+def _gemm(ta, tb, m, n, k, a, lda, b, ldb, c, ldc, beta):
+    _install()
+    _lib.call("toa_gemm", ta, tb, m, n, k, _lib.ptr(a), lda, _lib.ptr(b), ldb, _lib.ptr(c), ldc, float(beta),
+              int(c.dtype == torch.float32), _lib.stream(c))
+
+
+def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if not _ok(x2, w):
+        return torch.matmul(x2, w.t())
+    M, K = x2.shape
+    N = w.shape[0]
+    y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
+    _gemm(1, 0, N, M, K, w, w.stride(0), x2, x2.stride(0), y, N, 0.0)
+    return y
+
+
+def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if not _ok(dy2, w):
+        return torch.matmul(dy2, w)
+    M, N = dy2.shape
+    K = w.shape[1]
+    dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
+    _gemm(0, 0, K, M, N, w, w.stride(0), dy2, dy2.stride(0), dx, K, 0.0)
+    return dx
+
+
+def wgrad_acc_(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float = 1.0):
+    """g[N,K] = beta*g + dy2[M,N]^T @ x2[M,K]  (in place; g bf16 or fp32)."""
+    if not (_ok(dy2, x2) and g.is_contiguous() and g.dtype in (torch.bfloat16, torch.float32)):
+        if beta == 0.0:
+            g.copy_(torch.mm(dy2.t(), x2))
+        elif g.dtype == dy2.dtype:
+            g.addmm_(dy2.t(), x2)
+        else:
+            g.add_(torch.mm(dy2.t(), x2).to(g.dtype))
+        return g
+    M, N = dy2.shape
+    K = x2.shape[1]
+    _gemm(0, 1, K, N, M, x2, x2.stride(0), dy2, dy2.stride(0), g, K, beta)
+    return g
+
+
+def form_keys(T: int, shapes: dict) -> list:
+    """The (ta, tb, m, n, k, lda, ldb, ldc, beta_nz) forms of linear layers
+    `shapes` = {name: (K, N)} at T tokens (forward, dgrad, wgrad)."""
+    out = []
+    for name, (K, N) in shapes.items():
+        out.append((name, "fwd", (1, 0, N, T, K, K, K, N, 0)))
+        out.append((name, "dgrad", (0, 0, K, T, N, K, N, K, 0)))
+        out.append((name, "wgrad", (0, 1, K, N, T, K, N, K, 1)))
+    return out
+
+
+def current_algo(key) -> int:
+    return _lib.call_ret("toa_gemm_current_algo", *key, 0) if _lib.has("toa_gemm_current_algo") else -1
+
+
+def tune_form(key, device="cuda"):
+    """Time all hipBLASLt solutions for one form on scratch buffers."""
+    ta, tb, m, n, k, lda, ldb, ldc, beta_nz = key
+    a_rows, a_cols = (m, k) if not ta else (k, m)   # column-major op(A) source dims
+    b_rows, b_cols = (k, n) if not tb else (n, k)
+    # column-major X (rows x cols, ld) == row-major tensor [cols, ld]
+    A = torch.randn(a_cols, lda, device=device, dtype=torch.bfloat16)
+    B = torch.randn(b_cols, ldb, device=device, dtype=torch.bfloat16)
+    C = torch.zeros(n, ldc, device=device, dtype=torch.bfloat16)
+    del a_rows, b_rows
+    bi, bms, dms, nt = ctypes.c_int(-1), ctypes.c_float(0), ctypes.c_float(0), ctypes.c_int(0)
+    rc = _lib.call_ret("toa_gemm_tune", ta, tb, m, n, k, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc,
+                       float(beta_nz), 0, _lib.stream(C), ctypes.byref(bi), ctypes.byref(bms), ctypes.byref(dms),
+                       ctypes.byref(nt))
+    if rc != 0:
+        raise RuntimeError(f"toa_gemm_tune failed ({rc}) for {key}")
+    return bi.value, bms.value, dms.value, nt.value
+
+
+def save_table(entries: list, path: str = TABLE):
+    with open(path, "w") as f:
+        json.dump({"hipblaslt": hipblaslt_build(), "arch": "gfx950", "entries": entries}, f, indent=1)

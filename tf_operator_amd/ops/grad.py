@@ -37,7 +37,11 @@ def accumulate_mm(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
     if mg is None:
         return torch.mm(a, b).to(param.dtype).view_as(param)
     mg2 = mg.view(a.shape[0], b.shape[1])
-    if mg2.dtype == a.dtype:
+    if a.dim() == 2 and a.stride(0) == 1 and a.t().is_contiguous():
+        from . import gemm  # a = dy^T view: the tuned wgrad form
+
+        gemm.wgrad_acc_(mg2, a.t(), b)
+    elif mg2.dtype == a.dtype:
         mg2.addmm_(a, b)
     else:
         mg2.add_(torch.mm(a, b).to(mg2.dtype))

@@ -14,6 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import gemm
 from .grad import accumulate_mm
 
 
@@ -133,7 +134,7 @@ class _SwiGLUDown(torch.autograd.Function):
     def forward(ctx, gu, wd):
         s = swiglu(gu)
         ctx.save_for_backward(gu, wd)
-        return torch.matmul(s, wd.t())
+        return gemm.linear_fwd(s.reshape(-1, s.shape[-1]), wd).view(*s.shape[:-1], wd.shape[0])
 
     @staticmethod
     def backward(ctx, dout):
@@ -141,7 +142,7 @@ class _SwiGLUDown(torch.autograd.Function):
         s = swiglu(gu)
         d2 = dout.reshape(-1, dout.shape[-1])
         dw = accumulate_mm(wd, d2.t(), s.reshape(-1, s.shape[-1]))
-        ds = torch.matmul(dout, wd)
+        ds = gemm.linear_dgrad(d2, wd).view(*dout.shape[:-1], wd.shape[1])
         del s
         dgu = swiglu_bwd(ds, gu)
         return dgu, dw
