@@ -145,9 +145,20 @@ class LocalKubelet:
             if isinstance(v, str):
                 for m in SVC_RE.finditer(v):
                     emap[m.group(0)] = f"127.0.0.1:{self.service_port(m.group(3), m.group(1))}"
-        if emap:
-            import json as _json
+        # bare service names with a separate port: MX_CONFIG urls, XGBoost WORKER_ADDRS
+        import json as _json
 
+        if env.get("MX_CONFIG"):
+            try:
+                for ups in (_json.loads(env["MX_CONFIG"]).get("cluster") or {}).values():
+                    for u in ups:
+                        emap[f"{u['url']}:{u['port']}"] = f"127.0.0.1:{self.service_port(ns, u['url'])}"
+            except (ValueError, KeyError, TypeError):
+                pass
+        if env.get("WORKER_ADDRS"):
+            for w in env["WORKER_ADDRS"].split(","):
+                emap[f"{w}:{env.get('WORKER_PORT', '')}"] = f"127.0.0.1:{self.service_port(ns, w)}"
+        if emap:
             out["TOA_ENDPOINT_MAP"] = _json.dumps(emap, separators=(",", ":"))
 
         def host_to_port(host):
