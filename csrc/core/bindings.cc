@@ -39,6 +39,9 @@ PYBIND11_MODULE(_toa_core, m) {
   m.def("set_defaults", [](const std::string& job) { return set_defaults(J(job)).dump(); });
   m.def("validate", [](const std::string& job) { return validate(J(job)); });
   m.def("on_job_created", [](const std::string& job, double now) { return on_job_created(J(job), now).dump(); });
+  m.def("claim_objects", [](const std::string& job, const std::string& objs) {
+    return claim_objects(set_defaults(J(job)), J(objs)).dump();
+  });
   m.def(
       "reconcile",
       [](const std::string& job, const std::string& pods, const std::string& services, double now,

@@ -193,4 +193,8 @@ Json on_job_created(const Json& job, double now);  // defaults + Created conditi
 //   "expect": [{"key":..., "add":n}], "skipped": reason|null }
 Json reconcile(const Json& job, const Json& pods, const Json& services, double now, const Options& opt);
 
+// ControllerRef claiming (claim.cc): {claimed: [objs, adopted ones with our
+// controllerRef added], adopt: [names], release: [names], owner_reference}
+Json claim_objects(const Json& job, const Json& objs);
+
 }  // namespace toa

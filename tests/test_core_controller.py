@@ -454,3 +454,38 @@ def test_expectations():
     assert e.satisfied(key, NOW + 301)  # TTL expiry
     e.delete_key(key)
     assert not e.exists(key)
+
+
+# ---------------------------------------------------------------------------
+# ControllerRef claiming (client-go ClaimObject via GetPodsForJob,
+# tfjob_controller.go:251-289)
+# ---------------------------------------------------------------------------
+def test_claim_adopts_orphans_keeps_own_releases_mismatch_ignores_foreign():
+    job = fx.new_tfjob(3, 0)
+    own = fx.new_pod(job, "worker", 0)
+    orphan = fx.new_pod(job, "worker", 1)
+    orphan["metadata"].pop("ownerReferences", None)
+    foreign = fx.new_pod(job, "worker", 2)
+    foreign["metadata"]["ownerReferences"] = [{"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "name": "other",
+                                               "uid": "someone-else", "controller": True}]
+    drifted = fx.new_pod(job, "worker", 3, name="drifted")
+    drifted["metadata"]["labels"]["job-name"] = "not-this-job"
+    deleting_orphan = fx.new_pod(job, "worker", 4, name="going")
+    deleting_orphan["metadata"].pop("ownerReferences", None)
+    deleting_orphan["metadata"]["deletionTimestamp"] = "2024-01-01T00:00:00Z"
+    res = core.claim_objects(job, [own, orphan, foreign, drifted, deleting_orphan])
+    names = [o["metadata"]["name"] for o in res["claimed"]]
+    assert names == [own["metadata"]["name"], orphan["metadata"]["name"]]
+    assert res["adopt"] == [orphan["metadata"]["name"]]
+    assert res["release"] == ["drifted"]
+    adopted = res["claimed"][1]["metadata"]["ownerReferences"][-1]
+    assert adopted["uid"] == job["metadata"]["uid"] and adopted["controller"] is True
+
+
+def test_claim_nothing_adopted_while_job_deleting():
+    job = fx.new_tfjob(1, 0)
+    job["metadata"]["deletionTimestamp"] = "2024-01-01T00:00:00Z"
+    orphan = fx.new_pod(job, "worker", 0)
+    orphan["metadata"].pop("ownerReferences", None)
+    res = core.claim_objects(job, [orphan])
+    assert res["claimed"] == [] and res["adopt"] == []

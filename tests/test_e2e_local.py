@@ -267,3 +267,27 @@ def test_pytorchjob_e2e(cluster):
     c.create(job)
     done = c.wait_for_job("pt", polling_interval=POLL, timeout_seconds=60)
     assert conditions(done)[-1] == "Succeeded", done["status"]
+
+
+def test_orphan_pod_is_adopted_not_duplicated(cluster):
+    """ControllerRef adoption: a matching orphan pod created before its job is
+    claimed (ownerReference patched in) instead of a second pod being made."""
+    c = cluster.client
+    name = "adopt"
+    orphan = {"apiVersion": "v1", "kind": "Pod",
+              "metadata": {"name": f"{name}-worker-0", "namespace": "default",
+                           "labels": {"group-name": "kubeflow.org", "job-name": name, "replica-type": "worker",
+                                      "replica-index": "0"}},
+              "spec": {"restartPolicy": "Never",
+                       "containers": [{"name": "tensorflow", "image": "x",
+                                       "command": [sys.executable, "-c", "import time; time.sleep(1.5)"]}]}}
+    cluster.run(cluster.kube_kubelet.create("pods", "default", orphan))
+    job = tfjob(name, {"Worker": replica(1, sh("import time; time.sleep(1.5)"))})
+    c.create(job)
+    uid = cluster.api.get("kubeflow.org/tfjobs", "default", name)["metadata"]["uid"]
+    cluster.wait(lambda: any(r.get("uid") == uid for r in (cluster.api.get("pods", "default", f"{name}-worker-0") or {})
+                             .get("metadata", {}).get("ownerReferences") or []), 15, what="adoption")
+    done = c.wait_for_job(name, polling_interval=POLL, timeout_seconds=60)
+    assert conditions(done)[-1] == "Succeeded"
+    assert sum(1 for k in cluster.kubelet.start_times if k[1] == f"{name}-worker-0") == 1
+    c.delete(name)

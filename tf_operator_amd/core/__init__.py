@@ -62,6 +62,11 @@ def on_job_created(job: dict, now=None) -> dict:
     return json.loads(native().on_job_created(_d(job), _now(now)))
 
 
+def claim_objects(job: dict, objs) -> dict:
+    """ControllerRef claim (adopt orphans / release mismatches): see csrc/core/claim.cc."""
+    return json.loads(native().claim_objects(_d(job), _d(list(objs))))
+
+
 def reconcile(job: dict, pods=(), services=(), now=None, options: dict | None = None) -> dict:
     return json.loads(native().reconcile(_d(job), _d(list(pods)), _d(list(services)), _now(now), _d(options or {})))
 

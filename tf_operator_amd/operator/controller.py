@@ -176,6 +176,41 @@ class JobController:
             o["nccl_env"] = env
         return o
 
+    async def _claim(self, job, res_key, ns, kind, objs):
+        """ControllerRef claim (C++ claim_objects): adopt orphans that match
+        the job's selector, release ours that no longer do; returns the
+        objects this job owns.  Adoption re-reads the job first, like
+        RecheckDeletionTimestamp (tfjob_controller.go:276-287)."""
+        res = core.claim_objects(job, objs)
+        if res["adopt"]:
+            try:
+                fresh = await self.kube.get(res_key, ns, job["metadata"]["name"])
+            except ApiError:
+                fresh = None
+            ok = (fresh is not None and fresh["metadata"].get("uid") == job["metadata"].get("uid")
+                  and not fresh["metadata"].get("deletionTimestamp"))
+            if not ok:
+                adopted = set(res["adopt"])
+                return [o for o in res["claimed"] if o["metadata"]["name"] not in adopted]
+            by_name = {o["metadata"]["name"]: o for o in res["claimed"]}
+            for name in res["adopt"]:
+                refs = by_name[name]["metadata"]["ownerReferences"]
+                try:
+                    await self.kube.patch(kind, ns, name, {"metadata": {"ownerReferences": refs}})
+                except ApiError as e:
+                    log.warning("adopting %s/%s %s failed: %s", kind, ns, name, e)
+        for name in res["release"]:
+            o = next((x for x in objs if x["metadata"]["name"] == name), None)
+            if o is None:
+                continue
+            refs = [r for r in o["metadata"].get("ownerReferences") or []
+                    if r.get("uid") != job["metadata"].get("uid")]
+            try:
+                await self.kube.patch(kind, ns, name, {"metadata": {"ownerReferences": refs}})
+            except ApiError as e:
+                log.warning("releasing %s/%s %s failed: %s", kind, ns, name, e)
+        return res["claimed"]
+
     async def _elastic_free_gpus(self, uid):
         """GPUs an elastic job may use: node allocatable minus what other
         operator-managed pods hold (this job's own pods count as free).
@@ -225,19 +260,9 @@ class JobController:
         if not dynamic and not self._satisfied(job, kind):
             return None
         uid = job["metadata"].get("uid")
-        sel = format_selector({"group-name": "kubeflow.org", "job-name": name.replace("/", "-")})
-
-        def owned(objs):
-            out = []
-            for o in objs:
-                ref = controller_ref(o)
-                if ref is None or ref.get("uid") == uid:
-                    out.append(o)
-            return out
-
-        pods = owned(self.pods.list(ns, {"group-name": "kubeflow.org", "job-name": name.replace("/", "-")}))
-        svcs = owned(self.services.list(ns, {"group-name": "kubeflow.org", "job-name": name.replace("/", "-")}))
-        del sel
+        lbl = {"group-name": "kubeflow.org", "job-name": name.replace("/", "-")}
+        pods = await self._claim(job, res_key, ns, "pods", self.pods.list(ns, lbl))
+        svcs = await self._claim(job, res_key, ns, "services", self.services.list(ns, lbl))
         opts = self._options(key)
         if job.get("spec", {}).get("elasticPolicy"):
             free = await self._elastic_free_gpus(uid)
