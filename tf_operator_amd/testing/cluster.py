@@ -175,3 +175,50 @@ class LocalCluster:
 
     def metrics_text(self):
         return self.metrics.expose().decode()
+
+
+def main(argv=None):
+    """Run a single-node cluster in the foreground (the `kind` replacement of
+    BASELINE config #1): fake API server + operator + local kubelet.
+
+        python -m tf_operator_amd.testing.cluster --gpus 8 --apply manifests/examples/tfjob-dist-mnist.yaml --wait
+    """
+    import argparse
+
+    import yaml
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=0)
+    ap.add_argument("--gang", action="store_true", help="--enable-gang-scheduling")
+    ap.add_argument("--apply", action="append", default=[], help="job YAML to submit (repeatable)")
+    ap.add_argument("--wait", action="store_true", help="exit when every applied job finished")
+    ap.add_argument("--timeout", type=float, default=3600)
+    a = ap.parse_args(argv)
+    with LocalCluster(gpus=a.gpus, enable_gang_scheduling=a.gang) as c:
+        print(f"API server: {c.url}   metrics: {c.metrics_url}", flush=True)
+        names = []
+        for path in a.apply:
+            for doc in yaml.safe_load_all(open(path)):
+                if not doc:
+                    continue
+                c.sdk(doc["kind"]).create(doc)
+                names.append((doc["kind"], doc["metadata"]["name"]))
+                print(f"submitted {doc['kind']} {doc['metadata']['name']}", flush=True)
+        if a.wait and names:
+            rc = 0
+            for kind, name in names:
+                job = c.sdk(kind).wait_for_job(name, polling_interval=1, timeout_seconds=a.timeout)
+                conds = [x["type"] for x in (job.get("status") or {}).get("conditions") or []
+                         if x.get("status") == "True"]
+                print(f"{kind} {name}: {conds[-1] if conds else 'unknown'}", flush=True)
+                rc |= int("Succeeded" not in conds)
+            return rc
+        try:
+            while True:
+                time.sleep(3600)
+        except KeyboardInterrupt:
+            return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
