@@ -93,6 +93,13 @@ __device__ __forceinline__ float xhalf_sum(float v) {
   return a + b;
 }
 
+// Offset of row (b, h, s) of O / dO: [B, H, S, D] (head-major, like Q) or, with
+// bshd, [B, S, H, D] -- the layout the output projection consumes, so the
+// model needs no transpose copy of O forward or of dO backward.
+__device__ __forceinline__ int64_t o_off(int b, int h, int s, int H, int S, int bshd) {
+  return bshd ? (((int64_t)b * S + s) * H + h) * 128 : (((int64_t)b * H + h) * S + s) * 128;
+}
+
 // XCD-aware block order: the hardware deals workgroups to the 8 XCDs round
 // robin, so give every XCD whole (batch, kv-head) groups -- their K/V stay
 // in that XCD's L2 across the GQA heads and query blocks -- and walk each
@@ -120,7 +127,7 @@ template <int D>
 __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int H, int Hk, int S,
-                                                          float scale_log2) {
+                                                          float scale_log2, int o_bshd) {
   static_assert(D == 128, "D=128 path");
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16KB + V 16KB)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -293,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
   // ---- epilogue: O = O^T / l  (lane owns query row myq; d rows from the C map)
   const float l_tot = xhalf_sum(l_run);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  bf16_t* orow = O + qoff + (int64_t)myq * D;
+  bf16_t* orow = O + o_off(b, h, myq, H, S, o_bshd);
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -311,15 +318,18 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
 // backward preprocess: delta[b,h,q] = sum_d dO * O
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                                                           float* __restrict__ delta, int64_t rows, int D) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                           float* __restrict__ delta, int64_t rows, int D, int H,
+                                                           int S, int o_bshd) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // delta row, [B, H, S] order
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
+  const int s_ = (int)(row % S), h_ = (int)((row / S) % H), b_ = (int)(row / ((int64_t)S * H));
+  const int64_t base = o_off(b_, h_, s_, H, S, o_bshd);
   float acc = 0.f;
   for (int c = lane; c < D / 8; c += 64) {
     float a[8], g[8];
-    unpack8(ld16(O + row * D + c * 8), a);
-    unpack8(ld16(dO + row * D + c * 8), g);
+    unpack8(ld16(O + base + c * 8), a);
+    unpack8(ld16(dO + base + c * 8), g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc = fmaf(a[j], g[j], acc);
   }
@@ -379,7 +389,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int H, int Hk, int S, float scale,
-    float scale_log2) {
+    float scale_log2, int o_bshd) {
   // [Q/dO/lse/-delta buffer 0][buffer 1][K 32K][V 32K]
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* kimg = smem + 2 * DKV_QBUF;
@@ -441,7 +451,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
       const int row = e >> 4, c = e & 15;
       const int64_t g = qoff + (int64_t)(qt * 64 + row) * 128 + c * 8;
       sq[i] = ld16(Q + g);
-      sdo[i] = ld16(dO + g);
+      sdo[i] = ld16(dO + o_off(b, hq, qt * 64 + row, H, S, o_bshd) + c * 8);
     }
     if (tid < 64) {
       const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + tid;
@@ -596,7 +606,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
 __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16_t* __restrict__ dQ, int B, int H, int Hk, int S, float scale, float scale_log2) {
+    bf16_t* __restrict__ dQ, int B, int H, int Hk, int S, float scale, float scale_log2, int o_bshd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16K + V 16K)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -617,7 +627,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
     qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh)) : bf16x8{};
-    of[s] = live ? as_bf16x8(ld16(dO + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh)) : bf16x8{};
+    of[s] = live ? as_bf16x8(ld16(dO + o_off(b, h, myq, H, S, o_bshd) + 16 * s + 8 * hh)) : bf16x8{};
   }
   const float lse2 = live ? LSE[(int64_t)(b * H + h) * S + myq] * LOG2E : 0.f;
   const float del = live ? DELTA[(int64_t)(b * H + h) * S + myq] : 0.f;
@@ -748,29 +758,32 @@ static void attn_set_lds_limits() {
   done = true;
 }
 
+// flags: bit 0 causal (required), bit 1 O / dO in [B, S, H, D] (else [B, H, S, D]).
 extern "C" int toa_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int H,
-                            int Hk, int S, int D, int causal, float scale, hipStream_t stream) {
-  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !causal) return (int)hipErrorInvalidValue;
+                            int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
+  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !(flags & 1)) return (int)hipErrorInvalidValue;
+  const int o_bshd = (flags >> 1) & 1;
   attn_set_lds_limits();
   const int nqb = (S + FWD_QB - 1) / FWD_QB;
   hipLaunchKernelGGL(attn_fwd_kernel<128>, dim3(nqb * H * B), dim3(64 * FWD_WAVES), 65536, stream, q, k, v, o, lse,
-                     B, H, Hk, S, scale * LOG2E);
+                     B, H, Hk, S, scale * LOG2E, o_bshd);
   return (int)hipGetLastError();
 }
 
 // dq_acc is unused (kept in the ABI for an atomic-dQ variant); dq/dk/dv bf16.
 extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                             const float* lse, float* delta, float* dq_acc, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B,
-                            int H, int Hk, int S, int D, int causal, float scale, hipStream_t stream) {
+                            int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
   (void)dq_acc;
-  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !causal) return (int)hipErrorInvalidValue;
+  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !(flags & 1)) return (int)hipErrorInvalidValue;
+  const int o_bshd = (flags >> 1) & 1;
   attn_set_lds_limits();
   const int64_t rows = (int64_t)B * H * S;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, o, dout, delta,
-                     rows, D);
+                     rows, D, H, S, o_bshd);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S / 128) * B * Hk), dim3(512), DKV_LDS, stream, q, k, v, dout, lse,
-                     delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E);
+                     delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES), 65536,
-                     stream, q, k, v, dout, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E);
+                     stream, q, k, v, dout, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
   return (int)hipGetLastError();
 }

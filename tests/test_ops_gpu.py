@@ -311,6 +311,7 @@ def test_tuned_gemm_forms(M, K, N):
     _lib()
     from tf_operator_amd.ops import gemm
 
+    gemm._MODE = "tuned"  # exercise the native layer (default routes to torch.matmul)
     torch.manual_seed(0)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
@@ -330,3 +331,27 @@ def test_tuned_gemm_forms(M, K, N):
     assert n > 0 and best <= dflt * 1.05
     assert gemm.current_algo(key) == idx
     assert rel(gemm.linear_fwd(x, w), x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,Hk,S", [(2, 4, 2, 384), (1, 8, 2, 1024)])
+def test_flash_attention_bshd_output_layout(B, H, Hk, S):
+    """O written / dO read as [B, S, H, D] (no transpose copies in the model)
+    matches the head-major path exactly."""
+    _lib()
+    from tf_operator_amd.ops import llm
+
+    torch.manual_seed(11)
+    D = 128
+    scale = 1.0 / math.sqrt(D)
+    base = [torch.randn(B, h, S, D, device=DEV, dtype=torch.bfloat16) for h in (H, Hk, Hk)]
+    q1, k1, v1 = [t.clone().requires_grad_() for t in base]
+    q2, k2, v2 = [t.clone().requires_grad_() for t in base]
+    o1 = llm._FlashAttn.apply(q1, k1, v1, scale, False)
+    o2 = llm._FlashAttn.apply(q2, k2, v2, scale, True)
+    assert o2.shape == (B, S, H, D)
+    assert torch.equal(o1.transpose(1, 2), o2)
+    do = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    o1.backward(do.transpose(1, 2))
+    o2.backward(do)
+    for a, b in ((q1, q2), (k1, k2), (v1, v2)):
+        assert torch.equal(a.grad, b.grad)

@@ -100,8 +100,8 @@ class LlamaBlock(torch.nn.Module):
         if cfg.kv_layout == "packed" or (cfg.kv_layout == "auto" and _packed_kv_ok(qkv)):
             rep = 1
         q, k, v = rope_qkv(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim, rep)
-        o = causal_attention(q, k, v)
-        o = o.transpose(1, 2).reshape(B * S, cfg.heads * cfg.head_dim)
+        o = causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]: no transpose copy
+        o = o.reshape(B * S, cfg.heads * cfg.head_dim)
         a = linear(o, self.wo)
         h, x = self.mlp_norm(h, a)
         gu = linear(x, self.wgu)

@@ -10,7 +10,14 @@ transposition algebra).  The per-form solution table measured by
 ``scripts/tune_gemm.py`` on an MI355X is stored next to this file
 (``gemm_tuning_gfx950.json``, keyed by the hipBLASLt build it was measured
 with) and installed once per process; untuned forms use the library
-heuristic.  ``TOA_GEMM=torch`` routes everything through torch.matmul.
+heuristic.
+
+Default: OFF (``TOA_GEMM=torch``).  Measured on the MI355X (profiles/
+r1_gemm_tuning*.log, r1_gemm_ab_*.log): the per-form winners are 2-22 %
+faster in isolation, hot or cold cache, yet the full Llama-3-8B step is
+~1.3 % SLOWER with them (787.8 vs 777.1 ms, same box, back to back) -- a
+solution picked alone is not the best one in the sustained, power-limited
+sequence of the real step.  ``TOA_GEMM=tuned`` opts in.
 """
 from __future__ import annotations
 
@@ -23,7 +30,7 @@ import torch
 from . import _lib
 
 TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning_gfx950.json")
-_MODE = os.environ.get("TOA_GEMM", "auto")
+_MODE = os.environ.get("TOA_GEMM", "torch")
 _installed = False
 
 
@@ -54,7 +61,7 @@ def _install():
 
 
 def _ok(*ts):
-    if _MODE == "torch" or not _lib.has("toa_gemm"):
+    if _MODE not in ("tuned", "auto") or not _lib.has("toa_gemm"):
         return False
     for t in ts:
         if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):

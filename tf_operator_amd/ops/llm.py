@@ -219,16 +219,20 @@ def _attn_hip_ok(q):
 
 
 class _FlashAttn(torch.autograd.Function):
+    """HIP flash attention.  bshd=True returns O as [B, S, H, D] (what the
+    output projection reads) and takes dO in that layout: no transpose copies."""
+
     @staticmethod
-    def forward(ctx, q, k, v, scale):
+    def forward(ctx, q, k, v, scale, bshd=False):
         B, H, S, D = q.shape
         Hk = k.shape[1]
-        o = torch.empty_like(q)
+        o = torch.empty(B, S, H, D, device=q.device, dtype=q.dtype) if bshd else torch.empty_like(q)
         lse = torch.empty(B, H, S, device=q.device, dtype=torch.float32)
         _lib.call("toa_attn_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(lse), B, H, Hk, S, D,
-                  1, float(scale), _lib.stream(q))
+                  1 | (2 if bshd else 0), float(scale), _lib.stream(q))
         ctx.save_for_backward(q, k, v, o, lse)
         ctx.scale = scale
+        ctx.bshd = bshd
         return o
 
     @staticmethod
@@ -242,21 +246,23 @@ class _FlashAttn(torch.autograd.Function):
         dv = torch.empty_like(v)
         delta = torch.empty(B, H, S, device=q.device, dtype=torch.float32)
         _lib.call("toa_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do), _lib.ptr(lse),
-                  _lib.ptr(delta), None, _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D, 1,
-                  float(ctx.scale), _lib.stream(q))
-        return dq, dk, dv, None
+                  _lib.ptr(delta), None, _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D,
+                  1 | (2 if ctx.bshd else 0), float(ctx.scale), _lib.stream(q))
+        return dq, dk, dv, None, None
 
 
-def causal_attention(q, k, v, scale=None):
-    """q [B,H,S,D], k/v [B,Hk,S,D] (Hk == H unless the HIP kernel is used)."""
+def causal_attention(q, k, v, scale=None, out_layout="bhsd"):
+    """q [B,H,S,D], k/v [B,Hk,S,D] (Hk == H unless the HIP kernel is used).
+    Returns O as [B,H,S,D], or as [B,S,H,D] with out_layout="bshd"."""
     scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
     impl = _ATTN_IMPL
     if impl in ("auto", "hip") and _attn_hip_ok(q) and q.shape[2] % 128 == 0:
-        return _FlashAttn.apply(q.contiguous(), k.contiguous(), v.contiguous(), scale)
+        return _FlashAttn.apply(q.contiguous(), k.contiguous(), v.contiguous(), scale, out_layout == "bshd")
     if impl == "hip" and q.is_cuda:
         raise RuntimeError("TOA_ATTN=hip but the HIP attention kernel is unavailable")
     if k.shape[1] != q.shape[1]:
         rep = q.shape[1] // k.shape[1]
         k = k.repeat_interleave(rep, 1)
         v = v.repeat_interleave(rep, 1)
-    return F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale)
+    o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale)
+    return o.transpose(1, 2) if out_layout == "bshd" else o
