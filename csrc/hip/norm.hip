@@ -226,12 +226,32 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
 }
 
 // out[c] (+)= sum_b partial[b][c]; out dtype bf16 (out_bf16=1) or fp32.
-__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ partial, int nb, int cols,
+// One 512-thread workgroup per 64-column strip: wave w sums partial rows
+// b = w (mod 8) with 4 independent accumulators (coalesced 256-B rows), then
+// the 8 wave sums meet in LDS in a fixed order (deterministic).  The old
+// one-thread-per-column loop ran 16 workgroups on 256 CUs, latency-bound.
+__global__ __launch_bounds__(512) void col_reduce_kernel(const float* __restrict__ partial, int nb, int cols,
                                                          void* __restrict__ out, int out_bf16, int accumulate) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= cols) return;
+  __shared__ float red[8][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < cols) {
+    int b = wave;
+    for (; b + 24 < nb; b += 32) {
+      a0 += partial[(int64_t)b * cols + col];
+      a1 += partial[(int64_t)(b + 8) * cols + col];
+      a2 += partial[(int64_t)(b + 16) * cols + col];
+      a3 += partial[(int64_t)(b + 24) * cols + col];
+    }
+    for (; b < nb; b += 8) a0 += partial[(int64_t)b * cols + col];
+  }
+  red[wave][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wave != 0 || col >= cols) return;
   float t = 0.f;
-  for (int b = 0; b < nb; ++b) t += partial[(int64_t)b * cols + col];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) t += red[w][lane];
   if (out_bf16) {
     bf16_t* o = (bf16_t*)out;
     if (accumulate) t += bf2f(o[col]);
@@ -294,11 +314,11 @@ static int norm_bwd_launch(const void* dy, const void* h, const void* w, const f
   TOA_NORM_DISPATCH(chv, hipLaunchKernelGGL((norm_bwd_kernel<T, CH, RMS>), dim3(nb), dim3(256), lds, s,
                                             (const T*)dy, (const T*)h, (const T*)w, mean, rstd, (const T*)dadd,
                                             (T*)dx, partial, rows, cols));
-  dim3 rg((cols + 255) / 256);
+  dim3 rg((cols + 63) / 64);
   if (dw != nullptr)
-    hipLaunchKernelGGL(col_reduce_kernel, rg, dim3(256), 0, s, partial, nb, cols, dw, dw_bf16, accumulate);
+    hipLaunchKernelGGL(col_reduce_kernel, rg, dim3(512), 0, s, partial, nb, cols, dw, dw_bf16, accumulate);
   if (!RMS && db != nullptr)
-    hipLaunchKernelGGL(col_reduce_kernel, rg, dim3(256), 0, s, partial + (int64_t)nb * cols, nb, cols, db,
+    hipLaunchKernelGGL(col_reduce_kernel, rg, dim3(512), 0, s, partial + (int64_t)nb * cols, nb, cols, db,
                        db_bf16, accumulate);
   return (int)hipGetLastError();
 }

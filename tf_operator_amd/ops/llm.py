@@ -126,20 +126,27 @@ def swiglu_bwd(dout, gu):
     return torch.cat([dg, du], -1).to(gu.dtype)
 
 
+_SWIGLU_RECOMPUTE = os.environ.get("TOA_SWIGLU_RECOMPUTE", "0") == "1"
+
+
 class _SwiGLUDown(torch.autograd.Function):
-    """out = swiglu(gu) @ Wd^T, saving only gu (the [T, F] activation is
-    recomputed in backward: 1.5 GB/layer of HBM saved at Llama-3-8B x 16k tokens)."""
+    """out = swiglu(gu) @ Wd^T.  Saves gu and the [T, F] activation s for the
+    down-projection's weight gradient (470 MB/layer at Llama-3-8B x 16k
+    tokens, ~15 GB for 32 layers -- HBM has room at 288 GB); with
+    TOA_SWIGLU_RECOMPUTE=1 s is recomputed in backward instead (one extra
+    SwiGLU pass per layer, ~8 ms/step)."""
 
     @staticmethod
     def forward(ctx, gu, wd):
         s = swiglu(gu)
-        ctx.save_for_backward(gu, wd)
+        ctx.save_for_backward(gu, wd, None if _SWIGLU_RECOMPUTE else s)
         return gemm.linear_fwd(s.reshape(-1, s.shape[-1]), wd).view(*s.shape[:-1], wd.shape[0])
 
     @staticmethod
     def backward(ctx, dout):
-        gu, wd = ctx.saved_tensors
-        s = swiglu(gu)
+        gu, wd, s = ctx.saved_tensors
+        if s is None:
+            s = swiglu(gu)
         d2 = dout.reshape(-1, dout.shape[-1])
         dw = accumulate_mm(wd, d2.t(), s.reshape(-1, s.shape[-1]))
         ds = gemm.linear_dgrad(d2, wd).view(*dout.shape[:-1], wd.shape[1])
