@@ -605,8 +605,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16_t* __restrict__ dQ, int B, int H, int Hk, int S, float scale, float scale_log2, int o_bshd) {
+    const bf16_t* __restrict__ dO, const bf16_t* __restrict__ O, const float* __restrict__ LSE,
+    float* __restrict__ DELTA, bf16_t* __restrict__ dQ, int B, int H, int Hk, int S, float scale, float scale_log2,
+    int o_bshd) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16K + V 16K)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -630,7 +631,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     of[s] = live ? as_bf16x8(ld16(dO + o_off(b, h, myq, H, S, o_bshd) + 16 * s + 8 * hh)) : bf16x8{};
   }
   const float lse2 = live ? LSE[(int64_t)(b * H + h) * S + myq] * LOG2E : 0.f;
-  const float del = live ? DELTA[(int64_t)(b * H + h) * S + myq] : 0.f;
+  // delta = rowsum(dO * O), computed here (the lane already holds its half of
+  // the dO row) and published for the dK/dV kernel that runs next
+  float del = 0.f;
+  if (live) {
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      float a[8], g[8];
+      unpack8(ld16(O + o_off(b, h, myq, H, S, o_bshd) + 16 * s + 8 * hh), a);
+      unpack8(__builtin_bit_cast(u32x4, of[s]), g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part = fmaf(a[j], g[j], part);
+    }
+    del = xhalf_sum(part);
+    if (hh == 0) DELTA[(int64_t)(b * H + h) * S + myq] = del;
+  }
   f32x16 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -779,11 +795,11 @@ extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   const int o_bshd = (flags >> 1) & 1;
   attn_set_lds_limits();
   const int64_t rows = (int64_t)B * H * S;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, o, dout, delta,
-                     rows, D, H, S, o_bshd);
+  (void)rows;
+  // dQ first: it also computes delta = rowsum(dO * O), which dK/dV then reads
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES), 65536,
+                     stream, q, k, v, dout, o, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
   hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S / 128) * B * Hk), dim3(512), DKV_LDS, stream, q, k, v, dout, lse,
                      delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES), 65536,
-                     stream, q, k, v, dout, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
   return (int)hipGetLastError();
 }
