@@ -68,7 +68,11 @@ def one_run(c, i, a):
     c.client.wait_for_job(name, polling_interval=0.2, timeout_seconds=a.timeout)
     c.client.delete(name)
     c.wait(lambda: not c.pods(labels={"job-name": name}), 60, 0.05, "cleanup")
-    return {"total": t_first - t0, "to_pods": t_pods - t0, "to_spawn": t_spawn - t0, "spawn_to_first": t_first - t_spawn}
+    out = {"total": t_first - t0, "to_pods": t_pods - t0, "to_spawn": t_spawn - t0,
+           "spawn_to_first": t_first - t_spawn}
+    for k, v in (rep.get("phases") or {}).items():
+        out["phase:" + k] = v
+    return out
 
 
 def main():
@@ -100,7 +104,9 @@ def main():
            "p90": round(tot[min(len(tot) - 1, int(0.9 * len(tot)))], 4), "min": round(tot[0], 4),
            "max": round(tot[-1], 4), "repeats": len(runs), "n_gpus": a.workers * a.gpus_per_worker,
            "breakdown_p50": {"submit_to_pods_created": med("to_pods"), "submit_to_processes_spawned": med("to_spawn"),
-                             "spawn_to_first_step": med("spawn_to_first")},
+                             "spawn_to_first_step": med("spawn_to_first"),
+                             **{k[6:]: med(k) for k in runs[0] if k.startswith("phase:")
+                                and all(k in r for r in runs)}},
            "config": {"payload": a.payload, "model": a.model if a.payload == "llama" else a.payload,
                       "workers": a.workers, "ps": a.ps, "seq_len": a.seq_len, "micro_batch": a.micro_batch}}
     print(json.dumps(out))

@@ -29,6 +29,7 @@ def main(argv=None):
     rt = Runtime()
     rt.install_preemption_handler()
     info = rt.init_dist()
+    rt.mark("dist_init")
     with rt.guard():
         _train(a, rt, info)
 
@@ -36,10 +37,12 @@ def main(argv=None):
 def _train(a, rt, info):
     dev = pick_device() if info.backend != "gloo" else torch.device("cpu")
     tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr)
+    rt.mark("model_init")
     payload = ckpt.load_latest(rt.ckpt_dir)
     if payload is not None:
         load_trainer_state(tr, payload["state"])
         rt.log(f"resumed at step {tr.step_idx} (world {rt.world})")
+        rt.mark("checkpoint_load")
     batch = [tr.synthetic_batch(seed=100 + rt.rank)]
     t0, n0 = time.perf_counter(), tr.step_idx
     while tr.step_idx < a.steps:

@@ -34,6 +34,18 @@ def is_peer_failure(e: BaseException) -> bool:
     return isinstance(e, (RuntimeError, ConnectionError)) and any(m in str(e) for m in _PEER_MARKERS)
 
 
+def process_start_time() -> float | None:
+    """Wall-clock start of this process (Linux /proc), None if unknown."""
+    try:
+        with open("/proc/self/stat") as f:
+            ticks = int(f.read().rsplit(")", 1)[1].split()[19])
+        with open("/proc/stat") as f:
+            btime = next(int(l.split()[1]) for l in f if l.startswith("btime"))
+        return btime + ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, StopIteration, IndexError):
+        return None
+
+
 class Runtime:
     def __init__(self, backend=None):
         self.role = os.environ.get("TOA_ROLE") or os.environ.get("TOA_REPLICA_TYPE") or "worker"
@@ -45,6 +57,7 @@ class Runtime:
         self.preempted = threading.Event()
         self._first_reported = False
         self.t_start = time.time()
+        self.phases: dict[str, float] = {}
         self.info = None
         self.backend = backend
 
@@ -101,10 +114,21 @@ class Runtime:
         except Exception:
             pass  # reporting is best effort
 
+    def mark(self, phase: str):
+        """Record a start-up phase (for the submit -> first-step breakdown)."""
+        self.phases[phase] = time.time()
+
     def first_step_done(self):
         if not self._first_reported:
             self._first_reported = True
-            self.report(first_step_time=time.time())
+            now = time.time()
+            t0 = process_start_time() or self.t_start
+            marks = {"process_start": t0, "runtime": self.t_start, **self.phases, "first_step": now}
+            order = sorted(marks.items(), key=lambda kv: kv[1])
+            phases = {f"{a}->{b}": round(tb - ta, 4) for (a, ta), (b, tb) in zip(order, order[1:])}
+            if os.environ.get("TOA_LOG_PHASES", "1") == "1" and self.is_chief:
+                self.log("start-up phases (s): " + ", ".join(f"{k} {v}" for k, v in phases.items()))
+            self.report(first_step_time=now, phases=phases, process_start_time=t0)
 
     def log(self, *a):
         print(f"[{self.role} rank {self.rank}/{self.world}]", *a, flush=True)
