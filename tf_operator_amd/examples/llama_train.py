@@ -25,6 +25,7 @@ def main(argv=None):
     p.add_argument("--lr", type=float, default=1e-3)
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--step-sleep", type=float, default=0.0, help="testing: slow steps down")
+    p.add_argument("--report-every", type=int, default=0, help="report samples/sec to the operator every N steps")
     a = p.parse_args(argv)
     rt = Runtime()
     rt.install_preemption_handler()
@@ -51,8 +52,16 @@ def _train(a, rt, info):
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             rt.first_step_done()
+            t1 = time.perf_counter()
         if tr.step_idx % 5 == 0 or tr.step_idx == a.steps:
             rt.log(f"step {tr.step_idx} loss {float(loss):.4f}")
+        if a.report_every and (tr.step_idx - n0) % a.report_every == 0 and tr.step_idx > n0 + 1:
+            # throughput since the first step of this generation (excludes start-up)
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            el = time.perf_counter() - t1
+            rt.report(samples_per_sec=a.micro_batch * rt.world * (tr.step_idx - n0 - 1) / max(el, 1e-9),
+                      step=tr.step_idx, world=rt.world)
         if a.checkpoint_every and tr.step_idx % a.checkpoint_every == 0 and rt.is_chief:
             ckpt.save(rt.ckpt_dir, tr.step_idx, trainer_state(tr))
         if rt.preempted.is_set():
