@@ -291,3 +291,20 @@ def test_orphan_pod_is_adopted_not_duplicated(cluster):
     assert conditions(done)[-1] == "Succeeded"
     assert sum(1 for k in cluster.kubelet.start_times if k[1] == f"{name}-worker-0") == 1
     c.delete(name)
+
+
+def test_reconcile_span_log_is_structured(cluster, caplog):
+    """SURVEY 5 Tracing: one JSON span per reconcile (duration, actions, condition)."""
+    import logging
+
+    from tf_operator_amd.operator.main import JsonFormatter
+
+    with caplog.at_level(logging.INFO, logger="tf_operator_amd.reconcile"):
+        c = cluster.client
+        c.create(tfjob("spans", {"Worker": replica(1, sh("pass"))}))
+        c.wait_for_job("spans", polling_interval=POLL, timeout_seconds=30)
+    recs = [r for r in caplog.records if r.name == "tf_operator_amd.reconcile" and r.span["job"] == "default/spans"]
+    assert recs and any(r.span["actions"].get("create_pod") == 1 for r in recs)
+    line = json.loads(JsonFormatter().format(recs[0]))
+    assert line["msg"] == "reconcile" and line["duration_ms"] >= 0 and line["kind"] == "TFJob"
+    c.delete("spans")

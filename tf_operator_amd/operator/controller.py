@@ -30,6 +30,7 @@ from .kube import ApiError, KubeClient, plural_key
 from .metrics import OperatorMetrics
 
 log = logging.getLogger("tf_operator_amd.controller")
+span_log = logging.getLogger("tf_operator_amd.reconcile")
 
 KIND_PLURAL = {"TFJob": "tfjobs", "PyTorchJob": "pytorchjobs", "MXJob": "mxjobs", "XGBoostJob": "xgboostjobs"}
 PLURAL_KIND = {v: k for k, v in KIND_PLURAL.items()}
@@ -294,7 +295,18 @@ class JobController:
             self.metrics.restarted.labels(ns).inc(m["restarted"])
         if res.get("requeue_after") is not None:
             self.queue.add_after(key, max(0.05, float(res["requeue_after"])))
-        self.metrics.reconcile_seconds.labels(kind).observe(time.perf_counter() - t0)
+        dur = time.perf_counter() - t0
+        self.metrics.reconcile_seconds.labels(kind).observe(dur)
+        # one span per reconcile (SURVEY 5 "Tracing"): structured, JSON under --json-log-format
+        if span_log.isEnabledFor(logging.INFO):
+            ops = {}
+            for a in res.get("actions", []):
+                ops[a["op"]] = ops.get(a["op"], 0) + 1
+            conds = [c["type"] for c in (res.get("status") or {}).get("conditions") or [] if c.get("status") == "True"]
+            span_log.info("reconcile", extra={"span": {
+                "job": f"{ns}/{name}", "kind": kind, "duration_ms": round(dur * 1e3, 3), "actions": ops,
+                "condition": conds[-1] if conds else None, "requeue_after": res.get("requeue_after"),
+                "skipped": res.get("skipped")}})
         return res
 
     async def _execute(self, res, job, res_key):

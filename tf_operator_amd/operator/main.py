@@ -40,6 +40,9 @@ class JsonFormatter(logging.Formatter):
     def format(self, r):
         d = {"level": r.levelname.lower(), "msg": r.getMessage(), "time": self.formatTime(r, "%Y-%m-%dT%H:%M:%S"),
              "filename": f"{r.filename}:{r.lineno}", "logger": r.name}
+        span = getattr(r, "span", None)
+        if span is not None:
+            d.update(span)
         if r.exc_info:
             d["error"] = self.formatException(r.exc_info)
         return json.dumps(d)
@@ -84,6 +87,7 @@ def build_parser():
     p.add_argument("--nccl-env", action="append", default=[], help="K=V injected into trainer replicas")
     p.add_argument("--cluster-domain", default=os.environ.get("CUSTOM_CLUSTER_DOMAIN", ""))
     p.add_argument("--report-url", default=os.environ.get("TOA_OPERATOR_REPORT_URL"))
+    p.add_argument("--gpu-resource", default="amd.com/gpu", help="extended resource name of a GPU")
     p.add_argument("--config", default=None, help="optional YAML file with the same keys as the flags")
     return p
 
@@ -131,7 +135,8 @@ class Operator:
             namespace=args.namespace, threadiness=args.threadiness,
             enable_gang_scheduling=args.enable_gang_scheduling, gang_scheduler_name=args.gang_scheduler_name,
             inject_rocm_env=args.inject_rocm_env, cluster_domain=args.cluster_domain, nccl_env=nccl,
-            resync_period=_duration(str(args.resync_period)), report_url=args.report_url), self.metrics)
+            resync_period=_duration(str(args.resync_period)), report_url=args.report_url,
+            gpu_resource=args.gpu_resource), self.metrics)
         self.stop = asyncio.Event()
         self.ready = False
         self.runners = []
