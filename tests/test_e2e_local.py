@@ -82,7 +82,10 @@ def test_distributed_training_succeeds(cluster):
     c.create(job)
     done = c.wait_for_job("dist3", polling_interval=POLL, timeout_seconds=60)
     assert conditions(done)[-1] == "Succeeded", done["status"]
-    rs = done["status"]["replicaStatuses"]["Worker"]
+    # the terminal pass right after Succeeded folds still-active replicas into
+    # `succeeded` (ReconcileJobs terminal path); wait_for_job may return first
+    rs = cluster.wait(lambda: (lambda r: r if r["succeeded"] == 3 else None)(
+        c.get("dist3")["status"]["replicaStatuses"]["Worker"]), 10, what="final replica statuses")
     assert rs["succeeded"] == 3 and rs["active"] == 0
 
 
