@@ -1,0 +1,116 @@
+"""One-shot IPC all-reduce (csrc/hip/comm.hip) with 2 processes on the one
+GPU of the test box: handles exchanged over a gloo group, results vs the
+exact sum, 2-slot ring reuse over many calls, bf16 and fp32, odd sizes."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tf_operator_amd.parallel.ipc import IpcAllReduce
+
+        ar = IpcAllReduce(slot_bytes=4 << 20, timeout_ms=20000)
+        worst = 0.0
+        for it in range(24):
+            for n, dt in ((1000, torch.bfloat16), (262147, torch.float32), (1 << 20, torch.bfloat16)):
+                g = torch.Generator(device="cpu").manual_seed(1000 * it + n)
+                parts = [torch.randn(n, generator=g) for _ in range(world)]
+                t = parts[rank].to(dt).cuda()
+                ar(t)
+                want = sum(p.to(dt).float() for p in parts)
+                worst = max(worst, float((t.float().cpu() - want).abs().max() / (want.abs().max() + 1e-6)))
+        torch.cuda.synchronize()
+        ar.check()
+        ar.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, worst, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.timeout(240)
+def test_ipc_oneshot_allreduce_two_processes():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, worst, err in res:
+        assert err is None, (rank, err)
+        assert worst < 1e-2, (rank, worst)
+
+
+def _dp_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TOA_IPC_ALLREDUCE="1",
+                      LOCAL_WORLD_SIZE=str(world))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tf_operator_amd.models.vision import MnistMLP
+        from tf_operator_amd.ops.llm import cross_entropy
+        from tf_operator_amd.train import simple
+        from tf_operator_amd.train.data import SyntheticMNIST
+        from tf_operator_amd.train.runtime import Runtime
+
+        torch.manual_seed(0)
+        model = MnistMLP(100, dtype=torch.float32, device="cuda")
+        rt = Runtime()
+        rt.info = type("I", (), {"rank": rank, "world": world})()
+        tr = simple.DPTrainer(model, lambda o, y: cross_entropy(o, y), rt, lr=1e-3)
+        assert tr.bucketer.ipc is not None
+        data = SyntheticMNIST(100, rank, world, device="cuda")
+        for _ in range(20):
+            tr.step(*data.next())
+        torch.cuda.synchronize()
+        tr.bucketer.ipc.check()
+        flat = tr.flat.param.detach().float().cpu()
+        out = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(out, flat)
+        q.put((rank, bool(torch.equal(out[0], out[1])), None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.timeout(240)
+def test_dp_trainer_over_ipc_allreduce():
+    """GradBucketer routes a small model's buckets through the one-shot IPC
+    path; the replicas stay identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, same, err in res:
+        assert err is None, (rank, err)
+        assert same, rank

@@ -54,6 +54,15 @@ class GradBucketer:
         self.pending = [b[2] for b in self.buckets]
         self.works = []
         self.launched = [False] * len(self.buckets)
+        # one-shot IPC all-reduce (parallel/ipc.py) for small models on one node:
+        # TOA_IPC_ALLREDUCE=1, every rank local, the whole gradient fits a slot
+        self.ipc = None
+        nbytes = flat.grad.numel() * esz
+        if (self.enabled and os.environ.get("TOA_IPC_ALLREDUCE", "0") == "1" and flat.grad.is_cuda
+                and int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) == self.world and nbytes <= 64 << 20):
+            from .ipc import IpcAllReduce
+
+            self.ipc = IpcAllReduce(group, slot_bytes=max(1 << 20, nbytes))
 
     def _ready(self, param):
         b = param._toa_bucket
@@ -67,6 +76,9 @@ class GradBucketer:
         self.launched[b] = True
         s, e, _ = self.buckets[b]
         view = self.flat.grad[s:e]
+        if self.ipc is not None and self.ipc.fits(view):
+            self.ipc(view)  # one-shot on the compute stream: latency-bound small gradients
+            return
         self.works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def finish(self):

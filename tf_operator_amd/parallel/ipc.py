@@ -1,0 +1,106 @@
+"""One-shot all-reduce over IPC-mapped peer buffers,
+for latency-bound gradients of the small payloads; kernels in
+csrc/hip/comm.hip.  Large buffers stay on RCCL (ddp.GradBucketer).
+
+    ar = IpcAllReduce(group)          # collective: exchanges IPC handles
+    ar(t)                             # in-place sum over ranks of a bf16/fp32 tensor
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+
+class IpcAllReduce:
+    def __init__(self, group=None, slot_bytes: int = 8 << 20, timeout_ms: int = 20000):
+        if not (dist.is_initialized() and torch.cuda.is_available()):
+            raise RuntimeError("IpcAllReduce needs an initialised process group and a GPU")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > 8:
+            raise ValueError("one-shot IPC all-reduce is for one node (<= 8 ranks)")
+        self.slot = int(slot_bytes)
+        self.timeout_ms = int(timeout_ms)
+        L = _lib.lib()
+        for name, argt in (("toa_ipc_alloc", [ctypes.c_int64, ctypes.c_void_p]),
+                           ("toa_ipc_get_handle", [ctypes.c_void_p, ctypes.c_void_p]),
+                           ("toa_ipc_open_handle", [ctypes.c_void_p, ctypes.c_void_p]),
+                           ("toa_ipc_close_handle", [ctypes.c_void_p]), ("toa_ipc_free", [ctypes.c_void_p]),
+                           ("toa_ipc_handle_size", []),
+                           ("toa_allreduce_oneshot", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                                      ctypes.c_int64, ctypes.c_uint, ctypes.c_void_p, ctypes.c_int,
+                                                      ctypes.c_void_p])):
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = ctypes.c_int
+        self._L = L
+        hsz = L.toa_ipc_handle_size()
+        self._own = []
+        ptrs = {}
+        for what, nbytes in (("buf", 2 * self.slot), ("flags", 4 * 8)):
+            p = ctypes.c_void_p()
+            self._check(L.toa_ipc_alloc(nbytes, ctypes.byref(p)), "alloc")
+            self._own.append(p)
+            h = (ctypes.c_char * hsz)()
+            self._check(L.toa_ipc_get_handle(p, h), "get handle")
+            ptrs[what] = (p, bytes(h))
+        handles = [None] * self.world
+        dist.all_gather_object(handles, {k: v[1] for k, v in ptrs.items()}, group=group)
+        self._opened = []
+        self.bufs = (ctypes.c_void_p * self.world)()
+        self.flags = (ctypes.c_void_p * self.world)()
+        for r in range(self.world):
+            for what, arr in (("buf", self.bufs), ("flags", self.flags)):
+                if r == self.rank:
+                    arr[r] = ptrs[what][0]
+                else:
+                    q = ctypes.c_void_p()
+                    h = (ctypes.c_char * hsz).from_buffer_copy(handles[r][what])
+                    self._check(L.toa_ipc_open_handle(h, ctypes.byref(q)), f"open rank {r} {what}")
+                    self._opened.append(q)
+                    arr[r] = q
+        self.err = torch.zeros(1, device=torch.cuda.current_device(), dtype=torch.int32)
+        self.epoch = 0
+        torch.cuda.synchronize()
+        dist.barrier(group=group)
+
+    @staticmethod
+    def _check(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"IPC {what} failed (hipError {rc})")
+
+    def fits(self, t: torch.Tensor) -> bool:
+        return t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and t.numel() * t.element_size() <= self.slot
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the ranks (every rank gets bit-identical results)."""
+        if not (self.fits(t) and t.is_contiguous()):
+            raise ValueError("tensor does not fit the IPC staging slot")
+        self.epoch += 1
+        rc = self._L.toa_allreduce_oneshot(self.bufs, self.flags, self.rank, self.world,
+                                           0 if t.dtype == torch.bfloat16 else 1, ctypes.c_void_p(t.data_ptr()),
+                                           ctypes.c_void_p(t.data_ptr()), t.numel(), self.slot, self.epoch,
+                                           ctypes.c_void_p(self.err.data_ptr()), self.timeout_ms,
+                                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        self._check(rc, "all-reduce launch")
+        return t
+
+    def check(self):
+        """Raise if some rank never reached a barrier (kernel timed out)."""
+        e = int(self.err.item())
+        if e:
+            raise RuntimeError(f"IPC all-reduce: ranks {[r for r in range(8) if e >> r & 1]} timed out")
+
+    def close(self):
+        torch.cuda.synchronize()
+        for q in self._opened:
+            self._L.toa_ipc_close_handle(q)
+        for p in self._own:
+            self._L.toa_ipc_free(p)
+        self._opened, self._own = [], []
