@@ -1,9 +1,10 @@
 // Causal flash attention for gfx950 (bf16 in/out, fp32 accumulate), with
 // native GQA (K/V stay packed per kv-head; no repeat_interleave copies).
 //
-// Layouts: q/o [B, H, S, D], k/v [B, Hk, S, D], lse [B, H, S] (natural log),
-// D = 128 (or 64).  One workgroup = 4 waves = a 128-row query block of one
-// (batch, head); wave w owns 32 query rows.  K/V tiles of 64 keys are staged
+// Layouts: q [B, H, S, D], o/dO [B, H, S, D] or [B, S, H, D] (flag bit 1),
+// k/v [B, Hk, S, D], lse [B, H, S] (natural log), D = 128.  Forward / dQ:
+// one workgroup = 8 waves = a 256-row query block of one (batch, head);
+// wave w owns 32 query rows.  K/V tiles of 64 keys are staged
 // global -> registers -> LDS (double buffered, loads of tile t+1 in flight
 // while tile t is computed -- guide T14), K in a 16-way XOR-swizzled
 // row-major image read with ds_read_b128 (conflict-free for the 32x32 MFMA
@@ -21,9 +22,9 @@
 // wave's last row are skipped wave-uniformly; blocks are launched
 // heaviest-first for load balance.
 //
-// Backward = three kernels: preprocess (delta = rowsum(dO*O)), dK/dV
-// (workgroup per 128-key block, sweeping the GQA group's query heads), dQ
-// (workgroup per 128-query block).  No float atomics: deterministic.
+// Backward = two kernels: dQ (which also computes delta = rowsum(dO*O)),
+// then dK/dV (workgroup per 128-key block, sweeping the GQA group's query
+// heads).  No float atomics: deterministic.
 #include "toa_common.h"
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
@@ -312,29 +313,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
       *(uint2*)(orow + d) = w;
     }
   if (hh == 0) LSE[(int64_t)(b * H + h) * S + myq] = (m_run + log2f(l_tot)) * 0.6931471805599453f;
-}
-
-// ---------------------------------------------------------------------------
-// backward preprocess: delta[b,h,q] = sum_d dO * O
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                                                           float* __restrict__ delta, int64_t rows, int D, int H,
-                                                           int S, int o_bshd) {
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // delta row, [B, H, S] order
-  const int lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  const int s_ = (int)(row % S), h_ = (int)((row / S) % H), b_ = (int)(row / ((int64_t)S * H));
-  const int64_t base = o_off(b_, h_, s_, H, S, o_bshd);
-  float acc = 0.f;
-  for (int c = lane; c < D / 8; c += 64) {
-    float a[8], g[8];
-    unpack8(ld16(O + base + c * 8), a);
-    unpack8(ld16(dO + base + c * 8), g);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc = fmaf(a[j], g[j], acc);
-  }
-  acc = wave_sum(acc);
-  if (lane == 0) delta[row] = acc;
 }
 
 // One image for row reads (ds_read_b128, 32x32x16 A/B operand) AND
