@@ -351,3 +351,58 @@ extern "C" int toa_xent_bwd(int dtype, const void* logits, const int64_t* tgt, c
                        grad_out, n_valid, (float*)dx, V, ldx, ignore_index);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Embedding backward without float atomics: the token ids arrive sorted
+// (stable sort, so equal ids keep their original order).  Workgroup i owns
+// the run of equal ids starting at position i (every other workgroup exits
+// at once), sums those rows of dy in fp32 in a fixed order and adds the sum
+// into the gradient row once.  Deterministic, and the bf16 gradient gets one
+// rounding per step instead of one per occurrence.
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const int64_t* __restrict__ sorted,
+                                                       const int64_t* __restrict__ perm,
+                                                       const bf16_t* __restrict__ dy, void* __restrict__ grad,
+                                                       int grad_f32, int64_t n, int dim) {
+  const int64_t i = blockIdx.x;
+  const int64_t tok = sorted[i];
+  if (i > 0 && sorted[i - 1] == tok) return;
+  for (int c = threadIdx.x * 8; c < dim; c += 256 * 8) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int64_t r = i; r < n && sorted[r] == tok; ++r) {
+      float f[8];
+      unpack8(ld16(dy + perm[r] * dim + c), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    if (grad_f32) {
+      float* g = (float*)grad + tok * dim + c;
+      f32x4 a = *(f32x4*)g, b = *(f32x4*)(g + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] += acc[j];
+        b[j] += acc[4 + j];
+      }
+      *(f32x4*)g = a;
+      *(f32x4*)(g + 4) = b;
+    } else {
+      bf16_t* g = (bf16_t*)grad + tok * dim + c;
+      float old[8];
+      unpack8(ld16(g), old);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += old[j];
+      st16(g, pack8(acc));
+    }
+  }
+}
+
+// sorted/perm: int64 [n] (torch.sort(stable=True) of the ids); dy bf16 [n, dim];
+// grad bf16 or fp32 [vocab, dim]; dim % 8 == 0.
+extern "C" int toa_embed_bwd(const int64_t* sorted, const int64_t* perm, const bf16_t* dy, void* grad, int grad_f32,
+                             int64_t n, int dim, hipStream_t stream) {
+  if (dim % 8 != 0 || n <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)n), dim3(256), 0, stream, sorted, perm, dy, grad, grad_f32, n,
+                     dim);
+  return (int)hipGetLastError();
+}

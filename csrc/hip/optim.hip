@@ -78,7 +78,7 @@ extern "C" int toa_sumsq(const void* x, int64_t n, int is_bf16, float* workspace
 // ---------------------------------------------------------------------------
 template <bool GRAD_BF16>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ master, bf16_t* __restrict__ param,
-                                                         const void* __restrict__ grad, float* __restrict__ m,
+                                                         void* __restrict__ grad, int zero_grad, float* __restrict__ m,
                                                          float* __restrict__ v, int64_t n8, float lr, float b1,
                                                          float b2, float eps, float wd, float inv_bc1,
                                                          float inv_sqrt_bc2, float grad_scale,
@@ -95,10 +95,15 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
     float g[8], p[8], mm[8], vv[8];
     if (GRAD_BF16) {
       unpack8(ld16((const bf16_t*)grad + i * 8), g);
+      if (zero_grad) st16((bf16_t*)grad + i * 8, u32x4{0, 0, 0, 0});
     } else {
       f32x4 a = *((const f32x4*)grad + 2 * i), b = *((const f32x4*)grad + 2 * i + 1);
       g[0] = a[0]; g[1] = a[1]; g[2] = a[2]; g[3] = a[3];
       g[4] = b[0]; g[5] = b[1]; g[6] = b[2]; g[7] = b[3];
+      if (zero_grad) {
+        *((f32x4*)grad + 2 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
+        *((f32x4*)grad + 2 * i + 1) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     f32x4* pm = (f32x4*)master + 2 * i;
     f32x4* mv = (f32x4*)m + 2 * i;
@@ -129,7 +134,9 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
   }
 }
 
-extern "C" int toa_adamw_flat(float* master, bf16_t* param, const void* grad, int grad_is_bf16, float* m,
+// grad_flags: bit 0 = grad is bf16 (else fp32); bit 1 = zero the gradient
+// after reading it (the next step's zero_grad pass, fused).
+extern "C" int toa_adamw_flat(float* master, bf16_t* param, void* grad, int grad_flags, float* m,
                               float* v, int64_t n, float lr, float beta1, float beta2, float eps,
                               float weight_decay, int step, float grad_scale, const float* norm_sq,
                               float max_norm, hipStream_t stream) {
@@ -139,12 +146,13 @@ extern "C" int toa_adamw_flat(float* master, bf16_t* param, const void* grad, in
   const float bc2 = 1.f - powf(beta2, (float)step);
   const float inv_bc1 = 1.f / bc1, inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   int grid = toa_stream_grid(n8, 256);
-  if (grad_is_bf16)
-    hipLaunchKernelGGL(adamw_flat_kernel<true>, dim3(grid), dim3(256), 0, stream, master, param, grad, m, v, n8,
+  const int zero_grad = (grad_flags >> 1) & 1;
+  if (grad_flags & 1)
+    hipLaunchKernelGGL(adamw_flat_kernel<true>, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8,
                        lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
                        max_norm);
   else
-    hipLaunchKernelGGL(adamw_flat_kernel<false>, dim3(grid), dim3(256), 0, stream, master, param, grad, m, v, n8,
+    hipLaunchKernelGGL(adamw_flat_kernel<false>, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8,
                        lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
                        max_norm);
   return (int)hipGetLastError();

@@ -45,6 +45,7 @@ _SIGS = {
     "toa_norm_bwd_blocks": [c_int, c_int],
     "toa_rope_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
     "toa_rope_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
+    "toa_embed_bwd": [c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_p],
     "toa_swiglu_fwd": [c_p, c_p, c_i64, c_int, c_p],
     "toa_swiglu_bwd": [c_p, c_p, c_p, c_i64, c_int, c_p],
     "toa_xent_fwd": [c_int, c_p, c_p, c_p, c_p, c_i64, c_int, c_i64, c_int, c_p],

@@ -6,6 +6,7 @@ squared norm (``toa_sumsq``), so ``step()`` never synchronises with the host.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -40,9 +41,23 @@ def adamw_reference(master, grad, m, v, *, lr, beta1, beta2, eps, weight_decay, 
 
 
 class FlatAdamW:
-    """AdamW over a :class:`tf_operator_amd.parallel.flat.FlatParams`."""
+    """AdamW over a :class:`tf_operator_amd.parallel.flat.FlatParams`.
 
-    def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0):
+    overlap=True (GPU): after the global grad norm, the update runs on a side
+    stream bucket by bucket in FORWARD order, zeroing each gradient slice as
+    it reads it (no separate zero_grad pass), and records one event per
+    bucket.  The next step's forward waits per bucket (wait_bucket, called
+    from module pre-hooks), so the memory-bound update of late layers runs
+    under the compute-bound GEMMs of early ones; backward waits for all of it
+    (wait_all) before writing gradients.  Measured on Llama-3-8B it gains
+    nothing (1100 vs 1098 ms/step): the GEMMs already hold every CU, so the
+    update only slots in between them; it stays opt-in (TOA_OPT_OVERLAP=1).
+
+    fuse_zero_grad=True: the update zeroes the gradient as it reads it
+    (``grads_zeroed`` tells the caller to skip its own zero_grad pass)."""
+
+    def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
+                 overlap=False, buckets=None, fuse_zero_grad=False):
         self.flat = flat
         self.lr = lr
         self.beta1, self.beta2 = betas
@@ -57,6 +72,42 @@ class FlatAdamW:
         self._norm = torch.zeros(1, device=flat.device, dtype=torch.float32)
         self._ws = torch.empty(2048, device=flat.device, dtype=torch.float32)
         self.last_norm_sq = self._norm
+        self.overlap = bool(overlap) and flat.device.type == "cuda" and _lib.available()
+        # zero each gradient slice as the update reads it (the caller then skips zero_grad)
+        self.fuse_zero_grad = bool(fuse_zero_grad) or self.overlap
+        self.grads_zeroed = False  # the last step() zeroed the gradients itself
+        if self.overlap:
+            self.side = torch.cuda.Stream(device=flat.device)
+            ranges = [(b[0], b[1]) for b in buckets] if buckets else [(0, flat.numel)]
+            # flat order is backward order: the forward needs the last bucket first
+            self.order = list(range(len(ranges)))[::-1]
+            self.ranges = ranges
+            self.events = [None] * len(ranges)
+            self.waited = [True] * len(ranges)
+            self.done = None
+
+    def _launch(self, a, b, decay, lr, grad_scale, clip, zero, stream):
+        f = self.flat
+        gflags = int(f.grad.dtype == torch.bfloat16) | (2 if zero else 0)
+        pp = f.param.data_ptr() + 2 * a if f.param.dtype == torch.bfloat16 else None
+        _lib.call("toa_adamw_flat", f.master.data_ptr() + 4 * a, pp, f.grad.data_ptr() + f.grad.element_size() * a,
+                  gflags, f.exp_avg.data_ptr() + 4 * a, f.exp_avg_sq.data_ptr() + 4 * a, b - a, float(lr),
+                  float(self.beta1), float(self.beta2), float(self.eps),
+                  float(self.weight_decay if decay else 0.0), self.step_count, float(grad_scale),
+                  _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), stream)
+
+    def wait_bucket(self, b):
+        """Make the current stream wait until bucket b's parameters are updated."""
+        if self.overlap and not self.waited[b]:
+            torch.cuda.current_stream(self.flat.device).wait_event(self.events[b])
+            self.waited[b] = True
+
+    def wait_all(self):
+        """Current stream waits for the whole update (and the gradient zeroing)."""
+        if self.overlap and self.done is not None:
+            torch.cuda.current_stream(self.flat.device).wait_event(self.done)
+            self.waited = [True] * len(self.waited)
+            self.done = None
 
     @torch.no_grad()
     def step(self, grad_scale=1.0, lr=None):
@@ -66,21 +117,34 @@ class FlatAdamW:
         clip = self.max_grad_norm and self.max_grad_norm > 0
         if clip:
             grad_norm_sq(f.grad, self._ws, self._norm)
+        if self.overlap and f.param.dtype == torch.bfloat16:
+            main = torch.cuda.current_stream(f.device)
+            self.side.wait_stream(main)
+            s = ctypes.c_void_p(self.side.cuda_stream)
+            for bi in self.order:
+                lo, hi = self.ranges[bi]
+                for (a, b, decay) in self.runs:
+                    a2, b2 = max(a, lo), min(b, hi)
+                    if a2 < b2:
+                        self._launch(a2, b2, decay, lr, grad_scale, clip, True, s)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                self.events[bi] = ev
+                self.waited[bi] = False
+            self.done = torch.cuda.Event()
+            self.done.record(self.side)
+            # tensors used on the side stream must not be recycled by the main stream's allocator
+            for t in (f.grad, f.param, f.master, f.exp_avg, f.exp_avg_sq, self._norm):
+                t.record_stream(self.side)
+            self.grads_zeroed = True
+            return
+        self.grads_zeroed = False
         if _lib.use_hip(f.grad):
             s = _lib.stream(f.grad)
-            gbf = int(f.grad.dtype == torch.bfloat16)
             pbf = f.param.dtype == torch.bfloat16
-            esz_p, esz_g = f.param.element_size(), f.grad.element_size()
             for (a, b, decay) in self.runs:
-                n = b - a
-                wd = self.weight_decay if decay else 0.0
-                pp = _lib.ptr(f.param) if pbf else None
-                _lib.call("toa_adamw_flat", f.master.data_ptr() + 4 * a,
-                          (f.param.data_ptr() + esz_p * a) if pp is not None else None,
-                          f.grad.data_ptr() + esz_g * a, gbf, f.exp_avg.data_ptr() + 4 * a,
-                          f.exp_avg_sq.data_ptr() + 4 * a, n, float(lr), float(self.beta1), float(self.beta2),
-                          float(self.eps), float(wd), self.step_count, float(grad_scale),
-                          _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), s)
+                self._launch(a, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
+            self.grads_zeroed = self.fuse_zero_grad
             if not pbf:
                 f.param.copy_(f.master)
         else:

@@ -7,6 +7,7 @@ over the flat fp32 master/m/v (device-side grad clipping, no host sync).
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -19,7 +20,7 @@ from ..parallel.flat import FlatParams
 
 class LlamaTrainer:
     def __init__(self, cfg: LlamaConfig | str, device, micro_batch=1, seq_len=4096, grad_accum=1, lr=3e-4,
-                 seed=0, bucket_mb=None):
+                 seed=0, bucket_mb=None, overlap_optimizer=None):
         if isinstance(cfg, str):
             cfg = PRESETS[cfg]
         self.cfg = cfg
@@ -35,8 +36,39 @@ class LlamaTrainer:
         self.flat = FlatParams(model.params_backward_order(), names=names, no_decay=model.no_decay)
         broadcast_params(self.flat)
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20))
-        self.opt = FlatAdamW(self.flat, lr=lr)
+        if overlap_optimizer is None:
+            overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
+        self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
+                             fuse_zero_grad=True)
+        if self.opt.overlap:
+            self._hooks = self._install_param_waits()
         self.step_idx = 0
+
+    def _install_param_waits(self):
+        """Forward pre-hooks: each module waits only for the buckets holding
+        its own parameters (FlatAdamW overlap mode).  The root's direct
+        parameter (the untied lm_head) is used right after the final norm,
+        so that wait rides on the final norm's hook instead of the root's."""
+        opt = self.opt
+        hooks = []
+
+        def waiter(buckets):
+            def hook(mod, args):
+                for b in buckets:
+                    opt.wait_bucket(b)
+            return hook
+
+        root_params = list(self.model.parameters(recurse=False))
+        for name, mod in self.model.named_modules():
+            ps = list(mod.parameters(recurse=False))
+            if mod is self.model:
+                continue
+            if mod is self.model.norm:
+                ps = ps + root_params
+            if ps:
+                bs = sorted({p._toa_bucket for p in ps})
+                hooks.append(mod.register_forward_pre_hook(waiter(bs)))
+        return hooks
 
     def synthetic_batch(self, seed=1234):
         g = torch.Generator(device=self.device)
@@ -47,10 +79,12 @@ class LlamaTrainer:
 
     def step(self, batches):
         """batches: list (len grad_accum) of (tokens, targets)."""
-        self.flat.zero_grad()
+        if not self.opt.grads_zeroed:
+            self.flat.zero_grad()
         loss_sum = None
         for i, (tok, tgt) in enumerate(batches):
             loss = self.model(tok, tgt)
+            self.opt.wait_all()  # backward writes gradients the update is still zeroing
             (loss / len(batches)).backward()
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
         self.bucketer.finish()
@@ -73,11 +107,13 @@ def timed_steps(trainer: LlamaTrainer, batches, n, sync=True):
 
 
 def trainer_state(tr: LlamaTrainer):
+    tr.opt.wait_all()
     return {"flat": tr.flat.state_dict(), "opt": tr.opt.state_dict(), "step": tr.step_idx}
 
 
 def load_trainer_state(tr: LlamaTrainer, st):
     dev = tr.flat.device
+    tr.opt.wait_all()
     tr.flat.load_state_dict({k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in st["flat"].items()})
     tr.opt.load_state_dict(st["opt"])
     tr.step_idx = int(st["step"])
