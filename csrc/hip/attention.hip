@@ -41,13 +41,6 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 
-__device__ __forceinline__ uint32_t pack2(float a, float b) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  const f2 v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));  // one v_cvt_pk_bf16_f32
-}
-
 // LDS tile geometry: 64 keys x 128 d bf16 = 16 KB, rows of 256 B = 16 chunks of 16 B.
 #define TK 64
 #define ROWB 256

@@ -89,6 +89,14 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
   m = mn;
 }
 
+// two floats -> packed bf16x2, round-to-nearest-even (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));  // one v_cvt_pk_bf16_f32
+}
+
 // Grid size for memory-bound grid-stride kernels: cap at 256 CUs x 8 blocks
 // (CDNA guide G11).
 static inline int toa_stream_grid(int64_t work_items, int block) {

@@ -95,8 +95,51 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return dx
 
 
+_WGRAD = os.environ.get("TOA_WGRAD", "hip")
+_ws = {}
+
+
+def _workspace(dev, nbytes):
+    t = _ws.get(dev)
+    if t is None or t.numel() * 4 < nbytes:
+        t = torch.empty((nbytes + 3) // 4, device=dev, dtype=torch.float32)
+        _ws[dev] = t
+    return t
+
+
+def wgrad_hip_ok(g, dy2, x2) -> bool:
+    """Shapes/layouts csrc/hip/wgrad.hip takes: bf16, 256-multiple output
+    dims, token count a multiple of 64, unit column stride."""
+    if _WGRAD != "hip" or not _lib.has("toa_wgrad"):
+        return False
+    if not (dy2.is_cuda and g.dtype == dy2.dtype == x2.dtype == torch.bfloat16 and g.is_contiguous()):
+        return False
+    if dy2.dim() != 2 or x2.dim() != 2 or dy2.stride(1) != 1 or x2.stride(1) != 1:
+        return False
+    T, N = dy2.shape
+    K = x2.shape[1]
+    return (N % 256 == 0 and K % 256 == 0 and T % 128 == 0 and T >= 1024 and dy2.stride(0) % 8 == 0
+            and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0
+            and g.data_ptr() % 16 == 0 and tuple(g.shape) == (N, K))
+
+
+def wgrad_hip_(g, dy2, x2, beta=1.0, split=None):
+    """g[N,K] (+)= dy2[T,N]^T x2[T,K] on the hand-written MFMA kernel."""
+    _lib.use_hip(dy2)
+    T, N = dy2.shape
+    K = x2.shape[1]
+    if split is None:
+        split = _lib.call_ret("toa_wgrad_split", N, K, T)
+    ws = _workspace(dy2.device, split * N * K * 4) if split > 1 else None
+    _lib.call("toa_wgrad", _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(g), K, _lib.ptr(ws),
+              N, K, T, int(split), int(beta != 0.0), _lib.stream(dy2))
+    return g
+
+
 def wgrad_acc_(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float = 1.0):
     """g[N,K] = beta*g + dy2[M,N]^T @ x2[M,K]  (in place; g bf16 or fp32)."""
+    if beta in (0.0, 1.0) and wgrad_hip_ok(g, dy2, x2):
+        return wgrad_hip_(g, dy2, x2, beta)
     if not (_ok(dy2, x2) and g.is_contiguous() and g.dtype in (torch.bfloat16, torch.float32)):
         if beta == 0.0:
             g.copy_(torch.mm(dy2.t(), x2))
