@@ -253,6 +253,71 @@ def test_wgrad_routing_matches_hipblaslt():
     assert (w.main_grad.float() - ref.float()).abs().max() <= 2e-2 * ref.float().abs().max()
 
 
+@pytest.mark.parametrize("R,C,pad", [(64, 64, 0), (128, 320, 0), (6144, 4096, 0), (192, 256, 64)])
+def test_transpose_bf16_kernel(R, C, pad):
+    """csrc/hip/transpose.hip is an exact transpose, incl. strided source /
+    destination rows."""
+    _lib()
+    from tf_operator_amd.ops.wt import transpose_into
+
+    torch.manual_seed(R + C)
+    big = torch.randn(R, C + pad, device=DEV).to(torch.bfloat16)
+    src = big[:, :C]
+    dbig = torch.zeros(C, R + pad, device=DEV, dtype=torch.bfloat16)
+    dst = dbig[:, :R]
+    transpose_into(dst, src)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src.t())
+    if pad:
+        assert not dbig[:, R:].any()
+
+
+def test_dgrad_on_transposed_weight_matches_nn():
+    """linear_dgrad routes through param._toa_wt (dy (W^T)^T, the forward's
+    GEMM form) and matches hipBLASLt's dy @ W to bf16 rounding."""
+    _lib()
+    from tf_operator_amd.ops import gemm
+    from tf_operator_amd.ops.wt import transpose_into
+
+    torch.manual_seed(9)
+    w = torch.nn.Parameter(torch.randn(768, 512, device=DEV).to(torch.bfloat16))
+    dy = torch.randn(2048, 768, device=DEV).to(torch.bfloat16)
+    ref = dy.float() @ w.float()
+    w._toa_wt = transpose_into(torch.empty(512, 768, device=DEV, dtype=torch.bfloat16), w.data)
+    got = gemm.linear_dgrad(dy, w)
+    assert (got.float() - ref).abs().max() <= 1e-2 * ref.abs().max()
+
+
+def test_trainer_transposed_weights_refresh():
+    """With the W^T copies (TOA_DGRAD_WT default) every copy equals the
+    current weights after each optimizer step, and the training trajectory
+    matches the trainer without them to bf16 GEMM rounding."""
+    _lib()
+    from tf_operator_amd.models.llama import PRESETS
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    runs = []
+    for use_wt in (False, True):
+        for overlap in ((False, True) if use_wt else (False,)):
+            tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device(DEV), micro_batch=2, seq_len=128, lr=1e-3,
+                              bucket_mb=0.25, overlap_optimizer=overlap)
+            if not use_wt:
+                tr.wt.detach()
+                tr.wt = None
+                tr.opt.post_update = None
+            b = tr.synthetic_batch()
+            losses = [float(tr.step([b])) for _ in range(4)]
+            tr.opt.wait_all()
+            torch.cuda.synchronize()
+            if use_wt:
+                assert len(tr.wt.items) == 4 * 2 + 1
+                for _, _, p, view in tr.wt.items:
+                    assert torch.equal(view, p.data.t()), "stale W^T"
+            runs.append(losses)
+    for losses in runs[1:]:
+        assert max(abs(a - b) for a, b in zip(losses, runs[0])) < 2e-2, runs
+
+
 def test_trainer_overlapped_optimizer_matches_serial():
     """FlatAdamW overlap mode (per-bucket update on a side stream, fused grad
     zeroing, forward pre-hook waits) is bit-identical to the serial step."""

@@ -86,6 +86,9 @@ def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    wt = getattr(w, "_toa_wt", None)
+    if wt is not None:  # W^T kept by ops.wt.TransposedWeights: dx = dy (W^T)^T, the forward's form
+        return linear_fwd(dy2, wt)
     if not _ok(dy2, w):
         return torch.matmul(dy2, w)
     M, N = dy2.shape

@@ -54,10 +54,16 @@ class FlatAdamW:
     update only slots in between them; it stays opt-in (TOA_OPT_OVERLAP=1).
 
     fuse_zero_grad=True: the update zeroes the gradient as it reads it
-    (``grads_zeroed`` tells the caller to skip its own zero_grad pass)."""
+    (``grads_zeroed`` tells the caller to skip its own zero_grad pass).
+
+    post_update(lo, hi): called on the update's stream after the bf16
+    weights of flat range [lo, hi) are written (per bucket in overlap mode,
+    once for the whole buffer otherwise) -- derived weight copies (ops.wt)
+    refresh there."""
 
     def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
-                 overlap=False, buckets=None, fuse_zero_grad=False):
+                 overlap=False, buckets=None, fuse_zero_grad=False, post_update=None):
+        self.post_update = post_update
         self.flat = flat
         self.lr = lr
         self.beta1, self.beta2 = betas
@@ -127,6 +133,9 @@ class FlatAdamW:
                     a2, b2 = max(a, lo), min(b, hi)
                     if a2 < b2:
                         self._launch(a2, b2, decay, lr, grad_scale, clip, True, s)
+                if self.post_update is not None:
+                    with torch.cuda.stream(self.side):
+                        self.post_update(lo, hi)
                 ev = torch.cuda.Event()
                 ev.record(self.side)
                 self.events[bi] = ev
@@ -147,6 +156,8 @@ class FlatAdamW:
             self.grads_zeroed = self.fuse_zero_grad
             if not pbf:
                 f.param.copy_(f.master)
+            if self.post_update is not None:
+                self.post_update(0, f.numel)
         else:
             for (a, b, decay) in self.runs:
                 adamw_reference(f.master[a:b], f.grad[a:b], f.exp_avg[a:b], f.exp_avg_sq[a:b], lr=lr,
@@ -155,6 +166,8 @@ class FlatAdamW:
                                 grad_scale=grad_scale, norm_sq=self._norm if clip else None,
                                 max_norm=self.max_grad_norm or 0.0)
             f.param.copy_(f.master.to(f.param.dtype))
+            if self.post_update is not None:
+                self.post_update(0, f.numel)
 
     def state_dict(self):
         return {"step": self.step_count, "lr": self.lr}

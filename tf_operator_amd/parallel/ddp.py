@@ -107,3 +107,4 @@ def broadcast_params(flat: FlatParams, src=0, group=None):
     dist.broadcast(flat.param, src, group=group)
     if flat.master is not None:
         flat.master.copy_(flat.param.float())
+    flat.params_changed()

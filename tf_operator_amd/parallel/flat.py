@@ -75,6 +75,14 @@ class FlatParams:
             self.master = self.param.float() if dtype != torch.float32 else self.param.clone()
         self.exp_avg = None
         self.exp_avg_sq = None
+        # callbacks run after the bf16 weights are rewritten outside the
+        # optimizer (checkpoint load, broadcast): derived copies such as
+        # ops.wt.TransposedWeights re-derive themselves
+        self.on_param_change = []
+
+    def params_changed(self):
+        for fn in list(self.on_param_change):
+            fn()
 
     def decay_runs(self):
         """Contiguous [start, end, decay] runs (for per-run optimizer launches)."""
@@ -112,3 +120,4 @@ class FlatParams:
                 if getattr(self, k) is None:
                     setattr(self, k, torch.zeros_like(sd[k], device=self.device))
                 getattr(self, k).copy_(sd[k])
+        self.params_changed()

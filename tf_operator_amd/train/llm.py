@@ -14,6 +14,7 @@ import torch
 
 from ..models.llama import PRESETS, Llama, LlamaConfig
 from ..ops.optim import FlatAdamW
+from ..ops.wt import TransposedWeights, enabled_default
 from ..parallel.ddp import GradBucketer, broadcast_params
 from ..parallel.flat import FlatParams
 
@@ -34,12 +35,17 @@ class LlamaTrainer:
         self.model = model
         names = {id(p): n for n, p in model.named_parameters()}
         self.flat = FlatParams(model.params_backward_order(), names=names, no_decay=model.no_decay)
+        self.wt = None
+        if enabled_default(device):  # dgrad on W^T (ops/wt.py): +2 B/param of HBM
+            lin = [p for n, p in model.named_parameters() if p.dim() == 2 and not n.startswith("embed.")]
+            lin += [model.head_weight()]
+            self.wt = TransposedWeights(self.flat, lin)
         broadcast_params(self.flat)
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20))
         if overlap_optimizer is None:
             overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
         self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
-                             fuse_zero_grad=True)
+                             fuse_zero_grad=True, post_update=self.wt.refresh if self.wt else None)
         if self.opt.overlap:
             self._hooks = self._install_param_waits()
         self.step_idx = 0
