@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=6)  # 228 GB peak of 288 GB; 2 % over mb4
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--zero", choices=("auto", "0", "1"), default="auto",
+                    help="sharded optimizer (reduce-scatter / owned-shard AdamW / all-gather); auto = on for N > 1")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.cuda profiler markers")
     args = ap.parse_args()
 
@@ -48,8 +50,9 @@ def main():
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={n_gpus}; using WORLD_SIZE", file=sys.stderr)
     dev = info.device
     torch.manual_seed(0)
+    zero = n_gpus > 1 if args.zero == "auto" else args.zero == "1"
     tr = LlamaTrainer(args.model, dev, micro_batch=args.micro_batch, seq_len=args.seq_len,
-                      grad_accum=args.grad_accum, bucket_mb=args.bucket_mb)
+                      grad_accum=args.grad_accum, bucket_mb=args.bucket_mb, shard_optimizer=zero)
     batches = [tr.synthetic_batch(seed=1000 + info.rank * 97 + i) for i in range(args.grad_accum)]
 
     # first step (submit -> first-step proxy inside the replica: process start -> step 1 done)
@@ -102,7 +105,8 @@ def main():
                 "parallelism": f"dp{n_gpus}",
                 "micro_batch_per_gpu": args.micro_batch,
                 "grad_accum": args.grad_accum,
-                "optimizer": "AdamW (fused HIP, fp32 master, clip 1.0)",
+                "optimizer": "AdamW (fused HIP, fp32 master, clip 1.0)"
+                             + (", ZeRO-1 sharded" if tr.bucketer.shard else ""),
                 "tfjob": f"Worker={n_gpus}",
                 "weights": "random-init",
             },

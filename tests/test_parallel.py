@@ -90,3 +90,46 @@ def test_bench_contract_torchrun_two_ranks():
     assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 4
     assert res["value"] > 0 and res["higher_is_better"] is True
     assert abs(res["value"] - 4 / (res["ms_per_step"] / 1000)) / res["value"] < 0.01
+
+
+def _zero_worker(rank, world, port, bucket_mb, steps, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tf_operator_amd.train.llm import trainer_state
+
+        res = {}
+        for shard in (False, True):
+            tr = LlamaTrainer("llama-tiny", torch.device("cpu"), micro_batch=2, seq_len=32, lr=1e-3, seed=rank,
+                              bucket_mb=bucket_mb, shard_optimizer=shard, transposed_weights=shard)
+            assert tr.bucketer.shard == shard and (tr.gather is not None) == shard
+            batches = _batches(tr, world)
+            losses = [float(tr.step([batches[rank]])) for _ in range(steps)]
+            st = trainer_state(tr)  # collective in sharded mode
+            if shard:  # W^T copies re-derived after every gather
+                assert all(torch.equal(v, p.data.t()) for _, _, p, v in tr.wt.items)
+            res[shard] = (losses, tr.flat.param.detach().float().clone(), st["flat"]["master"].clone(),
+                          st["flat"]["exp_avg_sq"].clone())
+        if rank == 0:
+            torch.save({"res": res, "nbuckets": len(tr.bucketer.buckets), "owned": tr.bucketer.owned}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bucket_mb", [(2, 0.01), (4, 512)])
+def test_sharded_optimizer_matches_replicated(tmp_path, world, bucket_mb):
+    """ZeRO-1 (reduce-scatter, owned-shard AdamW, in-place all-gather of the
+    weights, parallel/zero.py) follows the replicated all-reduce DP step:
+    same losses, same weights, and the gathered checkpoint state (master,
+    second moment) equals the replicated one."""
+    steps = 3
+    out = str(tmp_path / "zero.pt")
+    mp.spawn(_zero_worker, args=(world, _free_port(), bucket_mb, steps, out), nprocs=world, join=True)
+    r = torch.load(out, weights_only=True)
+    (l0, p0, m0, v0), (l1, p1, m1, v1) = r["res"][False], r["res"][True]
+    assert len(r["owned"]) == r["nbuckets"]
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-3, (l0, l1)
+    for a, b in ((p0, p1), (m0, m1)):
+        assert float((a - b).abs().max()) <= 1e-2 * float(a.abs().max())
+    assert float((v0 - v1).abs().max()) <= 1e-2 * float(v0.abs().max())

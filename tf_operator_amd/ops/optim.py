@@ -59,11 +59,20 @@ class FlatAdamW:
     post_update(lo, hi): called on the update's stream after the bf16
     weights of flat range [lo, hi) are written (per bucket in overlap mode,
     once for the whole buffer otherwise) -- derived weight copies (ops.wt)
-    refresh there."""
+    refresh there.
+
+    owned=[(lo, hi), ...] (sharded data parallelism, parallel/zero.py): only
+    those flat ranges are updated; the clipping norm is the all-reduced sum
+    (over `group`) of the owned ranges' squared norms.  The caller zeroes
+    the gradients (the not-owned ranges hold this rank's unreduced ones)."""
 
     def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
-                 overlap=False, buckets=None, fuse_zero_grad=False, post_update=None):
+                 overlap=False, buckets=None, fuse_zero_grad=False, post_update=None, owned=None, group=None):
         self.post_update = post_update
+        self.owned = None if owned is None else [tuple(r) for r in owned]
+        self.group = group
+        if self.owned is not None and overlap:
+            raise ValueError("overlap mode and a sharded update are exclusive")
         self.flat = flat
         self.lr = lr
         self.beta1, self.beta2 = betas
@@ -102,6 +111,34 @@ class FlatAdamW:
                   float(self.weight_decay if decay else 0.0), self.step_count, float(grad_scale),
                   _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), stream)
 
+    def _work_runs(self):
+        """(a, b, decay) runs this rank updates."""
+        if self.owned is None:
+            yield from self.runs
+            return
+        for lo, hi in self.owned:
+            for a, b, decay in self.runs:
+                a2, b2 = max(a, lo), min(b, hi)
+                if a2 < b2:
+                    yield a2, b2, decay
+
+    def _norm_sq(self):
+        f = self.flat
+        if self.owned is None:
+            grad_norm_sq(f.grad, self._ws, self._norm)
+            return
+        import torch.distributed as dist
+
+        if _lib.use_hip(f.grad):
+            for i, (lo, hi) in enumerate(self.owned):
+                g = f.grad[lo:hi]
+                _lib.call("toa_sumsq", _lib.ptr(g), g.numel(), int(g.dtype == torch.bfloat16), _lib.ptr(self._ws),
+                          _lib.ptr(self._norm), int(i > 0), _lib.stream(g))
+        else:
+            self._norm.copy_(sum(f.grad[lo:hi].float().pow(2).sum() for lo, hi in self.owned).reshape(1))
+        if dist.is_initialized():
+            dist.all_reduce(self._norm, op=dist.ReduceOp.SUM, group=self.group)
+
     def wait_bucket(self, b):
         """Make the current stream wait until bucket b's parameters are updated."""
         if self.overlap and not self.waited[b]:
@@ -122,7 +159,7 @@ class FlatAdamW:
         lr = self.lr if lr is None else lr
         clip = self.max_grad_norm and self.max_grad_norm > 0
         if clip:
-            grad_norm_sq(f.grad, self._ws, self._norm)
+            self._norm_sq()
         if self.overlap and f.param.dtype == torch.bfloat16:
             main = torch.cuda.current_stream(f.device)
             self.side.wait_stream(main)
@@ -151,21 +188,22 @@ class FlatAdamW:
         if _lib.use_hip(f.grad):
             s = _lib.stream(f.grad)
             pbf = f.param.dtype == torch.bfloat16
-            for (a, b, decay) in self.runs:
+            for (a, b, decay) in self._work_runs():
                 self._launch(a, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
-            self.grads_zeroed = self.fuse_zero_grad
+            self.grads_zeroed = self.fuse_zero_grad and self.owned is None
             if not pbf:
                 f.param.copy_(f.master)
             if self.post_update is not None:
                 self.post_update(0, f.numel)
         else:
-            for (a, b, decay) in self.runs:
+            for (a, b, decay) in self._work_runs():
                 adamw_reference(f.master[a:b], f.grad[a:b], f.exp_avg[a:b], f.exp_avg_sq[a:b], lr=lr,
                                 beta1=self.beta1, beta2=self.beta2, eps=self.eps,
                                 weight_decay=self.weight_decay if decay else 0.0, step=self.step_count,
                                 grad_scale=grad_scale, norm_sq=self._norm if clip else None,
                                 max_norm=self.max_grad_norm or 0.0)
-            f.param.copy_(f.master.to(f.param.dtype))
+            for lo, hi in (self.owned or [(0, f.numel)]):
+                f.param[lo:hi].copy_(f.master[lo:hi].to(f.param.dtype))
             if self.post_update is not None:
                 self.post_update(0, f.numel)
 

@@ -23,14 +23,21 @@ import os
 import torch
 import torch.distributed as dist
 
+from . import zero
 from .flat import FlatParams, _round_up
 
 
 class GradBucketer:
-    def __init__(self, flat: FlatParams, bucket_bytes=None, group=None, average=True, enabled=None):
+    """shard=True: reduce-scatter each bucket instead of all-reducing it
+    (ZeRO-1, :mod:`tf_operator_amd.parallel.zero`); after finish() this
+    rank holds the summed gradient of ``owned`` only.  Falls back to
+    all-reduce when the world size does not divide the buckets."""
+
+    def __init__(self, flat: FlatParams, bucket_bytes=None, group=None, average=True, enabled=None, shard=False):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.enabled = (self.world > 1) if enabled is None else enabled
         self.average = average
         mb = float(os.environ.get("TOA_BUCKET_MB", "512"))
@@ -53,12 +60,16 @@ class GradBucketer:
             self.buckets[-1][1] = flat.numel
         self.pending = [b[2] for b in self.buckets]
         self.works = []
+        self.finishers = []
         self.launched = [False] * len(self.buckets)
+        self.shard = bool(shard) and self.enabled and zero.feasible(self.buckets, self.world)
+        self.owned = (zero.owned_ranges(self.buckets, self.world, self.rank) if self.shard
+                      else [(0, flat.numel)])
         # one-shot IPC all-reduce (parallel/ipc.py) for small models on one node:
         # TOA_IPC_ALLREDUCE=1, every rank local, the whole gradient fits a slot
         self.ipc = None
         nbytes = flat.grad.numel() * esz
-        if (self.enabled and os.environ.get("TOA_IPC_ALLREDUCE", "0") == "1" and flat.grad.is_cuda
+        if (self.enabled and not self.shard and os.environ.get("TOA_IPC_ALLREDUCE", "0") == "1" and flat.grad.is_cuda
                 and int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) == self.world and nbytes <= 64 << 20):
             from .ipc import IpcAllReduce
 
@@ -76,6 +87,12 @@ class GradBucketer:
         self.launched[b] = True
         s, e, _ = self.buckets[b]
         view = self.flat.grad[s:e]
+        if self.shard:
+            w, fin = zero.reduce_scatter_(view, self.rank, self.world, self.group)
+            self.works.append(w)
+            if fin is not None:
+                self.finishers.append(fin)
+            return
         if self.ipc is not None and self.ipc.fits(view):
             self.ipc(view)  # one-shot on the compute stream: latency-bound small gradients
             return
@@ -90,7 +107,10 @@ class GradBucketer:
                 self._launch(b)
         for w in self.works:
             w.wait()
+        for fin in self.finishers:
+            fin()
         self.works = []
+        self.finishers = []
         self.pending = [b[2] for b in self.buckets]
         self.launched = [False] * len(self.buckets)
 

@@ -1,0 +1,116 @@
+"""Sharded optimizer data parallelism (ZeRO stage 1) on the flat buffers.
+
+Plain DP (:class:`GradBucketer` with all-reduce) has every rank run the
+full AdamW: 28 B of HBM traffic per parameter, 43 ms per step at
+Llama-3-8B on one MI355X, whatever the world size.  Here each gradient
+bucket is split into ``world`` equal contiguous shards and
+
+1. backward: as a bucket's gradients complete, ``reduce_scatter`` (RCCL,
+   in place on the flat gradient buffer) leaves rank r the SUM of its
+   shard r -- half the bytes an all-reduce moves, issued at the same time;
+2. optimizer: each rank runs AdamW only over the shards it owns (the global
+   gradient norm is the all-reduced sum of the per-shard squared norms), so
+   the update costs 1/world of the replicated one;
+3. the updated bf16 shards are ``all_gather``-ed in place, bucket by
+   bucket in FORWARD order, on RCCL's stream; the next forward waits per
+   bucket in module pre-hooks (:meth:`ParamGather.wait`), so the gathers of
+   late layers run under the GEMMs of early ones.
+
+RS + AG move exactly the bytes of one ring all-reduce, so the xGMI traffic
+is unchanged; what shrinks is the optimizer (world x less HBM traffic) and
+its exposure at the end of the step.  fp32 master / m / v stay allocated
+full-size on every rank (only the owned shards are current): 288 GB of HBM
+holds them at 8B, and :func:`gather_state` can then assemble a full,
+world-size-independent checkpoint with in-place all-gathers.
+
+Shards must be a multiple of 8 elements (16-byte vectors in the AdamW
+kernel): with 64-element parameter padding that holds for world 1/2/4/8;
+other world sizes fall back to the all-reduce path (:func:`feasible`).
+
+Reference parity: the reference's only collective is the payloads'
+gradient all-reduce; sharding the update is the
+MI355X-first way of running that same data-parallel step.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def feasible(buckets, world: int) -> bool:
+    return world > 1 and all((e - s) % (8 * world) == 0 for s, e, *_ in buckets)
+
+
+def owned_ranges(buckets, world: int, rank: int):
+    """[(lo, hi)] of the flat buffer this rank updates: shard `rank` of
+    every bucket."""
+    out = []
+    for s, e, *_ in buckets:
+        n = (e - s) // world
+        out.append((s + rank * n, s + (rank + 1) * n))
+    return out
+
+
+def _is_nccl(group) -> bool:
+    return dist.get_backend(group) == "nccl"
+
+
+def reduce_scatter_(buf: torch.Tensor, rank: int, world: int, group=None, async_op=True):
+    """buf[shard rank] <- sum over ranks of buf[shard rank] (in place on
+    RCCL; gloo gets an out-of-place output copied back by the returned
+    finisher).  Returns (work, finisher)."""
+    n = buf.numel() // world
+    shard = buf[rank * n:(rank + 1) * n]
+    if _is_nccl(group):
+        return dist.reduce_scatter_tensor(shard, buf, op=dist.ReduceOp.SUM, group=group, async_op=async_op), None
+    out = torch.empty_like(shard)
+    w = dist.reduce_scatter_tensor(out, buf, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    return w, (lambda: shard.copy_(out))
+
+
+def all_gather_(buf: torch.Tensor, rank: int, world: int, group=None, async_op=True):
+    """Every rank's shard of `buf` to every rank, in place."""
+    n = buf.numel() // world
+    return dist.all_gather_into_tensor(buf, buf[rank * n:(rank + 1) * n], group=group, async_op=async_op)
+
+
+class ParamGather:
+    """In-place all-gather of the updated bf16 weights after a sharded
+    optimizer step, waited for per bucket by the next forward."""
+
+    def __init__(self, flat, buckets, rank, world, group=None, on_gathered=None):
+        self.flat = flat
+        self.ranges = [(b[0], b[1]) for b in buckets]
+        self.rank, self.world, self.group = rank, world, group
+        self.on_gathered = on_gathered  # fn(lo, hi) on the waiting stream (W^T refresh)
+        self.works = [None] * len(self.ranges)
+
+    def launch(self):
+        # flat order is backward order: the forward needs the last bucket first
+        for b in reversed(range(len(self.ranges))):
+            lo, hi = self.ranges[b]
+            self.works[b] = all_gather_(self.flat.param[lo:hi], self.rank, self.world, self.group)
+
+    def wait(self, b):
+        w = self.works[b]
+        if w is None:
+            return
+        self.works[b] = None
+        w.wait()  # RCCL: the current stream waits, the host does not
+        if self.on_gathered is not None:
+            self.on_gathered(*self.ranges[b])
+
+    def wait_all(self):
+        for b in range(len(self.ranges)):
+            self.wait(b)
+
+
+@torch.no_grad()
+def gather_state(flat, buckets, rank, world, group=None):
+    """Make master / exp_avg / exp_avg_sq complete on every rank (each rank
+    holds only its shards current).  Collective: every rank must call it."""
+    for t in (flat.master, flat.exp_avg, flat.exp_avg_sq):
+        if t is None:
+            continue
+        for s, e, *_ in buckets:
+            all_gather_(t[s:e], rank, world, group, async_op=False)

@@ -4,6 +4,11 @@ One process per GPU.  Per step: forward (fused HIP ops + hipBLASLt GEMMs),
 backward writing weight gradients straight into the flat bf16 gradient
 buffer, bucketed RCCL all-reduce overlapped with backward, one fused AdamW
 over the flat fp32 master/m/v (device-side grad clipping, no host sync).
+
+shard_optimizer=True (``TOA_ZERO=1``; bench.py's default for N > 1):
+reduce-scatter instead of all-reduce, AdamW over this rank's shards only,
+then an in-place all-gather of the bf16 weights that the next forward waits
+for per bucket (parallel/zero.py).
 """
 from __future__ import annotations
 
@@ -16,12 +21,15 @@ from ..models.llama import PRESETS, Llama, LlamaConfig
 from ..ops.optim import FlatAdamW
 from ..ops.wt import TransposedWeights, enabled_default
 from ..parallel.ddp import GradBucketer, broadcast_params
+from ..parallel import zero
 from ..parallel.flat import FlatParams
+from ..parallel.zero import ParamGather
 
 
 class LlamaTrainer:
     def __init__(self, cfg: LlamaConfig | str, device, micro_batch=1, seq_len=4096, grad_accum=1, lr=3e-4,
-                 seed=0, bucket_mb=None, overlap_optimizer=None):
+                 seed=0, bucket_mb=None, overlap_optimizer=None, shard_optimizer=None,
+                 transposed_weights=None):
         if isinstance(cfg, str):
             cfg = PRESETS[cfg]
         self.cfg = cfg
@@ -36,32 +44,48 @@ class LlamaTrainer:
         names = {id(p): n for n, p in model.named_parameters()}
         self.flat = FlatParams(model.params_backward_order(), names=names, no_decay=model.no_decay)
         self.wt = None
-        if enabled_default(device):  # dgrad on W^T (ops/wt.py): +2 B/param of HBM
+        if transposed_weights is None:
+            transposed_weights = enabled_default(device)
+        if transposed_weights:  # dgrad on W^T (ops/wt.py): +2 B/param of HBM
             lin = [p for n, p in model.named_parameters() if p.dim() == 2 and not n.startswith("embed.")]
             lin += [model.head_weight()]
             self.wt = TransposedWeights(self.flat, lin)
         broadcast_params(self.flat)
-        self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20))
-        if overlap_optimizer is None:
-            overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
-        self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
-                             fuse_zero_grad=True, post_update=self.wt.refresh if self.wt else None)
-        if self.opt.overlap:
+        if shard_optimizer is None:
+            shard_optimizer = os.environ.get("TOA_ZERO", "0") == "1"
+        self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20),
+                                     shard=shard_optimizer)
+        self.gather = None
+        if self.bucketer.shard:  # ZeRO-1: reduce-scatter, owned-shard AdamW, in-place all-gather
+            self.opt = FlatAdamW(self.flat, lr=lr, owned=self.bucketer.owned)
+            self.gather = ParamGather(self.flat, self.bucketer.buckets, self.bucketer.rank, self.bucketer.world,
+                                      on_gathered=self.wt.refresh if self.wt else None)
+        else:
+            if overlap_optimizer is None:
+                overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
+            self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
+                                 fuse_zero_grad=True, post_update=self.wt.refresh if self.wt else None)
+        if self.opt.overlap or self.gather is not None:
             self._hooks = self._install_param_waits()
         self.step_idx = 0
 
+    def _wait_bucket(self, b):
+        self.opt.wait_bucket(b)
+        if self.gather is not None:
+            self.gather.wait(b)
+
     def _install_param_waits(self):
         """Forward pre-hooks: each module waits only for the buckets holding
-        its own parameters (FlatAdamW overlap mode).  The root's direct
-        parameter (the untied lm_head) is used right after the final norm,
-        so that wait rides on the final norm's hook instead of the root's."""
-        opt = self.opt
+        its own parameters (FlatAdamW overlap mode; the sharded update's
+        parameter all-gather).  The root's direct parameter (the untied
+        lm_head) is used right after the final norm, so that wait rides on
+        the final norm's hook instead of the root's."""
         hooks = []
 
         def waiter(buckets):
             def hook(mod, args):
                 for b in buckets:
-                    opt.wait_bucket(b)
+                    self._wait_bucket(b)
             return hook
 
         root_params = list(self.model.parameters(recurse=False))
@@ -91,10 +115,14 @@ class LlamaTrainer:
         for i, (tok, tgt) in enumerate(batches):
             loss = self.model(tok, tgt)
             self.opt.wait_all()  # backward writes gradients the update is still zeroing
+            if self.gather is not None:
+                self.gather.wait_all()  # backward reads every weight (and W^T)
             (loss / len(batches)).backward()
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
         self.bucketer.finish()
         self.opt.step(grad_scale=self.bucketer.grad_scale)
+        if self.gather is not None:
+            self.gather.launch()
         self.step_idx += 1
         return loss_sum / len(batches)
 
@@ -113,13 +141,21 @@ def timed_steps(trainer: LlamaTrainer, batches, n, sync=True):
 
 
 def trainer_state(tr: LlamaTrainer):
+    """Full, world-size-independent training state.  With the sharded
+    optimizer this is a COLLECTIVE (every rank must call it): the owned
+    master / moment shards are all-gathered first."""
     tr.opt.wait_all()
+    if tr.gather is not None:
+        tr.gather.wait_all()
+        zero.gather_state(tr.flat, tr.bucketer.buckets, tr.bucketer.rank, tr.bucketer.world)
     return {"flat": tr.flat.state_dict(), "opt": tr.opt.state_dict(), "step": tr.step_idx}
 
 
 def load_trainer_state(tr: LlamaTrainer, st):
     dev = tr.flat.device
     tr.opt.wait_all()
+    if tr.gather is not None:
+        tr.gather.wait_all()
     tr.flat.load_state_dict({k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in st["flat"].items()})
     tr.opt.load_state_dict(st["opt"])
     tr.step_idx = int(st["step"])
