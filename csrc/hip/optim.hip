@@ -82,7 +82,13 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
                                                          float* __restrict__ v, int64_t n8, float lr, float b1,
                                                          float b2, float eps, float wd, float inv_bc1,
                                                          float inv_sqrt_bc2, float grad_scale,
-                                                         const float* __restrict__ norm_sq, float max_norm) {
+                                                         const float* __restrict__ norm_sq, float max_norm,
+                                                         const int* __restrict__ step_dev) {
+  if (step_dev != nullptr) {  // graph-replayable form: the step count lives on the device
+    const float st = (float)step_dev[0];
+    inv_bc1 = 1.f / (1.f - powf(b1, st));
+    inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(b2, st));
+  }
   float scale = grad_scale;
   if (norm_sq != nullptr && max_norm > 0.f) {
     float nrm = sqrtf(norm_sq[0]) * grad_scale;
@@ -136,10 +142,9 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
 
 // grad_flags: bit 0 = grad is bf16 (else fp32); bit 1 = zero the gradient
 // after reading it (the next step's zero_grad pass, fused).
-extern "C" int toa_adamw_flat(float* master, bf16_t* param, void* grad, int grad_flags, float* m,
-                              float* v, int64_t n, float lr, float beta1, float beta2, float eps,
-                              float weight_decay, int step, float grad_scale, const float* norm_sq,
-                              float max_norm, hipStream_t stream) {
+static int adamw_launch(float* master, bf16_t* param, void* grad, int grad_flags, float* m, float* v, int64_t n,
+                        float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale,
+                        const float* norm_sq, float max_norm, const int* step_dev, hipStream_t stream) {
   if (n % 8 != 0) return (int)hipErrorInvalidValue;
   const int64_t n8 = n / 8;
   const float bc1 = 1.f - powf(beta1, (float)step);
@@ -150,11 +155,38 @@ extern "C" int toa_adamw_flat(float* master, bf16_t* param, void* grad, int grad
   if (grad_flags & 1)
     hipLaunchKernelGGL(adamw_flat_kernel<true>, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8,
                        lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
-                       max_norm);
+                       max_norm, step_dev);
   else
     hipLaunchKernelGGL(adamw_flat_kernel<false>, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8,
                        lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
-                       max_norm);
+                       max_norm, step_dev);
+  return (int)hipGetLastError();
+}
+
+extern "C" int toa_adamw_flat(float* master, bf16_t* param, void* grad, int grad_flags, float* m,
+                              float* v, int64_t n, float lr, float beta1, float beta2, float eps,
+                              float weight_decay, int step, float grad_scale, const float* norm_sq,
+                              float max_norm, hipStream_t stream) {
+  return adamw_launch(master, param, grad, grad_flags, m, v, n, lr, beta1, beta2, eps, weight_decay, step, grad_scale,
+                      norm_sq, max_norm, nullptr, stream);
+}
+
+// Same update with the step count read from device memory (step_dev[0], the
+// step being taken): a captured HIP graph replays it with fresh bias
+// corrections.  toa_step_inc advances the counter inside the same graph.
+extern "C" int toa_adamw_flat_dstep(float* master, bf16_t* param, void* grad, int grad_flags, float* m, float* v,
+                                    int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
+                                    const int* step_dev, float grad_scale, const float* norm_sq, float max_norm,
+                                    hipStream_t stream) {
+  if (step_dev == nullptr) return (int)hipErrorInvalidValue;
+  return adamw_launch(master, param, grad, grad_flags, m, v, n, lr, beta1, beta2, eps, weight_decay, 1, grad_scale,
+                      norm_sq, max_norm, step_dev, stream);
+}
+
+__global__ void step_inc_kernel(int* step) { step[0] += 1; }
+
+extern "C" int toa_step_inc(int* step, hipStream_t stream) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, stream, step);
   return (int)hipGetLastError();
 }
 

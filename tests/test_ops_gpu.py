@@ -505,3 +505,76 @@ def test_flash_attention_bshd_output_layout(B, H, Hk, S):
     o2.backward(do)
     for a, b in ((q1, q2), (k1, k2), (v1, v2)):
         assert torch.equal(a.grad, b.grad)
+
+
+def _mnist_trainer(graph, lr=0.01):
+    from tf_operator_amd.models.vision import MnistMLP
+    from tf_operator_amd.ops.llm import cross_entropy
+    from tf_operator_amd.train import simple
+
+    class _RT:
+        is_chief, rank, world = True, 0, 1
+
+        def first_step_done(self):
+            pass
+
+        def log(self, msg):
+            print(msg)
+
+    torch.manual_seed(0)
+    model = MnistMLP(100, dtype=torch.bfloat16, device=DEV)
+    return simple.DPTrainer(model, lambda o, y: cross_entropy(o.float(), y), _RT(), lr=lr, graph=graph)
+
+
+def test_dp_trainer_hip_graph_matches_eager():
+    """The captured whole-step HIP graph (device-side Adam step count, input
+    copies + one replay per step, re-capture on a learning-rate change)
+    follows the eager step."""
+    _lib()
+    from tf_operator_amd.train.data import SyntheticMNIST
+
+    runs = []
+    for graph in (False, True):
+        tr = _mnist_trainer(graph)
+        assert tr.use_graph == graph
+        data = SyntheticMNIST(100, device=DEV, dtype=torch.bfloat16, pool=16)
+        losses = []
+        for i in range(12):
+            if i == 8:
+                tr.opt.lr = 0.002  # per-epoch decay: the graph must pick it up
+            x, y = data.next()
+            loss, _ = tr.step(x, y)
+            losses.append(float(loss))
+        if graph:
+            assert tr._graph is not None and tr._key[0] == 0.002
+            assert tr.opt.sync_step_count() == 12
+        runs.append((losses, tr.flat.master.clone()))
+    (l0, m0), (l1, m1) = runs
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-3, (l0, l1)
+    assert float((m0 - m1).abs().max()) <= 1e-4 * float(m0.abs().max()) + 1e-6
+
+
+def test_adamw_device_step_matches_host_step():
+    _lib()
+    from tf_operator_amd.ops import _lib as L
+
+    n = 4096
+    out = []
+    for dev_step in (False, True):
+        torch.manual_seed(3)
+        master = torch.randn(n, device=DEV)
+        g = torch.randn(n, device=DEV)
+        m = torch.zeros(n, device=DEV)
+        v = torch.zeros(n, device=DEV)
+        st = torch.zeros(1, device=DEV, dtype=torch.int32)
+        for k in range(1, 6):
+            s = L.stream(master)
+            if dev_step:
+                L.call("toa_step_inc", L.ptr(st), s)
+                L.call("toa_adamw_flat_dstep", L.ptr(master), None, L.ptr(g), 0, L.ptr(m), L.ptr(v), n, 1e-3, 0.9,
+                       0.999, 1e-8, 0.01, L.ptr(st), 1.0, None, 0.0, s)
+            else:
+                L.call("toa_adamw_flat", L.ptr(master), None, L.ptr(g), 0, L.ptr(m), L.ptr(v), n, 1e-3, 0.9, 0.999,
+                       1e-8, 0.01, k, 1.0, None, 0.0, s)
+        out.append(master)
+    assert float((out[0] - out[1]).abs().max()) < 1e-6

@@ -39,7 +39,8 @@ def main(argv=None):
     torch.manual_seed(0)
     model = KerasCNN(dtype=model_dtype(dev), device=dev)
     tr = simple.DPTrainer(model, lambda o, y: cross_entropy(o.float(), y), rt, lr=decay(0))
-    data = SyntheticMNIST(a.batch_per_replica, rt.rank, rt.world, device=dev, image=True, dtype=model_dtype(dev))
+    data = SyntheticMNIST(a.batch_per_replica, rt.rank, rt.world, device=dev, image=True, dtype=model_dtype(dev),
+                          pool=a.steps_per_epoch)
     start = tr.maybe_resume(a.saved_model_dir)
     if start:
         rt.log(f"resumed from checkpoint at step {start} (epoch {start // a.steps_per_epoch})")

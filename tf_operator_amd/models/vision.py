@@ -24,6 +24,8 @@ class MnistMLP(torch.nn.Module):
         super().__init__()
         self.hid = DenseAct(784, hidden, "relu", dtype, device, keep_prob=keep_prob)
         self.sm = DenseAct(hidden, 10, "none", dtype, device)
+        # dropout draws a fresh host seed per call: a captured graph would freeze it
+        self.graph_safe = keep_prob >= 1.0
 
     def forward(self, x):
         return self.sm(self.hid(x.reshape(x.shape[0], -1)))

@@ -67,8 +67,15 @@ class FlatAdamW:
     the gradients (the not-owned ranges hold this rank's unreduced ones)."""
 
     def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
-                 overlap=False, buckets=None, fuse_zero_grad=False, post_update=None, owned=None, group=None):
+                 overlap=False, buckets=None, fuse_zero_grad=False, post_update=None, owned=None, group=None,
+                 device_step=False):
         self.post_update = post_update
+        # device_step: the step count lives in device memory and is advanced
+        # by a kernel, so a captured HIP graph of the whole training step
+        # replays with fresh bias corrections (train/simple.py graph mode)
+        self.device_step = (bool(device_step) and flat.device.type == "cuda" and _lib.available()
+                            and _lib.has("toa_adamw_flat_dstep"))
+        self._dstep = torch.zeros(1, device=flat.device, dtype=torch.int32) if self.device_step else None
         self.owned = None if owned is None else [tuple(r) for r in owned]
         self.group = group
         if self.owned is not None and overlap:
@@ -105,10 +112,12 @@ class FlatAdamW:
         f = self.flat
         gflags = int(f.grad.dtype == torch.bfloat16) | (2 if zero else 0)
         pp = f.param.data_ptr() + 2 * a if f.param.dtype == torch.bfloat16 else None
-        _lib.call("toa_adamw_flat", f.master.data_ptr() + 4 * a, pp, f.grad.data_ptr() + f.grad.element_size() * a,
+        fn, step = ("toa_adamw_flat_dstep", _lib.ptr(self._dstep)) if self.device_step else ("toa_adamw_flat",
+                                                                                             self.step_count)
+        _lib.call(fn, f.master.data_ptr() + 4 * a, pp, f.grad.data_ptr() + f.grad.element_size() * a,
                   gflags, f.exp_avg.data_ptr() + 4 * a, f.exp_avg_sq.data_ptr() + 4 * a, b - a, float(lr),
                   float(self.beta1), float(self.beta2), float(self.eps),
-                  float(self.weight_decay if decay else 0.0), self.step_count, float(grad_scale),
+                  float(self.weight_decay if decay else 0.0), step, float(grad_scale),
                   _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), stream)
 
     def _work_runs(self):
@@ -188,6 +197,8 @@ class FlatAdamW:
         if _lib.use_hip(f.grad):
             s = _lib.stream(f.grad)
             pbf = f.param.dtype == torch.bfloat16
+            if self.device_step:
+                _lib.call("toa_step_inc", _lib.ptr(self._dstep), s)
             for (a, b, decay) in self._work_runs():
                 self._launch(a, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
             self.grads_zeroed = self.fuse_zero_grad and self.owned is None
@@ -207,11 +218,19 @@ class FlatAdamW:
             if self.post_update is not None:
                 self.post_update(0, f.numel)
 
+    def sync_step_count(self):
+        """Host copy of the device step count (after graph replays)."""
+        if self.device_step:
+            self.step_count = int(self._dstep.item())
+        return self.step_count
+
     def state_dict(self):
-        return {"step": self.step_count, "lr": self.lr}
+        return {"step": self.sync_step_count(), "lr": self.lr}
 
     def load_state_dict(self, sd):
         self.step_count = int(sd["step"])
+        if self.device_step:
+            self._dstep.fill_(self.step_count)
         self.lr = sd.get("lr", self.lr)
 
 

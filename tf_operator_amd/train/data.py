@@ -10,7 +10,12 @@ import torch
 
 
 class SyntheticMNIST:
-    def __init__(self, batch, rank=0, world=1, seed=0, device="cpu", image=False, dtype=torch.float32):
+    """pool > 0 on a GPU: the whole synthetic training set (`pool` batches,
+    e.g. 600 x 100 = one MNIST epoch, 188 MB) is generated once on the
+    device and next() hands out views of it, epoch after epoch -- no host
+    work or host-to-device copy per step (what a graph-replayed step needs)."""
+
+    def __init__(self, batch, rank=0, world=1, seed=0, device="cpu", image=False, dtype=torch.float32, pool=0):
         g = torch.Generator().manual_seed(1234)
         self.proj = torch.randn(784, 10, generator=g)
         self.batch = batch
@@ -18,8 +23,21 @@ class SyntheticMNIST:
         self.device = device
         self.image = image
         self.dtype = dtype
+        self.pool = None
+        if pool > 0 and torch.device(device).type == "cuda":
+            gd = torch.Generator(device=device).manual_seed(seed * 1000003 + rank)
+            x = torch.rand(pool, batch, 784, generator=gd, device=device)
+            y = (x @ self.proj.to(device)).argmax(-1)
+            if image:
+                x = x.view(pool, batch, 1, 28, 28)
+            self.pool = (x.to(dtype), y)
+            self.i = 0
 
     def next(self):
+        if self.pool is not None:
+            x, y = self.pool[0][self.i], self.pool[1][self.i]
+            self.i = (self.i + 1) % self.pool[0].shape[0]
+            return x, y
         x = torch.rand(self.batch, 784, generator=self.gen)
         y = (x @ self.proj).argmax(-1)
         if self.image:

@@ -4,6 +4,7 @@ RCCL/gloo all-reduce, fused HIP Adam/SGD, checkpoint/resume, first-step
 reporting.  The Llama path has its own trainer (:mod:`.llm`)."""
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -34,8 +35,20 @@ def attach_autograd_hooks(flat: FlatParams):
 
 
 class DPTrainer:
+    """graph=True (default on a GPU, ``TOA_HIP_GRAPH=0`` turns it off): after
+    GRAPH_WARMUP eager steps (run on a side stream, so every library handle
+    and workspace exists before capture) the whole training step -- zero
+    grad, forward, loss, backward, optimizer -- is captured once as a HIP
+    graph and each later step is two input copies plus one graph launch.
+    The bundled payloads' models are tiny (79K-400K parameters), so their
+    eager step is bound by kernel-launch overhead, not by the GPU.  Single
+    replica only (world size 1): multi-replica steps keep the eager path
+    with the bucketed all-reduce."""
+
+    GRAPH_WARMUP = 3
+
     def __init__(self, model, loss_fn, runtime, lr=1e-3, optimizer="adam", weight_decay=0.0, bucket_mb=None,
-                 max_grad_norm=0.0, grad_dtype=torch.float32):
+                 max_grad_norm=0.0, grad_dtype=torch.float32, graph=None):
         self.model = model
         self.loss_fn = loss_fn
         self.rt = runtime
@@ -46,26 +59,73 @@ class DPTrainer:
         attach_autograd_hooks(self.flat)
         broadcast_params(self.flat)
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20))
+        if graph is None:
+            graph = os.environ.get("TOA_HIP_GRAPH", "1") == "1"
+        self.use_graph = (bool(graph) and self.flat.device.type == "cuda" and not self.bucketer.enabled
+                          and getattr(model, "graph_safe", True))
         if optimizer == "adam":
             self.opt = FlatAdamW(self.flat, lr=lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=weight_decay,
-                                 max_grad_norm=max_grad_norm)
+                                 max_grad_norm=max_grad_norm, device_step=self.use_graph)
         else:
             self.opt = FlatSGD(self.flat, lr=lr, weight_decay=weight_decay)
         self.step_idx = 0
+        self._graph = None
+        self._side = torch.cuda.Stream(self.flat.device) if self.use_graph else None
 
-    def step(self, x, y):
+    def _body(self, x, y):
         self.flat.zero_grad()
         out = self.model(x)
         loss = self.loss_fn(out, y)
         loss.backward()
         self.bucketer.finish()
         self.opt.step(grad_scale=self.bucketer.grad_scale)
+        return loss.detach(), out.detach()
+
+    def _graph_key(self, x, y):
+        # host scalars a capture freezes: a new learning rate (per-epoch
+        # decay) or new input shapes re-capture
+        return (float(self.opt.lr), tuple(x.shape), tuple(y.shape), x.dtype, y.dtype)
+
+    def _capture(self, x, y):
+        self._sx, self._sy = x.detach().clone(), y.detach().clone()
+        torch.cuda.synchronize(self.flat.device)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self._sloss, self._sout = self._body(self._sx, self._sy)
+        except RuntimeError as e:  # an op that cannot be captured: stay eager
+            self.rt.log(f"HIP graph capture failed ({e}); continuing eagerly")
+            self.use_graph = False
+            self._graph = None
+            torch.cuda.synchronize(self.flat.device)
+            return
+        self._graph = g
+        self._key = self._graph_key(x, y)
+
+    def step(self, x, y):
+        if self._graph is not None and self._graph_key(x, y) != self._key:
+            self._graph = None
+        if self.use_graph and self._graph is None and self.step_idx >= self.GRAPH_WARMUP:
+            self._capture(x, y)  # records only: the replay below takes this step
+        if self._graph is not None:
+            self._sx.copy_(x, non_blocking=True)
+            self._sy.copy_(y, non_blocking=True)
+            self._graph.replay()
+            self.step_idx += 1
+            return self._sloss, self._sout
+        if self.use_graph:  # warm-up steps on a side stream (CUDA/HIP graph capture rules)
+            self._side.wait_stream(torch.cuda.current_stream(self.flat.device))
+            with torch.cuda.stream(self._side):
+                loss, out = self._body(x, y)
+            torch.cuda.current_stream(self.flat.device).wait_stream(self._side)
+        else:
+            loss, out = self._body(x, y)
         self.step_idx += 1
         if self.step_idx == 1:
             if torch.cuda.is_available() and x.is_cuda:
                 torch.cuda.synchronize()
             self.rt.first_step_done()
-        return loss.detach(), out.detach()
+        return loss, out
 
     # ------------------------------------------------------------------ checkpoint
     def state(self):
