@@ -141,35 +141,49 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const T* __restrict__
                                                            const T* __restrict__ Zpre, T* __restrict__ dZ,
                                                            float* __restrict__ db, int M, int N, int act,
                                                            float keep_prob, uint64_t seed) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+  // block = 32 columns x 8 row groups; each thread walks every 8th row (the
+  // loads are independent, so the unrolled loop keeps several in flight),
+  // then the 8 partial column sums meet in LDS
+  __shared__ float red[8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int n = blockIdx.x * 32 + tx;
   const uint32_t thresh = (uint32_t)fminf(keep_prob * 4294967296.f, 4294967295.f);
   float acc = 0.f;
-  for (int m = 0; m < M; ++m) {
-    const int64_t i = (int64_t)m * N + n;
-    float g = sizeof(T) == 2 ? bf2f(((const bf16_t*)dY)[i]) : ((const float*)dY)[i];
-    if (keep_prob < 1.f) g = keep_elem(seed, (uint64_t)i, thresh) ? g / keep_prob : 0.f;
-    if (act == 1) {
-      const float y = sizeof(T) == 2 ? bf2f(((const bf16_t*)Yo)[i]) : ((const float*)Yo)[i];
-      if (!(y > 0.f)) g = 0.f;
-    } else if (act == 2) {
-      const float z = sizeof(T) == 2 ? bf2f(((const bf16_t*)Zpre)[i]) : ((const float*)Zpre)[i];
-      const float cdf = 0.5f * (1.f + erff(z * 0.7071067811865476f));
-      const float pdf = 0.3989422804014327f * __expf(-0.5f * z * z);
-      g *= cdf + z * pdf;
+  if (n < N) {
+#pragma unroll 4
+    for (int m = ty; m < M; m += 8) {
+      const int64_t i = (int64_t)m * N + n;
+      float g = sizeof(T) == 2 ? bf2f(((const bf16_t*)dY)[i]) : ((const float*)dY)[i];
+      if (keep_prob < 1.f) g = keep_elem(seed, (uint64_t)i, thresh) ? g / keep_prob : 0.f;
+      if (act == 1) {
+        const float y = sizeof(T) == 2 ? bf2f(((const bf16_t*)Yo)[i]) : ((const float*)Yo)[i];
+        if (!(y > 0.f)) g = 0.f;
+      } else if (act == 2) {
+        const float z = sizeof(T) == 2 ? bf2f(((const bf16_t*)Zpre)[i]) : ((const float*)Zpre)[i];
+        const float cdf = 0.5f * (1.f + erff(z * 0.7071067811865476f));
+        const float pdf = 0.3989422804014327f * __expf(-0.5f * z * z);
+        g *= cdf + z * pdf;
+      }
+      if (sizeof(T) == 2)
+        ((bf16_t*)dZ)[i] = f2bf(g);
+      else
+        ((float*)dZ)[i] = g;
+      acc += g;
     }
-    if (sizeof(T) == 2)
-      ((bf16_t*)dZ)[i] = f2bf(g);
-    else
-      ((float*)dZ)[i] = g;
-    acc += g;
   }
-  if (db != nullptr) db[n] = acc;
+  red[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && n < N && db != nullptr) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][tx];  // fixed order: deterministic
+    db[n] = t;
+  }
 }
 
 extern "C" int toa_bias_act_bwd(int dtype, const void* dY, const void* Y, void* dZ, float* db, int M, int N, int act,
                                 hipStream_t stream) {
-  dim3 grid((N + 255) / 256);
+  dim3 grid((N + 31) / 32);
   if (dtype == 0)
     hipLaunchKernelGGL(bias_act_bwd_kernel<bf16_t>, grid, dim3(256), 0, stream, (const bf16_t*)dY, (const bf16_t*)Y,
                        (const bf16_t*)nullptr, (bf16_t*)dZ, db, M, N, act, 1.f, (uint64_t)0);
@@ -182,7 +196,7 @@ extern "C" int toa_bias_act_bwd(int dtype, const void* dY, const void* Y, void* 
 extern "C" int toa_bias_act_dropout_bwd(int dtype, const void* dY, const void* Y, const void* Zpre, void* dZ,
                                         float* db, int M, int N, int act, float keep_prob, uint64_t seed,
                                         hipStream_t stream) {
-  dim3 grid((N + 255) / 256);
+  dim3 grid((N + 31) / 32);
   if (dtype == 0)
     hipLaunchKernelGGL(bias_act_bwd_kernel<bf16_t>, grid, dim3(256), 0, stream, (const bf16_t*)dY, (const bf16_t*)Y,
                        (const bf16_t*)Zpre, (bf16_t*)dZ, db, M, N, act, keep_prob, seed);

@@ -578,3 +578,35 @@ def test_adamw_device_step_matches_host_step():
                        1e-8, 0.01, k, 1.0, None, 0.0, s)
         out.append(master)
     assert float((out[0] - out[1]).abs().max()) < 1e-6
+
+
+@pytest.mark.parametrize("N,K,T", [(100, 784, 100), (10, 100, 100), (64, 576, 64)])
+def test_wgrad_fp32_accumulate(N, K, T):
+    """bf16 dY^T X accumulated straight into an fp32 master gradient (one
+    hipBLASLt call, beta = 1) against an fp32 reference."""
+    _lib()
+    from tf_operator_amd.ops import gemm
+
+    torch.manual_seed(N + K)
+    dy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    g = torch.randn(N, K, device=DEV)
+    ref = g + dy.float().t() @ x.float()
+    gemm.wgrad_acc_(g, dy, x)
+    assert float((g - ref).abs().max()) <= 1e-3 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("M,N", [(100, 100), (100, 10), (150, 500), (1, 33)])
+def test_bias_act_bwd_column_sums(M, N):
+    _lib()
+    from tf_operator_amd.ops import _lib as L
+
+    torch.manual_seed(M * N)
+    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    y = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    dz = torch.empty_like(dy)
+    db = torch.empty(N, device=DEV)
+    L.call("toa_bias_act_bwd", 0, L.ptr(dy), L.ptr(y), L.ptr(dz), L.ptr(db), M, N, 1, L.stream(dy))
+    g = dy.float() * (y.float() > 0)
+    assert torch.equal(dz, g.to(torch.bfloat16))
+    assert float((db - g.sum(0)).abs().max()) <= 1e-4 * max(1.0, float(g.abs().sum(0).max()))

@@ -143,6 +143,14 @@ def wgrad_acc_(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float
     """g[N,K] = beta*g + dy2[M,N]^T @ x2[M,K]  (in place; g bf16 or fp32)."""
     if beta in (0.0, 1.0) and wgrad_hip_ok(g, dy2, x2):
         return wgrad_hip_(g, dy2, x2, beta)
+    if (g.dtype == torch.float32 and dy2.dtype == x2.dtype == torch.bfloat16 and g.is_cuda and g.is_contiguous()
+            and dy2.stride(1) == 1 and x2.stride(1) == 1 and _lib.has("toa_gemm")):
+        # fp32 master-gradient accumulation (small payloads): one hipBLASLt call
+        # with bf16 inputs, fp32 C/D and beta = 1 -- no bf16 temporary, cast or add
+        M, N = dy2.shape
+        K = x2.shape[1]
+        _gemm(0, 1, K, N, M, x2, x2.stride(0), dy2, dy2.stride(0), g, K, beta)
+        return g
     if not (_ok(dy2, x2) and g.is_contiguous() and g.dtype in (torch.bfloat16, torch.float32)):
         if beta == 0.0:
             g.copy_(torch.mm(dy2.t(), x2))

@@ -100,7 +100,7 @@ class _LinearBiasAct(torch.autograd.Function):
                 g = g * (cdf + zz * pdf)
             dz = g.to(dy.dtype)
             db = g.sum(0) if ctx.has_b else None
-        dx = (dz @ w.to(dz.dtype)).to(x.dtype)
+        dx = (dz @ w.to(dz.dtype)).to(x.dtype) if ctx.needs_input_grad[0] else None
         dw = accumulate_mm(w, dz.t().to(w.dtype), x.to(w.dtype))
         dbias = deliver_weight_grad(ctx.b, db) if ctx.has_b else None
         return dx, dw, dbias, None, None, None

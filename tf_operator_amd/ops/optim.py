@@ -90,7 +90,8 @@ class FlatAdamW:
         if flat.exp_avg is None:
             flat.exp_avg = torch.zeros(flat.numel, device=flat.device, dtype=torch.float32)
             flat.exp_avg_sq = torch.zeros(flat.numel, device=flat.device, dtype=torch.float32)
-        self.runs = flat.decay_runs()
+        # without weight decay the decay split is moot: one launch over the whole buffer
+        self.runs = flat.decay_runs() if weight_decay else [[0, flat.numel, False]]
         self._norm = torch.zeros(1, device=flat.device, dtype=torch.float32)
         self._ws = torch.empty(2048, device=flat.device, dtype=torch.float32)
         self.last_norm_sq = self._norm
