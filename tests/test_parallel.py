@@ -92,6 +92,55 @@ def test_bench_contract_torchrun_two_ranks():
     assert abs(res["value"] - 4 / (res["ms_per_step"] / 1000)) / res["value"] < 0.01
 
 
+def _capture_reduced_grad(tr, box):
+    """Wrap the optimizer so the first step records the reduced gradient."""
+    inner = tr.opt.step
+
+    def step(*a, **k):
+        if not box:
+            box.append(tr.flat.grad.float().clone())
+        return inner(*a, **k)
+
+    tr.opt.step = step
+
+
+def _accum_worker(rank, world, port, shard, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = LlamaTrainer("llama-tiny", torch.device("cpu"), micro_batch=2, seq_len=32, lr=1e-3, seed=0,
+                          bucket_mb=0.01, shard_optimizer=shard, grad_accum=2)
+        assert tr.bucketer.shard == shard
+        box = []
+        _capture_reduced_grad(tr, box)
+        batches = _batches(tr, 2 * world)
+        tr.step(batches[2 * rank:2 * rank + 2])
+        if rank == 0:
+            torch.save({"grad": box[0] * tr.bucketer.grad_scale, "owned": tr.bucketer.owned}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shard", [False, True])
+def test_grad_accumulation_reduces_once(tmp_path, shard):
+    """grad_accum=2 on 2 ranks reduces the same gradient as one process
+    accumulating all 4 micro-batches: collectives fire only after the last
+    micro-batch (an earlier reduce would be summed into again by the next
+    backward).  Compared where rank 0 owns the reduced gradient."""
+    world = 2
+    out = str(tmp_path / "acc.pt")
+    mp.spawn(_accum_worker, args=(world, _free_port(), shard, out), nprocs=world, join=True)
+    res = torch.load(out, weights_only=True)
+    ref = LlamaTrainer("llama-tiny", torch.device("cpu"), micro_batch=2, seq_len=32, lr=1e-3, seed=0, grad_accum=4)
+    box = []
+    _capture_reduced_grad(ref, box)
+    ref.step(_batches(ref, 2 * world))
+    for lo, hi in res["owned"]:
+        got, want = res["grad"][lo:hi], box[0][lo:hi]
+        assert float((got - want).abs().max()) <= 2e-2 * float(want.abs().max()) + 1e-6, (lo, hi)
+
+
 def _zero_worker(rank, world, port, bucket_mb, steps, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(1)

@@ -61,6 +61,9 @@ class GradBucketer:
         self.pending = [b[2] for b in self.buckets]
         self.works = []
         self.finishers = []
+        # with gradient accumulation only the LAST micro-batch's backward may
+        # launch collectives (the trainer disarms the others); armed by default
+        self.armed = True
         self.launched = [False] * len(self.buckets)
         self.shard = bool(shard) and self.enabled and zero.feasible(self.buckets, self.world)
         self.owned = (zero.owned_ranges(self.buckets, self.world, self.rank) if self.shard
@@ -76,6 +79,8 @@ class GradBucketer:
             self.ipc = IpcAllReduce(group, slot_bytes=max(1 << 20, nbytes))
 
     def _ready(self, param):
+        if not self.armed:  # an accumulation micro-step: gradients keep summing locally
+            return
         b = param._toa_bucket
         self.pending[b] -= 1
         if self.pending[b] == 0:

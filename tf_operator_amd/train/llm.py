@@ -117,8 +117,10 @@ class LlamaTrainer:
             self.opt.wait_all()  # backward writes gradients the update is still zeroing
             if self.gather is not None:
                 self.gather.wait_all()  # backward reads every weight (and W^T)
+            self.bucketer.armed = i == len(batches) - 1  # reduce once, after the last micro-batch
             (loss / len(batches)).backward()
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
+        self.bucketer.armed = True
         self.bucketer.finish()
         self.opt.step(grad_scale=self.bucketer.grad_scale)
         if self.gather is not None:
