@@ -89,6 +89,39 @@ static std::string master_role_type(const KindInfo& ki, const Json& specs) {
   return "Master";
 }
 
+// Annotation amd.com/rocprof = kernel-trace | stats | pmc:C1,C2 (new; the
+// reference has no profiler hook): the replica's main container (the kind's
+// default container, else the first) runs its command under the profiling
+// launcher tf_operator_amd/utils/profiling.py, output in
+// <amd.com/rocprof-dir, default /tmp/rocprof>/<pod>.  A container without an
+// explicit command (image entrypoint) is left alone.
+static void wrap_rocprof(const Json& ann, const KindInfo& ki, const std::string& pod, Json& pspec) {
+  if (!ann.is_object()) return;
+  const std::string mode = ann.get("amd.com/rocprof").str();
+  if (mode.empty()) return;
+  std::string dir = ann.get("amd.com/rocprof-dir").str("/tmp/rocprof");
+  if (dir.empty()) dir = "/tmp/rocprof";
+  Json& cs = pspec["containers"];
+  if (!cs.is_array() || cs.size() == 0) return;
+  size_t target = 0;
+  for (size_t i = 0; i < cs.size(); ++i)
+    if (cs[i].get("name").str() == ki.container) {
+      target = i;
+      break;
+    }
+  Json& c = cs.at(target);
+  const Json cmd = c.get("command");
+  if (!cmd.is_array() || cmd.size() == 0) return;
+  Json wrapped = Json::array();
+  for (const char* w : {"python3", "-m", "tf_operator_amd.utils.profiling", "--mode"}) wrapped.push_back(w);
+  wrapped.push_back(mode);
+  wrapped.push_back("--out");
+  wrapped.push_back(dir + "/" + pod);
+  wrapped.push_back("--");
+  for (const auto& x : cmd.items()) wrapped.push_back(x);
+  c.set("command", wrapped);
+}
+
 static Json new_pod(const Json& job, const KindInfo& ki, const std::string& rtype, int index, const Json& spec,
                     const Options& opt, Json& events) {
   const Json& md = job.get("metadata");
@@ -111,6 +144,7 @@ static Json new_pod(const Json& job, const KindInfo& ki, const std::string& rtyp
   tmd.set("labels", labels);
   tmd.set("name", gen_general_name(name, rt, std::to_string(index)));
   set_cluster_spec(job, tpl, rtype, index, opt);
+  wrap_rocprof(md.get("annotations"), ki, tmd.get("name").str(), tpl["spec"]);
   Json& ps = tpl["spec"];
   if (!ps.get("restartPolicy").str().empty())
     add_event(events, "Warning", "SettedPodTemplateRestartPolicy",

@@ -19,6 +19,7 @@ from tf_operator_amd.ops.mlp import accuracy
 from tf_operator_amd.train import simple
 from tf_operator_amd.train.data import SyntheticMNIST
 from tf_operator_amd.train.runtime import Runtime
+from tf_operator_amd.utils.profiling import trace_step
 
 
 class SummaryWriter:
@@ -38,6 +39,9 @@ def main(argv=None):
     p.add_argument("--batch_size", type=int, default=150)
     p.add_argument("--dropout", type=float, default=0.9, help="keep probability")
     p.add_argument("--log_dir", default=os.environ.get("TOA_LOG_DIR", "/tmp/tensorflow/mnist/logs"))
+    p.add_argument("--trace_every", type=int, default=100,
+                   help="FULL_TRACE analog (mnist_with_summaries.py:162-171): every N-th step runs under "
+                        "torch.profiler and is written as a Chrome trace; 0 disables")
     a = p.parse_args(argv)
     rt = Runtime()
     rt.init_dist()
@@ -51,7 +55,12 @@ def main(argv=None):
     for i in range(1, a.max_steps + 1):
         x, y = data.next()
         model.train()
-        loss, _ = tr.step(x, y)
+        if a.trace_every and i % a.trace_every == a.trace_every - 1:
+            path = os.path.join(a.log_dir, "train", f"trace_step{i}.json")
+            loss, _ = trace_step(lambda: tr.step(x, y), path)
+            sw.scalar("trace_written", 1, i)
+        else:
+            loss, _ = tr.step(x, y)
         if i % 10 == 0:
             model.eval()
             with torch.no_grad():
@@ -59,9 +68,6 @@ def main(argv=None):
             sw.scalar("accuracy", acc, i)
             sw.scalar("cross_entropy", float(loss), i)
             rt.log(f"Accuracy at step {i}: {acc:.3f}")
-        if i % 100 == 99 and torch.cuda.is_available():
-            torch.cuda.synchronize()
-            sw.scalar("trace_marker", 1, i)
     rt.report(samples_per_sec=None)
 
 
