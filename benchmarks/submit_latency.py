@@ -87,10 +87,14 @@ def main():
     p.add_argument("--gpus", type=int, default=None, help="node GPUs (default: workers if --gpus-per-worker)")
     p.add_argument("--gpus-per-worker", type=int, default=1)
     p.add_argument("--timeout", type=float, default=600)
+    p.add_argument("--warm", action="store_true", help="start replicas from the kubelet's warm fork server")
     a = p.parse_args()
     node_gpus = a.gpus if a.gpus is not None else (a.workers if a.gpus_per_worker else 0)
     runs = []
-    with LocalCluster(gpus=node_gpus, grace_seconds=5.0) as c:
+    with LocalCluster(gpus=node_gpus, grace_seconds=5.0, warm_python=a.warm) as c:
+        if a.warm:
+            c.wait(lambda: c.kubelet._fs_ready is not None and c.kubelet._fs_ready.is_set(), 300,
+                   what="fork server ready")
         for i in range(a.repeats):
             r = one_run(c, i, a)
             runs.append(r)
@@ -102,7 +106,7 @@ def main():
 
     out = {"metric": "p50 submit->first-step latency", "unit": "s", "value": med("total"),
            "p90": round(tot[min(len(tot) - 1, int(0.9 * len(tot)))], 4), "min": round(tot[0], 4),
-           "max": round(tot[-1], 4), "repeats": len(runs), "n_gpus": a.workers * a.gpus_per_worker,
+           "max": round(tot[-1], 4), "repeats": len(runs), "warm_start": a.warm, "n_gpus": a.workers * a.gpus_per_worker,
            "breakdown_p50": {"submit_to_pods_created": med("to_pods"), "submit_to_processes_spawned": med("to_spawn"),
                              "spawn_to_first_step": med("spawn_to_first"),
                              **{k[6:]: med(k) for k in runs[0] if k.startswith("phase:")

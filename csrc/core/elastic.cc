@@ -128,7 +128,7 @@ ElasticPlan elastic_prepass(Json& job, const Json& pods, Json& status, double no
   for (const auto& p : pods.items()) (pod_generation(p) == gen ? current : stale).push_back(p);
 
   const bool terminal = is_succeeded(status) || is_failed(status);
-  std::string reason;
+  std::string reason, peer_reason;
   bool failure = false;
   if (!terminal && stale.size() == 0) {
     int64_t expected = 0;
@@ -140,12 +140,16 @@ ElasticPlan elastic_prepass(Json& job, const Json& pods, Json& status, double no
       if (ph == "Running") running++;
       if (ph == "Succeeded") succeeded++;
       if (!pod_deleting(p)) present++;
-      if (ph == "Failed" && reason.empty()) {
+      if (ph == "Failed") {
         const int code = exit_code_of(p, ki.container);
         const std::string& rp = policy[rt];
         if (is_retryable_exit_code(code) || rp == "OnFailure" || rp == "Always") {
           failure = true;
-          reason = p.path({"metadata", "name"}).str() + " failed with exit code " + std::to_string(code);
+          // survivors of a lost peer exit 143 (PEER_LOST_EXIT, train/runtime.py):
+          // the reason names the member whose failure started the restart
+          std::string& slot = code == 143 ? peer_reason : reason;
+          if (slot.empty())
+            slot = p.path({"metadata", "name"}).str() + " failed with exit code " + std::to_string(code);
         }
       }
       if (launched && pod_deleting(p) && reason.empty()) {
@@ -157,6 +161,7 @@ ElasticPlan elastic_prepass(Json& job, const Json& pods, Json& status, double no
       failure = true;
       reason = "a member of generation " + std::to_string(gen) + " disappeared";
     }
+    if (reason.empty()) reason = peer_reason;
     if (!launched && running == expected && expected > 0) {
       launched = true;
       es.set("launchTime", rfc3339(now));

@@ -116,6 +116,21 @@ def test_retryable_failure_restarts_whole_group():
     assert s.es()["launched"] and "lastResumeSeconds" in s.es()
 
 
+def test_restart_reason_names_the_root_failure_not_a_lost_peer():
+    # survivors of a killed worker exit 143 (PEER_LOST_EXIT), possibly first
+    s = Sim(elastic_job())
+    launch(s, free=4)
+    s.fail("test-tfjob-worker-0", 143)
+    s.fail("test-tfjob-worker-3", 137)
+    s.sync(free=4)
+    assert s.es()["lastTransitionReason"].endswith("test-tfjob-worker-3 failed with exit code 137")
+    s2 = Sim(elastic_job())
+    launch(s2, free=4)
+    s2.fail("test-tfjob-worker-1", 143)
+    s2.sync(free=4)
+    assert "test-tfjob-worker-1 failed with exit code 143" in s2.es()["lastTransitionReason"]
+
+
 def test_preemption_shrinks_to_capacity_then_grows_back():
     s = Sim(elastic_job(scaleUpCooldownSeconds=10))
     launch(s, free=4)

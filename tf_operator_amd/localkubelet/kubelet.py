@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import asyncio
 import copy
+import json
 import logging
 import os
 import re
@@ -81,10 +82,41 @@ class _Proc:
         self.deleting = False
 
 
+class _ForkedProc:
+    """asyncio.subprocess.Process look-alike for a child of the fork server."""
+
+    def __init__(self, pid):
+        self.pid = pid
+        self.returncode = None
+        self._done = asyncio.get_running_loop().create_future()
+
+    def _exited(self, status):
+        self.returncode = status
+        if not self._done.done():
+            self._done.set_result(status)
+
+    async def wait(self):
+        return await asyncio.shield(self._done)
+
+
 class LocalKubelet:
+    """warm_python (opt-in; ``TOA_KUBELET_WARM=1`` turns it on): Python
+    containers start as forks of a warm interpreter that has already imported
+    torch (``forkserver.py``) instead of a cold ``python`` process."""
+
     def __init__(self, kube: KubeClient, api=None, node_name="mi355x-node-0", gpus=0, workdir="/tmp/toa-kubelet",
-                 python=sys.executable, grace_seconds=3.0, restart_backoff=0.2, gpu_resource="amd.com/gpu"):
+                 python=sys.executable, grace_seconds=3.0, restart_backoff=0.2, gpu_resource="amd.com/gpu",
+                 warm_python=None):
         self.kube = kube
+        if warm_python is None:
+            warm_python = os.environ.get("TOA_KUBELET_WARM", "0") == "1"
+        self.warm_python = warm_python
+        self._fs = None  # fork server process
+        self._fs_ready = None
+        self._fs_pending: dict[int, asyncio.Future] = {}
+        self._fs_procs: dict[int, _ForkedProc] = {}
+        self._fs_exits: dict[int, int] = {}
+        self._fs_seq = 0
         self.api = api
         if api is not None:
             api.kubelet = self
@@ -315,8 +347,10 @@ class LocalKubelet:
                 self.start_times.setdefault(key, []).append(p.started_at)
                 p.exit_code = None
                 try:
-                    p.proc = await asyncio.create_subprocess_exec(*argv, stdout=lf, stderr=subprocess.STDOUT,
-                                                                  env=env, cwd=d, start_new_session=True)
+                    p.proc = await self._warm_spawn(argv, env, d, logf)
+                    if p.proc is None:
+                        p.proc = await asyncio.create_subprocess_exec(*argv, stdout=lf, stderr=subprocess.STDOUT,
+                                                                      env=env, cwd=d, start_new_session=True)
                 except (FileNotFoundError, PermissionError, IndexError) as e:
                     lf.write(f"failed to start container: {e}\n".encode())
                     p.proc = None
@@ -338,6 +372,76 @@ class LocalKubelet:
             await asyncio.sleep(min(5.0, self.restart_backoff * (2 ** min(p.restart_count - 1, 5))))
             if p.deleting or self._stop.is_set():
                 return
+
+    # ---------------------------------------------------------------- warm starts
+    async def _start_forkserver(self):
+        env = dict(os.environ)
+        env["PYTHONPATH"] = REPO_ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        env.pop("HIP_VISIBLE_DEVICES", None)
+        self._fs_ready = asyncio.Event()
+        self._fs_lock = asyncio.Lock()
+        self._fs = await asyncio.create_subprocess_exec(self.python, "-m", "tf_operator_amd.localkubelet.forkserver",
+                                                        stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=env,
+                                                        cwd=REPO_ROOT, start_new_session=True)
+        self._tasks.append(asyncio.create_task(self._forkserver_reader()))
+
+    async def _forkserver_reader(self):
+        while True:
+            line = await self._fs.stdout.readline()
+            if not line:
+                break
+            try:
+                msg = json.loads(line)
+            except ValueError:
+                continue
+            if "ready" in msg:
+                self._fs_ready.set()
+            elif "exit" in msg:
+                pr = self._fs_procs.pop(msg["exit"], None)
+                if pr is not None:
+                    pr._exited(int(msg["status"]))
+                else:
+                    self._fs_exits[msg["exit"]] = int(msg["status"])
+            elif "id" in msg:
+                fut = self._fs_pending.pop(msg["id"], None)
+                if fut is not None and not fut.done():
+                    fut.set_result(msg)
+        self._fs_ready.clear()  # server gone: cold starts from here on
+        for fut in self._fs_pending.values():
+            if not fut.done():
+                fut.set_result({"error": "fork server exited"})
+        self._fs_pending.clear()
+        for pr in list(self._fs_procs.values()):
+            pr._exited(-signal.SIGKILL)
+        self._fs_procs.clear()
+
+    async def _warm_spawn(self, argv, env, cwd, logpath):
+        """Fork the container off the warm interpreter; None = use a cold start."""
+        if not (self.warm_python and self._fs is not None and self._fs_ready.is_set() and len(argv) >= 2
+                and argv[0] == self.python and (argv[1] in ("-m", "-c") or argv[1].endswith(".py"))):
+            return None
+        self._fs_seq += 1
+        rid = self._fs_seq
+        fut = asyncio.get_running_loop().create_future()
+        self._fs_pending[rid] = fut
+        req = {"id": rid, "argv": argv[1:], "env": env, "cwd": cwd, "log": logpath}
+        try:
+            async with self._fs_lock:  # one drain() at a time on the pipe
+                self._fs.stdin.write((json.dumps(req) + "\n").encode())
+                await self._fs.stdin.drain()
+            msg = await asyncio.wait_for(fut, 30)
+        except (OSError, asyncio.TimeoutError) as e:
+            self._fs_pending.pop(rid, None)
+            log.warning("fork server: %s; cold start", e)
+            return None
+        if "pid" not in msg:
+            return None
+        pr = _ForkedProc(msg["pid"])
+        if msg["pid"] in self._fs_exits:  # (cannot happen: the reply precedes the exit) defensive
+            pr._exited(self._fs_exits.pop(msg["pid"]))
+        else:
+            self._fs_procs[msg["pid"]] = pr
+        return pr
 
     async def _sync_status(self, key, rec):
         procs = rec["procs"]
@@ -490,11 +594,20 @@ class LocalKubelet:
         os.makedirs(self.workdir, exist_ok=True)
         await self._register_node()
         self._tasks = [asyncio.create_task(self._loop()), asyncio.create_task(self._scheduler())]
+        if self.warm_python:
+            await self._start_forkserver()  # not awaited ready: cold starts until it is
 
     async def stop(self):
         self._stop.set()
         for key in list(self.running):
             await self._kill(key)
+        if self._fs is not None and self._fs.returncode is None:
+            self._fs.stdin.close()  # the server's loop ends on EOF
+            try:
+                await asyncio.wait_for(self._fs.wait(), 5)
+            except asyncio.TimeoutError:
+                self._fs.kill()
+                await self._fs.wait()
         for t in self._tasks:
             t.cancel()
         for t in self._tasks:

@@ -39,10 +39,11 @@ def process_start_time() -> float | None:
     try:
         with open("/proc/self/stat") as f:
             ticks = int(f.read().rsplit(")", 1)[1].split()[19])
-        with open("/proc/stat") as f:
-            btime = next(int(l.split()[1]) for l in f if l.startswith("btime"))
-        return btime + ticks / os.sysconf("SC_CLK_TCK")
-    except (OSError, ValueError, StopIteration, IndexError):
+        # boot time from the clocks, not /proc/stat's whole-second btime (that
+        # one is up to 1 s off, which swamped the sub-second start-up phases)
+        boot = time.time() - time.clock_gettime(time.CLOCK_BOOTTIME)
+        return boot + ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, IndexError):
         return None
 
 
