@@ -1,0 +1,87 @@
+"""bench.py contract on CPU/gloo (the driver's launches, scaled down):
+* ``python bench.py --gpus 2`` really runs 2 ranks -- as a TFJob Worker=2
+  through the local operator stack -- and reports n_gpus 2, the process
+  group size, identical replicas, and the p50 submit->first-step latency;
+* the torchrun launch (WORLD_SIZE set by the elastic agent) runs the latency
+  probes on rank 0 before any rank starts, then the same measurement;
+* a --gpus / world-size mismatch fails instead of mislabelling the run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--model", "llama-tiny", "--seq-len", "64", "--micro-batch", "2", "--steps", "3", "--warmup", "1"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("TORCHELASTIC_")}
+    env["OMP_NUM_THREADS"] = "2"
+    return env
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-3000:]
+    return json.loads(lines[0])
+
+
+def _check(r, n):
+    assert r["n_gpus"] == n and r["rccl_world"] == n and r["config"]["tfjob"] == f"Worker={n}"
+    assert r["metric"] == f"samples/sec ({n}-worker TFJob)"
+    assert r["config"]["parallelism"] == f"dp{n}" and r["config"]["global_batch"] == 2 * n
+    assert r["replicas_identical"] is True
+    assert r["value"] > 0 and r["steps"] == 3 and r["warmup"] == 1
+    assert set(r["startup_phases_s"]) == {"process_start->imports", "imports->dist_init", "dist_init->model_init",
+                                          "model_init->first_step"}
+    lat = r["submit_to_first_step"]
+    assert "error" not in lat and r.get("submit_to_first_step_p50_s", 0) > 0, lat
+    assert lat["breakdown_p50_s"]["submit_to_pods_created"] < r["submit_to_first_step_p50_s"]
+
+
+@pytest.mark.timeout(600)
+def test_bench_launcher_two_workers_through_operator():
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1"], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=580)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json_line(p.stdout)
+    _check(r, 2)
+    assert r["config"]["launched_by"] == "operator"
+    assert len(r["submit_to_first_step"]["samples_s"]) == 2  # 1 probe + the benchmark job itself
+    assert "ZeRO-1" in r["config"]["optimizer"]
+
+
+@pytest.mark.timeout(600)
+def test_bench_under_torchrun_probes_first():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1"]
+    p = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=580)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json_line(p.stdout)
+    _check(r, 2)
+    assert r["config"]["launched_by"] == "torchrun"
+    assert len(r["submit_to_first_step"]["samples_s"]) == 1
+
+
+@pytest.mark.timeout(300)
+def test_bench_world_mismatch_fails():
+    env = _env()
+    env.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "FATAL" in p.stderr

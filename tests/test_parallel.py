@@ -14,6 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from tf_operator_amd.parallel import zero
 from tf_operator_amd.train.llm import LlamaTrainer
 
 
@@ -155,11 +156,18 @@ def _zero_worker(rank, world, port, bucket_mb, steps, out):
             assert tr.bucketer.shard == shard and (tr.gather is not None) == shard
             batches = _batches(tr, world)
             losses = [float(tr.step([batches[rank]])) for _ in range(steps)]
-            st = trainer_state(tr)  # collective in sharded mode
+            st = trainer_state(tr)  # this rank's share: compact owned shards when sharded
             if shard:  # W^T copies re-derived after every gather
                 assert all(torch.equal(v, p.data.t()) for _, _, p, v in tr.wt.items)
-            res[shard] = (losses, tr.flat.param.detach().float().clone(), st["flat"]["master"].clone(),
-                          st["flat"]["exp_avg_sq"].clone())
+                # fp32 state really is sharded: 1/world of the flat buffer per rank
+                assert tr.flat.master.numel() * world == tr.flat.numel
+                assert tr.flat.exp_avg.numel() * world == tr.flat.numel
+                assert st["flat"]["master"].numel() * world == tr.flat.numel
+                full = zero.gather_full_state(tr.flat, world)
+            else:
+                full = {k: st["flat"][k] for k in ("master", "exp_avg_sq")}
+            res[shard] = (losses, tr.flat.param.detach().float().clone(), full["master"].clone(),
+                          full["exp_avg_sq"].clone())
         if rank == 0:
             torch.save({"res": res, "nbuckets": len(tr.bucketer.buckets), "owned": tr.bucketer.owned}, out)
     finally:

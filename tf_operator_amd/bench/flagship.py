@@ -1,0 +1,466 @@
+"""The headline benchmark: "samples/sec (N-worker TFJob) + p50 submit->first-step
+latency at 1/2/4/8 GPUs" (BASELINE.json) on config #3, TFJob Worker=N
+all-reduce Llama-3-8B bf16 over RCCL/xGMI, one GPU per worker.
+
+Three ways in, one measurement:
+
+* **launcher** (``python bench.py --gpus N``, no ``WORLD_SIZE`` in the env):
+  the whole operator stack runs in this process -- fake API server, the
+  operator (C++ reconcile core), local kubelet with node-visible devices --
+  and the benchmark is SUBMITTED as a ``TFJob`` with ``Worker=N`` whose
+  replicas run :func:`run_replica`.  Before it, ``--latency-probes`` TFJobs
+  running the user-facing ``examples/llama_train`` payload for one step are
+  submitted and timed from ``create()`` to rank 0's first completed
+  optimizer step (reported back to the operator).  This process never
+  touches the GPU.
+* **torchrun** (the driver's N > 1 launch: ``WORLD_SIZE`` set by the
+  elastic agent): every rank runs :func:`run_replica` directly.  Before any
+  rank touches a GPU, rank 0 runs the same latency probes (TFJob Worker=N
+  through a local operator stack) while the other ranks wait on the agent's
+  store.
+* **replica** (an operator-launched worker, or ``--direct``): just the
+  timed steps.
+
+The replica: W untimed warm-up steps, then exactly K steps bracketed by a
+barrier + ``torch.cuda.synchronize()`` on both sides, MAX over ranks; full
+forward + backward + gradient reduce-scatter/all-reduce + AdamW.  Rank 0
+builds the one JSON line; ``n_gpus`` is the size of the initialised RCCL
+process group, and the run fails when it differs from ``--gpus``.
+
+Reference: the metric's 8-worker job is
+``examples/v1/distribution_strategy/keras-API/multi_worker_strategy-with-keras.py:76-77``
+(MultiWorkerMirroredStrategy, NCCL all-reduce), submitted as the TFJob of
+``multi_worker_tfjob.yaml``.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+BENCH_PY = os.path.join(REPO_ROOT, "bench.py")
+METRIC = "samples/sec ({n}-worker TFJob)"
+
+
+def parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=6)  # 243 GiB peak of 288 GB at N=1
+    ap.add_argument("--grad-accum", type=int, default=1)
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--zero", choices=("auto", "0", "1"), default="auto",
+                    help="sharded optimizer (reduce-scatter / owned-shard AdamW / all-gather); auto = on for N > 1")
+    ap.add_argument("--latency-probes", type=int, default=3,
+                    help="TFJobs submitted (and timed submit -> first step) before the throughput run; 0 = skip")
+    ap.add_argument("--probe-timeout", type=float, default=180.0, help="per probe job (s)")
+    ap.add_argument("--direct", action="store_true",
+                    help="run the replica in this process (no operator; for profilers)")
+    ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)  # replica -> launcher
+    ap.add_argument("--rccl-log", choices=("auto", "0", "1"), default="auto",
+                    help="capture RCCL's transport selection (NCCL_DEBUG=INFO to a file) into the JSON line")
+    return ap
+
+
+def mode() -> str:
+    if "WORLD_SIZE" in os.environ or "RANK" in os.environ:
+        return "torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else "replica"
+    return "launcher"
+
+
+def main(argv=None, t_proc_start=None) -> int:
+    args = parser().parse_args(argv)
+    t_proc_start = t_proc_start or time.time()
+    m = "replica" if args.direct else mode()
+    if m == "launcher":
+        return run_launcher(args)
+    probe = None
+    if m == "torchrun" and args.latency_probes > 0:
+        probe = _torchrun_probe_phase(args)
+    return run_replica(args, t_proc_start, probe=probe, launched_by=m)
+
+
+# =============================================================================
+# submit -> first-step latency probes (through the operator)
+# =============================================================================
+def _payload(args) -> list[str]:
+    return [sys.executable, "-m", "tf_operator_amd.examples.llama_train", "--model", args.model, "--steps", "1",
+            "--seq-len", str(args.seq_len), "--micro-batch", str(args.micro_batch)]
+
+
+def _tfjob(name: str, n: int, command: list[str], env: dict | None = None) -> dict:
+    from ..sdk import container, pod_template
+
+    tpl = pod_template(container(image="toa/trainer:latest", command=command, gpus=1,
+                                 env={"OMP_NUM_THREADS": "8", **(env or {})}))
+    return {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": name, "namespace": "default"},
+            "spec": {"runPolicy": {"cleanPodPolicy": "All"},
+                     "tfReplicaSpecs": {"Worker": {"replicas": n, "restartPolicy": "Never", "template": tpl}}}}
+
+
+def _pod_log_tail(c, name: str, n: int = 40) -> str:
+    out = []
+    for p in sorted(glob.glob(os.path.join(c.workdir, "pods", "default", name + "-*", "*.log"))):
+        try:
+            with open(p, errors="replace") as f:
+                lines = f.read().splitlines()[-n:]
+        except OSError:
+            continue
+        out.append(f"---- {os.path.relpath(p, c.workdir)}\n" + "\n".join(lines))
+    return "\n".join(out)
+
+
+def _run_job(c, name: str, n: int, command: list[str], timeout: float, env=None) -> dict:
+    """Submit one TFJob Worker=n, wait for it to succeed; return the client
+    clock from create() to rank 0's first step plus the breakdown."""
+    key = ("default", name)
+    t0 = time.time()
+    c.client.create(_tfjob(name, n, command, env))
+    t_pods = c.wait(lambda: len(c.pods(labels={"job-name": name})) >= n and time.time(), timeout, 0.005,
+                    f"{name}: pods created")
+
+    def spawned():
+        ts = [v[0] for k, v in c.kubelet.start_times.items() if k[1].startswith(name + "-")]
+        return max(ts) if len(ts) >= n else None
+
+    t_spawn = c.wait(spawned, timeout, 0.005, f"{name}: processes spawned")
+    deadline = time.monotonic() + timeout
+    rep = None
+    while time.monotonic() < deadline:
+        rep = c.controller.reports.get(key) or {}
+        if rep.get("first_step_time"):
+            break
+        job = c.client.get(name)
+        conds = {x["type"] for x in (job.get("status") or {}).get("conditions") or [] if x.get("status") == "True"}
+        if "Failed" in conds:
+            raise RuntimeError(f"{name} failed before its first step\n{_pod_log_tail(c, name)}")
+        time.sleep(0.01)
+    else:
+        raise TimeoutError(f"{name}: no first step within {timeout:.0f}s\n{_pod_log_tail(c, name)}")
+    job = c.client.wait_for_job(name, polling_interval=0.2, timeout_seconds=timeout)
+    conds = {x["type"] for x in (job.get("status") or {}).get("conditions") or [] if x.get("status") == "True"}
+    if "Succeeded" not in conds:
+        raise RuntimeError(f"{name} did not succeed: {sorted(conds)}\n{_pod_log_tail(c, name)}")
+    logs = _pod_log_tail(c, name, 400)
+    c.client.delete(name)
+    # every replica process has exited (and released its HBM) before the next job
+    c.wait(lambda: not c.pods(labels={"job-name": name}) and not any(
+        k[1].startswith(name + "-") for k in c.kubelet.running), 120, 0.05, f"{name}: cleanup")
+    t_first = float(rep["first_step_time"])
+    return {"submit_to_first_step_s": round(t_first - t0, 4),
+            "submit_to_pods_created_s": round(t_pods - t0, 4),
+            "submit_to_processes_spawned_s": round(t_spawn - t0, 4),
+            "spawn_to_first_step_s": round(t_first - t_spawn, 4),
+            "replica_phases_s": rep.get("phases") or {}, "_logs": logs}
+
+
+def _summary(samples: list[dict]) -> dict:
+    if not samples:
+        return {}
+    tot = [s["submit_to_first_step_s"] for s in samples]
+
+    def med(k):
+        return round(statistics.median(s[k] for s in samples), 4)
+
+    phases = {}
+    for k in samples[0]["replica_phases_s"]:
+        if all(k in s["replica_phases_s"] for s in samples):
+            phases[k] = round(statistics.median(s["replica_phases_s"][k] for s in samples), 4)
+    return {"p50_s": round(statistics.median(tot), 4), "samples_s": tot, "min_s": min(tot), "max_s": max(tot),
+            "breakdown_p50_s": {"submit_to_pods_created": med("submit_to_pods_created_s"),
+                                "submit_to_processes_spawned": med("submit_to_processes_spawned_s"),
+                                "spawn_to_first_step": med("spawn_to_first_step_s"),
+                                "replica_phases": phases}}
+
+
+def _cluster(n: int):
+    from ..testing.cluster import LocalCluster
+
+    return LocalCluster(gpus=n, grace_seconds=10.0, device_visibility="node", threadiness=2)
+
+
+def probe_latency(args, n: int, c=None) -> dict:
+    """`args.latency_probes` TFJob Worker=n submissions of the llama_train
+    payload (one optimizer step each), sequentially."""
+    own = c is None
+    if own:
+        c = _cluster(n).start()
+    samples, err = [], None
+    try:
+        for i in range(args.latency_probes):
+            try:
+                s = _run_job(c, f"probe-{i}", n, _payload(args), args.probe_timeout)
+            except Exception as e:  # keep the throughput run alive; report why latency is missing
+                err = f"{type(e).__name__}: {str(e)[:2000]}"
+                break
+            s.pop("_logs", None)
+            samples.append(s)
+            print(f"[bench] probe {i}: submit->first-step {s['submit_to_first_step_s']:.3f}s", file=sys.stderr,
+                  flush=True)
+    finally:
+        if own:
+            c.stop()
+    out = _summary(samples)
+    out["_raw"] = samples
+    if err:
+        out["error"] = err
+    return out
+
+
+def _torchrun_probe_phase(args) -> dict | None:
+    """Rank 0 runs the probes while the other ranks wait on the elastic
+    agent's store -- before any rank has initialised a GPU."""
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    key = f"toa_bench/{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+    budget = args.latency_probes * args.probe_timeout + 120
+    try:
+        store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
+                              world_size=None, is_master=False, timeout=__import__("datetime").timedelta(
+                                  seconds=budget), wait_for_workers=False)
+    except Exception as e:  # no agent store to sync on: skip rather than race the GPUs
+        if rank == 0:
+            print(f"[bench] latency probes skipped: {e}", file=sys.stderr)
+        return {"error": f"no agent store: {e}"}
+    if rank == 0:
+        try:
+            res = probe_latency(args, world)
+        finally:
+            store.set(key, "done")
+        return res
+    store.wait([key])
+    return None
+
+
+# =============================================================================
+# replica: the timed training steps
+# =============================================================================
+def _rccl_log_setup(args, launched_by: str):
+    """RCCL writes its transport choice per channel at INFO level; send it to
+    a per-process file (never to stdout, which carries the JSON line)."""
+    want = args.rccl_log == "1" or (args.rccl_log == "auto" and int(os.environ.get("WORLD_SIZE", "1")) > 1)
+    if not want or os.environ.get("NCCL_DEBUG"):
+        return None
+    d = os.environ.get("TOA_BENCH_RCCL_DIR") or os.path.join(tempfile.gettempdir(), "toa_rccl_logs")
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, f"rccl.{os.getpid()}.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT,P2P"
+    os.environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def summarize_rccl_log(path: str | None) -> dict | None:
+    """Count channel connections per transport (P2P/IPC, SHM, NET...) from an
+    RCCL INFO log."""
+    if not path or not os.path.exists(path):
+        return None
+    import re
+
+    trans, ver, nch = {}, None, None
+    with open(path, errors="replace") as f:
+        for line in f:
+            m = re.search(r"via (\S+)", line)
+            if m and "Channel" in line:
+                t = m.group(1)
+                trans[t] = trans.get(t, 0) + 1
+            m = re.search(r"(?:RCCL|NCCL) version (\S+)", line)
+            if m:
+                ver = m.group(1)
+            m = re.search(r"(\d+) coll channels", line)
+            if m:
+                nch = int(m.group(1))
+    return {"version": ver, "channel_connections_by_transport": trans, "coll_channels": nch, "log": path}
+
+
+def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_by: str = "replica") -> int:
+    phases = {"process_start": t_proc_start}
+    rccl_log = _rccl_log_setup(args, launched_by)
+    import torch
+
+    from ..train import dist as tdist
+    from ..train.llm import LlamaTrainer
+    from ..train.runtime import Runtime
+
+    phases["imports"] = time.time()
+    rt = Runtime()
+    info = tdist.init()
+    rt.info = info
+    rt.mark("dist_init")
+    phases["dist_init"] = time.time()
+    import torch.distributed as dist
+
+    rccl_world = dist.get_world_size() if dist.is_initialized() else 1
+    backend = dist.get_backend() if dist.is_initialized() else None
+    n_gpus = info.world
+    dev = info.device
+    if n_gpus != args.gpus or rccl_world != args.gpus:
+        if info.rank == 0:
+            print(f"[bench] FATAL: --gpus {args.gpus} but the process group has {rccl_world} ranks "
+                  f"(WORLD_SIZE={n_gpus})", file=sys.stderr, flush=True)
+        tdist.shutdown()
+        return 3
+    torch.manual_seed(0)
+    zero = n_gpus > 1 if args.zero == "auto" else args.zero == "1"
+    tr = LlamaTrainer(args.model, dev, micro_batch=args.micro_batch, seq_len=args.seq_len,
+                      grad_accum=args.grad_accum, bucket_mb=args.bucket_mb, shard_optimizer=zero)
+    batches = [tr.synthetic_batch(seed=1000 + info.rank * 97 + i) for i in range(args.grad_accum)]
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    rt.mark("model_init")
+    phases["model_init"] = time.time()
+
+    loss = tr.step(batches)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    phases["first_step"] = time.time()
+    rt.first_step_done()  # -> operator (TFJob launches): the submit->first-step clock of this job
+    for _ in range(max(args.warmup - 1, 0)):
+        loss = tr.step(batches)
+    tdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.step(batches)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    tdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = tdist.all_max(dt, dev)
+    loss_v = float(loss)
+    # data parallelism keeps every replica's weights identical: check it
+    # (one fp64 reduction over the flat bf16 buffer, outside the timed region)
+    if tr.gather is not None:
+        tr.gather.wait_all()
+    csum = float(tr.flat.param.sum(dtype=torch.float64))  # no fp32 copy of 16 GB of weights
+    in_sync = tdist.all_max(csum, dev) == -tdist.all_max(-csum, dev)
+    loss_max = tdist.all_max(loss_v, dev)
+    peak_mem = torch.cuda.max_memory_allocated(dev) / 2**30 if dev.type == "cuda" else 0.0
+    peak_mem = tdist.all_max(peak_mem, dev)
+    steps = max(args.steps, 1)
+    ms = dt / steps * 1e3
+    global_batch = args.micro_batch * args.grad_accum * n_gpus
+    samples_s = global_batch * args.steps / dt if dt > 0 else 0.0
+    tokens_s = samples_s * args.seq_len
+    flops = tr.cfg.flops_per_token(args.seq_len) * tokens_s
+    order = ["process_start", "imports", "dist_init", "model_init", "first_step"]
+    startup = {f"{a}->{b}": round(phases[b] - phases[a], 3) for a, b in zip(order, order[1:])}
+    on_gpu = dev.type == "cuda"
+    rc = 0
+    if info.rank == 0:
+        out = {
+            "metric": METRIC.format(n=n_gpus),
+            "value": round(samples_s, 4),
+            "unit": "samples/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if on_gpu else "bf16-cpu-reference",
+            "data": "synthetic",
+            "config": {
+                "model": "Llama-3-8B" if args.model == "llama3-8b" else args.model,
+                "global_batch": global_batch,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{n_gpus}",
+                "micro_batch_per_gpu": args.micro_batch,
+                "grad_accum": args.grad_accum,
+                "optimizer": ("AdamW (fused HIP, fp32 master, clip 1.0)" if on_gpu
+                              else "AdamW (PyTorch CPU reference, fp32 master, clip 1.0)")
+                             + (", ZeRO-1 sharded" if tr.bucketer.shard else ""),
+                "tfjob": f"Worker={n_gpus}",
+                "launched_by": {"launcher": "operator", "replica": "operator" if os.environ.get("TOA_JOB_NAME")
+                                else "direct", "torchrun": "torchrun"}.get(launched_by, launched_by),
+                "weights": "random-init",
+            },
+            "rccl_world": rccl_world,
+            "backend": backend,
+            "tokens_per_sec": round(tokens_s, 1),
+            "model_tflops_per_gpu": round(flops / n_gpus / 1e12, 1),
+            "first_step_s": round(phases["first_step"] - t_proc_start, 2),
+            "startup_phases_s": startup,
+            "loss": round(loss_v, 4),
+            "loss_max_over_ranks": round(loss_max, 4),
+            "replicas_identical": bool(in_sync),
+            "peak_mem_gib": round(peak_mem, 1),
+        }
+        rl = summarize_rccl_log(rccl_log)
+        if rl:
+            out["rccl"] = rl
+        if probe is not None:
+            _attach_probe(out, probe)
+        if args.result_file:
+            tmp = args.result_file + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(out, f)
+            os.replace(tmp, args.result_file)
+        else:
+            print(json.dumps(out), flush=True)
+    tdist.shutdown()
+    return rc
+
+
+def _attach_probe(out: dict, probe: dict):
+    if probe.get("p50_s") is not None:
+        out["submit_to_first_step_p50_s"] = probe["p50_s"]
+    out["submit_to_first_step"] = {k: v for k, v in probe.items() if k not in ("p50_s", "_raw")}
+
+
+# =============================================================================
+# launcher: the benchmark itself is a TFJob
+# =============================================================================
+def run_launcher(args) -> int:
+    n = args.gpus
+    if n < 1:
+        print("[bench] --gpus must be >= 1", file=sys.stderr)
+        return 2
+    c = _cluster(n).start()
+    try:
+        probe = probe_latency(args, n, c) if args.latency_probes > 0 else {}
+        res_dir = tempfile.mkdtemp(prefix="toa-bench-")
+        res_file = os.path.join(res_dir, "result.json")
+        cmd = [sys.executable, "-u", BENCH_PY, "--gpus", str(n), "--steps", str(args.steps), "--warmup",
+               str(args.warmup), "--model", args.model, "--seq-len", str(args.seq_len), "--micro-batch",
+               str(args.micro_batch), "--grad-accum", str(args.grad_accum), "--zero", args.zero,
+               "--rccl-log", args.rccl_log, "--latency-probes", "0", "--result-file", res_file]
+        if args.bucket_mb is not None:
+            cmd += ["--bucket-mb", str(args.bucket_mb)]
+        timeout = args.probe_timeout + 60 + 30 * (args.steps + args.warmup)
+        try:
+            job = _run_job(c, "bench", n, cmd, timeout, env={"TOA_BENCH_RCCL_DIR": res_dir})
+        except Exception as e:
+            print(f"[bench] benchmark TFJob failed: {e}", file=sys.stderr, flush=True)
+            return 1
+        if not os.path.exists(res_file):
+            print("[bench] benchmark TFJob succeeded but wrote no result\n" + job["_logs"], file=sys.stderr)
+            return 1
+        with open(res_file) as f:
+            out = json.load(f)
+    finally:
+        c.stop()
+    job.pop("_logs", None)
+    # the benchmark job is one more submission of the same TFJob shape: part of the p50
+    p = _summary(list(probe.get("_raw", [])) + [job])
+    if probe.get("error"):
+        p["error"] = probe["error"]
+    p["bench_job_submit_to_first_step_s"] = job["submit_to_first_step_s"]
+    _attach_probe(out, p)
+    print(json.dumps(out), flush=True)
+    return 0

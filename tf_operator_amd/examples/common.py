@@ -9,7 +9,11 @@ import torch
 def pick_device():
     if os.environ.get("TOA_NO_GPU") or os.environ.get("TOA_FORCE_CPU"):
         return torch.device("cpu")
-    return torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    if not torch.cuda.is_available():
+        return torch.device("cpu")
+    from ..train.dist import local_device_index
+
+    return torch.device("cuda", local_device_index() % max(torch.cuda.device_count(), 1))
 
 
 def model_dtype(device):

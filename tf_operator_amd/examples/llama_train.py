@@ -1,8 +1,11 @@
 """Llama-family DP training payload (BASELINE configs #3 / #4 / #5):
-TFJob/PyTorchJob Worker=N, one GPU per worker, RCCL all-reduce over xGMI,
-fused HIP kernels, AdamW.  Checkpoints every `--checkpoint-every` steps and on
-SIGTERM (preemption) to TOA_CHECKPOINT_DIR, resumes from it on restart --
-with ANY world size, which is what the elastic policy relies on."""
+TFJob/PyTorchJob Worker=N, one GPU per worker, RCCL over xGMI, fused HIP
+kernels, AdamW -- the same step as bench.py (ZeRO-1 sharded optimizer for
+N > 1 unless ``--zero 0``).  Every rank checkpoints its own optimizer shard
+(train/sharded_ckpt.py, asynchronous) every `--checkpoint-every` steps and
+on SIGTERM (preemption; the ranks agree on the stop step first) to
+TOA_CHECKPOINT_DIR, and resumes from it on restart -- with ANY world size,
+which is what the elastic policy relies on."""
 from __future__ import annotations
 
 import argparse
@@ -11,7 +14,8 @@ import time
 import torch
 
 from tf_operator_amd.examples.common import pick_device
-from tf_operator_amd.train import checkpoint as ckpt
+from tf_operator_amd.train import dist as tdist
+from tf_operator_amd.train import sharded_ckpt
 from tf_operator_amd.train.llm import LlamaTrainer, load_trainer_state, trainer_state
 from tf_operator_amd.train.runtime import Runtime
 
@@ -26,6 +30,8 @@ def main(argv=None):
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--step-sleep", type=float, default=0.0, help="testing: slow steps down")
     p.add_argument("--report-every", type=int, default=0, help="report samples/sec to the operator every N steps")
+    p.add_argument("--zero", choices=("auto", "0", "1"), default="auto",
+                   help="ZeRO-1 sharded optimizer; auto = on for world > 1 (bench.py's default)")
     a = p.parse_args(argv)
     rt = Runtime()
     rt.install_preemption_handler()
@@ -35,14 +41,27 @@ def main(argv=None):
         _train(a, rt, info)
 
 
+def _stop_agreed(rt, dev) -> bool:
+    """True on every rank once ANY rank got SIGTERM (a MAX all-reduce of the
+    flag), so all ranks stop -- and save -- after the same step."""
+    flag = rt.preempted.is_set()
+    if rt.world == 1 or not torch.distributed.is_initialized():
+        return flag
+    t = torch.tensor([1.0 if flag else 0.0], device=dev)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return bool(t.item() > 0)
+
+
 def _train(a, rt, info):
     dev = pick_device() if info.backend != "gloo" else torch.device("cpu")
-    tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr)
+    zero = rt.world > 1 if a.zero == "auto" else a.zero == "1"
+    tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr, shard_optimizer=zero)
     rt.mark("model_init")
-    payload = ckpt.load_latest(rt.ckpt_dir)
-    if payload is not None:
-        load_trainer_state(tr, payload["state"])
-        rt.log(f"resumed at step {tr.step_idx} (world {rt.world})")
+    ck = sharded_ckpt.Checkpointer(rt.ckpt_dir, rt.rank, rt.world) if rt.ckpt_dir else None
+    shares = sharded_ckpt.load_latest(rt.ckpt_dir)
+    if shares is not None:
+        load_trainer_state(tr, shares)  # re-shards a checkpoint of any world size
+        rt.log(f"resumed at step {tr.step_idx} (world {rt.world}) from a world-{shares[0]['world']} checkpoint")
         rt.mark("checkpoint_load")
     batch = [tr.synthetic_batch(seed=100 + rt.rank)]
     t0, n0 = time.perf_counter(), tr.step_idx
@@ -62,12 +81,16 @@ def _train(a, rt, info):
             el = time.perf_counter() - t1
             rt.report(samples_per_sec=a.micro_batch * rt.world * (tr.step_idx - n0 - 1) / max(el, 1e-9),
                       step=tr.step_idx, world=rt.world)
-        if a.checkpoint_every and tr.step_idx % a.checkpoint_every == 0 and rt.is_chief:
-            ckpt.save(rt.ckpt_dir, tr.step_idx, trainer_state(tr))
-        if rt.preempted.is_set():
-            if rt.is_chief and rt.ckpt_dir:
-                ckpt.save(rt.ckpt_dir, tr.step_idx, trainer_state(tr))
+        if ck and a.checkpoint_every and tr.step_idx % a.checkpoint_every == 0:
+            ck.save(tr.step_idx, trainer_state(tr))  # every rank, its own shard; asynchronous
+        if _stop_agreed(rt, dev):
+            if ck:
+                t_s = time.time()
+                ck.save(tr.step_idx, trainer_state(tr), block=True)
+                rt.log(f"preemption checkpoint at step {tr.step_idx} in {time.time() - t_s:.2f}s "
+                       f"{ck.last_timing}")
             rt.log(f"preempted at step {tr.step_idx}")
+            tdist.shutdown()
             raise SystemExit(143)
         if a.step_sleep:
             time.sleep(a.step_sleep)
@@ -77,8 +100,8 @@ def _train(a, rt, info):
     done = tr.step_idx - n0
     if done:
         rt.report(samples_per_sec=a.micro_batch * rt.world * done / dt)
-    if rt.is_chief and rt.ckpt_dir:
-        ckpt.save(rt.ckpt_dir, tr.step_idx, trainer_state(tr))
+    if ck:
+        ck.save(tr.step_idx, trainer_state(tr), block=True)
     rt.log(f"done: {tr.step_idx} steps")
 
 

@@ -6,7 +6,11 @@ item 2; replaces the reference's EKS-based E2E):
 * **scheduling**: a pod is bound when its ``amd.com/gpu`` request fits the
   node's free GPUs (each pod gets exclusive device indices, exported as
   ``HIP_VISIBLE_DEVICES`` -- the role the AMD device plugin plays on a real
-  node); ``schedulerName: volcano`` pods are gang-admitted only when their
+  node).  ``device_visibility="node"`` (``TOA_KUBELET_DEVICES=node``) instead
+  leaves every GPU of the node visible and names the pod's device in
+  ``TOA_LOCAL_DEVICE``: the single-node data-parallel layout in which RCCL
+  sees all peers and picks its P2P/xGMI transport directly;
+  ``schedulerName: volcano`` pods are gang-admitted only when their
   PodGroup's ``minMember`` pods all fit at once (Volcano semantics);
 * **networking**: every per-replica headless Service name gets a unique
   localhost port; MASTER_ADDR/PORT and DMLC_PS_ROOT_* are rewritten to
@@ -61,6 +65,15 @@ def _quantity_int(v):
         return 0
 
 
+_RENDEZVOUS_VARS = {"RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                    "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TF_CONFIG",
+                    "TOA_LOCAL_DEVICE", "TOA_POD_DEVICES"}
+
+
+def _inherited_rendezvous(k: str) -> bool:
+    return k in _RENDEZVOUS_VARS or k.startswith("TORCHELASTIC_")
+
+
 def pod_gpus(pod, resource="amd.com/gpu"):
     n = 0
     for c in pod.get("spec", {}).get("containers", []):
@@ -80,6 +93,24 @@ class _Proc:
         self.finished_at = None
         self.exit_code = None
         self.deleting = False
+
+
+def _pid_alive(pid: int) -> bool:
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except (OSError, IndexError):
+        return False
+
+
+async def _kill_group_and_wait(pid: int, timeout: float = 10.0):
+    try:
+        os.killpg(pid, signal.SIGKILL)
+    except (ProcessLookupError, PermissionError):
+        pass
+    deadline = time.monotonic() + timeout
+    while _pid_alive(pid) and time.monotonic() < deadline:
+        await asyncio.sleep(0.02)
 
 
 class _ForkedProc:
@@ -106,8 +137,13 @@ class LocalKubelet:
 
     def __init__(self, kube: KubeClient, api=None, node_name="mi355x-node-0", gpus=0, workdir="/tmp/toa-kubelet",
                  python=sys.executable, grace_seconds=3.0, restart_backoff=0.2, gpu_resource="amd.com/gpu",
-                 warm_python=None):
+                 warm_python=None, device_visibility=None):
         self.kube = kube
+        if device_visibility is None:
+            device_visibility = os.environ.get("TOA_KUBELET_DEVICES", "pod")
+        if device_visibility not in ("pod", "node"):
+            raise ValueError(f"device_visibility must be 'pod' or 'node', not {device_visibility!r}")
+        self.device_visibility = device_visibility
         if warm_python is None:
             warm_python = os.environ.get("TOA_KUBELET_WARM", "0") == "1"
         self.warm_python = warm_python
@@ -312,7 +348,11 @@ class LocalKubelet:
                 env[e["name"]] = str(e["value"])
         env = self._rewrite_env(pod, env)
         ns = pod["metadata"].get("namespace", "default")
-        base = dict(os.environ)
+        # a real kubelet starts containers from the image's env, not its own:
+        # never leak the host process's rendezvous (e.g. a torchrun agent's
+        # TORCHELASTIC_USE_AGENT_STORE would send the replica's
+        # init_process_group to a store nobody serves)
+        base = {k: v for k, v in os.environ.items() if not _inherited_rendezvous(k)}
         base.update(env)
         base["HOSTNAME"] = pod["metadata"]["name"]
         base["PORT"] = str(self.service_port(ns, pod["metadata"]["name"]))
@@ -320,7 +360,12 @@ class LocalKubelet:
         base["TOA_POD_NAMESPACE"] = ns
         base["TOA_NODE_NAME"] = self.node
         base["PYTHONPATH"] = REPO_ROOT + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
-        if gpus:
+        if gpus and self.device_visibility == "node":
+            base.pop("HIP_VISIBLE_DEVICES", None)
+            base.pop("TOA_NO_GPU", None)
+            base["TOA_LOCAL_DEVICE"] = str(gpus[0])
+            base["TOA_POD_DEVICES"] = ",".join(str(g) for g in gpus)
+        elif gpus:
             base["HIP_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpus)
         else:
             base.pop("HIP_VISIBLE_DEVICES", None)
@@ -411,7 +456,11 @@ class LocalKubelet:
             if not fut.done():
                 fut.set_result({"error": "fork server exited"})
         self._fs_pending.clear()
-        for pr in list(self._fs_procs.values()):
+        # the forked containers called setsid() and outlive their parent: kill
+        # each group and wait until it is really gone before reporting the
+        # exit, or a restart would share GPUs/ports with an untracked orphan
+        for pid, pr in list(self._fs_procs.items()):
+            await _kill_group_and_wait(pid)
             pr._exited(-signal.SIGKILL)
         self._fs_procs.clear()
 

@@ -70,6 +70,8 @@ PRESETS = {
     "llama3-1b": LlamaConfig(vocab_size=128256, hidden=2048, layers=16, heads=32, kv_heads=8, ffn=8192,
                              tie_embeddings=True),
     "llama-tiny": LlamaConfig(vocab_size=512, hidden=256, layers=2, heads=4, kv_heads=2, ffn=512, max_seq=512),
+    # head_dim 128 like Llama-3-8B: the smoke model runs the same attention kernel as the flagship
+    "llama-tiny128": LlamaConfig(vocab_size=1024, hidden=512, layers=2, heads=4, kv_heads=2, ffn=1024, max_seq=1024),
 }
 
 

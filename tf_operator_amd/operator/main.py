@@ -68,6 +68,10 @@ def build_parser():
     p.add_argument("--health-probe-bind-address", default=":8081")
     p.add_argument("--leader-elect", action="store_true")
     p.add_argument("--leader-election-id", default="1ca428e5.tf-operator")
+    # server.go:56-58: lease 15 s, renew deadline 5 s, retry 3 s
+    p.add_argument("--leader-lease-duration", type=float, default=15.0)
+    p.add_argument("--leader-renew-deadline", type=float, default=5.0)
+    p.add_argument("--leader-retry-period", type=float, default=3.0)
     p.add_argument("--enable-scheme", action="append", default=[],
                    help="TFJob|PyTorchJob|MXJob|XGBoostJob (case-insensitive; repeatable; default all)")
     p.add_argument("--master", default=None, help="API server URL (overrides kubeconfig)")
@@ -79,7 +83,8 @@ def build_parser():
     p.add_argument("--json-log-format", type=lambda v: v.lower() != "false", default=True)
     p.add_argument("--enable-gang-scheduling", action="store_true")
     p.add_argument("--gang-scheduler-name", default="volcano")
-    p.add_argument("--monitoring-port", type=int, default=0, help="legacy /metrics port (0 disables)")
+    p.add_argument("--monitoring-port", type=int, default=8443,
+                   help="legacy /metrics port (options.go:75: default 8443, 0 disables)")
     p.add_argument("--resyc-period", dest="resync_period", default="12h")
     p.add_argument("--qps", type=float, default=5.0)
     p.add_argument("--burst", type=int, default=10)
@@ -211,7 +216,11 @@ class Operator:
         await self._check_crds()
         if self.args.leader_elect:
             el = LeaderElector(self.kube, default_namespace(), self.args.leader_election_id,
+                               lease_duration=self.args.leader_lease_duration,
+                               renew_deadline=self.args.leader_renew_deadline,
+                               retry_period=self.args.leader_retry_period,
                                on_started=self._lead, on_stopped=self._lost)
+            self.elector = el
             elect = asyncio.create_task(el.run(self.stop))
         else:
             await self._lead()

@@ -87,9 +87,9 @@ class FlatAdamW:
         self.weight_decay = weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
-        if flat.exp_avg is None:
-            flat.exp_avg = torch.zeros(flat.numel, device=flat.device, dtype=torch.float32)
-            flat.exp_avg_sq = torch.zeros(flat.numel, device=flat.device, dtype=torch.float32)
+        if flat.exp_avg is None:  # sized to the fp32 state this rank holds (all, or its ZeRO shards)
+            flat.exp_avg = torch.zeros(flat.state_numel, device=flat.device, dtype=torch.float32)
+            flat.exp_avg_sq = torch.zeros(flat.state_numel, device=flat.device, dtype=torch.float32)
         # without weight decay the decay split is moot: one launch over the whole buffer
         self.runs = flat.decay_runs() if weight_decay else [[0, flat.numel, False]]
         self._norm = torch.zeros(1, device=flat.device, dtype=torch.float32)
@@ -115,8 +115,11 @@ class FlatAdamW:
         pp = f.param.data_ptr() + 2 * a if f.param.dtype == torch.bfloat16 else None
         fn, step = ("toa_adamw_flat_dstep", _lib.ptr(self._dstep)) if self.device_step else ("toa_adamw_flat",
                                                                                              self.step_count)
-        _lib.call(fn, f.master.data_ptr() + 4 * a, pp, f.grad.data_ptr() + f.grad.element_size() * a,
-                  gflags, f.exp_avg.data_ptr() + 4 * a, f.exp_avg_sq.data_ptr() + 4 * a, b - a, float(lr),
+        si = f.state_index(a)  # compact fp32 state (ZeRO shards) or == a
+        if f.state_index(b - 1) != si + (b - a - 1):
+            raise ValueError(f"update run [{a}, {b}) crosses fp32 state ranges")
+        _lib.call(fn, f.master.data_ptr() + 4 * si, pp, f.grad.data_ptr() + f.grad.element_size() * a,
+                  gflags, f.exp_avg.data_ptr() + 4 * si, f.exp_avg_sq.data_ptr() + 4 * si, b - a, float(lr),
                   float(self.beta1), float(self.beta2), float(self.eps),
                   float(self.weight_decay if decay else 0.0), step, float(grad_scale),
                   _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), stream)
@@ -204,18 +207,19 @@ class FlatAdamW:
                 self._launch(a, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
             self.grads_zeroed = self.fuse_zero_grad and self.owned is None
             if not pbf:
-                f.param.copy_(f.master)
+                f.param_from_master()
             if self.post_update is not None:
                 self.post_update(0, f.numel)
         else:
             for (a, b, decay) in self._work_runs():
-                adamw_reference(f.master[a:b], f.grad[a:b], f.exp_avg[a:b], f.exp_avg_sq[a:b], lr=lr,
+                adamw_reference(f.state_view(f.master, a, b), f.grad[a:b], f.state_view(f.exp_avg, a, b),
+                                f.state_view(f.exp_avg_sq, a, b), lr=lr,
                                 beta1=self.beta1, beta2=self.beta2, eps=self.eps,
                                 weight_decay=self.weight_decay if decay else 0.0, step=self.step_count,
                                 grad_scale=grad_scale, norm_sq=self._norm if clip else None,
                                 max_norm=self.max_grad_norm or 0.0)
             for lo, hi in (self.owned or [(0, f.numel)]):
-                f.param[lo:hi].copy_(f.master[lo:hi].to(f.param.dtype))
+                f.param[lo:hi].copy_(f.state_view(f.master, lo, hi).to(f.param.dtype))
             if self.post_update is not None:
                 self.post_update(0, f.numel)
 

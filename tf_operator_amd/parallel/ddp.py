@@ -130,6 +130,5 @@ def broadcast_params(flat: FlatParams, src=0, group=None):
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
     dist.broadcast(flat.param, src, group=group)
-    if flat.master is not None:
-        flat.master.copy_(flat.param.float())
+    flat.master_from_param()
     flat.params_changed()

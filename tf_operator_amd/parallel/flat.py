@@ -11,17 +11,38 @@ states as ONE contiguous buffer:
 * the optimizer streams ``self.master`` / ``self.exp_avg`` /
   ``self.exp_avg_sq`` with one kernel per contiguous weight-decay run.
 
+The fp32 state need not cover the whole flat buffer: :meth:`shard_state`
+keeps master / m / v only for the flat ranges this rank updates (ZeRO-1,
+parallel/zero.py), packed back to back ("compact" storage), which frees
+12 B/param x (1 - 1/world) of HBM.  ``state_ranges`` lists the covered
+flat ranges and :meth:`state_index` maps a flat offset into the compact
+buffers.
+
 Parameters are laid out in *backward order* (first gradient produced =
 lowest offset) so gradient buckets become ready front-to-back and their
 RCCL all-reduces overlap the rest of backward.
 """
 from __future__ import annotations
 
+import bisect
 import dataclasses
 
 import torch
 
 ALIGN = 64  # elements; keeps every view 128-B aligned for 16-B vector access
+
+
+def _as_tensor(x):
+    """numpy (incl. read-only checkpoint memmaps) or torch -> torch, no copy."""
+    if torch.is_tensor(x):
+        return x
+    import warnings
+
+    import numpy as np
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")  # read-only memmap: only ever read
+        return torch.from_numpy(np.ascontiguousarray(x))
 
 
 def _round_up(n, a=ALIGN):
@@ -73,12 +94,75 @@ class FlatParams:
         self.master = None
         if master:
             self.master = self.param.float() if dtype != torch.float32 else self.param.clone()
+        # flat ranges covered by master / exp_avg / exp_avg_sq, and where each
+        # starts in those (compact) buffers
+        self.state_ranges = [(0, self.numel)]
+        self._state_lo = [0]
+        self._state_off = [0]
+        self.state_numel = self.numel
         self.exp_avg = None
         self.exp_avg_sq = None
         # callbacks run after the bf16 weights are rewritten outside the
         # optimizer (checkpoint load, broadcast): derived copies such as
         # ops.wt.TransposedWeights re-derive themselves
         self.on_param_change = []
+
+    # ------------------------------------------------------------------ sharded state
+    @property
+    def state_sharded(self) -> bool:
+        return self.state_ranges != [(0, self.numel)]
+
+    @torch.no_grad()
+    def shard_state(self, ranges):
+        """Keep the fp32 state only for flat `ranges` (sorted, disjoint),
+        packed in that order.  Existing master / moments are carried over."""
+        ranges = [(int(lo), int(hi)) for lo, hi in ranges]
+        offs, tot = [], 0
+        for lo, hi in ranges:
+            offs.append(tot)
+            tot += hi - lo
+        new = {}
+        for k in ("master", "exp_avg", "exp_avg_sq"):
+            old = getattr(self, k)
+            if old is None:
+                continue
+            t = torch.empty(tot, device=old.device, dtype=old.dtype)
+            for (lo, hi), o in zip(ranges, offs):
+                t[o:o + hi - lo].copy_(old[self.state_index(lo):self.state_index(lo) + hi - lo])
+            new[k] = t
+        for k in ("master", "exp_avg", "exp_avg_sq"):
+            setattr(self, k, None)
+        for k, t in new.items():
+            setattr(self, k, t)
+        self.state_ranges = ranges
+        self._state_lo = [lo for lo, _ in ranges]
+        self._state_off = offs
+        self.state_numel = tot
+
+    def state_index(self, a: int) -> int:
+        """Offset in the compact state buffers of flat element `a`."""
+        i = bisect.bisect_right(self._state_lo, a) - 1
+        if i < 0 or a >= self.state_ranges[i][1]:
+            raise IndexError(f"flat offset {a} has no fp32 state on this rank")
+        return self._state_off[i] + a - self.state_ranges[i][0]
+
+    def state_view(self, t, lo: int, hi: int):
+        """View of compact state tensor `t` for flat range [lo, hi) (inside one state range)."""
+        i = self.state_index(lo)
+        return t[i:i + hi - lo]
+
+    @torch.no_grad()
+    def master_from_param(self):
+        """Re-derive the fp32 master of every held range from the bf16 weights."""
+        if self.master is None:
+            return
+        for lo, hi in self.state_ranges:
+            self.state_view(self.master, lo, hi).copy_(self.param[lo:hi].float())
+
+    @torch.no_grad()
+    def param_from_master(self):
+        for lo, hi in self.state_ranges:
+            self.param[lo:hi].copy_(self.state_view(self.master, lo, hi).to(self.param.dtype))
 
     def params_changed(self):
         for fn in list(self.on_param_change):
@@ -101,23 +185,64 @@ class FlatParams:
         self.grad.zero_()
 
     def state_dict(self):
+        """This rank's fp32 state (compact) and where it belongs in the flat
+        buffer.  World-size independent when combined with the other ranks'
+        (see :func:`load_state_shards`)."""
         return {
             "master": self.master,
             "exp_avg": self.exp_avg,
             "exp_avg_sq": self.exp_avg_sq,
-            "layout": [(s.name, s.offset, s.numel) for s in self.segments],
+            "state_ranges": [tuple(r) for r in self.state_ranges],
+            "numel": self.numel,
+            "layout": self.layout(),
         }
 
-    def load_state_dict(self, sd):
-        layout = [(s.name, s.offset, s.numel) for s in self.segments]
-        if [tuple(x) for x in sd["layout"]] != layout:
+    def layout(self):
+        return [(s.name, s.offset, s.numel) for s in self.segments]
+
+    def check_layout(self, layout):
+        if [tuple(x) for x in layout] != self.layout():
             raise ValueError("flat layout mismatch between checkpoint and model")
-        if sd.get("master") is not None and self.master is not None:
-            self.master.copy_(sd["master"])
-            self.param.copy_(self.master.to(self.param.dtype))
-        for k in ("exp_avg", "exp_avg_sq"):
-            if sd.get(k) is not None:
-                if getattr(self, k) is None:
-                    setattr(self, k, torch.zeros_like(sd[k], device=self.device))
-                getattr(self, k).copy_(sd[k])
+
+    @torch.no_grad()
+    def load_state_shards(self, shards, set_params="held"):
+        """Fill this rank's state ranges from any set of saved shards
+        (``state_dict()`` outputs of ANY world size; tensors may be CPU,
+        device or numpy memmaps) that together cover them.  ``set_params``:
+        "held" re-derives the bf16 weights of the held ranges, "all" of every
+        range the shards cover (then no weight all-gather is needed)."""
+        covered = []
+        for sh in shards:
+            if "layout" in sh:
+                self.check_layout(sh["layout"])
+            src_off = 0
+            for lo, hi in sh["state_ranges"]:
+                lo, hi = int(lo), int(hi)
+                for k in ("master", "exp_avg", "exp_avg_sq"):
+                    src = sh.get(k)
+                    if src is None:
+                        continue
+                    if getattr(self, k) is None:
+                        setattr(self, k, torch.zeros(self.state_numel, device=self.device, dtype=torch.float32))
+                    dst = getattr(self, k)
+                    for (a, b) in self.state_ranges:
+                        x, y = max(a, lo), min(b, hi)
+                        if x >= y:
+                            continue
+                        piece = _as_tensor(src[src_off + x - lo:src_off + y - lo])
+                        self.state_view(dst, x, y).copy_(piece, non_blocking=False)
+                        if k == "master":
+                            covered.append((x, y))
+                if set_params == "all" and sh.get("master") is not None:
+                    piece = _as_tensor(sh["master"][src_off:src_off + hi - lo])
+                    self.param[lo:hi].copy_(piece.to(self.device).to(self.param.dtype))
+                src_off += hi - lo
+        need = sum(b - a for a, b in self.state_ranges)
+        if self.master is not None and sum(b - a for a, b in covered) != need:
+            raise ValueError("checkpoint shards do not cover this rank's optimizer state")
+        if set_params == "held":
+            self.param_from_master()
+
+    def load_state_dict(self, sd):
+        self.load_state_shards([sd], set_params="all")
         self.params_changed()

@@ -28,8 +28,9 @@ from ..operator.metrics import OperatorMetrics
 class LocalCluster:
     def __init__(self, gpus=0, kinds=("TFJob", "PyTorchJob", "MXJob", "XGBoostJob"), enable_gang_scheduling=False,
                  threadiness=2, workdir=None, cluster_domain="", nccl_env=None, start_operator=True, qps=0,
-                 grace_seconds=2.0, warm_python=None):
+                 grace_seconds=2.0, warm_python=None, device_visibility=None):
         self.gpus = gpus
+        self.device_visibility = device_visibility
         self.warm_python = warm_python
         self.kinds = kinds
         self.opts = ControllerOptions(threadiness=threadiness, enable_gang_scheduling=enable_gang_scheduling,
@@ -61,7 +62,7 @@ class LocalCluster:
         self.kube_kubelet = KubeClient(self.url, qps=0)
         self.kubelet = LocalKubelet(self.kube_kubelet, self.api, gpus=self.gpus,
                                     workdir=os.path.join(self.workdir, "pods"), grace_seconds=self.grace,
-                                    warm_python=self.warm_python)
+                                    warm_python=self.warm_python, device_visibility=self.device_visibility)
         await self.kubelet.start()
         if self.start_operator:
             await self._start_report_server()

@@ -46,10 +46,20 @@ def env_rank_world():
     return 0, 1
 
 
+def local_device_index() -> int:
+    """GPU this replica drives: ``TOA_LOCAL_DEVICE`` (the local kubelet's
+    node-visible mode names the pod's device there) else ``LOCAL_RANK``
+    (torchrun; 0 under per-pod HIP_VISIBLE_DEVICES pinning)."""
+    v = os.environ.get("TOA_LOCAL_DEVICE")
+    if v not in (None, ""):
+        return int(v)
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def init(backend=None, timeout_s=1800) -> DistInfo:
     rank, world = env_rank_world()
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    use_cuda = torch.cuda.is_available()
+    local_rank = local_device_index()
+    use_cuda = torch.cuda.is_available() and not os.environ.get("TOA_NO_GPU")
     if use_cuda:
         torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
         device = torch.device("cuda", torch.cuda.current_device())

@@ -29,7 +29,7 @@ from ..parallel.zero import ParamGather
 class LlamaTrainer:
     def __init__(self, cfg: LlamaConfig | str, device, micro_batch=1, seq_len=4096, grad_accum=1, lr=3e-4,
                  seed=0, bucket_mb=None, overlap_optimizer=None, shard_optimizer=None,
-                 transposed_weights=None):
+                 transposed_weights=None, force_collectives=False):
         if isinstance(cfg, str):
             cfg = PRESETS[cfg]
         self.cfg = cfg
@@ -53,10 +53,14 @@ class LlamaTrainer:
         broadcast_params(self.flat)
         if shard_optimizer is None:
             shard_optimizer = os.environ.get("TOA_ZERO", "0") == "1"
+        # force_collectives: run the bucketed collectives even at world 1 (the
+        # RCCL world-1 test drives the real reduce-scatter / all-gather path)
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20),
-                                     shard=shard_optimizer)
+                                     shard=shard_optimizer, enabled=True if force_collectives else None)
         self.gather = None
         if self.bucketer.shard:  # ZeRO-1: reduce-scatter, owned-shard AdamW, in-place all-gather
+            # fp32 master / m / v only for the owned shards: 12 B/param x (1 - 1/world) of HBM freed
+            self.flat.shard_state(self.bucketer.owned)
             self.opt = FlatAdamW(self.flat, lr=lr, owned=self.bucketer.owned)
             self.gather = ParamGather(self.flat, self.bucketer.buckets, self.bucketer.rank, self.bucketer.world,
                                       on_gathered=self.wt.refresh if self.wt else None)
@@ -143,21 +147,31 @@ def timed_steps(trainer: LlamaTrainer, batches, n, sync=True):
 
 
 def trainer_state(tr: LlamaTrainer):
-    """Full, world-size-independent training state.  With the sharded
-    optimizer this is a COLLECTIVE (every rank must call it): the owned
-    master / moment shards are all-gathered first."""
+    """This rank's share of the training state: the fp32 master / moment
+    shards it holds (all of them without ZeRO) plus where they belong in the
+    flat buffer.  NOT a collective -- every rank saves its own share
+    (train/sharded_ckpt.py), and the shares of any world size re-shard on
+    load (:func:`load_trainer_state`)."""
     tr.opt.wait_all()
     if tr.gather is not None:
         tr.gather.wait_all()
-        zero.gather_state(tr.flat, tr.bucketer.buckets, tr.bucketer.rank, tr.bucketer.world)
-    return {"flat": tr.flat.state_dict(), "opt": tr.opt.state_dict(), "step": tr.step_idx}
+    return {"flat": tr.flat.state_dict(), "opt": tr.opt.state_dict(), "step": tr.step_idx,
+            "rank": tr.bucketer.rank, "world": tr.bucketer.world}
 
 
 def load_trainer_state(tr: LlamaTrainer, st):
-    dev = tr.flat.device
+    """Restore from one state (``trainer_state`` of an unsharded run) or a
+    list of per-rank shares of any world size.  Collective when this
+    trainer shards its optimizer: the restored weights are all-gathered."""
+    shards = st if isinstance(st, (list, tuple)) else [st]
     tr.opt.wait_all()
     if tr.gather is not None:
         tr.gather.wait_all()
-    tr.flat.load_state_dict({k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in st["flat"].items()})
-    tr.opt.load_state_dict(st["opt"])
-    tr.step_idx = int(st["step"])
+    full = not tr.flat.state_sharded
+    tr.flat.load_state_shards([s["flat"] for s in shards], set_params="all" if full else "held")
+    if tr.gather is not None:  # held shards -> every rank's bf16 weights
+        tr.gather.launch()
+        tr.gather.wait_all()
+    tr.flat.params_changed()
+    tr.opt.load_state_dict(shards[0]["opt"])
+    tr.step_idx = int(shards[0]["step"])

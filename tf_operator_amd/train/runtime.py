@@ -91,6 +91,10 @@ class Runtime:
                 self.log(f"lost a peer ({type(e).__name__}: {str(e)[:200]}); exiting {PEER_LOST_EXIT}")
                 os._exit(PEER_LOST_EXIT)
             raise
+        # normal end: tear the process group down before interpreter exit
+        # (a live gloo/RCCL group at exit can abort: "terminate called
+        # without an active exception")
+        tdist.shutdown()
 
     # -------------------------------------------------------------- preemption
     def install_preemption_handler(self):
