@@ -95,7 +95,18 @@ static std::string master_role_type(const KindInfo& ki, const Json& specs) {
 // launcher tf_operator_amd/utils/profiling.py, output in
 // <amd.com/rocprof-dir, default /tmp/rocprof>/<pod>.  A container without an
 // explicit command (image entrypoint) is left alone.
-static void wrap_rocprof(const Json& ann, const KindInfo& ki, const std::string& pod, Json& pspec) {
+// A command that starts with a shell or a launcher (env, bash, taskset, ...)
+// would re-exec under the profiler's preloaded library: that hop is refused,
+// so such a container is left unwrapped and a Warning event says why.
+static bool is_launcher(const std::string& argv0) {
+  const size_t slash = argv0.rfind('/');
+  const std::string base = slash == std::string::npos ? argv0 : argv0.substr(slash + 1);
+  for (const char* l : {"env", "bash", "sh", "dash", "zsh", "taskset", "numactl", "nohup", "exec", "time"})
+    if (base == l) return true;
+  return false;
+}
+
+static void wrap_rocprof(const Json& ann, const KindInfo& ki, const std::string& pod, Json& pspec, Json& events) {
   if (!ann.is_object()) return;
   const std::string mode = ann.get("amd.com/rocprof").str();
   if (mode.empty()) return;
@@ -112,6 +123,12 @@ static void wrap_rocprof(const Json& ann, const KindInfo& ki, const std::string&
   Json& c = cs.at(target);
   const Json cmd = c.get("command");
   if (!cmd.is_array() || cmd.size() == 0) return;
+  if (is_launcher(cmd[0].str())) {
+    add_event(events, "Warning", "RocprofSkipped",
+              "amd.com/rocprof: command of pod " + pod + " starts with launcher '" + cmd[0].str() +
+                  "'; put the program itself first to profile it (running unprofiled)");
+    return;
+  }
   Json wrapped = Json::array();
   for (const char* w : {"python3", "-m", "tf_operator_amd.utils.profiling", "--mode"}) wrapped.push_back(w);
   wrapped.push_back(mode);
@@ -144,7 +161,7 @@ static Json new_pod(const Json& job, const KindInfo& ki, const std::string& rtyp
   tmd.set("labels", labels);
   tmd.set("name", gen_general_name(name, rt, std::to_string(index)));
   set_cluster_spec(job, tpl, rtype, index, opt);
-  wrap_rocprof(md.get("annotations"), ki, tmd.get("name").str(), tpl["spec"]);
+  wrap_rocprof(md.get("annotations"), ki, tmd.get("name").str(), tpl["spec"], events);
   Json& ps = tpl["spec"];
   if (!ps.get("restartPolicy").str().empty())
     add_event(events, "Warning", "SettedPodTemplateRestartPolicy",

@@ -114,3 +114,48 @@ def test_dp_trainer_over_ipc_allreduce():
     for rank, same, err in res:
         assert err is None, (rank, err)
         assert same, rank
+
+
+def _lost_peer_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tf_operator_amd.parallel.ipc import IpcAllReduce
+
+        ar = IpcAllReduce(slot_bytes=1 << 20, timeout_ms=300)
+        raised = None
+        if rank == 0:  # rank 1 never joins this all-reduce: a lost peer
+            ar(torch.ones(1024, device="cuda"))
+            try:
+                for _ in range(3):  # poll() looks at the copy queued one step earlier
+                    torch.cuda.synchronize()
+                    ar.poll()
+            except RuntimeError as e:
+                raised = str(e)
+        dist.barrier()
+        ar.close()
+        dist.destroy_process_group()
+        q.put((rank, raised, None))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.timeout(120)
+def test_ipc_lost_peer_raises_from_poll():
+    """A peer that never arrives sets the sticky error word after the bounded
+    spin; GradBucketer.finish()'s per-step poll() turns it into an exception
+    instead of letting stale peer slots be summed into the gradient."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_lost_peer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (m, e)) for r, m, e in (q.get(timeout=100) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=30)
+    assert res[0][1] is None and res[1][1] is None, res
+    assert res[0][0] and "rank" in res[0][0] and "1" in res[0][0], res

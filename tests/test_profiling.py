@@ -83,3 +83,25 @@ def test_launcher_runs_child_and_writes_summary(tmp_path, monkeypatch):
         pytest.skip("rocprofv3 present: the unprofiled fallback is not reachable")
     rc = profiling.main(["--out", str(tmp_path), "--", "python3", "-c", "import sys; sys.exit(3)"])
     assert rc == 3
+
+
+def test_launcher_command_is_left_unwrapped_with_warning():
+    """A shell/launcher first (bare or by path) is never wrapped: the hop would
+    re-exec under rocprofv3's preload.  The core emits a Warning instead."""
+    for argv0 in ("bash", "/bin/sh", "/usr/bin/env"):
+        job = fx.new_tfjob(worker=1)
+        c = job["spec"]["tfReplicaSpecs"]["Worker"]["template"]["spec"]["containers"][0]
+        c["command"] = [argv0, "-c", "python3 train.py"]
+        job["metadata"]["annotations"] = {"amd.com/rocprof": "stats"}
+        res = core.reconcile(job, [], [], now=NOW, options={})
+        pod = [a["pod"] for a in res["actions"] if a["op"] == "create_pod"][0]
+        assert pod["spec"]["containers"][0]["command"] == [argv0, "-c", "python3 train.py"]
+        assert any(e["reason"] == "RocprofSkipped" for e in res["events"]), res["events"]
+    with pytest.raises(ValueError):
+        profiling.rocprof_argv(["/usr/bin/env", "python3"], "out")
+
+
+def test_launcher_falls_back_to_unprofiled_run_for_launcher_hop(tmp_path, monkeypatch):
+    monkeypatch.setattr(profiling.shutil, "which", lambda n: "/opt/rocm/bin/rocprofv3")
+    rc = profiling.main(["--out", str(tmp_path), "--", "/bin/sh", "-c", "exit 7"])
+    assert rc == 7

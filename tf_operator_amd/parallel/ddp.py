@@ -114,6 +114,8 @@ class GradBucketer:
             w.wait()
         for fin in self.finishers:
             fin()
+        if self.ipc is not None:
+            self.ipc.poll()  # a peer timeout in the one-shot kernel must not pass silently
         self.works = []
         self.finishers = []
         self.pending = [b[2] for b in self.buckets]

@@ -93,9 +93,32 @@ class IpcAllReduce:
 
     def check(self):
         """Raise if some rank never reached a barrier (kernel timed out)."""
-        e = int(self.err.item())
+        self._raise(int(self.err.item()))
+
+    def _raise(self, e: int):
         if e:
-            raise RuntimeError(f"IPC all-reduce: ranks {[r for r in range(8) if e >> r & 1]} timed out")
+            self.broken = True
+            raise RuntimeError(f"IPC all-reduce: ranks {[r for r in range(8) if e >> r & 1]} timed out "
+                               "(peer lost or stalled); the reduced gradients are invalid")
+
+    def poll(self):
+        """Non-blocking error check, once per step: the sticky device error
+        word is copied into pinned host memory behind this step's reduces and
+        the copy queued one step earlier is inspected (an event query, no
+        host sync).  A set bit raises, so the peer-loss exit path runs instead
+        of the optimizer consuming sums built from stale peer slots."""
+        if getattr(self, "broken", False):
+            raise RuntimeError("IPC all-reduce already failed; refusing to reuse it")
+        if not hasattr(self, "_host_err"):
+            self._host_err = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._err_ev = None
+        if self._err_ev is not None and self._err_ev.query():
+            self._raise(int(self._host_err[0]))
+            self._err_ev = None
+        if self._err_ev is None:
+            self._host_err.copy_(self.err, non_blocking=True)
+            self._err_ev = torch.cuda.Event()
+            self._err_ev.record()
 
     def close(self):
         torch.cuda.synchronize()

@@ -30,6 +30,13 @@ import subprocess
 import sys
 
 MODES = ("kernel-trace", "stats", "pmc")
+LAUNCHERS = ("env", "bash", "sh", "dash", "zsh", "taskset", "numactl", "nohup", "exec", "time")
+
+
+def is_launcher(argv0: str) -> bool:
+    """True for a shell or launcher (by basename: /usr/bin/env too) -- a hop
+    that would re-exec under the profiler's preloaded library."""
+    return os.path.basename(argv0) in LAUNCHERS
 
 
 def rocprof_argv(program: list, out_dir: str, mode: str = "stats", counters=None, name: str = "run") -> list:
@@ -47,7 +54,7 @@ def rocprof_argv(program: list, out_dir: str, mode: str = "stats", counters=None
         if not counters:
             raise ValueError("pmc mode needs counters")
         argv[1:1] = ["--pmc", *counters]
-    if not program or program[0] in ("env", "bash", "sh", "taskset", "numactl"):
+    if not program or is_launcher(program[0]):
         raise ValueError("put the program itself after `--` (no launcher hops under the profiler)")
     return argv + ["--"] + list(program)
 
@@ -146,6 +153,11 @@ def main(argv=None):
     if shutil.which("rocprofv3") is None and not os.path.exists("/opt/rocm/bin/rocprofv3"):
         print("[profiling] rocprofv3 not found: running unprofiled", file=sys.stderr)
         return subprocess.call(program, env=env)
+    if not program or is_launcher(program[0]):
+        # the operator core already skips such commands; a hand-written pod
+        # spec still gets its job run, just unprofiled, instead of exit 1
+        print(f"[profiling] {program[:1]} is a launcher hop: running unprofiled", file=sys.stderr)
+        return subprocess.call(program, env=env) if program else 2
     rc = subprocess.call(rocprof_argv(program, a.out, mode, counters), env=env)
     try:
         with open(os.path.join(a.out, "summary.md"), "w") as f:
