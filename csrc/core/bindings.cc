@@ -71,6 +71,15 @@ PYBIND11_MODULE(_toa_core, m) {
         return gen_env(j, rtype, index, options_from_json(J(options))).dump();
       },
       py::arg("job"), py::arg("rtype"), py::arg("index"), py::arg("options") = "");
+  m.def(
+      "set_cluster_spec",
+      [](const std::string& job, const std::string& tpl, const std::string& rtype, int index,
+         const std::string& options) {
+        Json t = J(tpl);
+        set_cluster_spec(set_defaults(J(job)), t, rtype, index, options_from_json(J(options)));
+        return t.dump();
+      },
+      py::arg("job"), py::arg("template"), py::arg("rtype"), py::arg("index"), py::arg("options") = "");
   m.def("tf_is_distributed", [](const std::string& job) { return tf_is_distributed(set_defaults(J(job))); });
   m.def(
       "gen_podgroup",

@@ -105,6 +105,7 @@ struct Options {
   bool inject_rocm_env = true;          // MASTER_ADDR/RANK/... + NCCL_* for TFJob
   int previous_retry = 0;               // workqueue NumRequeues(job)
   Json nccl_env = Json::object();       // extra NCCL_*/RCCL_* knobs
+  bool rccl_defaults = true;            // xGMI-oriented defaults (never override the user's env)
   std::string gpu_resource = "amd.com/gpu";
   int64_t elastic_free_gpus = -1;       // free GPUs for an elastic job (own pods count as free); -1 unknown
 };

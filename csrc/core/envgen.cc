@@ -28,6 +28,7 @@ Options options_from_json(const Json& o) {
   if (o.has("inject_rocm_env")) opt.inject_rocm_env = o.get("inject_rocm_env").as_bool(true);
   opt.previous_retry = (int)o.get("previous_retry").as_int(0);
   if (o.get("nccl_env").is_object()) opt.nccl_env = o.get("nccl_env");
+  if (o.has("rccl_defaults")) opt.rccl_defaults = o.get("rccl_defaults").as_bool(true);
   opt.gpu_resource = o.get("gpu_resource").str("amd.com/gpu");
   opt.elastic_free_gpus = o.get("elastic_free_gpus").as_int(-1);
   return opt;
@@ -109,6 +110,33 @@ static void add_env(Json& out, const std::string& container, const std::string& 
   out.push_back(e);
 }
 
+// Defaults for RCCL over xGMI on an MI355X node, appended only when neither
+// --nccl-env nor the container itself sets the variable (set_cluster_spec
+// skips entries marked "default" that the container already defines):
+//  * TORCH_NCCL_HIGH_PRIORITY: the bucketed reduce-scatter / all-gather run on
+//    high-priority HIP streams, so they are not queued behind the backward
+//    GEMMs they are meant to overlap;
+//  * TORCH_NCCL_AVOID_RECORD_STREAMS: async collectives keep their inputs
+//    alive by reference instead of recordStream (no delayed frees of the
+//    flat gradient buckets in the caching allocator);
+//  * HSA_ENABLE_IPC_MODE_LEGACY=0: dmabuf IPC, which RCCL's P2P transport and
+//    CUDA-tensor sharing between processes need on ROCm 7 drivers.
+static const char* const kRcclDefaults[][2] = {
+    {"TORCH_NCCL_HIGH_PRIORITY", "1"},
+    {"TORCH_NCCL_AVOID_RECORD_STREAMS", "1"},
+    {"HSA_ENABLE_IPC_MODE_LEGACY", "0"},
+};
+
+static void add_default_env(Json& out, const std::string& container, const std::string& name,
+                            const std::string& value) {
+  Json e = Json::object();
+  e.set("container", container);
+  e.set("name", name);
+  e.set("value", value);
+  e.set("default", true);
+  out.push_back(e);
+}
+
 static int64_t spec_replicas(const Json& job, const std::string& rt) {
   const Json* s = replica_specs(job).find(rt);
   return (s && !s->is_null()) ? replicas_of(*s) : 0;
@@ -124,6 +152,9 @@ static void rocm_block(const Json& job, const std::string& rtype, int index, con
   add_env(out, container, "TOA_REPLICA_TYPE", lower(rtype));
   add_env(out, container, "TOA_REPLICA_INDEX", std::to_string(index));
   for (const auto& kv : opt.nccl_env.fields()) add_env(out, container, kv.first, kv.second.is_string() ? kv.second.str() : kv.second.dump());
+  if (opt.rccl_defaults)
+    for (const auto& d : kRcclDefaults)
+      if (!opt.nccl_env.has(d[0])) add_default_env(out, container, d[0], d[1]);
   const Json& ann = md.get("annotations");
   if (ann.has("amd.com/checkpoint-dir")) add_env(out, container, "TOA_CHECKPOINT_DIR", ann.get("amd.com/checkpoint-dir").str());
 }
@@ -277,6 +308,12 @@ void set_cluster_spec(const Json& job, Json& pod_template, const std::string& rt
     for (const auto& e : env.items()) {
       const std::string target = e.get("container").str();
       if (target != "*" && target != cname) continue;
+      if (e.get("default").as_bool(false)) {  // never override the user's own setting
+        bool set = false;
+        const Json& cur = c.get("env");
+        for (size_t j = 0; j < cur.size(); ++j) set = set || cur[j].get("name").str() == e.get("name").str();
+        if (set) continue;
+      }
       Json ev = Json::object();
       ev.set("name", e.get("name"));
       ev.set("value", e.get("value"));

@@ -2,7 +2,8 @@
 // native GQA (K/V stay packed per kv-head; no repeat_interleave copies).
 //
 // Layouts: q [B, H, S, D], o/dO [B, H, S, D] or [B, S, H, D] (flag bit 1),
-// k/v [B, Hk, S, D], lse [B, H, S] (natural log), D = 128.  Forward / dQ:
+// k/v [B, Hk, S, D], lse [B, H, S] (natural log), D = 64 or 128 (template;
+// LDS rows of 2D bytes = D/8 16-byte chunks), any S >= 1.  Forward / dQ:
 // one workgroup = 8 waves = a 256-row query block of one (batch, head);
 // wave w owns 32 query rows.  K/V tiles of 64 keys are staged
 // global -> registers -> LDS (double buffered, loads of tile t+1 in flight
@@ -25,6 +26,13 @@
 // Backward = two kernels: dQ (which also computes delta = rowsum(dO*O)),
 // then dK/dV (workgroup per 128-key block, sweeping the GQA group's query
 // heads).  No float atomics: deterministic.
+//
+// Ragged S (S % 64 != 0): every row index that feeds a LOAD is clamped to
+// S - 1, so tiles past the end re-read the last row instead of branching
+// around loads (a per-load select makes hipcc wait vmcnt(0) per element).
+// That is exact for causal attention: a padded key sits after every real
+// query (the diagonal mask removes it), a padded query's outputs are never
+// stored, and in dK/dV a padded query row gets lse = +inf, i.e. p = 0.
 #include "toa_common.h"
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
@@ -41,14 +49,28 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 
 __device__ __forceinline__ bf16x8 as_bf16x8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 
-// LDS tile geometry: 64 keys x 128 d bf16 = 16 KB, rows of 256 B = 16 chunks of 16 B.
+// LDS tile geometry: 64 keys x D bf16, rows of ROWB = 2D bytes = NCH chunks
+// of 16 B (D = 128: 256-B rows, 16 chunks; D = 64: 128-B rows, 8 chunks).
 #define TK 64
-#define ROWB 256
+template <int D>
+struct AG {
+  static constexpr int NCH = D / 8;     // 16-B chunks per row
+  static constexpr int ROWB = 2 * D;    // bytes per row
+  static constexpr int NS = D / 16;     // k-steps of a 32x32x16 MFMA over d
+  static constexpr int ND = D / 32;     // 32-row d tiles of an O^T / dK^T accumulator
+  static constexpr int TILEB = TK * ROWB;
+};
 
-// K image: chunk c of row `key` stored at chunk position c ^ (key & 15)
-__device__ __forceinline__ int k_off(int key, int chunk) { return key * ROWB + ((chunk ^ (key & 15)) << 4); }
-// V image: chunk c of row `key` stored at chunk position c ^ ((key & 3) << 2)
-__device__ __forceinline__ int v_off(int key, int chunk) { return key * ROWB + ((chunk ^ ((key & 3) << 2)) << 4); }
+// K image: chunk c of row `key` stored at chunk position c ^ (key & (NCH-1))
+template <int D>
+__device__ __forceinline__ int k_off(int key, int chunk) {
+  return key * AG<D>::ROWB + ((chunk ^ (key & (AG<D>::NCH - 1))) << 4);
+}
+// V image (read transposed): chunk c of row `key` at c ^ ((key & 3) << 2) (D = 128) / << 1 (D = 64)
+template <int D>
+__device__ __forceinline__ int v_off(int key, int chunk) {
+  return key * AG<D>::ROWB + ((chunk ^ ((key & 3) << (D == 128 ? 2 : 1))) << 4);
+}
 
 typedef short __attribute__((ext_vector_type(4))) s16x4;
 __device__ __forceinline__ bf16x4 tr_read(const char* lds_base, int byte_off) {
@@ -90,8 +112,9 @@ __device__ __forceinline__ float xhalf_sum(float v) {
 // Offset of row (b, h, s) of O / dO: [B, H, S, D] (head-major, like Q) or, with
 // bshd, [B, S, H, D] -- the layout the output projection consumes, so the
 // model needs no transpose copy of O forward or of dO backward.
+template <int D>
 __device__ __forceinline__ int64_t o_off(int b, int h, int s, int H, int S, int bshd) {
-  return bshd ? (((int64_t)b * S + s) * H + h) * 128 : (((int64_t)b * H + h) * S + s) * 128;
+  return bshd ? (((int64_t)b * S + s) * H + h) * D : (((int64_t)b * H + h) * S + s) * D;
 }
 
 // XCD-aware block order: the hardware deals workgroups to the 8 XCDs round
@@ -117,13 +140,15 @@ __device__ __forceinline__ void fwd_block_coords(int pid, int nqb, int B, int H,
   }
 }
 
-template <int D>
+template <int D, bool TAIL>
 __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int H, int Hk, int S,
                                                           float scale_log2, int o_bshd) {
-  static_assert(D == 128, "D=128 path");
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16KB + V 16KB)
+  using G = AG<D>;
+  constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
+  constexpr int NL = TK * NCH / 512;  // 16-B chunks of K (and of V) per thread per tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K tile + V tile)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = (S + FWD_QB - 1) / FWD_QB;
@@ -133,78 +158,74 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
   const int64_t qoff = ((int64_t)(b * H + h) * S) * D;
   const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
   const int q0 = qb * FWD_QB + wave * 32;  // first row of this wave
-  const bool live = q0 < S;                // S % 128 == 0: a wave is all in or all out
-  const int myq = q0 + r;                  // the query row this lane owns
+  const bool live = q0 < S;                // wave has at least one real row
+  const int myq = q0 + r;                  // the query row this lane owns (>= S: padding)
+  const int myq_ld = TAIL ? min(myq, S - 1) : myq;
   const int kend = min(S, (qb + 1) * FWD_QB);
-  const int ntiles = kend / TK;
+  const int ntiles = (kend + TK - 1) / TK;
   const int t_diag = live ? (q0 + 31) / TK : -1;  // this wave's last (masked) tile
 
-  // Q fragments: Q[myq][16s + 8hh .. +7], s = 0..7
-  bf16x8 qf[8];
+  // Q fragments: Q[myq][16s + 8hh .. +7], s = 0..NS-1
+  bf16x8 qf[NS];
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
-    qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq * D + 16 * s + 8 * hh)) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int s = 0; s < NS; ++s)
+    qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq_ld * D + 16 * s + 8 * hh)) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
 
   // lane-constant LDS read offsets (buffer / half / k-step parts are immediates)
-  // K: k_off(32n + r, 2s + hh) = r*256 + ((2s ^ x) << 4) + 8192 n,  x = hh ^ (r & 15)
-  int kro[8];
-  {
-    const int x = hh ^ (r & 15);
+  int kro[NS];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) kro[s] = r * ROWB + (((2 * s) ^ x) << 4);
-  }
+  for (int s = 0; s < NS; ++s) kro[s] = k_off<D>(r, 2 * s + hh);
   // V^T: key = 32n + 16s' + 4hh + qq (+8), column block 32dt + 16(g&1) + 4pp
-  int vro[4];
+  int vro[ND];
   {
     const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-      vro[dt] = (4 * hh + qq) * ROWB + ((4 * (dt ^ qq) + 2 * (g & 1) + (pp >> 1)) << 4) + (pp & 1) * 8;
+    for (int dt = 0; dt < ND; ++dt) vro[dt] = v_off<D>(4 * hh + qq, 4 * dt + 2 * (g & 1) + (pp >> 1)) + (pp & 1) * 8;
   }
 
-  f32x16 acc[4];
+  f32x16 acc[ND];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < ND; ++i)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  // staging: 512 threads x (2 x 16 B of K + 2 x 16 B of V) = one 64-key tile
-  u32x4 stk[2], stv[2];
+  // staging: 512 threads x NL x (16 B of K + 16 B of V) = one 64-key tile
+  u32x4 stk[NL], stv[NL];
   auto gload = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NL; ++i) {
       const int e = tid + 512 * i;
-      const int key = e >> 4, c = e & 15;
-      const int64_t gidx = koff + (int64_t)(t * TK + key) * D + c * 8;
+      const int key = e / NCH, c = e % NCH;
+      const int64_t gidx = koff + (int64_t)(TAIL ? min(t * TK + key, S - 1) : t * TK + key) * D + c * 8;
       stk[i] = ld16(K + gidx);
       stv[i] = ld16(V + gidx);
     }
   };
   auto swrite = [&](int buf) {
-    char* kb = smem + buf * 32768;
-    char* vb = kb + 16384;
+    char* kb = smem + buf * 2 * TILEB;
+    char* vb = kb + TILEB;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NL; ++i) {
       const int e = tid + 512 * i;
-      const int key = e >> 4, c = e & 15;
-      *(u32x4*)(kb + k_off(key, c)) = stk[i];
-      *(u32x4*)(vb + v_off(key, c)) = stv[i];
+      const int key = e / NCH, c = e % NCH;
+      *(u32x4*)(kb + k_off<D>(key, c)) = stk[i];
+      *(u32x4*)(vb + v_off<D>(key, c)) = stv[i];
     }
   };
 
   auto compute = [&](int t, int buf, bool mask) {
-    const char* kb = smem + buf * 32768;
-    const char* vb = kb + 16384;
+    const char* kb = smem + buf * 2 * TILEB;
+    const char* vb = kb + TILEB;
     // ---- S^T = K Q^T : two 32-key halves (first MFMA of each chain starts from 0)
     f32x16 sc[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       const f32x16 z = {};
-      sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[0] + 8192 * n)), qf[0], z);
+      sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[0] + 32 * ROWB * n)), qf[0], z);
 #pragma unroll
-      for (int s = 1; s < 8; ++s)
-        sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[s] + 8192 * n)), qf[s], sc[n]);
+      for (int s = 1; s < NS; ++s)
+        sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[s] + 32 * ROWB * n)), qf[s], sc[n]);
     }
     // ---- causal mask (diagonal tile only) and row max of the raw scores
     if (mask) {
@@ -229,7 +250,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
       l_run *= alpha;
       m_run = m_new;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < ND; ++i)
 #pragma unroll
         for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
     }
@@ -259,7 +280,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
         const bf16x8 pf = as_bf16x8(w);
         const int kb0 = (32 * n + 16 * s) * ROWB;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
+        for (int dt = 0; dt < ND; ++dt) {
           const bf16x4 va = tr_read(vb, vro[dt] + kb0);
           const bf16x4 vbv = tr_read(vb, vro[dt] + kb0 + 8 * ROWB);
           const bf16x8 vf = __builtin_shufflevector(va, vbv, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -281,7 +302,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
   // barrier; the loop then inherits "Q pending" and, vmcnt being in-order,
   // its first MFMA waits on the K/V prefetch of the same iteration.
 #pragma unroll
-  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
+  for (int s = 0; s < NS; ++s) asm volatile("" ::"v"(qf[s]));
   __syncthreads();
   int t = 0;
   for (; t + 1 < ntiles; t += 2) {  // unrolled by 2: buffer offsets become immediates
@@ -290,13 +311,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
   }
   if (t < ntiles) step(t, 0);
 
-  if (!live) return;
+  if (!live || (TAIL && myq >= S)) return;
   // ---- epilogue: O = O^T / l  (lane owns query row myq; d rows from the C map)
   const float l_tot = xhalf_sum(l_run);
   const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  bf16_t* orow = O + o_off(b, h, myq, H, S, o_bshd);
+  bf16_t* orow = O + o_off<D>(b, h, myq, H, S, o_bshd);
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = 32 * dt + 8 * g + 4 * hh;
@@ -310,35 +331,14 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
 
 // One image for row reads (ds_read_b128, 32x32x16 A/B operand) AND
 // transposed reads (ds_read_b64_tr_b16): guide T10 layout (b),
-// chunk' = chunk ^ (((row & 3) << 2) | ((row >> 2) & 3)).
+// D = 128: chunk' = chunk ^ (((row & 3) << 2) | ((row >> 2) & 3));
+// D = 64 (8 chunks): chunk' = chunk ^ (((row & 3) << 1) | ((row >> 2) & 1)).
+// The XOR depends on row & 15 only, so offsets of rows 16k apart differ by
+// exactly 16k rows (the row-block parts of every read are immediates).
+template <int D>
 __device__ __forceinline__ int rt_off(int row, int chunk) {
-  return row * ROWB + ((chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
-}
-
-// A-operand fragment of X^T . Y where X is a row-major [rows][128] bf16 LDS
-// image read transposed: lane (r, hh) gets X[rows rb + 4hh + (0..3)][32dt + r]
-// and X[rows rb + 8 + 4hh + (0..3)][32dt + r]  (the permuted k order that
-// matches a C-layout accumulator used as the B operand).
-__device__ __forceinline__ bf16x8 tr_frag(const char* img, int rb, int dt, int lane) {
-  const int g = lane >> 4, i16 = lane & 15, hh = lane >> 5;
-  const int qq = i16 >> 2, pp = i16 & 3;
-  const int col = 32 * dt + 16 * (g & 1) + 4 * pp;
-  const int ra = rb + 4 * hh + qq;
-  const bf16x4 a = tr_read(img, rt_off(ra, col >> 3) + (col & 7) * 2);
-  const bf16x4 b = tr_read(img, rt_off(ra + 8, col >> 3) + (col & 7) * 2);
-  bf16x8 f;
-  f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
-  f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
-  return f;
-}
-
-__device__ __forceinline__ bf16x8 pack_frag(const f32x16& x, int s) {
-  u32x4 w;
-  w[0] = pack2(x[8 * s + 0], x[8 * s + 1]);
-  w[1] = pack2(x[8 * s + 2], x[8 * s + 3]);
-  w[2] = pack2(x[8 * s + 4], x[8 * s + 5]);
-  w[3] = pack2(x[8 * s + 6], x[8 * s + 7]);
-  return as_bf16x8(w);
+  const int swz = D == 128 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 3) << 1) | ((row >> 2) & 1));
+  return row * AG<D>::ROWB + ((chunk ^ swz) << 4);
 }
 
 // ---------------------------------------------------------------------------
@@ -353,93 +353,103 @@ __device__ __forceinline__ bf16x8 pack_frag(const f32x16& x, int s) {
 //   dV^T += dO^T P, dK^T += Q^T dS   (A = transposed reads, B = the accumulators)
 // The block sweeps every query head of the GQA group and every causal tile.
 // ---------------------------------------------------------------------------
-#define DKV_QBUF (32768 + 512)
-#define DKV_LDS (2 * DKV_QBUF + 65536)
+template <int D>
+struct DKV {
+  static constexpr int QBUF = 2 * TK * AG<D>::ROWB + 512;  // Q tile, dO tile, lse, -delta
+  static constexpr int KVB = 128 * AG<D>::ROWB;             // K (or V) of the 128-key block
+  static constexpr int LDS = 2 * QBUF + 2 * KVB;
+};
 
+template <int D, bool TAIL>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int H, int Hk, int S, float scale,
     float scale_log2, int o_bshd) {
-  // [Q/dO/lse/-delta buffer 0][buffer 1][K 32K][V 32K]
+  using G = AG<D>;
+  constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
+  constexpr int QBUF = DKV<D>::QBUF, KVB = DKV<D>::KVB;
+  constexpr int NLQ = TK * NCH / 512, NLK = 128 * NCH / 512;
+  // [Q/dO/lse/-delta buffer 0][buffer 1][K][V]
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* kimg = smem + 2 * DKV_QBUF;
-  char* vimg = kimg + 32768;
+  char* kimg = smem + 2 * QBUF;
+  char* vimg = kimg + KVB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int kg = wave & 3, m = wave >> 2;
   // heaviest (most query tiles) key blocks first; (b, hk) fastest
-  const int nkb = S / 128;
+  const int nkb = (S + 127) / 128;
   const int kb = nkb - 1 - (int)(blockIdx.x / (B * Hk));
   const int bh = blockIdx.x % (B * Hk);
   const int b = bh / Hk, hk = bh % Hk;
   const int rep = H / Hk;
   const int kw = kb * 128 + kg * 32;  // first key of this wave
   const int mykey = kw + r;
-  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * 128;
+  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
 
   // K / V of the block -> LDS (rt_off image: row reads give the B operands)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NLK; ++i) {
     const int e = tid + 512 * i;
-    const int row = e >> 4, c = e & 15;
-    const int64_t g = koff + (int64_t)(kb * 128 + row) * 128 + c * 8;
-    *(u32x4*)(kimg + rt_off(row, c)) = ld16(K + g);
-    *(u32x4*)(vimg + rt_off(row, c)) = ld16(V + g);
+    const int row = e / NCH, c = e % NCH;
+    const int64_t g = koff + (int64_t)(TAIL ? min(kb * 128 + row, S - 1) : kb * 128 + row) * D + c * 8;
+    *(u32x4*)(kimg + rt_off<D>(row, c)) = ld16(K + g);
+    *(u32x4*)(vimg + rt_off<D>(row, c)) = ld16(V + g);
   }
-  f32x16 dk[4], dv[4];
+  f32x16 dk[ND], dv[ND];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < ND; ++i)
 #pragma unroll
     for (int j = 0; j < 16; ++j) { dk[i][j] = 0.f; dv[i][j] = 0.f; }
 
-  int rro[8], tro[4], tro8[4];
+  int rro[NS], tro[ND], tro8[ND];
   {
-    const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) rro[s] = r * ROWB + (((2 * s + hh) ^ swz) << 4);
+    for (int s = 0; s < NS; ++s) rro[s] = rt_off<D>(r, 2 * s + hh);
     const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-    const int lo = 2 * (g & 1) + (pp >> 1);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      tro[dt] = (4 * hh + qq) * ROWB + ((4 * (dt ^ qq) + (lo ^ hh)) << 4) + (pp & 1) * 8;
-      tro8[dt] = (4 * hh + qq + 8) * ROWB + ((4 * (dt ^ qq) + (lo ^ ((hh + 2) & 3))) << 4) + (pp & 1) * 8;
+    for (int dt = 0; dt < ND; ++dt) {
+      const int c = 4 * dt + 2 * (g & 1) + (pp >> 1);
+      tro[dt] = rt_off<D>(4 * hh + qq, c) + (pp & 1) * 8;
+      tro8[dt] = rt_off<D>(4 * hh + qq + 8, c) + (pp & 1) * 8;
     }
   }
 
   const int qt0 = (kb * 128) / 64;  // first causal 64-row query tile
-  const int nqt = S / 64 - qt0;
+  const int nqt = (S + TK - 1) / TK - qt0;
   const int total = nqt * rep;
-  u32x4 sq[2], sdo[2];
+  u32x4 sq[NLQ], sdo[NLQ];
   float slse = 0.f, sdel = 0.f;
   auto gload = [&](int it) {
     const int hq = hk * rep + it / nqt;
     const int qt = qt0 + it % nqt;
-    const int64_t qoff = ((int64_t)(b * H + hq) * S) * 128;
+    const int64_t qoff = ((int64_t)(b * H + hq) * S) * D;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NLQ; ++i) {
       const int e = tid + 512 * i;
-      const int row = e >> 4, c = e & 15;
-      const int64_t g = qoff + (int64_t)(qt * 64 + row) * 128 + c * 8;
-      sq[i] = ld16(Q + g);
-      sdo[i] = ld16(dO + o_off(b, hq, qt * 64 + row, H, S, o_bshd) + c * 8);
+      const int row = e / NCH, c = e % NCH;
+      const int qr = TAIL ? min(qt * 64 + row, S - 1) : qt * 64 + row;
+      sq[i] = ld16(Q + qoff + (int64_t)qr * D + c * 8);
+      sdo[i] = ld16(dO + o_off<D>(b, hq, qr, H, S, o_bshd) + c * 8);
     }
     if (tid < 64) {
-      const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + tid;
-      slse = LSE[li];  // scaled at swrite: consuming it here would wait on the whole prefetch
+      const int q = qt * 64 + tid;
+      const int64_t li = (int64_t)(b * H + hq) * S + (TAIL ? min(q, S - 1) : q);
+      const float x = LSE[li];  // scaled at swrite: consuming it here would wait on the whole prefetch
+      slse = (!TAIL || q < S) ? x : INFINITY;  // padded query row: p = exp2(. - inf) = 0
       sdel = DELTA[li];
     }
   };
   auto swrite = [&](int buf) {
-    char* qb_ = smem + buf * DKV_QBUF;
-    char* ob = qb_ + 16384;
-    float* lb = (float*)(qb_ + 32768);
+    char* qb_ = smem + buf * QBUF;
+    char* ob = qb_ + TILEB;
+    float* lb = (float*)(qb_ + 2 * TILEB);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NLQ; ++i) {
       const int e = tid + 512 * i;
-      const int row = e >> 4, c = e & 15;
-      *(u32x4*)(qb_ + rt_off(row, c)) = sq[i];
-      *(u32x4*)(ob + rt_off(row, c)) = sdo[i];
+      const int row = e / NCH, c = e % NCH;
+      *(u32x4*)(qb_ + rt_off<D>(row, c)) = sq[i];
+      *(u32x4*)(ob + rt_off<D>(row, c)) = sdo[i];
     }
     if (tid < 64) {
       lb[tid] = slse * LOG2E;
@@ -448,9 +458,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
   };
 
   auto subtile = [&](int buf, int qs, bool mask) {
-    const char* qi = smem + buf * DKV_QBUF;
-    const char* oi = qi + 16384;
-    const float* lb = (const float*)(qi + 32768);
+    const char* qi = smem + buf * QBUF;
+    const char* oi = qi + TILEB;
+    const float* lb = (const float*)(qi + 2 * TILEB);
     f32x16 nd;
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -461,12 +471,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
     const f32x16 z = {};
     f32x16 sc = z, dp = nd;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const bf16x8 qa = as_bf16x8(*(const u32x4*)(qi + rro[s] + 8192 * m));
-      const bf16x8 kf = as_bf16x8(*(const u32x4*)(kimg + rro[s] + 8192 * kg));
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 qa = as_bf16x8(*(const u32x4*)(qi + rro[s] + 32 * ROWB * m));
+      const bf16x8 kf = as_bf16x8(*(const u32x4*)(kimg + rro[s] + 32 * ROWB * kg));
       sc = mfma32(qa, kf, sc);
-      const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rro[s] + 8192 * m));
-      const bf16x8 vf = as_bf16x8(*(const u32x4*)(vimg + rro[s] + 8192 * kg));
+      const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rro[s] + 32 * ROWB * m));
+      const bf16x8 vf = as_bf16x8(*(const u32x4*)(vimg + rro[s] + 32 * ROWB * kg));
       dp = mfma32(oa, vf, dp);
     }
     uint32_t pw[8], sw[8];
@@ -494,7 +504,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
       const bf16x8 pb = as_bf16x8(a), sb = as_bf16x8(c);
       const int rb = (32 * m + 16 * s2) * ROWB;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < ND; ++dt) {
         const bf16x4 o0 = tr_read(oi, tro[dt] + rb), o1 = tr_read(oi, tro8[dt] + rb);
         dv[dt] = mfma32((bf16x8)__builtin_shufflevector(o0, o1, 0, 1, 2, 3, 4, 5, 6, 7), pb, dv[dt]);
         const bf16x4 q0 = tr_read(qi, tro[dt] + rb), q1 = tr_read(qi, tro8[dt] + rb);
@@ -522,26 +532,28 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
   if (it < total) step(it, 0);
 
   // sum the two query halves' partials: waves m = 1 park theirs in LDS
-  float* red = (float*)smem;  // 4 waves x 2 x 64 lanes x 64 floats = 128 KB, Q/dO/K/V are dead
+  // (4 waves x 2 x 64 lanes x 16 ND floats; Q/dO/K/V are dead)
+  constexpr int RW = ND * 16 * 64;  // floats per (wave, dk|dv)
+  float* red = (float*)smem;
   if (m == 1) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
       for (int j = 0; j < 16; j += 4) {
-        *(f32x4*)(red + ((kg * 2 + 0) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4) =
+        *(f32x4*)(red + (kg * 2 + 0) * RW + (dt * 16 + j) * 64 + lane * 4) =
             f32x4{dk[dt][j], dk[dt][j + 1], dk[dt][j + 2], dk[dt][j + 3]};
-        *(f32x4*)(red + ((kg * 2 + 1) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4) =
+        *(f32x4*)(red + (kg * 2 + 1) * RW + (dt * 16 + j) * 64 + lane * 4) =
             f32x4{dv[dt][j], dv[dt][j + 1], dv[dt][j + 2], dv[dt][j + 3]};
       }
   }
   __syncthreads();
-  if (m == 1) return;
+  if (m == 1 || (TAIL && mykey >= S)) return;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
     for (int j = 0; j < 16; j += 4) {
-      const f32x4 a = *(const f32x4*)(red + ((kg * 2 + 0) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4);
-      const f32x4 c = *(const f32x4*)(red + ((kg * 2 + 1) * 64 * 64) + (dt * 16 + j) * 64 + lane * 4);
+      const f32x4 a = *(const f32x4*)(red + (kg * 2 + 0) * RW + (dt * 16 + j) * 64 + lane * 4);
+      const f32x4 c = *(const f32x4*)(red + (kg * 2 + 1) * RW + (dt * 16 + j) * 64 + lane * 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         dk[dt][j + i] += a[i];
@@ -549,10 +561,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
       }
     }
   // store: lane owns key `mykey`, d rows 32dt + 8g + 4hh + (0..3)
-  bf16_t* dkr = dK + koff + (int64_t)mykey * 128;
-  bf16_t* dvr = dV + koff + (int64_t)mykey * 128;
+  bf16_t* dkr = dK + koff + (int64_t)mykey * D;
+  bf16_t* dvr = dV + koff + (int64_t)mykey * D;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = 32 * dt + 8 * g + 4 * hh;
@@ -574,104 +586,108 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
 // the B operand straight from the accumulator.  K and V share the
 // one-image-two-ways layout (rt_off).
 // ---------------------------------------------------------------------------
+template <int D, bool TAIL>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const bf16_t* __restrict__ O, const float* __restrict__ LSE,
     float* __restrict__ DELTA, bf16_t* __restrict__ dQ, int B, int H, int Hk, int S, float scale, float scale_log2,
     int o_bshd) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K 16K + V 16K)
+  using G = AG<D>;
+  constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
+  constexpr int NL = TK * NCH / 512;
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // 2 x (K tile + V tile)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = (S + FWD_QB - 1) / FWD_QB;
   int qb, h, b;
   fwd_block_coords(blockIdx.x, nqb, B, H, Hk, &qb, &h, &b);
   const int hk = h / (H / Hk);
-  const int64_t qoff = ((int64_t)(b * H + h) * S) * 128;
-  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * 128;
+  const int64_t qoff = ((int64_t)(b * H + h) * S) * D;
+  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
   const int q0 = qb * FWD_QB + wave * 32;
   const bool live = q0 < S;
   const int myq = q0 + r;
+  const int myq_ld = TAIL ? min(myq, S - 1) : myq;
   const int kend = min(S, (qb + 1) * FWD_QB);
-  const int ntiles = kend / TK;
+  const int ntiles = (kend + TK - 1) / TK;
   const int t_diag = live ? (q0 + 31) / TK : -1;
 
-  bf16x8 qf[8], of[8];
+  bf16x8 qf[NS], of[NS];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq * 128 + 16 * s + 8 * hh)) : bf16x8{};
-    of[s] = live ? as_bf16x8(ld16(dO + o_off(b, h, myq, H, S, o_bshd) + 16 * s + 8 * hh)) : bf16x8{};
+  for (int s = 0; s < NS; ++s) {
+    qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq_ld * D + 16 * s + 8 * hh)) : bf16x8{};
+    of[s] = live ? as_bf16x8(ld16(dO + o_off<D>(b, h, myq_ld, H, S, o_bshd) + 16 * s + 8 * hh)) : bf16x8{};
   }
-  const float lse2 = live ? LSE[(int64_t)(b * H + h) * S + myq] * LOG2E : 0.f;
+  const float lse2 = live ? LSE[(int64_t)(b * H + h) * S + myq_ld] * LOG2E : 0.f;
   // delta = rowsum(dO * O), computed here (the lane already holds its half of
   // the dO row) and published for the dK/dV kernel that runs next
   float del = 0.f;
   if (live) {
     float part = 0.f;
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < NS; ++s) {
       float a[8], g[8];
-      unpack8(ld16(O + o_off(b, h, myq, H, S, o_bshd) + 16 * s + 8 * hh), a);
+      unpack8(ld16(O + o_off<D>(b, h, myq_ld, H, S, o_bshd) + 16 * s + 8 * hh), a);
       unpack8(__builtin_bit_cast(u32x4, of[s]), g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) part = fmaf(a[j], g[j], part);
     }
     del = xhalf_sum(part);
-    if (hh == 0) DELTA[(int64_t)(b * H + h) * S + myq] = del;
+    if (hh == 0 && (!TAIL || myq < S)) DELTA[(int64_t)(b * H + h) * S + myq] = del;
   }
-  f32x16 acc[4];
+  f32x16 acc[ND];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < ND; ++i)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
 
-  int rro[8], tro[4], tro8[4];
+  int rro[NS], tro[ND], tro8[ND];
   {
-    const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) rro[s] = r * ROWB + (((2 * s + hh) ^ swz) << 4);
+    for (int s = 0; s < NS; ++s) rro[s] = rt_off<D>(r, 2 * s + hh);
     const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-    const int lo = 2 * (g & 1) + (pp >> 1);
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      tro[dt] = (4 * hh + qq) * ROWB + ((4 * (dt ^ qq) + (lo ^ hh)) << 4) + (pp & 1) * 8;
-      tro8[dt] = (4 * hh + qq + 8) * ROWB + ((4 * (dt ^ qq) + (lo ^ ((hh + 2) & 3))) << 4) + (pp & 1) * 8;
+    for (int dt = 0; dt < ND; ++dt) {
+      const int c = 4 * dt + 2 * (g & 1) + (pp >> 1);
+      tro[dt] = rt_off<D>(4 * hh + qq, c) + (pp & 1) * 8;
+      tro8[dt] = rt_off<D>(4 * hh + qq + 8, c) + (pp & 1) * 8;
     }
   }
 
-  u32x4 stk[2], stv[2];
+  u32x4 stk[NL], stv[NL];
   auto gload = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NL; ++i) {
       const int e = tid + 512 * i;
-      const int key = e >> 4, c = e & 15;
-      const int64_t gidx = koff + (int64_t)(t * TK + key) * 128 + c * 8;
+      const int key = e / NCH, c = e % NCH;
+      const int64_t gidx = koff + (int64_t)(TAIL ? min(t * TK + key, S - 1) : t * TK + key) * D + c * 8;
       stk[i] = ld16(K + gidx);
       stv[i] = ld16(V + gidx);
     }
   };
   auto swrite = [&](int buf) {
-    char* kb = smem + buf * 32768;
-    char* vb = kb + 16384;
+    char* kb = smem + buf * 2 * TILEB;
+    char* vb = kb + TILEB;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NL; ++i) {
       const int e = tid + 512 * i;
-      const int key = e >> 4, c = e & 15;
-      *(u32x4*)(kb + rt_off(key, c)) = stk[i];
-      *(u32x4*)(vb + rt_off(key, c)) = stv[i];
+      const int key = e / NCH, c = e % NCH;
+      *(u32x4*)(kb + rt_off<D>(key, c)) = stk[i];
+      *(u32x4*)(vb + rt_off<D>(key, c)) = stv[i];
     }
   };
   auto compute = [&](int t, int buf, bool mask) {
-    const char* kb = smem + buf * 32768;
-    const char* vb = kb + 16384;
+    const char* kb = smem + buf * 2 * TILEB;
+    const char* vb = kb + TILEB;
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       const f32x16 z = {};
-      f32x16 sc = mfma32(as_bf16x8(*(const u32x4*)(kb + rro[0] + 8192 * n)), qf[0], z);
-      f32x16 dp = mfma32(as_bf16x8(*(const u32x4*)(vb + rro[0] + 8192 * n)), of[0], z);
+      f32x16 sc = mfma32(as_bf16x8(*(const u32x4*)(kb + rro[0] + 32 * ROWB * n)), qf[0], z);
+      f32x16 dp = mfma32(as_bf16x8(*(const u32x4*)(vb + rro[0] + 32 * ROWB * n)), of[0], z);
 #pragma unroll
-      for (int s = 1; s < 8; ++s) {
-        sc = mfma32(as_bf16x8(*(const u32x4*)(kb + rro[s] + 8192 * n)), qf[s], sc);
-        dp = mfma32(as_bf16x8(*(const u32x4*)(vb + rro[s] + 8192 * n)), of[s], dp);
+      for (int s = 1; s < NS; ++s) {
+        sc = mfma32(as_bf16x8(*(const u32x4*)(kb + rro[s] + 32 * ROWB * n)), qf[s], sc);
+        dp = mfma32(as_bf16x8(*(const u32x4*)(vb + rro[s] + 32 * ROWB * n)), of[s], dp);
       }
       uint32_t sw[8];
 #pragma unroll
@@ -693,7 +709,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
         const bf16x8 sb = as_bf16x8(w);
         const int rb = 32 * n + 16 * s2;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
+        for (int dt = 0; dt < ND; ++dt) {
           const bf16x4 a = tr_read(kb, tro[dt] + rb * ROWB);
           const bf16x4 c = tr_read(kb, tro8[dt] + rb * ROWB);
           acc[dt] = mfma32((bf16x8)__builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7), sb, acc[dt]);
@@ -712,7 +728,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
   gload(0);
   swrite(0);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]), "v"(of[s]));  // retire resident loads (see fwd)
+  for (int s = 0; s < NS; ++s) asm volatile("" ::"v"(qf[s]), "v"(of[s]));  // retire resident loads (see fwd)
   asm volatile("" ::"v"(lse2), "v"(del));
   __syncthreads();
   int t = 0;
@@ -722,10 +738,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
   }
   if (t < ntiles) step(t, 0);
 
-  if (!live) return;
-  bf16_t* qrow = dQ + qoff + (int64_t)myq * 128;
+  if (!live || (TAIL && myq >= S)) return;
+  bf16_t* qrow = dQ + qoff + (int64_t)myq * D;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = 32 * dt + 8 * g + 4 * hh;
@@ -736,25 +752,63 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     }
 }
 
+template <int D, bool TAIL>
 static void attn_set_lds_limits() {
   static bool done = false;
   if (done) return;
-  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, DKV_LDS);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D, TAIL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            4 * AG<D>::TILEB);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, TAIL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            DKV<D>::LDS);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, TAIL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            4 * AG<D>::TILEB);
   done = true;
+}
+
+template <int D, bool TAIL>
+static int attn_fwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int H,
+                           int Hk, int S, int o_bshd, float scale, hipStream_t stream) {
+  attn_set_lds_limits<D, TAIL>();
+  const int nqb = (S + FWD_QB - 1) / FWD_QB;
+  hipLaunchKernelGGL((attn_fwd_kernel<D, TAIL>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 4 * AG<D>::TILEB, stream, q, k, v,
+                     o, lse, B, H, Hk, S, scale * LOG2E, o_bshd);
+  return (int)hipGetLastError();
+}
+
+template <int D, bool TAIL>
+static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                           const float* lse, float* delta, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B, int H, int Hk,
+                           int S, int o_bshd, float scale, hipStream_t stream) {
+  attn_set_lds_limits<D, TAIL>();
+  // dQ first: it also computes delta = rowsum(dO * O), which dK/dV then reads
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, TAIL>), dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES),
+                     4 * AG<D>::TILEB, stream, q, k, v, dout, o, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E,
+                     o_bshd);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, TAIL>), dim3(((S + 127) / 128) * B * Hk), dim3(512), DKV<D>::LDS, stream, q,
+                     k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
+  return (int)hipGetLastError();
+}
+
+static bool attn_shape_ok(int B, int H, int Hk, int S, int D, int flags) {
+  return (D == 64 || D == 128) && B > 0 && S > 0 && Hk > 0 && H % Hk == 0 && (flags & 1);
 }
 
 // flags: bit 0 causal (required), bit 1 O / dO in [B, S, H, D] (else [B, H, S, D]).
 extern "C" int toa_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int H,
                             int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
-  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !(flags & 1)) return (int)hipErrorInvalidValue;
+  if (!attn_shape_ok(B, H, Hk, S, D, flags)) return (int)hipErrorInvalidValue;
   const int o_bshd = (flags >> 1) & 1;
-  attn_set_lds_limits();
-  const int nqb = (S + FWD_QB - 1) / FWD_QB;
-  hipLaunchKernelGGL(attn_fwd_kernel<128>, dim3(nqb * H * B), dim3(64 * FWD_WAVES), 65536, stream, q, k, v, o, lse,
-                     B, H, Hk, S, scale * LOG2E, o_bshd);
-  return (int)hipGetLastError();
+  // S % 256 == 0: every 256-row block and 64-key tile is full, no clamping
+  const bool tail = S % FWD_QB != 0;
+#define TOA_ATTN_FWD(DD, TT) attn_fwd_launch<DD, TT>(q, k, v, o, lse, B, H, Hk, S, o_bshd, scale, stream)
+#ifdef TOA_ATTN_D128_ONLY
+  if (D != 128) return (int)hipErrorInvalidValue;
+  return tail ? TOA_ATTN_FWD(128, true) : TOA_ATTN_FWD(128, false);
+#else
+  if (D == 128) return tail ? TOA_ATTN_FWD(128, true) : TOA_ATTN_FWD(128, false);
+  return tail ? TOA_ATTN_FWD(64, true) : TOA_ATTN_FWD(64, false);
+#endif
+#undef TOA_ATTN_FWD
 }
 
 // dq_acc is unused (kept in the ABI for an atomic-dQ variant); dq/dk/dv bf16.
@@ -762,15 +816,17 @@ extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
                             const float* lse, float* delta, float* dq_acc, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B,
                             int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
   (void)dq_acc;
-  if (D != 128 || S % 128 != 0 || H % Hk != 0 || !(flags & 1)) return (int)hipErrorInvalidValue;
+  if (!attn_shape_ok(B, H, Hk, S, D, flags)) return (int)hipErrorInvalidValue;
   const int o_bshd = (flags >> 1) & 1;
-  attn_set_lds_limits();
-  const int64_t rows = (int64_t)B * H * S;
-  (void)rows;
-  // dQ first: it also computes delta = rowsum(dO * O), which dK/dV then reads
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES), 65536,
-                     stream, q, k, v, dout, o, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((S / 128) * B * Hk), dim3(512), DKV_LDS, stream, q, k, v, dout, lse,
-                     delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
-  return (int)hipGetLastError();
+  const bool tail = S % FWD_QB != 0;
+#define TOA_ATTN_BWD(DD, TT) \
+  attn_bwd_launch<DD, TT>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, H, Hk, S, o_bshd, scale, stream)
+#ifdef TOA_ATTN_D128_ONLY
+  if (D != 128) return (int)hipErrorInvalidValue;
+  return tail ? TOA_ATTN_BWD(128, true) : TOA_ATTN_BWD(128, false);
+#else
+  if (D == 128) return tail ? TOA_ATTN_BWD(128, true) : TOA_ATTN_BWD(128, false);
+  return tail ? TOA_ATTN_BWD(64, true) : TOA_ATTN_BWD(64, false);
+#endif
+#undef TOA_ATTN_BWD
 }

@@ -176,6 +176,30 @@ def test_rocm_env_block():
     assert knobs["NCCL_MIN_NCHANNELS"] == "32"
 
 
+def test_rccl_defaults_never_override_user_env():
+    """xGMI defaults (envgen.cc kRcclDefaults) are injected into TFJob and
+    PyTorchJob trainers unless --nccl-env or the container already sets them."""
+    job = fx.new_tfjob(2, 0)
+    env = {e["name"]: e["value"] for e in core.gen_env(job, "Worker", 0)}
+    assert env["TORCH_NCCL_HIGH_PRIORITY"] == "1"
+    assert env["TORCH_NCCL_AVOID_RECORD_STREAMS"] == "1"
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    over = {e["name"]: e["value"] for e in core.gen_env(job, "Worker", 0, {"nccl_env": {"TORCH_NCCL_HIGH_PRIORITY": "0"}})}
+    assert over["TORCH_NCCL_HIGH_PRIORITY"] == "0"
+    assert [e["name"] for e in core.gen_env(job, "Worker", 0, {"nccl_env": {"TORCH_NCCL_HIGH_PRIORITY": "0"}})].count(
+        "TORCH_NCCL_HIGH_PRIORITY") == 1
+    off = {e["name"] for e in core.gen_env(job, "Worker", 0, {"rccl_defaults": False})}
+    assert "TORCH_NCCL_HIGH_PRIORITY" not in off
+    # a container that sets one keeps its own value (and gets no duplicate entry)
+    tpl = job["spec"]["tfReplicaSpecs"]["Worker"]["template"]
+    tpl["spec"]["containers"][0].setdefault("env", []).append({"name": "TORCH_NCCL_HIGH_PRIORITY", "value": "0"})
+    out = core.set_cluster_spec(job, tpl, "Worker", 0)
+    names = [e["name"] for e in out["spec"]["containers"][0]["env"]]
+    assert names.count("TORCH_NCCL_HIGH_PRIORITY") == 1
+    assert {e["name"]: e["value"] for e in out["spec"]["containers"][0]["env"]}["TORCH_NCCL_HIGH_PRIORITY"] == "0"
+    assert "TORCH_NCCL_AVOID_RECORD_STREAMS" in names
+
+
 # ---------------------------------------------------------------------------
 # status_test.go TestStatus (SURVEY Appendix A) -- assert the LAST condition
 # ---------------------------------------------------------------------------

@@ -353,14 +353,20 @@ def _attn_ref(q, k, v, scale):
     return torch.matmul(torch.softmax(s, -1), vf), lse
 
 
-@pytest.mark.parametrize("B,H,Hk,S,spike", [(1, 2, 2, 128, False), (2, 4, 2, 384, False), (1, 8, 2, 1024, False),
-                                             (1, 2, 1, 1024, True)])
-def test_flash_attention_fwd_bwd(B, H, Hk, S, spike):
+@pytest.mark.parametrize("B,H,Hk,S,D,spike", [(1, 2, 2, 128, 128, False), (2, 4, 2, 384, 128, False),
+                                               (1, 8, 2, 1024, 128, False), (1, 2, 1, 1024, 128, True),
+                                               # ragged S: tails of the 64-key tiles / 256-row and 128-key blocks
+                                               (1, 2, 1, 1, 128, False), (2, 4, 2, 100, 128, False),
+                                               (1, 4, 4, 333, 128, False), (1, 2, 2, 1000, 128, True),
+                                               # head_dim 64 (Llama-3.2-1B / llama-tiny)
+                                               (1, 2, 2, 128, 64, False), (2, 4, 2, 384, 64, False),
+                                               (1, 8, 2, 1024, 64, True), (2, 4, 1, 77, 64, False),
+                                               (1, 4, 2, 530, 64, False)])
+def test_flash_attention_fwd_bwd(B, H, Hk, S, D, spike):
     L = _lib()
     from tf_operator_amd.ops import llm
 
     torch.manual_seed(7)
-    D = 128
     scale = 1.0 / math.sqrt(D)
     q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -383,9 +389,59 @@ def test_flash_attention_fwd_bwd(B, H, Hk, S, spike):
     do = torch.randn_like(o)
     o.backward(do)
     orf.backward(do.float())
-    assert rel(q.grad, qr.grad) < 3e-2, rel(q.grad, qr.grad)
-    assert rel(k.grad, kr.grad) < 3e-2, rel(k.grad, kr.grad)
-    assert rel(v.grad, vr.grad) < 3e-2, rel(v.grad, vr.grad)
+    # relative error with a floor: at S = 1 the exact dK is 0 (one key, p = 1)
+    # and the kernel's is bf16 rounding noise of delta = rowsum(dO * O)
+    for got, ref in ((q.grad, qr.grad), (k.grad, kr.grad), (v.grad, vr.grad)):
+        err = float((got.float() - ref).norm())
+        assert err <= 3e-2 * max(float(ref.norm()), 1e-2 * ref.numel() ** 0.5), err
+
+
+def test_flash_attention_bench_shape():
+    """The flagship shape (Llama-3-8B, micro-batch 6: B=6, H=32, Hkv=8,
+    S=4096, D=128, O/dO in [B,S,H,D]) through the model's entry point; the
+    fp32 reference is computed for sampled (batch, kv-group) slices (the
+    first and last of each), which checks the XCD-aware block mapping at
+    the corners of the grid."""
+    _lib()
+    from tf_operator_amd.ops import llm
+
+    torch.manual_seed(11)
+    B, H, Hk, S, D = 6, 32, 8, 4096, 128
+    rep = H // Hk
+    scale = 1.0 / math.sqrt(D)
+    q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = llm.causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]
+    do = torch.randn_like(o)
+    o.backward(do)
+    torch.cuda.synchronize()
+    for b, g in ((0, 0), (B - 1, Hk - 1), (2, 3)):
+        hs = slice(g * rep, (g + 1) * rep)
+        qr = q[b:b + 1, hs].detach().float().requires_grad_()
+        kr = k[b:b + 1, g:g + 1].detach().float().requires_grad_()
+        vr = v[b:b + 1, g:g + 1].detach().float().requires_grad_()
+        orf, _ = _attn_ref(qr, kr, vr, scale)
+        got = o[b:b + 1, :, hs].transpose(1, 2)
+        assert rel(got, orf) < 2e-2, (b, g, rel(got, orf))
+        orf.backward(do[b:b + 1, :, hs].transpose(1, 2).float())
+        assert rel(q.grad[b:b + 1, hs], qr.grad) < 3e-2, (b, g)
+        assert rel(k.grad[b:b + 1, g:g + 1], kr.grad) < 3e-2, (b, g)
+        assert rel(v.grad[b:b + 1, g:g + 1], vr.grad) < 3e-2, (b, g)
+        del qr, kr, vr, orf
+
+
+def test_attention_gpu_has_no_library_fallback():
+    """A GPU tensor the HIP kernel cannot take raises instead of silently
+    running a library (SDPA / aotriton) kernel."""
+    _lib()
+    from tf_operator_amd.ops import llm
+
+    q = torch.randn(1, 2, 64, 96, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="head_dim"):
+        llm.causal_attention(q, q, q)
+    with pytest.raises(RuntimeError, match="bf16"):
+        llm.causal_attention(q.float()[..., :64], q.float()[..., :64], q.float()[..., :64])
 
 
 def test_flash_attention_in_llama_layer():

@@ -119,7 +119,38 @@ def _pod_log_tail(c, name: str, n: int = 40) -> str:
     return "\n".join(out)
 
 
-def _run_job(c, name: str, n: int, command: list[str], timeout: float, env=None) -> dict:
+def vram_used_bytes() -> int | None:
+    """HBM in use on every GPU of the node, from the amdgpu driver's sysfs
+    counters (no HIP call: the launcher never initialises a GPU)."""
+    tot, seen = 0, False
+    for p in glob.glob("/sys/class/drm/card*/device/mem_info_vram_used"):
+        try:
+            with open(p) as f:
+                tot += int(f.read())
+            seen = True
+        except (OSError, ValueError):
+            pass
+    return tot if seen else None
+
+
+def wait_vram_drained(baseline: int | None, timeout: float = 60.0, slack: int = 4 << 30) -> float:
+    """After a job's processes exit the driver still scrubs their HBM (about
+    33 GB/s on MI355X: ~7 s for a 243 GB Llama-3-8B replica), and a job
+    started meanwhile waits for that memory.  Each latency probe starts on a
+    drained node; the drain time is reported (``node_drain_s``)."""
+    if baseline is None:
+        return 0.0
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < timeout:
+        u = vram_used_bytes()
+        if u is None or u <= baseline + slack:
+            break
+        time.sleep(0.05)
+    return round(time.monotonic() - t0, 3)
+
+
+def _run_job(c, name: str, n: int, command: list[str], timeout: float, env=None,
+             vram_baseline: int | None = None) -> dict:
     """Submit one TFJob Worker=n, wait for it to succeed; return the client
     clock from create() to rank 0's first step plus the breakdown."""
     key = ("default", name)
@@ -155,8 +186,9 @@ def _run_job(c, name: str, n: int, command: list[str], timeout: float, env=None)
     # every replica process has exited (and released its HBM) before the next job
     c.wait(lambda: not c.pods(labels={"job-name": name}) and not any(
         k[1].startswith(name + "-") for k in c.kubelet.running), 120, 0.05, f"{name}: cleanup")
+    drain_s = wait_vram_drained(vram_baseline)
     t_first = float(rep["first_step_time"])
-    return {"submit_to_first_step_s": round(t_first - t0, 4),
+    return {"submit_to_first_step_s": round(t_first - t0, 4), "node_drain_s": drain_s,
             "submit_to_pods_created_s": round(t_pods - t0, 4),
             "submit_to_processes_spawned_s": round(t_spawn - t0, 4),
             "spawn_to_first_step_s": round(t_first - t_spawn, 4),
@@ -179,6 +211,7 @@ def _summary(samples: list[dict]) -> dict:
             "breakdown_p50_s": {"submit_to_pods_created": med("submit_to_pods_created_s"),
                                 "submit_to_processes_spawned": med("submit_to_processes_spawned_s"),
                                 "spawn_to_first_step": med("spawn_to_first_step_s"),
+                                "node_drain_after_job": med("node_drain_s"),
                                 "replica_phases": phases}}
 
 
@@ -195,10 +228,11 @@ def probe_latency(args, n: int, c=None) -> dict:
     if own:
         c = _cluster(n).start()
     samples, err = [], None
+    base = vram_used_bytes()
     try:
         for i in range(args.latency_probes):
             try:
-                s = _run_job(c, f"probe-{i}", n, _payload(args), args.probe_timeout)
+                s = _run_job(c, f"probe-{i}", n, _payload(args), args.probe_timeout, vram_baseline=base)
             except Exception as e:  # keep the throughput run alive; report why latency is missing
                 err = f"{type(e).__name__}: {str(e)[:2000]}"
                 break

@@ -79,6 +79,12 @@ def gen_env(job: dict, rtype: str, index: int, options: dict | None = None) -> l
     return json.loads(native().gen_env(_d(job), rtype, int(index), _d(options or {})))
 
 
+def set_cluster_spec(job: dict, template: dict, rtype: str, index: int, options: dict | None = None) -> dict:
+    """The pod template with the replica's environment applied (what the
+    reconciler does to every pod it creates)."""
+    return json.loads(native().set_cluster_spec(_d(job), _d(template), rtype, int(index), _d(options or {})))
+
+
 def tf_is_distributed(job: dict) -> bool:
     return bool(native().tf_is_distributed(_d(job)))
 

@@ -630,6 +630,25 @@ class LocalKubelet:
             except ApiError:
                 pass
 
+    # ---------------------------------------------------------------- device metrics
+    def gpu_owners(self) -> dict:
+        """{device index: (namespace, pod, container)} of the running pods --
+        the attribution the node agent gives the accelerator series."""
+        out = {}
+        for (ns, name), rec in self.running.items():
+            ctrs = [c.get("name", "") for c in (rec.get("pod") or {}).get("spec", {}).get("containers", [])]
+            for g in rec.get("gpus") or []:
+                out[g] = (ns, name, ctrs[0] if ctrs else "")
+        return out
+
+    def gpu_metrics_text(self, sysfs_root: str | None = None) -> str:
+        """cAdvisor-style ``container_accelerator_*`` series for this node's
+        GPUs, attributed to the pods holding them (utils/gpu_metrics.py)."""
+        from ..utils import gpu_metrics
+
+        return gpu_metrics.exposition(gpu_metrics.read_devices(sysfs_root or gpu_metrics.SYSFS_DRM),
+                                      self.gpu_owners())
+
     async def set_capacity(self, gpus: int):
         """Change the node's allocatable GPUs (fault injection: a device or
         node slice lost / returned).  Devices >= `gpus` are not handed out

@@ -6,7 +6,7 @@ Llama-3-8B bf16).  Per layer the forward is:
     (h, x) = add_rms_norm(h_prev, delta_prev)      HIP, residual add fused
     qkv    = x @ Wqkv^T                             hipBLASLt (fused Q|K|V weight)
     q,k,v  = rope_qkv(qkv)                          HIP, RoPE + head-major relayout
-    o      = causal_attention(q, k, v)              HIP flash attention / SDPA
+    o      = causal_attention(q, k, v)              HIP flash attention (packed GQA)
     a      = o^T @ Wo^T                             hipBLASLt
     (h, x) = add_rms_norm(h, a)                     HIP
     gu     = x @ Wgu^T                              hipBLASLt (fused gate|up weight)
@@ -43,8 +43,8 @@ class LlamaConfig:
     max_seq: int = 8192
     tie_embeddings: bool = False
     init_std: float = 0.02
-    # "expand" materialises K/V per query head (needed by SDPA); the HIP
-    # flash-attention kernel reads packed GQA K/V directly.
+    # "expand" materialises K/V per query head (kept for A/B runs); the HIP
+    # flash-attention kernel (and the CPU reference) read packed GQA K/V directly.
     kv_layout: str = "auto"
 
     @property
@@ -99,7 +99,7 @@ class LlamaBlock(torch.nn.Module):
             h, x = self.attn_norm(h, delta)
         qkv = linear(x, self.wqkv)
         rep = cfg.heads // cfg.kv_heads
-        if cfg.kv_layout == "packed" or (cfg.kv_layout == "auto" and _packed_kv_ok(qkv)):
+        if cfg.kv_layout in ("packed", "auto"):  # the attention kernel reads packed GQA K/V natively
             rep = 1
         q, k, v = rope_qkv(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim, rep)
         o = causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]: no transpose copy
@@ -109,12 +109,6 @@ class LlamaBlock(torch.nn.Module):
         gu = linear(x, self.wgu)
         delta = swiglu_down(gu, self.wd)
         return h, delta
-
-
-def _packed_kv_ok(t):
-    from ..ops import llm
-
-    return llm._ATTN_IMPL in ("auto", "hip") and llm._attn_hip_ok(t.new_empty(1, 1, 1, 128))
 
 
 class Llama(torch.nn.Module):

@@ -45,6 +45,7 @@ class ControllerOptions:
     inject_rocm_env: bool = True
     cluster_domain: str = ""              # CUSTOM_CLUSTER_DOMAIN
     nccl_env: dict = dataclasses.field(default_factory=dict)
+    rccl_defaults: bool = True  # xGMI defaults (envgen.cc kRcclDefaults); never override a container's env
     resync_period: float = 12 * 3600.0    # --resyc-period (12h)
     report_url: str | None = None         # injected as TOA_REPORT_URL
     gpu_resource: str = "amd.com/gpu"
@@ -169,7 +170,8 @@ class JobController:
     def _options(self, key):
         o = {"cluster_domain": self.opt.cluster_domain, "enable_gang_scheduling": self.opt.enable_gang_scheduling,
              "gang_scheduler_name": self.opt.gang_scheduler_name, "inject_rocm_env": self.opt.inject_rocm_env,
-             "gpu_resource": self.opt.gpu_resource, "previous_retry": self.queue.num_requeues(key)}
+             "gpu_resource": self.opt.gpu_resource, "previous_retry": self.queue.num_requeues(key),
+             "rccl_defaults": self.opt.rccl_defaults}
         env = dict(self.opt.nccl_env)
         if self.opt.report_url:
             env["TOA_REPORT_URL"] = self.opt.report_url

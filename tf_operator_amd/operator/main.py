@@ -90,6 +90,8 @@ def build_parser():
     p.add_argument("--burst", type=int, default=10)
     p.add_argument("--inject-rocm-env", type=lambda v: v.lower() != "false", default=True)
     p.add_argument("--nccl-env", action="append", default=[], help="K=V injected into trainer replicas")
+    p.add_argument("--rccl-defaults", type=lambda v: v.lower() != "false", default=True,
+                   help="inject xGMI-oriented RCCL/torch defaults a container does not set itself")
     p.add_argument("--cluster-domain", default=os.environ.get("CUSTOM_CLUSTER_DOMAIN", ""))
     p.add_argument("--report-url", default=os.environ.get("TOA_OPERATOR_REPORT_URL"))
     p.add_argument("--gpu-resource", default="amd.com/gpu", help="extended resource name of a GPU")
@@ -140,6 +142,7 @@ class Operator:
             namespace=args.namespace, threadiness=args.threadiness,
             enable_gang_scheduling=args.enable_gang_scheduling, gang_scheduler_name=args.gang_scheduler_name,
             inject_rocm_env=args.inject_rocm_env, cluster_domain=args.cluster_domain, nccl_env=nccl,
+            rccl_defaults=args.rccl_defaults,
             resync_period=_duration(str(args.resync_period)), report_url=args.report_url,
             gpu_resource=args.gpu_resource), self.metrics)
         self.stop = asyncio.Event()

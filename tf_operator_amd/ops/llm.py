@@ -217,11 +217,11 @@ def cross_entropy(logits, target, ignore_index=-100, inplace_grad=False):
 # ---------------------------------------------------------------------------
 # Causal attention
 # ---------------------------------------------------------------------------
-_ATTN_IMPL = os.environ.get("TOA_ATTN", "auto")  # auto | hip | sdpa
+ATTN_HEAD_DIMS = (64, 128)  # the HIP kernel's head-dim instantiations (csrc/hip/attention.hip)
 
 
 def _attn_hip_ok(q):
-    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] == 128 and _lib.has("toa_attn_fwd")
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in ATTN_HEAD_DIMS and _lib.has("toa_attn_fwd")
             and _lib.has("toa_attn_bwd"))
 
 
@@ -258,18 +258,33 @@ class _FlashAttn(torch.autograd.Function):
         return dq, dk, dv, None, None
 
 
-def causal_attention(q, k, v, scale=None, out_layout="bhsd"):
-    """q [B,H,S,D], k/v [B,Hk,S,D] (Hk == H unless the HIP kernel is used).
-    Returns O as [B,H,S,D], or as [B,S,H,D] with out_layout="bshd"."""
-    scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
-    impl = _ATTN_IMPL
-    if impl in ("auto", "hip") and _attn_hip_ok(q) and q.shape[2] % 128 == 0:
-        return _FlashAttn.apply(q.contiguous(), k.contiguous(), v.contiguous(), scale, out_layout == "bshd")
-    if impl == "hip" and q.is_cuda:
-        raise RuntimeError("TOA_ATTN=hip but the HIP attention kernel is unavailable")
-    if k.shape[1] != q.shape[1]:
-        rep = q.shape[1] // k.shape[1]
+def _attention_reference(q, k, v, scale):
+    """Plain PyTorch causal attention (fp32 math, packed GQA expanded): the
+    CPU path and the numerics reference of the HIP kernel."""
+    rep = q.shape[1] // k.shape[1]
+    if rep > 1:
         k = k.repeat_interleave(rep, 1)
         v = v.repeat_interleave(rep, 1)
-    o = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale)
+    S = q.shape[2]
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
+    s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+    return torch.matmul(torch.softmax(s, -1), v.float()).to(q.dtype)
+
+
+def causal_attention(q, k, v, scale=None, out_layout="bhsd"):
+    """q [B,H,S,D], k/v [B,Hk,S,D] (packed GQA, H % Hk == 0), any S.
+    Returns O as [B,H,S,D], or as [B,S,H,D] with out_layout="bshd".
+
+    On a GPU tensor this is ALWAYS the HIP flash-attention kernel (bf16,
+    head_dim 64 or 128); anything else raises -- there is no library
+    fallback.  CPU tensors take the plain PyTorch reference."""
+    scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
+    if q.is_cuda:
+        if not _attn_hip_ok(q):
+            raise RuntimeError(f"HIP flash attention needs bf16 and head_dim in {ATTN_HEAD_DIMS} "
+                               f"(got {q.dtype}, head_dim {q.shape[-1]}; library: {_lib.load_error() or 'ok'})")
+        if q.shape[1] % k.shape[1]:
+            raise ValueError(f"query heads {q.shape[1]} not a multiple of kv heads {k.shape[1]}")
+        return _FlashAttn.apply(q.contiguous(), k.contiguous(), v.contiguous(), scale, out_layout == "bshd")
+    o = _attention_reference(q, k, v, scale)
     return o.transpose(1, 2) if out_layout == "bshd" else o

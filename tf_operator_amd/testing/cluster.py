@@ -179,6 +179,9 @@ class LocalCluster:
     def metrics_text(self):
         return self.metrics.expose().decode()
 
+    def gpu_metrics_text(self, sysfs_root: str | None = None) -> str:
+        return self.kubelet.gpu_metrics_text(sysfs_root)
+
 
 def main(argv=None):
     """Run a single-node cluster in the foreground (the `kind` replacement of
