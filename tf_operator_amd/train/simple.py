@@ -156,6 +156,50 @@ class DPTrainer:
         return self.step_idx
 
 
+class PSTrainer:
+    """Worker side of parameter-server training (TFJob with PS replicas;
+    :mod:`tf_operator_amd.parallel.ps_collective`): forward + backward on
+    this GPU, gradients reduced onto / pushed to the servers during (sync)
+    or after (async) backward, fresh parameters received from them.  The
+    worker keeps no optimizer state -- the servers own it."""
+
+    def __init__(self, model, loss_fn, runtime, workers, servers, mode="sync", lr=1e-3, bucket_mb=64.0,
+                 grad_dtype=torch.float32):
+        from ..parallel.ps_collective import CollectivePS
+
+        self.model, self.loss_fn, self.rt = model, loss_fn, runtime
+        params = [p for p in model.parameters() if p.requires_grad]
+        names = {id(p): n for n, p in model.named_parameters()}
+        self.flat = FlatParams(list(reversed(params)), names=names, grad_dtype=grad_dtype, master=False)
+        attach_autograd_hooks(self.flat)
+        self.ps = CollectivePS(self.flat, workers, servers, mode=mode, lr=lr, bucket_mb=bucket_mb)
+        self.step_idx = 0
+
+    def step(self, x, y):
+        self.flat.zero_grad()
+        out = self.model(x)
+        loss = self.loss_fn(out, y)
+        loss.backward()
+        self.ps.worker_step()
+        self.step_idx += 1
+        if self.step_idx == 1:
+            if torch.cuda.is_available() and x.is_cuda:
+                torch.cuda.synchronize()
+            self.rt.first_step_done()
+        return loss.detach(), out.detach()
+
+
+def parameter_server(model, workers, servers, mode="sync", lr=1e-3, bucket_mb=64.0, grad_dtype=torch.float32):
+    """Server side: the same model (for the flat layout; its activations are
+    never computed), the fp32 master / Adam state of this server's shard."""
+    from ..parallel.ps_collective import CollectivePS
+
+    params = [p for p in model.parameters() if p.requires_grad]
+    names = {id(p): n for n, p in model.named_parameters()}
+    flat = FlatParams(list(reversed(params)), names=names, grad_dtype=grad_dtype)
+    return CollectivePS(flat, workers, servers, mode=mode, lr=lr, bucket_mb=bucket_mb)
+
+
 def run(trainer: DPTrainer, data, steps, log_every=50, ckpt_dir=None, ckpt_every=0, metric_fn=None,
         samples_per_step=None):
     rt = trainer.rt
