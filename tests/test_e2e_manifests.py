@@ -136,3 +136,59 @@ def test_example_runs_from_yaml(cluster, name, overrides, kind):
         assert "round 10 logloss" in logs[job["metadata"]["name"] + "-master-0"]
     if kind == "MXJob":
         assert "accuracy" in logs[job["metadata"]["name"] + "-worker-0"]
+
+
+def test_pod_template_schema_is_structural_and_admits_examples():
+    """The replica pod template is validated (not preserve-unknown at the
+    top): every example job passes; the API server refuses malformed
+    containers with the API server's field paths."""
+    from tf_operator_amd.api.validate import job_errors
+
+    tpl = schema.spec_schema("TFJob")["properties"]["tfReplicaSpecs"]["additionalProperties"]["properties"]["template"]
+    assert "x-kubernetes-preserve-unknown-fields" not in tpl
+    assert tpl["properties"]["spec"]["required"] == ["containers"]
+    n = 0
+    for path in sorted(glob.glob(os.path.join(MAN, "examples", "*.yaml"))):
+        for doc in yaml.safe_load_all(open(path)):
+            if doc and doc.get("kind") in schema.KINDS:
+                assert job_errors(doc, doc["kind"]) == [], path
+                n += 1
+    assert n >= 3
+
+
+@pytest.mark.parametrize("mutate,field", [
+    (lambda c: c.pop("name"), "spec.tfReplicaSpecs.Worker.template.spec.containers[0].name: Required value"),
+    (lambda c: c.update(command="python train.py"),
+     "spec.tfReplicaSpecs.Worker.template.spec.containers[0].command: Invalid value"),
+    (lambda c: c.update(ports=[{"name": "tfjob-port"}]),
+     "spec.tfReplicaSpecs.Worker.template.spec.containers[0].ports[0].containerPort: Required value"),
+    (lambda c: c.update(resources={"limits": {"amd.com/gpu": "one"}}),
+     "spec.tfReplicaSpecs.Worker.template.spec.containers[0].resources.limits.amd.com/gpu: Invalid value"),
+    (lambda c: c.update(env=[{"value": "1"}]),
+     "spec.tfReplicaSpecs.Worker.template.spec.containers[0].env[0].name: Required value"),
+    (lambda c: c.update(imagePullPolicy="Sometimes"),
+     "spec.tfReplicaSpecs.Worker.template.spec.containers[0].imagePullPolicy: Unsupported value"),
+])
+def test_api_server_rejects_malformed_container(mutate, field):
+    from tf_operator_amd.sdk import container, pod_template
+
+    c = container(image="toa/trainer", command=["python", "-c", "pass"], gpus=1)
+    mutate(c)
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": "bad", "namespace": "default"},
+           "spec": {"tfReplicaSpecs": {"Worker": {"replicas": 1, "template": pod_template(c)}}}}
+    with LocalCluster(gpus=0) as cl:
+        with pytest.raises(Exception) as ei:
+            cl.client.create(job)
+        assert field in str(ei.value), str(ei.value)
+        assert 'TFJob.kubeflow.org \\"bad\\" is invalid' in str(ei.value) and "(422)" in str(ei.value)
+        assert cl.api.get("kubeflow.org/tfjobs", "default", "bad") is None
+
+
+def test_api_server_rejects_empty_container_list():
+    from tf_operator_amd.api.validate import job_errors
+
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": "x"},
+           "spec": {"tfReplicaSpecs": {"Worker": {"replicas": 1, "template": {"spec": {"containers": []}}}}}}
+    errs = job_errors(job, "TFJob")
+    assert errs == ["spec.tfReplicaSpecs.Worker.template.spec.containers: Invalid value: 0: "
+                    "spec.tfReplicaSpecs.Worker.template.spec.containers in body should have at least 1 items"]

@@ -5,9 +5,16 @@ Go types (manifests/base/kubeflow.org_tfjobs.yaml) plus deepcopy/OpenAPI/
 swagger code.  Here the job-level schema is written once, in Python; the
 CRD YAML under ``manifests/base`` is generated from it and a test checks
 that the SDK dataclasses (``tf_operator_amd.sdk.models``) and the generated
-files stay in sync with it.  The embedded pod template keeps
-``x-kubernetes-preserve-unknown-fields`` (the API server validates pods
-when the operator creates them), which keeps each CRD a few hundred lines.
+files stay in sync with it.  The embedded pod template is a STRUCTURAL
+schema of the PodTemplateSpec fields a training job uses (containers,
+their command / env / ports / resources / volume mounts, volumes,
+scheduling fields), so the API server rejects a malformed replica at
+create time -- like the reference's controller-gen schema
+(manifests/base/kubeflow.org_tfjobs.yaml:108-~6800) -- while nested
+objects outside that set (affinity, probes, security contexts, volume
+sources) keep ``x-kubernetes-preserve-unknown-fields``, which keeps each
+CRD under a thousand lines.  ``api/validate.py`` applies the same schema
+in the in-process API server.
 
     python -m tf_operator_amd.api.schema --out manifests/base
 """
@@ -92,6 +99,106 @@ ELASTIC_POLICY = {
 }
 
 
+def _obj(desc=None, **props):
+    """Open object: listed properties are validated, others preserved."""
+    o = {"type": "object", "x-kubernetes-preserve-unknown-fields": True}
+    if props:
+        o["properties"] = props
+    if desc:
+        o["description"] = desc
+    return o
+
+
+_STR = {"type": "string"}
+_STRMAP = {"type": "object", "additionalProperties": {"type": "string"}}
+_STRLIST = {"type": "array", "items": {"type": "string"}}
+
+CONTAINER = {
+    "type": "object",
+    "x-kubernetes-preserve-unknown-fields": True,
+    "required": ["name"],
+    "description": "A container of the replica's pod (core/v1 Container).",
+    "properties": {
+        "name": {"type": "string", "minLength": 1, "maxLength": 63,
+                 "pattern": "^[a-z0-9]([-a-z0-9]*[a-z0-9])?$", "description": "DNS-1123 label."},
+        "image": _STR,
+        "imagePullPolicy": {"type": "string", "enum": ["Always", "IfNotPresent", "Never"]},
+        "command": _STRLIST,
+        "args": _STRLIST,
+        "workingDir": _STR,
+        "env": {"type": "array", "items": {
+            "type": "object", "required": ["name"],
+            "properties": {"name": {"type": "string", "minLength": 1}, "value": _STR,
+                           "valueFrom": _obj("ConfigMap / Secret / field / resource reference.")}}},
+        "envFrom": {"type": "array", "items": _obj()},
+        "ports": {"type": "array", "items": {
+            "type": "object", "required": ["containerPort"],
+            "properties": {"containerPort": _int("Port the container listens on.", "int32", 1) | {"maximum": 65535},
+                           "hostPort": _int("Host port.", "int32", 0) | {"maximum": 65535},
+                           "name": {"type": "string", "maxLength": 15},
+                           "protocol": {"type": "string", "enum": ["TCP", "UDP", "SCTP"]},
+                           "hostIP": _STR}}},
+        "resources": {"type": "object", "description": "amd.com/gpu goes in limits (and requests).",
+                      "properties": {"limits": {"type": "object", "additionalProperties": QUANTITY},
+                                     "requests": {"type": "object", "additionalProperties": QUANTITY}}},
+        "volumeMounts": {"type": "array", "items": {
+            "type": "object", "required": ["name", "mountPath"],
+            "properties": {"name": _STR, "mountPath": _STR, "readOnly": {"type": "boolean"}, "subPath": _STR,
+                           "mountPropagation": _STR}}},
+        "securityContext": _obj(),
+        "livenessProbe": _obj(), "readinessProbe": _obj(), "startupProbe": _obj(), "lifecycle": _obj(),
+        "stdin": {"type": "boolean"}, "tty": {"type": "boolean"},
+        "terminationMessagePath": _STR,
+        "terminationMessagePolicy": {"type": "string", "enum": ["File", "FallbackToLogsOnError"]},
+    },
+}
+
+POD_TEMPLATE = {
+    "type": "object",
+    "description": "PodTemplateSpec of the replica (core/v1).",
+    "properties": {
+        "metadata": _obj("Labels and annotations are merged with the operator's.",
+                         labels=_STRMAP, annotations=_STRMAP, name=_STR, namespace=_STR),
+        "spec": {
+            "type": "object",
+            "x-kubernetes-preserve-unknown-fields": True,
+            "required": ["containers"],
+            "description": "PodSpec (core/v1); fields not listed are passed through to the pod.",
+            "properties": {
+                "containers": {"type": "array", "minItems": 1, "items": CONTAINER},
+                "initContainers": {"type": "array", "items": CONTAINER},
+                "volumes": {"type": "array", "items": {
+                    "type": "object", "x-kubernetes-preserve-unknown-fields": True, "required": ["name"],
+                    "properties": {"name": {"type": "string", "minLength": 1}}}},
+                "restartPolicy": {"type": "string", "enum": ["Always", "OnFailure", "Never"],
+                                  "description": "Overwritten by the replica spec's restartPolicy."},
+                "nodeSelector": _STRMAP,
+                "tolerations": {"type": "array", "items": {
+                    "type": "object",
+                    "properties": {"key": _STR, "operator": {"type": "string", "enum": ["Exists", "Equal"]},
+                                   "value": _STR,
+                                   "effect": {"type": "string",
+                                              "enum": ["", "NoSchedule", "PreferNoSchedule", "NoExecute"]},
+                                   "tolerationSeconds": _int("Seconds the toleration lasts.", "int64")}}},
+                "affinity": _obj(),
+                "schedulerName": _STR,
+                "serviceAccountName": _STR,
+                "priorityClassName": _STR,
+                "hostNetwork": {"type": "boolean"},
+                "hostIPC": {"type": "boolean"},
+                "shareProcessNamespace": {"type": "boolean"},
+                "terminationGracePeriodSeconds": _int("Grace period before SIGKILL.", "int64", 0),
+                "activeDeadlineSeconds": _int("Pod deadline.", "int64", 1),
+                "dnsPolicy": {"type": "string", "enum": ["ClusterFirst", "ClusterFirstWithHostNet", "Default",
+                                                         "None"]},
+                "imagePullSecrets": {"type": "array", "items": {"type": "object", "properties": {"name": _STR}}},
+                "securityContext": _obj(),
+            },
+        },
+    },
+}
+
+
 def replica_spec(default_restart):
     return {
         "type": "object",
@@ -101,9 +208,7 @@ def replica_spec(default_restart):
             "restartPolicy": {"type": "string", "enum": ["Always", "OnFailure", "Never", "ExitCode"],
                               "description": f"Restart policy (default {default_restart}). ExitCode restarts "
                                              "on retryable exit codes (>= 128)."},
-            "template": {"type": "object", "x-kubernetes-preserve-unknown-fields": True,
-                         "description": "PodTemplateSpec of the replica (validated by the API server when the "
-                                        "operator creates the pods)."},
+            "template": copy.deepcopy(POD_TEMPLATE),
         },
     }
 

@@ -229,6 +229,13 @@ class FakeAPIServer:
             if not isinstance(spec, dict) or not spec.get(field):
                 return f'{kind}.kubeflow.org "{obj.get("metadata", {}).get("name", "")}" is invalid: spec.{field}: ' \
                        f"Required value"
+            from ..api.validate import job_errors
+
+            errs = job_errors(obj, kind)
+            if errs:  # the API server's structural-schema admission of the CRD
+                name = obj.get("metadata", {}).get("name", "")
+                return f'{kind}.kubeflow.org "{name}" is invalid: ' + (errs[0] if len(errs) == 1 else
+                                                                        "[" + ", ".join(errs) + "]")
         if not obj.get("metadata", {}).get("name"):
             gen = obj.get("metadata", {}).get("generateName")
             if gen:
