@@ -109,6 +109,26 @@ __device__ __forceinline__ float xhalf_sum(float v) {
   return a + b;
 }
 
+// Softmax VALU trimmed to what the MFMA gaps can hide (guide §5.5 T12 and
+// MI355X_MICROARCH 'vector-instruction ISSUE cost': at two waves per SIMD the
+// issue port, not the MFMA pipe, bounded these kernels):
+//  * row max as two independent v_max3_f32 chains;
+//  * scale-and-subtract and the row sum on PAIRS of scores with
+//    v_pk_fma_f32 / v_pk_add_f32 (consecutive accumulator registers).
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+// max over the 32 scores of sc[0], sc[1] (one lane's row half): two
+// independent chains the compiler turns into v_max3_f32
+__device__ __forceinline__ float rowmax32(const f32x16& a, const f32x16& b) {
+  float m0 = fmaxf(a[0], a[1]), m1 = fmaxf(b[0], b[1]);
+#pragma unroll
+  for (int j = 2; j < 16; ++j) {
+    m0 = fmaxf(m0, a[j]);
+    m1 = fmaxf(m1, b[j]);
+  }
+  return fmaxf(m0, m1);
+}
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // Offset of row (b, h, s) of O / dO: [B, H, S, D] (head-major, like Q) or, with
 // bshd, [B, S, H, D] -- the layout the output projection consumes, so the
 // model needs no transpose copy of O forward or of dO backward.
@@ -237,11 +257,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
           if (key > myq) sc[n][j] = -INFINITY;
         }
     }
-    float mx = sc[0][0];
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) mx = fmaxf(mx, sc[n][j]);
+    float mx = rowmax32(sc[0], sc[1]);
     mx = xhalf_max(mx) * scale_log2;
     // T13: rescale O / l only when some row's max grew by more than THR
     if (__any(mx > m_run + RESCALE_THR)) {
@@ -255,18 +271,20 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
         for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
     }
     // ---- P = exp2(s*c - m) packed straight into the PV B operand
-    float ls = 0.f;
+    f32x2 ls;
+    const f32x2 c2 = {scale_log2, scale_log2}, nm2 = {-m_run, -m_run};
     uint32_t pw[2][8];
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int j = 0; j < 16; j += 2) {
-        const float p0 = EXP2(fmaf(sc[n][j], scale_log2, -m_run));
-        const float p1 = EXP2(fmaf(sc[n][j + 1], scale_log2, -m_run));
-        ls += p0 + p1;
-        pw[n][j >> 1] = cvt_pk(p0, p1);
+        f32x2 x = pk_fma(f32x2{sc[n][j], sc[n][j + 1]}, c2, nm2);
+        x[0] = EXP2(x[0]);
+        x[1] = EXP2(x[1]);
+        ls = (n == 0 && j == 0) ? x : ls + x;
+        pw[n][j >> 1] = cvt_pk(x[0], x[1]);
       }
-    l_run += ls;
+    l_run += ls[0] + ls[1];
     // ---- O^T += V^T P^T (k permutation of the accumulator handled by the V^T read order)
 #pragma unroll
     for (int n = 0; n < 2; ++n)
@@ -452,7 +470,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
       *(u32x4*)(ob + rt_off<D>(row, c)) = sdo[i];
     }
     if (tid < 64) {
-      lb[tid] = slse * LOG2E;
+      lb[tid] = -(slse * LOG2E);  // the exp2 argument's addend (pk_fma); padded rows: -inf -> p = 0
       lb[64 + tid] = -sdel;
     }
   };
@@ -479,12 +497,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
       const bf16x8 vf = as_bf16x8(*(const u32x4*)(vimg + rro[s] + 32 * ROWB * kg));
       dp = mfma32(oa, vf, dp);
     }
+    // (scalar VALU here: the packed forms need aligned register pairs, and at
+    // 256 VGPRs with resident dK^T / dV^T accumulators that spills in the loop)
     uint32_t pw[8], sw[8];
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
-      const f32x4 l4 = *(const f32x4*)(lb + 32 * m + 8 * (j >> 2) + 4 * hh);
-      float p0 = EXP2(fmaf(sc[j], scale_log2, -l4[j & 3]));
-      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, -l4[(j + 1) & 3]));
+      const f32x4 l4 = *(const f32x4*)(lb + 32 * m + 8 * (j >> 2) + 4 * hh);  // -lse * log2(e)
+      float p0 = EXP2(fmaf(sc[j], scale_log2, l4[j & 3]));
+      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, l4[(j + 1) & 3]));
       if (mask) {
         const int q = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
         if (q < mykey) p0 = 0.f;
@@ -690,16 +710,19 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
         dp = mfma32(as_bf16x8(*(const u32x4*)(vb + rro[s] + 32 * ROWB * n)), of[s], dp);
       }
       uint32_t sw[8];
+      const f32x2 c2 = {scale_log2, scale_log2}, nl2 = {-lse2, -lse2}, del2 = {del, del};
 #pragma unroll
       for (int j = 0; j < 16; j += 2) {
-        float p0 = EXP2(fmaf(sc[j], scale_log2, -lse2));
-        float p1 = EXP2(fmaf(sc[j + 1], scale_log2, -lse2));
+        const f32x2 x = pk_fma(f32x2{sc[j], sc[j + 1]}, c2, nl2);
+        float p0 = EXP2(x[0]);
+        float p1 = EXP2(x[1]);
         if (mask) {
           const int key = t * TK + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
           if (key > myq) p0 = 0.f;
           if (key + 1 > myq) p1 = 0.f;
         }
-        sw[j >> 1] = pack2(p0 * (dp[j] - del), p1 * (dp[j + 1] - del));
+        const f32x2 d = (f32x2{dp[j], dp[j + 1]} - del2) * f32x2{p0, p1};
+        sw[j >> 1] = pack2(d[0], d[1]);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {

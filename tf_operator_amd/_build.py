@@ -31,6 +31,12 @@ HIP_LIB = os.path.join(PKG, "lib", "libtoa_hip.so")
 ARCH = os.environ.get("TOA_OFFLOAD_ARCH", "gfx950")
 
 
+# extra hipcc flags per source file (none at present; an A/B of attention.hip
+# with -fno-honor-nans -mno-amdgpu-ieee measured 9 % slower forward and a
+# spilling dK/dV kernel, profiles/r2_attention/ab_valu.log)
+PER_FILE_FLAGS: dict[str, list[str]] = {}
+
+
 def _hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.sep not in c or os.path.exists(c)):
@@ -70,8 +76,8 @@ def build_hip(force=False, verbose=False):
     for s in srcs:
         o = os.path.join(BUILD, "hip", os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _stale(o, [s] + hdrs):
-            todo.append([_hipcc()] + flags + ["-c", s, "-o", o])
+        if force or _stale(o, [s] + hdrs + [os.path.abspath(__file__)]):
+            todo.append([_hipcc()] + flags + PER_FILE_FLAGS.get(os.path.basename(s), []) + ["-c", s, "-o", o])
     with cf.ThreadPoolExecutor(_jobs()) as ex:
         for out in ex.map(_run, todo):
             if verbose and out.strip():
