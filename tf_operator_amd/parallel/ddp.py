@@ -68,15 +68,51 @@ class GradBucketer:
         self.shard = bool(shard) and self.enabled and zero.feasible(self.buckets, self.world)
         self.owned = (zero.owned_ranges(self.buckets, self.world, self.rank) if self.shard
                       else [(0, flat.numel)])
-        # one-shot IPC all-reduce (parallel/ipc.py) for small models on one node:
-        # TOA_IPC_ALLREDUCE=1, every rank local, the whole gradient fits a slot
-        self.ipc = None
-        nbytes = flat.grad.numel() * esz
-        if (self.enabled and not self.shard and os.environ.get("TOA_IPC_ALLREDUCE", "0") == "1" and flat.grad.is_cuda
-                and int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) == self.world and nbytes <= 64 << 20):
-            from .ipc import IpcAllReduce
+        # one-shot IPC all-reduce (parallel/ipc.py) for the latency-bound
+        # buckets: selected per bucket by size (<= IPC_MAX_BUCKET) when every
+        # rank is on this node; larger buckets stay on RCCL's ring
+        self.ipc = self._maybe_ipc(group, flat, esz)
 
-            self.ipc = IpcAllReduce(group, slot_bytes=max(1 << 20, nbytes))
+    IPC_MAX_BUCKET = 8 << 20  # bytes: above this RCCL's ring is at bandwidth and wins
+
+    def _maybe_ipc(self, group, flat, esz):
+        """TOA_IPC_ALLREDUCE: "auto" (default) = on when the job is one node
+        (LOCAL_WORLD_SIZE == world, <= 8 ranks, RCCL) and at least one bucket
+        is small enough; "1" forces it, "0" disables it.  The decision is the
+        same on every rank (it depends on env and layout only), and a
+        one-time self-check against RCCL turns it off everywhere if the IPC
+        path is unavailable or wrong on this node."""
+        mode = os.environ.get("TOA_IPC_ALLREDUCE", "auto")
+        if mode == "0" or not (self.enabled and not self.shard and flat.grad.is_cuda):
+            return None
+        if not dist.is_initialized():
+            return None
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) == self.world
+        small = [(e - s) * esz for s, e, _ in self.buckets if (e - s) * esz <= self.IPC_MAX_BUCKET]
+        if mode != "1" and not (_is_nccl(group) and local and 1 < self.world <= 8 and small):
+            return None
+        from .ipc import IpcAllReduce
+
+        ok, ipc = 1, None
+        try:
+            ipc = IpcAllReduce(group, slot_bytes=max(1 << 20, max(small or [1 << 20])))
+            probe = torch.full((4099,), float(self.rank + 1), device=flat.grad.device, dtype=torch.float32)
+            ipc(probe)
+            torch.cuda.synchronize()
+            ipc.check()
+            ok = int(bool(torch.all(probe == self.world * (self.world + 1) / 2)))
+        except Exception:  # noqa: BLE001 - any failure: stay on RCCL
+            ok = 0
+        flag = torch.tensor([ok], device=flat.grad.device, dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if int(flag.item()) == 1:
+            return ipc
+        if ipc is not None:
+            try:
+                ipc.close()
+            except Exception:  # noqa: BLE001
+                pass
+        return None
 
     def _ready(self, param):
         if not self.armed:  # an accumulation micro-step: gradients keep summing locally
@@ -125,6 +161,10 @@ class GradBucketer:
     def grad_scale(self):
         """Factor the optimizer applies to the summed gradients."""
         return 1.0 / self.world if (self.enabled and self.average) else 1.0
+
+
+def _is_nccl(group) -> bool:
+    return dist.get_backend(group) == "nccl"
 
 
 def broadcast_params(flat: FlatParams, src=0, group=None):
