@@ -321,6 +321,12 @@ def summarize_rccl_log(path: str | None) -> dict | None:
 def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_by: str = "replica") -> int:
     phases = {"process_start": t_proc_start}
     rccl_log = _rccl_log_setup(args, launched_by)
+    # the RCCL defaults the operator injects into every trainer pod
+    # (csrc/core/envgen.cc kRcclDefaults), also under torchrun: collective
+    # streams at high priority so the bucketed reduce-scatter / all-gather are
+    # not queued behind the GEMMs they overlap
+    for k, v in (("TORCH_NCCL_HIGH_PRIORITY", "1"), ("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")):
+        os.environ.setdefault(k, v)
     import torch
 
     from ..train import dist as tdist
