@@ -666,3 +666,67 @@ def test_bias_act_bwd_column_sums(M, N):
     g = dy.float() * (y.float() > 0)
     assert torch.equal(dz, g.to(torch.bfloat16))
     assert float((db - g.sum(0)).abs().max()) <= 1e-4 * max(1.0, float(g.abs().sum(0).max()))
+
+
+@pytest.mark.parametrize("N,C,H,W,relu,res", [(4, 64, 28, 28, True, False), (2, 256, 14, 14, True, True),
+                                              (3, 2048, 7, 7, False, True), (1, 24, 5, 9, True, False),
+                                              (64, 128, 3, 3, False, False)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_fused_batchnorm_act(N, C, H, W, relu, res, dt):
+    """HIP BatchNorm(+residual)(+ReLU), channels-last (csrc/hip/bn.hip), vs
+    the fp32 PyTorch reference: output, running statistics, dx, dres,
+    dgamma, dbeta; then eval mode with the updated running statistics."""
+    _lib()
+    from tf_operator_amd.ops.bn import batch_norm_act
+
+    torch.manual_seed(3)
+    x = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.7).to(dt).to(memory_format=torch.channels_last)
+    r = torch.randn(N, C, H, W, device=DEV).to(dt).to(memory_format=torch.channels_last) if res else None
+    g = (torch.rand(C, device=DEV) + 0.5).to(dt)
+    b = (torch.randn(C, device=DEV) * 0.1).to(dt)
+    rm, rv = torch.zeros(C, device=DEV, dtype=dt), torch.ones(C, device=DEV, dtype=dt)
+    xa, ga, ba = x.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+    ra = r.clone().requires_grad_() if res else None
+    y = batch_norm_act(xa, ga, ba, rm, rv, training=True, momentum=0.1, eps=1e-5, relu=relu, residual=ra)
+    xf, gf, bf = x.float().requires_grad_(), g.float().requires_grad_(), b.float().requires_grad_()
+    rf = r.float().requires_grad_() if res else None
+    rmf, rvf = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yf = torch.nn.functional.batch_norm(xf, rmf, rvf, gf, bf, True, 0.1, 1e-5)
+    if res:
+        yf = yf + rf
+    if relu:
+        yf = torch.relu(yf)
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert rel(y, yf) < tol, rel(y, yf)
+    assert rel(rm, rmf) < tol and rel(rv, rvf) < tol
+    dy = torch.randn_like(yf)
+    y.backward(dy.to(dt))
+    yf.backward(dy)
+    assert rel(xa.grad, xf.grad) < 3 * tol, rel(xa.grad, xf.grad)
+    assert rel(ga.grad, gf.grad) < 3 * tol, rel(ga.grad, gf.grad)
+    assert rel(ba.grad, bf.grad) < 3 * tol, rel(ba.grad, bf.grad)
+    if res:
+        assert rel(ra.grad, rf.grad) < 3 * tol
+    with torch.no_grad():
+        ye = batch_norm_act(x, g, b, rm, rv, training=False, eps=1e-5, relu=relu, residual=r)
+        yef = torch.nn.functional.batch_norm(x.float(), rm.float(), rv.float(), g.float(), b.float(), False, 0.1, 1e-5)
+        if res:
+            yef = yef + r.float()
+        if relu:
+            yef = torch.relu(yef)
+    assert rel(ye, yef) < tol
+
+
+def test_fused_batchnorm_large_mean_variance():
+    """Shifted-data variance: a channel with mean 1000 and std 0.5 keeps its
+    variance (no E[x^2] - E[x]^2 cancellation)."""
+    _lib()
+    from tf_operator_amd.ops.bn import batch_norm_act
+
+    torch.manual_seed(4)
+    x = (torch.randn(8, 64, 32, 32, device=DEV) * 0.5 + 1000.0).to(memory_format=torch.channels_last)
+    rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    batch_norm_act(x, None, None, rm, rv, training=True, momentum=1.0, relu=False)
+    ref = x.float().permute(1, 0, 2, 3).reshape(64, -1).var(1)
+    assert float(((rv - ref) / ref).abs().max()) < 1e-3

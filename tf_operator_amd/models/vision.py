@@ -9,13 +9,15 @@
 * :class:`EstimatorDNN` -- keras_model_to_estimator.py:47-52 (10 -> 16 ReLU
   -> 1 sigmoid, 193 params).
 * :func:`resnet50` -- BASELINE.json config #2 (ResNet-50, 25.6M params),
-  channels-last bf16 convs through MIOpen, fused dense head.
+  channels-last bf16 convs through MIOpen, BatchNorm + ReLU (+ residual)
+  as one fused HIP pass (ops/bn.py), fused dense head.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
+from ..ops.bn import FusedBatchNorm2d
 from ..ops.mlp import DenseAct
 
 
@@ -62,24 +64,26 @@ class EstimatorDNN(torch.nn.Module):
 # ResNet-50 (He et al. 2015), bottleneck v1.5 (stride on the 3x3)
 # ---------------------------------------------------------------------------
 class Bottleneck(torch.nn.Module):
+    """BatchNorm + ReLU (and, after conv3, the residual add) are one fused
+    HIP pass each (ops/bn.py, csrc/hip/bn.hip); convolutions are MIOpen."""
+
     expansion = 4
 
     def __init__(self, cin, width, stride=1, downsample=None, **kw):
         super().__init__()
         self.conv1 = torch.nn.Conv2d(cin, width, 1, bias=False, **kw)
-        self.bn1 = torch.nn.BatchNorm2d(width, **kw)
+        self.bn1 = FusedBatchNorm2d(width, relu=True, **kw)
         self.conv2 = torch.nn.Conv2d(width, width, 3, stride, 1, bias=False, **kw)
-        self.bn2 = torch.nn.BatchNorm2d(width, **kw)
+        self.bn2 = FusedBatchNorm2d(width, relu=True, **kw)
         self.conv3 = torch.nn.Conv2d(width, width * 4, 1, bias=False, **kw)
-        self.bn3 = torch.nn.BatchNorm2d(width * 4, **kw)
+        self.bn3 = FusedBatchNorm2d(width * 4, relu=True, **kw)  # relu(bn3(conv3(y)) + identity)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        y = F.relu(self.bn1(self.conv1(x)))
-        y = F.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return F.relu(y + idt)
+        y = self.bn1(self.conv1(x))
+        y = self.bn2(self.conv2(y))
+        return self.bn3(self.conv3(y), residual=idt)
 
 
 class ResNet(torch.nn.Module):
@@ -87,8 +91,7 @@ class ResNet(torch.nn.Module):
         super().__init__()
         kw = dict(dtype=dtype, device=device)
         self.stem = torch.nn.Sequential(torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False, **kw),
-                                        torch.nn.BatchNorm2d(64, **kw), torch.nn.ReLU(inplace=True),
-                                        torch.nn.MaxPool2d(3, 2, 1))
+                                        FusedBatchNorm2d(64, relu=True, **kw), torch.nn.MaxPool2d(3, 2, 1))
         cin = 64
         stages = []
         for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
@@ -98,7 +101,7 @@ class ResNet(torch.nn.Module):
                 ds = None
                 if j == 0:
                     ds = torch.nn.Sequential(torch.nn.Conv2d(cin, width * 4, 1, stride, bias=False, **kw),
-                                             torch.nn.BatchNorm2d(width * 4, **kw))
+                                             FusedBatchNorm2d(width * 4, relu=False, **kw))
                 blocks.append(Bottleneck(cin, width, stride, ds, **kw))
                 cin = width * 4
             stages.append(torch.nn.Sequential(*blocks))

@@ -396,6 +396,9 @@ class JobController:
         for k, v in payload.items():
             if k not in rec or k != "first_step_time":
                 rec[k] = v
+        if payload.get("first_step_time"):  # every (re)start of rank 0: restart-recovery measurements
+            rec["last_first_step_time"] = payload["first_step_time"]
+            rec["first_steps"] = int(rec.get("first_steps", 0)) + 1
         gen = int(payload.get("elastic_generation") or 0)
         seen_key = (ns, name, gen)
         if payload.get("first_step_time") and seen_key not in self._first_step_seen and job is not None:

@@ -69,6 +69,10 @@ _SIGS = {
     "toa_gemm": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p],
     "toa_gemm_set_algo": [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int],
     "toa_gemm_current_algo": [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int],
+    "toa_bn_fwd_train": [c_int, c_int, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_f, c_f, c_int, c_p, c_p,
+                         c_p],
+    "toa_bn_fwd_eval": [c_int, c_int, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_f, c_int, c_p, c_p],
+    "toa_bn_bwd": [c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_p],
     "toa_gemm_tune": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p, c_p, c_p,
                       c_p, c_p],
 }
@@ -93,6 +97,9 @@ def _load():
                 continue
             fn.argtypes = argt
             fn.restype = c_int
+        ws = getattr(lib, "toa_bn_ws_floats", None)
+        if ws is not None:
+            ws.argtypes, ws.restype = [c_i64, c_int], c_i64
         _lib = lib
 
 
