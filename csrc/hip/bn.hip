@@ -140,7 +140,8 @@ __device__ __forceinline__ bool bn_sum_partials(const float* __restrict__ ws, in
   return true;
 }
 
-// stats[0..C) = mean, stats[C..2C) = invstd (saved for backward);
+// stats[0..C) = mean, stats[C..2C) = invstd, stats[2C..4C) = scale, shift
+// (saved for backward);
 // sc[0..C) = scale, sc[C..2C) = shift; running stats updated with momentum
 // (unbiased variance), as torch.nn.BatchNorm2d does.
 template <typename T, typename P>
@@ -165,6 +166,8 @@ __global__ __launch_bounds__(BN_THREADS) void bn_finalize_kernel(const T* __rest
   const float gm = gamma ? ldp(gamma, c) : 1.f, bt = beta ? ldp(beta, c) : 0.f;
   sc[c] = gm * invstd;
   sc[C + c] = bt - mean * gm * invstd;
+  stats[2 * C + c] = sc[c];  // kept for the backward's ReLU mask (mask mode 2)
+  stats[3 * C + c] = sc[C + c];
   if (rmean) {
     const float unb = R > 1 ? var * (float)R / (float)(R - 1) : var;
     stp(rmean, c, (1.f - momentum) * ldp(rmean, c) + momentum * mean);
@@ -213,32 +216,46 @@ __global__ __launch_bounds__(BN_THREADS) void bn_apply_kernel(const T* __restric
 // ---------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------
+// ReLU mask of the backward: mode 0 none, 1 from the saved output y (a
+// residual was added before the ReLU), 2 recomputed from x with the forward's
+// own fmaf(x, scale, shift) -- bit-identical sign, and one tensor less to read.
+template <typename T>
+__device__ __forceinline__ void bn_mask(int mode, const T* __restrict__ y, int64_t off, const float* v,
+                                        const float* sc, const float* sh, float* d) {
+  if (mode == 1) {
+    float o[8];
+    ld8(y + off, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+  } else if (mode == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = fmaf(v[j], sc[j], sh[j]) > 0.f ? d[j] : 0.f;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_partial_kernel(const T* __restrict__ dy,
                                                                     const T* __restrict__ x,
-                                                                    const T* __restrict__ y,
+                                                                    const T* __restrict__ y, int mask,
                                                                     const float* __restrict__ stats, int64_t R, int C,
                                                                     float* __restrict__ ws) {
   __shared__ float lds[2 * BN_THREADS * 8];
   const BnGeo g(C);
   const int t = threadIdx.x, ro = t / g.cg, cgi = t - ro * g.cg;
-  float sd[8] = {}, sx[8] = {}, mu[8], is[8];
+  float sd[8] = {}, sx[8] = {}, mu[8], is[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mu[j] = stats[cgi * 8 + j];
     is[j] = stats[C + cgi * 8 + j];
+    sc[j] = stats[2 * C + cgi * 8 + j];
+    sh[j] = stats[3 * C + cgi * 8 + j];
   }
   if (ro < g.rpi) {
     for (int64_t r = (int64_t)blockIdx.x * g.rpi + ro; r < R; r += (int64_t)gridDim.x * g.rpi) {
       float d[8], v[8];
       ld8(dy + r * C + cgi * 8, d);
       ld8(x + r * C + cgi * 8, v);
-      if (y) {
-        float o[8];
-        ld8(y + r * C + cgi * 8, o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
-      }
+      bn_mask(mask, y, r * C + cgi * 8, v, sc, sh, d);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         sd[j] += d[j];
@@ -278,7 +295,8 @@ __device__ __forceinline__ void ld8f(const float* p, float* f) { ld8<float>(p, f
 
 template <typename T>
 __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                                  const T* __restrict__ y,
+                                                                  const T* __restrict__ y, int mask,
+                                                                  const float* __restrict__ stats,
                                                                   const float* __restrict__ k, int64_t n8, int C,
                                                                   T* __restrict__ dx, T* __restrict__ dres) {
   for (int64_t i = (int64_t)blockIdx.x * BN_THREADS + threadIdx.x; i < n8; i += (int64_t)gridDim.x * BN_THREADS) {
@@ -286,11 +304,13 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_apply_kernel(const T* __res
     float d[8], v[8], k1[8], k2[8], k3[8];
     ld8(dy + i * 8, d);
     ld8(x + i * 8, v);
-    if (y) {
-      float o[8];
-      ld8(y + i * 8, o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+    if (mask == 2) {
+      float sc[8], sh[8];
+      ld8f(stats + 2 * C + c0, sc);
+      ld8f(stats + 3 * C + c0, sh);
+      bn_mask(2, y, i * 8, v, sc, sh, d);
+    } else {
+      bn_mask(mask, y, i * 8, v, nullptr, nullptr, d);
     }
     if (dres) st8(dres + i * 8, d);
     ld8f(k + c0, k1);
@@ -365,20 +385,23 @@ extern "C" int toa_bn_fwd_eval(int dtype, int pdtype, const void* x, const void*
 
 // backward: y = the forward output when relu was fused (its sign is the
 // mask), else null; dres (may be null) receives dy' for a fused residual
-extern "C" int toa_bn_bwd(int dtype, int pdtype, const void* dy, const void* x, const void* y, const float* stats,
+// mask: 0 no ReLU, 1 ReLU mask from y (the saved output), 2 from x and the
+// saved scale / shift (y unused)
+extern "C" int toa_bn_bwd(int dtype, int pdtype, const void* dy, const void* x, const void* y, int mask,
+                          const float* stats,
                           const void* gamma, int64_t R, int C, void* dx, void* dres, void* dgamma, void* dbeta,
                           float* ws, hipStream_t st) {
-  if (!bn_shape_ok(R, C)) return (int)hipErrorInvalidValue;
+  if (!bn_shape_ok(R, C) || mask < 0 || mask > 2 || (mask == 1 && !y)) return (int)hipErrorInvalidValue;
   const int nb = bn_blocks(R, C);
   float* g = ws + (int64_t)nb * 2 * C;
   float* k = g + 2 * C;
   BN_DISPATCH(dtype, pdtype, {
     hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, dim3(nb), dim3(BN_THREADS), 0, st, (const T*)dy, (const T*)x,
-                       (const T*)y, stats, R, C, ws);
+                       (const T*)y, mask, stats, R, C, ws);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<P>, dim3(C / 8), dim3(BN_THREADS), 0, st,
                        ws, nb, R, C, stats, (const P*)gamma, g, k, (P*)dgamma, (P*)dbeta);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_grid(R * C / 8)), dim3(BN_THREADS), 0, st, (const T*)dy,
-                       (const T*)x, (const T*)y, k, R * C / 8, C, (T*)dx, (T*)dres);
+                       (const T*)x, (const T*)y, mask, stats, k, R * C / 8, C, (T*)dx, (T*)dres);
   });
   return (int)hipGetLastError();
 }

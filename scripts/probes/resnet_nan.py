@@ -23,7 +23,7 @@ class RT:
         print(*a, flush=True)
 
 
-def run(graph, steps=12, batch=int(os.environ.get("B", "64"))):
+def run(graph, steps=int(os.environ.get("STEPS", "12")), batch=int(os.environ.get("B", "64"))):
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     m = resnet50(dtype=torch.bfloat16, device=dev).to(memory_format=torch.channels_last)

@@ -48,3 +48,27 @@ def test_transposed_weights_follow_steps_and_checkpoints():
     load_trainer_state(tr, st)
     assert _fresh(tr)
     assert torch.equal(tr.flat.param, base.flat.param)
+
+
+def test_fused_batchnorm_module_matches_batchnorm2d_on_cpu():
+    """FusedBatchNorm2d keeps BatchNorm2d's parameters, buffers and
+    semantics (CPU path = PyTorch reference; the GPU path is compared with
+    it in tests/test_ops_gpu.py)."""
+    from tf_operator_amd.ops.bn import FusedBatchNorm2d
+
+    torch.manual_seed(0)
+    ref = torch.nn.BatchNorm2d(16)
+    fused = FusedBatchNorm2d(16, relu=True)
+    fused.load_state_dict(ref.state_dict())
+    x = torch.randn(4, 16, 5, 5).to(memory_format=torch.channels_last)
+    r = torch.randn(4, 16, 5, 5).to(memory_format=torch.channels_last)
+    for _ in range(3):
+        y_ref = torch.relu(ref(x) + r)
+        y = fused(x, residual=r)
+        assert torch.allclose(y, y_ref, atol=1e-5)
+    assert torch.allclose(fused.running_mean, ref.running_mean) and torch.allclose(fused.running_var, ref.running_var)
+    assert int(fused.num_batches_tracked) == int(ref.num_batches_tracked) == 3
+    assert set(fused.state_dict()) == set(ref.state_dict())
+    ref.eval()
+    fused.eval()
+    assert torch.allclose(fused(x), ref(x).relu(), atol=1e-5)

@@ -7,8 +7,9 @@
 Training mode normalises with the batch statistics and updates the running
 ones (momentum, unbiased variance: torch.nn.BatchNorm2d semantics); eval
 mode uses the running statistics.  The backward re-derives the ReLU mask
-from the saved output (the next layer keeps it alive anyway), so nothing
-extra is stored.  dgamma / dbeta go straight into the flat gradient buffer
+from x and the saved per-channel scale / shift (bit-identical to the
+forward's sign), or from the saved output when a residual was added before
+the ReLU, so nothing extra is stored.  dgamma / dbeta go straight into the flat gradient buffer
 (``param.main_grad``) when the parameters are managed by FlatParams.
 
 On a GPU tensor this is the HIP path only (channels-last bf16/fp32, C % 8 ==
@@ -75,7 +76,7 @@ class _BatchNormAct(torch.autograd.Function):
         pdt = _lib.dtype_code(pd) if pd is not None else 1
         st = _lib.stream(x)
         if training:
-            stats = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+            stats = torch.empty(4 * C, device=x.device, dtype=torch.float32)  # mean, invstd, scale, shift
             _lib.call("toa_bn_fwd_train", _lib.dtype_code(x2), pdt, _lib.ptr(x2), _lib.ptr(r2), _lib.ptr(y2),
                       R, C, _lib.ptr(weight), _lib.ptr(bias), _lib.ptr(running_mean),
                       _lib.ptr(running_var), float(momentum), float(eps), int(relu), _lib.ptr(stats), _lib.ptr(ws), st)
@@ -86,7 +87,10 @@ class _BatchNormAct(torch.autograd.Function):
                       _lib.ptr(running_var), float(eps), int(relu), _lib.ptr(ws), st)
         y = _like(y2, x)
         ctx.training, ctx.relu, ctx.has_res = training, relu, res is not None
-        ctx.save_for_backward(x, y if relu else None, stats, weight, bias)
+        # ReLU mask in backward: from x and the saved scale / shift unless a
+        # residual was added before the ReLU (then from the saved output)
+        ctx.mask = 0 if not relu else (1 if res is not None else 2)
+        ctx.save_for_backward(x, y if ctx.mask == 1 else None, stats, weight, bias)
         return y
 
     @staticmethod
@@ -104,7 +108,8 @@ class _BatchNormAct(torch.autograd.Function):
         dg = torch.empty(C, device=x.device, dtype=weight.dtype) if weight is not None else None
         db = torch.empty(C, device=x.device, dtype=bias.dtype) if bias is not None else None
         ws = _ws(R, C, x.device)
-        _lib.call("toa_bn_bwd", _lib.dtype_code(x2), pdt, _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(y2), _lib.ptr(stats),
+        _lib.call("toa_bn_bwd", _lib.dtype_code(x2), pdt, _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(y2), ctx.mask,
+                  _lib.ptr(stats),
                   _lib.ptr(weight), R, C, _lib.ptr(dx2), _lib.ptr(dres2), _lib.ptr(dg), _lib.ptr(db),
                   _lib.ptr(ws), _lib.stream(x))
         gw = deliver_weight_grad(weight, dg) if weight is not None else None

@@ -25,7 +25,7 @@ def attach_autograd_hooks(flat: FlatParams):
         def hook(param):
             if param.grad is None:
                 return
-            param.main_grad.add_(param.grad.view_as(param.main_grad).to(param.main_grad.dtype))
+            param.main_grad.add_(param.grad.view_as(param.main_grad))  # mixed-dtype add: one kernel, no cast copy
             param.grad = None
             h = getattr(param, "_toa_ready", None)
             if h is not None:
