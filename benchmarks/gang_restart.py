@@ -97,6 +97,7 @@ def main(argv=None):
            "config": {"model": a.model, "workers": a.workers, "seq_len": a.seq_len, "micro_batch": a.micro_batch,
                       "device": "gpu" if a.gpu else "cpu/gloo", "restartPolicy": "OnFailure", "gang": True}}
     print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":

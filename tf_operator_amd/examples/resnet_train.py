@@ -18,7 +18,7 @@ import time
 
 import torch
 
-from tf_operator_amd.examples.common import model_dtype, pick_device
+from tf_operator_amd.examples.common import model_dtype, pick_device, use_shipped_miopen_find_db
 from tf_operator_amd.models.vision import ResNet, resnet50
 from tf_operator_amd.ops.llm import cross_entropy
 from tf_operator_amd.parallel import ps_collective
@@ -49,6 +49,7 @@ def main(argv=None):
     p.add_argument("--ps-mode", default="auto", choices=("auto", "sync", "async", "none"),
                    help="auto = sync when the job has PS replicas")
     a = p.parse_args(argv)
+    use_shipped_miopen_find_db()
     rt = Runtime()
     workers, servers, role, idx = ps_collective.ps_world_env()
     mode = a.ps_mode if a.ps_mode != "auto" else ("sync" if servers else "none")
@@ -84,8 +85,10 @@ def main(argv=None):
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss = None
-    for _ in range(a.steps):
+    for i in range(a.steps):
         loss, _ = tr.step(*data.next())
+        if (i + 1) % 10 == 0 or i + 1 == a.steps:
+            rt.log(f"step {a.warmup + i + 1} loss {float(loss):.4f}")
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
