@@ -17,6 +17,7 @@
 #   pmc:<script>:<counters>  rocprofv3 --pmc <counters> --kernel-trace of python3 <script>
 #   py:<module>:<args>       python -m <module> <args, comma separated>
 #   examples         the bundled payloads (smoke, mnist, summaries, resnet)
+#   resnet           the ResNet-50 payload twice (fresh box: MIOpen find-db path), batch 256
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 NAME=${1:?out name}; shift
@@ -59,6 +60,9 @@ for st in "$@"; do
       run ex_mnist 300 python -m tf_operator_amd.examples.dist_mnist --train_steps 500 &&
       run ex_summaries 300 python -m tf_operator_amd.examples.mnist_with_summaries &&
       run ex_resnet 300 python -m tf_operator_amd.examples.resnet_train --steps 20 --warmup 5 --batch 256 || exit $? ;;
+    resnet)
+      run resnet1 300 python -m tf_operator_amd.examples.resnet_train --steps 40 --warmup 8 --batch 256 &&
+      run resnet2 300 python -m tf_operator_amd.examples.resnet_train --steps 40 --warmup 8 --batch 256 || exit $? ;;
     *) echo "unknown step $st" >&2; exit 2 ;;
   esac
 done

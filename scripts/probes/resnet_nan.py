@@ -33,11 +33,15 @@ def run(graph, steps=int(os.environ.get("STEPS", "12")), batch=int(os.environ.ge
         loss, out = tr.step(*data.next())
         torch.cuda.synchronize()
         f = tr.flat
-        print(f"graph={graph} step {i}: loss {float(loss):.4f} out_finite {bool(torch.isfinite(out).all())} "
+        print(f"bn={os.environ.get('TOA_BN', 'hip')} graph={graph} step {i}: loss {float(loss):.4f} out_finite {bool(torch.isfinite(out).all())} "
               f"param_finite {bool(torch.isfinite(f.param).all())} master_finite {bool(torch.isfinite(f.master).all())} "
               f"|m| {float(f.exp_avg.abs().max()):.3e} |v| {float(f.exp_avg_sq.abs().max()):.3e}", flush=True)
 
 
 if __name__ == "__main__":
-    run(graph=False)
-    run(graph=True)
+    from tf_operator_amd.examples.common import use_shipped_miopen_find_db
+
+    if os.environ.get("FINDDB", "1") == "1":
+        use_shipped_miopen_find_db()
+    for g in os.environ.get("GRAPH", "0,1").split(","):
+        run(graph=g == "1")

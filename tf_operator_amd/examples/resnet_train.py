@@ -46,6 +46,10 @@ def main(argv=None):
     p.add_argument("--arch", default="resnet50", choices=("resnet50", "resnet-tiny"))
     p.add_argument("--classes", type=int, default=1000)
     p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--clip", type=float, default=0.0,
+                   help="global gradient-norm clipping (device-side, in the fused AdamW); 0 = off")
+    p.add_argument("--fixed-labels", action="store_true",
+                   help="one fixed batch (the model memorises it; see train/data.SyntheticImages)")
     p.add_argument("--ps-mode", default="auto", choices=("auto", "sync", "async", "none"),
                    help="auto = sync when the job has PS replicas")
     a = p.parse_args(argv)
@@ -77,8 +81,9 @@ def main(argv=None):
     if mode != "none":
         tr = simple.PSTrainer(model, loss_fn, rt, workers, servers, mode=mode, lr=a.lr)
     else:
-        tr = simple.DPTrainer(model, loss_fn, rt, lr=a.lr, bucket_mb=64)
-    data = SyntheticImages(a.batch, (3, a.image, a.image), classes=a.classes, rank=rt.rank, device=dev, dtype=dt_)
+        tr = simple.DPTrainer(model, loss_fn, rt, lr=a.lr, bucket_mb=64, max_grad_norm=a.clip)
+    data = SyntheticImages(a.batch, (3, a.image, a.image), classes=a.classes, rank=rt.rank, device=dev, dtype=dt_,
+                           fresh_labels=not a.fixed_labels)
     for _ in range(a.warmup):
         tr.step(*data.next())
     if dev.type == "cuda":

@@ -50,17 +50,28 @@ class SyntheticMNIST:
 
 
 class SyntheticImages:
-    """ImageNet-shaped (3x224x224) random batches with random labels."""
+    """ImageNet-shaped (3x224x224) random batches with random labels.
+
+    ``fresh_labels=True`` draws new labels every step (on the device, into
+    the same buffer): the images stay resident, but the model cannot
+    memorise the batch.  With one fixed batch, Adam drives the loss to ~0
+    within ~20 steps and then occasionally blows up into a dead network
+    (loss stuck at ~ln(#distinct labels)), with PyTorch's or the fused HIP
+    BatchNorm alike (profiles/r2_resnet/divergence_*.log) -- a property of
+    memorising random labels, not of the kernels."""
 
     def __init__(self, batch, shape=(3, 224, 224), classes=1000, rank=0, device="cpu", dtype=torch.bfloat16,
-                 channels_last=True):
+                 channels_last=True, fresh_labels=False):
         g = torch.Generator(device=device).manual_seed(77 + rank)
         self.x = torch.randn(batch, *shape, generator=g, device=device).to(dtype)
         if channels_last:
             self.x = self.x.contiguous(memory_format=torch.channels_last)
         self.y = torch.randint(0, classes, (batch,), generator=g, device=device)
+        self.classes, self.fresh, self.g = classes, fresh_labels, g
 
     def next(self):
+        if self.fresh:
+            torch.randint(0, self.classes, self.y.shape, generator=self.g, device=self.y.device, out=self.y)
         return self.x, self.y
 
 
