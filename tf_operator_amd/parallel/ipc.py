@@ -41,34 +41,51 @@ class IpcAllReduce:
             fn.restype = ctypes.c_int
         self._L = L
         hsz = L.toa_ipc_handle_size()
-        self._own = []
-        ptrs = {}
-        for what, nbytes in (("buf", 2 * self.slot), ("flags", 4 * 8)):
-            p = ctypes.c_void_p()
-            self._check(L.toa_ipc_alloc(nbytes, ctypes.byref(p)), "alloc")
-            self._own.append(p)
-            h = (ctypes.c_char * hsz)()
-            self._check(L.toa_ipc_get_handle(p, h), "get handle")
-            ptrs[what] = (p, bytes(h))
+        self._own, self._opened = [], []
+        # Every step below that can fail locally still reaches the collectives
+        # (a rank that raised before them would leave its peers blocked in
+        # all_gather_object / the barrier): failures are exchanged and every
+        # rank raises together.
+        ptrs, err = {}, None
+        try:
+            for what, nbytes in (("buf", 2 * self.slot), ("flags", 4 * 8)):
+                p = ctypes.c_void_p()
+                self._check(L.toa_ipc_alloc(nbytes, ctypes.byref(p)), "alloc")
+                self._own.append(p)
+                h = (ctypes.c_char * hsz)()
+                self._check(L.toa_ipc_get_handle(p, h), "get handle")
+                ptrs[what] = (p, bytes(h))
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {self.rank}: {e}"
         handles = [None] * self.world
-        dist.all_gather_object(handles, {k: v[1] for k, v in ptrs.items()}, group=group)
-        self._opened = []
+        dist.all_gather_object(handles, {"err": err, **{k: v[1] for k, v in ptrs.items()}}, group=group)
+        errs = [h["err"] for h in handles if h["err"]]
         self.bufs = (ctypes.c_void_p * self.world)()
         self.flags = (ctypes.c_void_p * self.world)()
-        for r in range(self.world):
-            for what, arr in (("buf", self.bufs), ("flags", self.flags)):
-                if r == self.rank:
-                    arr[r] = ptrs[what][0]
-                else:
-                    q = ctypes.c_void_p()
-                    h = (ctypes.c_char * hsz).from_buffer_copy(handles[r][what])
-                    self._check(L.toa_ipc_open_handle(h, ctypes.byref(q)), f"open rank {r} {what}")
-                    self._opened.append(q)
-                    arr[r] = q
+        if not errs:
+            try:
+                for r in range(self.world):
+                    for what, arr in (("buf", self.bufs), ("flags", self.flags)):
+                        if r == self.rank:
+                            arr[r] = ptrs[what][0]
+                        else:
+                            q = ctypes.c_void_p()
+                            h = (ctypes.c_char * hsz).from_buffer_copy(handles[r][what])
+                            self._check(L.toa_ipc_open_handle(h, ctypes.byref(q)), f"open rank {r} {what}")
+                            self._opened.append(q)
+                            arr[r] = q
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {self.rank}: {e}"
+        # collective verdict (replaces a barrier, which a failed rank would skip)
+        ok = torch.tensor([0 if (errs or err) else 1], device=torch.cuda.current_device(), dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if int(ok.item()) != 1:
+            self.close()
+            raise RuntimeError("IPC all-reduce setup failed: " + "; ".join(errs + ([err] if err else [])
+                                                                        or ["on a peer rank"]))
         self.err = torch.zeros(1, device=torch.cuda.current_device(), dtype=torch.int32)
         self.epoch = 0
-        torch.cuda.synchronize()
-        dist.barrier(group=group)
 
     @staticmethod
     def _check(rc, what):
