@@ -123,13 +123,22 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
 // per-workgroup fp32 partials of dw (and db for LayerNorm).
 // partial layout: [gridDim.x][cols] for dw, then [gridDim.x][cols] for db.
 // ---------------------------------------------------------------------------
+// A/B knobs (scripts/norm_bench.py, profiles/r2_norm): keep the row in
+// registers between the two passes below this CH; resident workgroups per CU
+#ifndef NORM_KEEP_BELOW
+#define NORM_KEEP_BELOW 8
+#endif
+#ifndef NORM_BWD_WG_PER_CU
+#define NORM_BWD_WG_PER_CU 3
+#endif
+
 template <typename T, int CH, bool RMS>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ h,
                                                        const T* __restrict__ w, const float* __restrict__ mean_in,
                                                        const float* __restrict__ rstd_in,
                                                        const T* __restrict__ dadd, T* __restrict__ dx,
                                                        float* __restrict__ partial, int rows, int cols) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][cols] (+[4][cols] for db)
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][512] (+[4][512] for db)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nch = cols >> 3;
   // register budget at CH=8 (4096 cols): dw partial 64 + db partial 64 (LN only)
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
     // At CH >= 8 the row is NOT kept in registers between the two passes: the
     // second pass re-reads h / dy (L2 / Infinity-Cache hits) so the kernel
     // stays at ~100 VGPRs (4 waves/SIMD) instead of 256 (1 wave/SIMD).
-    constexpr bool KEEP = CH < 8;
+    constexpr bool KEEP = CH < NORM_KEEP_BELOW;
     float xh[KEEP ? CH : 1][8], d[KEEP ? CH : 1][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -202,25 +211,30 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
       }
     }
   }
-  // reduce the 4 waves' column partials through LDS
+  // reduce the 4 waves' column partials through LDS, one 512-column chunk at a
+  // time: 8 KB of LDS (16 KB for LayerNorm) instead of 64 KB for a 4096-wide
+  // row, so LDS no longer caps the kernel at 2 workgroups per CU
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
     const int ch = lane + c * 64;
+    if (c) __syncthreads();
     if (ch < nch) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        lds[wid * cols + ch * 8 + j] = dwacc[c][j];
-        if (!RMS) lds[4 * cols + wid * cols + ch * 8 + j] = dbacc[c][j];
+        lds[wid * 512 + lane * 8 + j] = dwacc[c][j];
+        if (!RMS) lds[4 * 512 + wid * 512 + lane * 8 + j] = dbacc[c][j];
       }
     }
-  }
-  __syncthreads();
-  for (int col = threadIdx.x; col < cols; col += blockDim.x) {
-    float t = lds[col] + lds[cols + col] + lds[2 * cols + col] + lds[3 * cols + col];
-    partial[(int64_t)blockIdx.x * cols + col] = t;
-    if (!RMS) {
-      float tb = lds[4 * cols + col] + lds[5 * cols + col] + lds[6 * cols + col] + lds[7 * cols + col];
-      partial[(int64_t)gridDim.x * cols + (int64_t)blockIdx.x * cols + col] = tb;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int lc = threadIdx.x + k * 256, col = c * 512 + lc;
+      if (col < cols) {
+        partial[(int64_t)blockIdx.x * cols + col] = lds[lc] + lds[512 + lc] + lds[1024 + lc] + lds[1536 + lc];
+        if (!RMS)
+          partial[(int64_t)gridDim.x * cols + (int64_t)blockIdx.x * cols + col] =
+              lds[2048 + lc] + lds[2560 + lc] + lds[3072 + lc] + lds[3584 + lc];
+      }
     }
   }
 }
@@ -297,8 +311,9 @@ static int norm_fwd_launch(const void* x, const void* res, void* h_out, const vo
 // number of workgroups the backward uses (=> partial rows); caller sizes the
 // partial workspace as nb * cols * (RMS ? 1 : 2) floats.
 extern "C" int toa_norm_bwd_blocks(int rows, int cols) {
+  // ~154 VGPRs at <= 4096 columns: 3 workgroups (12 waves) resident per CU on 256 CUs
   int nb = (rows + 3) / 4;
-  int cap = cols > 4096 ? 256 : 512;
+  int cap = cols > 4096 ? 256 : 256 * NORM_BWD_WG_PER_CU;
   return nb < cap ? nb : cap;
 }
 
@@ -309,8 +324,7 @@ static int norm_bwd_launch(const void* dy, const void* h, const void* w, const f
   if (cols % 8 != 0) return (int)hipErrorInvalidValue;
   int chv = pick_ch(cols);
   int nb = toa_norm_bwd_blocks(rows, cols);
-  size_t lds = (size_t)4 * cols * sizeof(float) * (RMS ? 1 : 2);
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  size_t lds = (size_t)4 * 512 * sizeof(float) * (RMS ? 1 : 2);
   TOA_NORM_DISPATCH(chv, hipLaunchKernelGGL((norm_bwd_kernel<T, CH, RMS>), dim3(nb), dim3(256), lds, s,
                                             (const T*)dy, (const T*)h, (const T*)w, mean, rstd, (const T*)dadd,
                                             (T*)dx, partial, rows, cols));

@@ -20,7 +20,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtoa_hip.so")
+# TOA_HIP_LIB: load another build of the library (in-process A/B of kernel variants)
+LIB_PATH = os.environ.get("TOA_HIP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libtoa_hip.so")
 
 _lock = threading.Lock()
 _lib = None
