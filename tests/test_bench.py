@@ -61,7 +61,22 @@ def test_bench_launcher_two_workers_through_operator():
     _check(r, 2)
     assert r["config"]["launched_by"] == "operator"
     assert len(r["submit_to_first_step"]["samples_s"]) == 2  # 1 probe + the benchmark job itself
+    assert r["submit_to_first_step"]["replica_start"].startswith("warm")  # the default
     assert "ZeRO-1" in r["config"]["optimizer"]
+
+
+@pytest.mark.timeout(600)
+def test_bench_launcher_cold_start():
+    """--warm-start 0: every replica is a fresh python process (its import
+    phase is paid inside submit -> first step); the default forks the
+    kubelet's warm interpreter, whose import phase is near zero."""
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1", "--warm-start", "0"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=580)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json_line(p.stdout)
+    _check(r, 2)
+    assert r["submit_to_first_step"]["replica_start"] == "cold process"
+    assert r["startup_phases_s"]["process_start->imports"] > 0.2, r["startup_phases_s"]
 
 
 @pytest.mark.timeout(600)

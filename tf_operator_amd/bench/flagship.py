@@ -63,6 +63,9 @@ def parser() -> argparse.ArgumentParser:
     ap.add_argument("--latency-probes", type=int, default=3,
                     help="TFJobs submitted (and timed submit -> first step) before the throughput run; 0 = skip")
     ap.add_argument("--probe-timeout", type=float, default=180.0, help="per probe job (s)")
+    ap.add_argument("--warm-start", choices=("0", "1"), default="1",
+                    help="replicas start as forks of the local kubelet's warm interpreter (torch pre-imported, "
+                         "no GPU touched); 0 = a cold python process per replica")
     ap.add_argument("--direct", action="store_true",
                     help="run the replica in this process (no operator; for profilers)")
     ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)  # replica -> launcher
@@ -119,11 +122,29 @@ def _pod_log_tail(c, name: str, n: int = 40) -> str:
     return "\n".join(out)
 
 
-def vram_used_bytes() -> int | None:
-    """HBM in use on every GPU of the node, from the amdgpu driver's sysfs
-    counters (no HIP call: the launcher never initialises a GPU)."""
-    tot, seen = 0, False
+def _own_vram_counters() -> list[str]:
+    """sysfs VRAM counters of the GPUs this process can open: sysfs lists
+    every card of the host (other tenants' too), /dev/dri only ours.  Each
+    accessible render node maps to the card with the same PCI device."""
+    cards = {}
     for p in glob.glob("/sys/class/drm/card*/device/mem_info_vram_used"):
+        cards[os.path.realpath(os.path.dirname(p))] = p
+    own = []
+    for node in glob.glob("/dev/dri/renderD*"):
+        if not os.access(node, os.R_OK | os.W_OK):
+            continue
+        dev = os.path.realpath(os.path.join("/sys/class/drm", os.path.basename(node), "device"))
+        if dev in cards and cards[dev] not in own:
+            own.append(cards[dev])
+    return own
+
+
+def vram_used_bytes() -> int | None:
+    """HBM in use on the node's GPUs that this process can access, from the
+    amdgpu driver's sysfs counters (no HIP call: the launcher never
+    initialises a GPU)."""
+    tot, seen = 0, False
+    for p in _own_vram_counters():
         try:
             with open(p) as f:
                 tot += int(f.read())
@@ -215,10 +236,22 @@ def _summary(samples: list[dict]) -> dict:
                                 "replica_phases": phases}}
 
 
-def _cluster(n: int):
+def _cluster(n: int, warm: bool = False):
+    """Started local cluster; with warm start, returned once the kubelet's fork
+    server has imported torch (a job submitted earlier would start cold)."""
     from ..testing.cluster import LocalCluster
 
-    return LocalCluster(gpus=n, grace_seconds=10.0, device_visibility="node", threadiness=2)
+    c = LocalCluster(gpus=n, grace_seconds=10.0, device_visibility="node", threadiness=2, warm_python=warm).start()
+    if warm:
+        try:
+            c.wait(c.kubelet.warm_ready, 120, 0.05, "kubelet fork server ready")
+        except TimeoutError:  # the kubelet starts replicas cold instead
+            print("[bench] kubelet fork server not ready: replicas start cold", file=sys.stderr, flush=True)
+    return c
+
+
+def _start_mode(c) -> str:
+    return "warm fork (torch pre-imported)" if c.kubelet.warm_ready() else "cold process"
 
 
 def probe_latency(args, n: int, c=None) -> dict:
@@ -226,9 +259,10 @@ def probe_latency(args, n: int, c=None) -> dict:
     payload (one optimizer step each), sequentially."""
     own = c is None
     if own:
-        c = _cluster(n).start()
+        c = _cluster(n, args.warm_start == "1")
     samples, err = [], None
     base = vram_used_bytes()
+    start_mode = _start_mode(c)
     try:
         for i in range(args.latency_probes):
             try:
@@ -245,6 +279,7 @@ def probe_latency(args, n: int, c=None) -> dict:
             c.stop()
     out = _summary(samples)
     out["_raw"] = samples
+    out["replica_start"] = start_mode
     if err:
         out["error"] = err
     return out
@@ -461,6 +496,8 @@ def _attach_probe(out: dict, probe: dict):
     if probe.get("p50_s") is not None:
         out["submit_to_first_step_p50_s"] = probe["p50_s"]
     out["submit_to_first_step"] = {k: v for k, v in probe.items() if k not in ("p50_s", "_raw")}
+    if probe.get("replica_start"):
+        out["submit_to_first_step"]["replica_start"] = probe["replica_start"]
 
 
 # =============================================================================
@@ -471,20 +508,21 @@ def run_launcher(args) -> int:
     if n < 1:
         print("[bench] --gpus must be >= 1", file=sys.stderr)
         return 2
-    c = _cluster(n).start()
+    c = _cluster(n, args.warm_start == "1")
     try:
         probe = probe_latency(args, n, c) if args.latency_probes > 0 else {}
         res_dir = tempfile.mkdtemp(prefix="toa-bench-")
         res_file = os.path.join(res_dir, "result.json")
-        cmd = [sys.executable, "-u", BENCH_PY, "--gpus", str(n), "--steps", str(args.steps), "--warmup",
+        cmd = [sys.executable, BENCH_PY, "--gpus", str(n), "--steps", str(args.steps), "--warmup",
                str(args.warmup), "--model", args.model, "--seq-len", str(args.seq_len), "--micro-batch",
                str(args.micro_batch), "--grad-accum", str(args.grad_accum), "--zero", args.zero,
+               "--warm-start", args.warm_start,
                "--rccl-log", args.rccl_log, "--latency-probes", "0", "--result-file", res_file]
         if args.bucket_mb is not None:
             cmd += ["--bucket-mb", str(args.bucket_mb)]
         timeout = args.probe_timeout + 60 + 30 * (args.steps + args.warmup)
         try:
-            job = _run_job(c, "bench", n, cmd, timeout, env={"TOA_BENCH_RCCL_DIR": res_dir})
+            job = _run_job(c, "bench", n, cmd, timeout, env={"TOA_BENCH_RCCL_DIR": res_dir, "PYTHONUNBUFFERED": "1"})
         except Exception as e:
             print(f"[bench] benchmark TFJob failed: {e}", file=sys.stderr, flush=True)
             return 1
@@ -493,6 +531,7 @@ def run_launcher(args) -> int:
             return 1
         with open(res_file) as f:
             out = json.load(f)
+        start_mode = _start_mode(c)
     finally:
         c.stop()
     job.pop("_logs", None)
@@ -501,6 +540,7 @@ def run_launcher(args) -> int:
     if probe.get("error"):
         p["error"] = probe["error"]
     p["bench_job_submit_to_first_step_s"] = job["submit_to_first_step_s"]
+    p["replica_start"] = start_mode
     _attach_probe(out, p)
     print(json.dumps(out), flush=True)
     return 0

@@ -464,6 +464,10 @@ class LocalKubelet:
             pr._exited(-signal.SIGKILL)
         self._fs_procs.clear()
 
+    def warm_ready(self) -> bool:
+        """The fork server has imported torch and takes container starts."""
+        return bool(self.warm_python and self._fs is not None and self._fs_ready.is_set())
+
     async def _warm_spawn(self, argv, env, cwd, logpath):
         """Fork the container off the warm interpreter; None = use a cold start."""
         if not (self.warm_python and self._fs is not None and self._fs_ready.is_set() and len(argv) >= 2
