@@ -77,6 +77,39 @@ def test_compact_state_roundtrip_any_world(tmp_path):
             assert torch.equal(getattr(h, k), ref[k][lo:hi]), (k, lo)
 
 
+def test_replicated_shares_restore_once(tmp_path):
+    """Without ZeRO every rank of a world-2 job saves the WHOLE state: a
+    resume (any world size) takes each range once instead of rejecting the
+    doubled coverage."""
+    from tf_operator_amd.parallel.flat import _uncovered
+
+    assert _uncovered(0, 10, []) == [(0, 10)]
+    assert _uncovered(0, 10, [(2, 4), (6, 12)]) == [(0, 2), (4, 6)]
+    assert _uncovered(3, 5, [(0, 10)]) == []
+    full = _flat()
+    ref = {k: getattr(full, k).clone() for k in sharded_ckpt.STATE_KEYS}
+    cks = []
+    for r in range(2):
+        ck = sharded_ckpt.Checkpointer(str(tmp_path), rank=r, world=2, commit_timeout=60)
+        ck.save(7, _state(_flat()))
+        cks.append(ck)
+    for ck in cks:
+        ck.wait()
+    shares = sharded_ckpt.load_latest(str(tmp_path))
+    assert len(shares) == 2 and all(s["flat"]["state_ranges"] == [[0, full.numel]] or
+                                    [tuple(x) for x in s["flat"]["state_ranges"]] == [(0, full.numel)]
+                                    for s in shares)
+    g = _flat(seed=1)
+    g.load_state_shards([s["flat"] for s in shares], set_params="all")
+    for k in sharded_ckpt.STATE_KEYS:
+        assert torch.equal(getattr(g, k), ref[k]), k
+    n = full.numel
+    h = _flat(seed=2)
+    h.shard_state([(64, n // 2 // 64 * 64)])
+    h.load_state_shards([s["flat"] for s in shares], set_params="held")
+    assert torch.equal(h.master, ref["master"][64:n // 2 // 64 * 64])
+
+
 def test_uncommitted_step_is_not_latest(tmp_path):
     """Only rank 0 of a world-2 save finished: no manifest, the previous
     committed step stays `latest` (a crash mid-save loses nothing)."""
@@ -165,11 +198,11 @@ def test_zero_checkpoint_resume_and_reshard(tmp_path):
         assert torch.equal(got["param"], ref_master.to(torch.bfloat16).float()), w
 
 
-@pytest.mark.parametrize("world", [2])
-def test_llama_train_zero_checkpoint_every(tmp_path, world):
-    """The operator payload with ZeRO on (its default for world > 1) and
-    --checkpoint-every runs to completion on every rank (no chief-only
-    collective) and leaves a committed world-2 checkpoint."""
+@pytest.mark.parametrize("world,zero", [(2, "auto"), (2, "0")])
+def test_llama_train_zero_checkpoint_every(tmp_path, world, zero):
+    """The operator payload with ZeRO on (its default for world > 1) or off,
+    and --checkpoint-every, runs to completion on every rank (no chief-only
+    collective), leaves a committed world-2 checkpoint and resumes from it."""
     root = str(tmp_path / "ck")
     port = _free_port()
     import subprocess
@@ -179,12 +212,23 @@ def test_llama_train_zero_checkpoint_every(tmp_path, world):
     for r in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(world),
                    TOA_CHECKPOINT_DIR=root, TOA_NO_GPU="1", OMP_NUM_THREADS="1")
-        procs.append(subprocess.Popen([sys.executable, "-m", "tf_operator_amd.examples.llama_train", "--steps", "4",
-                                       "--seq-len", "32", "--checkpoint-every", "2"], env=env,
-                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
-    outs = [p.communicate(timeout=300)[0].decode() for p in procs]
-    assert all(p.returncode == 0 for p in procs), outs
+    def run(steps):
+        procs = []
+        for r in range(world):
+            env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                       WORLD_SIZE=str(world), TOA_CHECKPOINT_DIR=root, TOA_NO_GPU="1", OMP_NUM_THREADS="1")
+            procs.append(subprocess.Popen([sys.executable, "-m", "tf_operator_amd.examples.llama_train", "--steps",
+                                           str(steps), "--seq-len", "32", "--checkpoint-every", "2", "--zero", zero],
+                                          env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        outs = [p.communicate(timeout=300)[0].decode() for p in procs]
+        assert all(p.returncode == 0 for p in procs), outs
+
+    run(4)
     shares = sharded_ckpt.load_latest(root)
     assert shares[0]["step"] == 4 and shares[0]["world"] == world and len(shares) == world
     n = shares[0]["flat"]["numel"]
-    assert sum(hi - lo for s in shares for lo, hi in s["flat"]["state_ranges"]) == n
+    per_rank = sum(hi - lo for s in shares for lo, hi in s["flat"]["state_ranges"])
+    assert per_rank == (n if zero == "auto" else world * n)
+    port = _free_port()
+    run(6)  # resumes at step 4 from the world-2 shares, runs to 6
+    assert sharded_ckpt.load_latest(root)[0]["step"] == 6

@@ -9,6 +9,7 @@ which is what the elastic policy relies on."""
 from __future__ import annotations
 
 import argparse
+import os
 import time
 
 import torch
@@ -53,7 +54,9 @@ def _stop_agreed(rt, dev) -> bool:
 
 
 def _train(a, rt, info):
-    dev = pick_device() if info.backend != "gloo" else torch.device("cpu")
+    # gloo is the CPU plumbing backend, unless asked for explicitly
+    # (TOA_DIST_BACKEND=gloo: replicas sharing one GPU, device tensors over gloo)
+    dev = pick_device() if info.backend != "gloo" or os.environ.get("TOA_DIST_BACKEND") else torch.device("cpu")
     zero = rt.world > 1 if a.zero == "auto" else a.zero == "1"
     tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr, shard_optimizer=zero)
     rt.mark("model_init")

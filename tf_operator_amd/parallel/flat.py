@@ -32,6 +32,23 @@ import torch
 ALIGN = 64  # elements; keeps every view 128-B aligned for 16-B vector access
 
 
+def _uncovered(x: int, y: int, covered) -> list:
+    """Sub-ranges of [x, y) not in any of the (disjoint) `covered` ranges."""
+    out = [(x, y)]
+    for a, b in covered:
+        nxt = []
+        for p, q in out:
+            if b <= p or a >= q:
+                nxt.append((p, q))
+                continue
+            if p < a:
+                nxt.append((p, a))
+            if b < q:
+                nxt.append((b, q))
+        out = nxt
+    return out
+
+
 def _as_tensor(x):
     """numpy (incl. read-only checkpoint memmaps) or torch -> torch, no copy."""
     if torch.is_tensor(x):
@@ -211,31 +228,33 @@ class FlatParams:
         device or numpy memmaps) that together cover them.  ``set_params``:
         "held" re-derives the bf16 weights of the held ranges, "all" of every
         range the shards cover (then no weight all-gather is needed)."""
-        covered = []
+        covered, pcovered = [], []  # ranges already restored (state / bf16 weights)
         for sh in shards:
             if "layout" in sh:
                 self.check_layout(sh["layout"])
             src_off = 0
             for lo, hi in sh["state_ranges"]:
                 lo, hi = int(lo), int(hi)
-                for k in ("master", "exp_avg", "exp_avg_sq"):
-                    src = sh.get(k)
-                    if src is None:
-                        continue
-                    if getattr(self, k) is None:
-                        setattr(self, k, torch.zeros(self.state_numel, device=self.device, dtype=torch.float32))
-                    dst = getattr(self, k)
-                    for (a, b) in self.state_ranges:
-                        x, y = max(a, lo), min(b, hi)
-                        if x >= y:
-                            continue
-                        piece = _as_tensor(src[src_off + x - lo:src_off + y - lo])
-                        self.state_view(dst, x, y).copy_(piece, non_blocking=False)
-                        if k == "master":
-                            covered.append((x, y))
+                for (a, b) in self.state_ranges:
+                    x, y = max(a, lo), min(b, hi)
+                    # replicated (non-ZeRO) ranks each saved the whole state:
+                    # copy every range once, from the first share that has it
+                    for p, q in (_uncovered(x, y, covered) if x < y and sh.get("master") is not None else []):
+                        for k in ("master", "exp_avg", "exp_avg_sq"):
+                            src = sh.get(k)
+                            if src is None:
+                                continue
+                            if getattr(self, k) is None:
+                                setattr(self, k, torch.zeros(self.state_numel, device=self.device,
+                                                             dtype=torch.float32))
+                            piece = _as_tensor(src[src_off + p - lo:src_off + q - lo])
+                            self.state_view(getattr(self, k), p, q).copy_(piece, non_blocking=False)
+                        covered.append((p, q))
                 if set_params == "all" and sh.get("master") is not None:
-                    piece = _as_tensor(sh["master"][src_off:src_off + hi - lo])
-                    self.param[lo:hi].copy_(piece.to(self.device).to(self.param.dtype))
+                    for p, q in _uncovered(lo, hi, pcovered):
+                        piece = _as_tensor(sh["master"][src_off + p - lo:src_off + q - lo])
+                        self.param[p:q].copy_(piece.to(self.device).to(self.param.dtype))
+                        pcovered.append((p, q))
                 src_off += hi - lo
         need = sum(b - a for a, b in self.state_ranges)
         if self.master is not None and sum(b - a for a, b in covered) != need:

@@ -65,7 +65,9 @@ def init(backend=None, timeout_s=1800) -> DistInfo:
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
-    backend = backend or ("nccl" if use_cuda else "gloo")
+    # TOA_DIST_BACKEND=gloo: several replicas sharing one GPU (RCCL refuses two
+    # ranks on one device), e.g. restart benchmarks on a one-GPU box
+    backend = backend or os.environ.get("TOA_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")

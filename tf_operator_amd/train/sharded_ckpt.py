@@ -91,6 +91,7 @@ class Checkpointer:
         self._staging: dict[str, torch.Tensor] = {}
         self._thread: threading.Thread | None = None
         self._error: BaseException | None = None
+        self._last_step: int | None = None
         self.last_timing: dict = {}
         os.makedirs(root, exist_ok=True)
 
@@ -106,8 +107,15 @@ class Checkpointer:
 
     # ------------------------------------------------------------------ save
     def save(self, step: int, state: dict, extra: dict | None = None, block: bool = False):
-        """`state` = ``train.llm.trainer_state`` (this rank's share)."""
+        """`state` = ``train.llm.trainer_state`` (this rank's share).  A step
+        this rank already saved is not written again (a periodic save that
+        lands on the last step, then the final save): a second round of the
+        same step directory could race rank 0's rename of the first and leave
+        its commit waiting for a share written into the old directory."""
         self.wait()  # one save in flight: the staging buffers are reused
+        if self._last_step == int(step):
+            return
+        self._last_step = int(step)
         t0 = time.time()
         fl = state["flat"]
         staged = {k: self._stage(k, fl[k]) for k in STATE_KEYS if fl.get(k) is not None}
