@@ -11,6 +11,7 @@ SIGKILLed.  Reports, from the operator's own records:
 
     python benchmarks/elastic_resume.py                       # CPU / gloo, llama-tiny
     python benchmarks/elastic_resume.py --model llama3-1b --gpu   # one process per GPU
+    python benchmarks/elastic_resume.py --gpu --share-gpu         # every worker on GPU 0, gloo
 """
 from __future__ import annotations
 
@@ -36,7 +37,10 @@ def main():
     ap.add_argument("--micro-batch", type=int, default=2)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--gpu", action="store_true", help="workers use real GPUs (HIP_VISIBLE_DEVICES)")
+    ap.add_argument("--share-gpu", action="store_true", help="with --gpu: all workers on device 0, gloo collectives")
+    ap.add_argument("--warm", action="store_true", help="replicas start as forks of the kubelet's warm interpreter")
     ap.add_argument("--run-before", type=float, default=8.0, help="seconds of steady training before the fault")
+    ap.add_argument("--workdir", default=None, help="local kubelet workdir (pod logs land under it)")
     a = ap.parse_args()
     ckpt = tempfile.mkdtemp(prefix="toa-elastic-")
     cmd = [sys.executable, "-m", "tf_operator_amd.examples.llama_train", "--model", a.model, "--steps", str(a.steps),
@@ -45,6 +49,9 @@ def main():
     env = {"OMP_NUM_THREADS": "1", "TOA_LOG_PHASES": "0"}
     if not a.gpu:
         env["CUDA_VISIBLE_DEVICES"] = ""
+    elif a.share_gpu:
+        env["TOA_DIST_BACKEND"] = "gloo"
+        cmd += ["--zero", "0"]  # replicated AdamW: gloo all-reduce on device tensors
     tpl = pod_template(container(image="toa/trainer", command=cmd, gpus=1, env=env),
                        annotations={"amd.com/checkpoint-dir": ckpt})
     job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
@@ -54,7 +61,10 @@ def main():
                     "tfReplicaSpecs": {"Worker": {"replicas": a.workers, "restartPolicy": "ExitCode",
                                                   "template": tpl}}}}
     key = ("default", "elastic")
-    with LocalCluster(gpus=a.workers, grace_seconds=2.0) as c:
+    with LocalCluster(gpus=a.workers, grace_seconds=2.0, warm_python=a.warm, workdir=a.workdir,
+                      device_visibility="node" if a.share_gpu else None) as c:
+        if a.warm:
+            c.wait(c.kubelet.warm_ready, 120, 0.05, "kubelet fork server ready")
         c.client.create(job)
         st = lambda: (c.api.get("kubeflow.org/tfjobs", "default", "elastic") or {}).get("status") or {}
         c.wait(lambda: (c.controller.reports.get(key) or {}).get("samples_per_sec"), 600, 0.1, "first throughput")
@@ -81,7 +91,8 @@ def main():
            "samples_per_sec_after": round(after["samples_per_sec"], 2), "world_after": after.get("world"),
            "generation": es.get("generation"), "restarts": es.get("restarts"),
            "config": {"model": a.model, "workers": a.workers, "seq_len": a.seq_len, "micro_batch": a.micro_batch,
-                      "device": "gpu" if a.gpu else "cpu/gloo"}}
+                      "device": ("gpu0 shared, gloo" if a.share_gpu else "gpu, rccl") if a.gpu else "cpu/gloo",
+                      "replica_start": "warm fork" if a.warm else "cold process"}}
     print(json.dumps(out))
 
 
