@@ -81,3 +81,18 @@ def test_kubelet_attributes_devices_to_pods(tmp_path):
         assert text.count('pod=""') == 3  # the free device: memory used / total / duty cycle
         c.client.delete("gm")
     assert json.loads(json.dumps(owners))  # serialisable for the --owners file of the exporter
+
+
+def test_read_devices_accessible_only(tmp_path):
+    """A shared host: sysfs lists every card, /dev/dri only this process's
+    render node (card1's here) -- accessible_only keeps just that GPU."""
+    root = str(tmp_path / "drm")
+    _fake_sysfs(root)
+    os.makedirs(os.path.join(root, "renderD129"))
+    os.symlink(os.path.join(root, "card1", "device"), os.path.join(root, "renderD129", "device"))
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    (dri / "renderD129").write_text("")
+    devs = gpu_metrics.read_devices(root, accessible_only=True, dev_dri=str(dri))
+    assert [d["acc_id"] for d in devs] == ["card1"] and devs[0]["index"] == 0
+    assert len(gpu_metrics.read_devices(root)) == 2

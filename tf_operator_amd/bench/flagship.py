@@ -124,19 +124,12 @@ def _pod_log_tail(c, name: str, n: int = 40) -> str:
 
 def _own_vram_counters() -> list[str]:
     """sysfs VRAM counters of the GPUs this process can open: sysfs lists
-    every card of the host (other tenants' too), /dev/dri only ours.  Each
-    accessible render node maps to the card with the same PCI device."""
-    cards = {}
-    for p in glob.glob("/sys/class/drm/card*/device/mem_info_vram_used"):
-        cards[os.path.realpath(os.path.dirname(p))] = p
-    own = []
-    for node in glob.glob("/dev/dri/renderD*"):
-        if not os.access(node, os.R_OK | os.W_OK):
-            continue
-        dev = os.path.realpath(os.path.join("/sys/class/drm", os.path.basename(node), "device"))
-        if dev in cards and cards[dev] not in own:
-            own.append(cards[dev])
-    return own
+    every card of the host (other tenants' too), /dev/dri only ours."""
+    from ..utils.gpu_metrics import accessible_devices
+
+    own = accessible_devices()
+    return [p for p in sorted(glob.glob("/sys/class/drm/card*/device/mem_info_vram_used"))
+            if os.path.realpath(os.path.dirname(p)) in own]
 
 
 def vram_used_bytes() -> int | None:

@@ -53,13 +53,29 @@ def _num(s):
         return None
 
 
-def read_devices(root: str = SYSFS_DRM) -> list[dict]:
+def accessible_devices(root: str = SYSFS_DRM, dev_dri: str = "/dev/dri") -> set[str]:
+    """PCI devices (sysfs realpaths) of the render nodes this process can
+    open.  sysfs lists every GPU of the host; a container or a shared box
+    exposes only its own render nodes under /dev/dri."""
+    out = set()
+    for node in glob.glob(os.path.join(dev_dri, "renderD*")):
+        if os.access(node, os.R_OK | os.W_OK):
+            out.add(os.path.realpath(os.path.join(root, os.path.basename(node), "device")))
+    return out
+
+
+def read_devices(root: str = SYSFS_DRM, accessible_only: bool = False, dev_dri: str = "/dev/dri") -> list[dict]:
     """One record per amdgpu device with VRAM (compute GPUs), ordered by
-    card number = the HIP device order on a node with only these GPUs."""
+    card number = the HIP device order on a node with only these GPUs.
+    ``accessible_only``: only the GPUs whose render node this process can
+    open (:func:`accessible_devices`)."""
     out = []
+    own = accessible_devices(root, dev_dri) if accessible_only else None
     cards = [p for p in glob.glob(os.path.join(root, "card*")) if re.fullmatch(r"card\d+", os.path.basename(p))]
     for card in sorted(cards, key=lambda p: int(os.path.basename(p)[4:])):
         dev = os.path.join(card, "device")
+        if own is not None and os.path.realpath(dev) not in own:
+            continue
         total = _num(_read(os.path.join(dev, "mem_info_vram_total")))
         if not total:
             continue
@@ -153,7 +169,7 @@ def exposition(devices: list[dict], owners: dict | None = None, model: str = "MI
     return "\n".join(out) + "\n"
 
 
-def serve(port: int, owners_path: str | None = None, root: str = SYSFS_DRM):
+def serve(port: int, owners_path: str | None = None, root: str = SYSFS_DRM, accessible_only: bool = False):
     class H(http.server.BaseHTTPRequestHandler):
         def do_GET(self):
             if self.path.split("?")[0] != "/metrics":
@@ -164,7 +180,7 @@ def serve(port: int, owners_path: str | None = None, root: str = SYSFS_DRM):
             if owners_path and os.path.exists(owners_path):
                 with open(owners_path) as f:
                     owners = {int(k): tuple(v) for k, v in json.load(f).items()}
-            body = exposition(read_devices(root), owners).encode()
+            body = exposition(read_devices(root, accessible_only), owners).encode()
             self.send_response(200)
             self.send_header("Content-Type", "text/plain; version=0.0.4")
             self.send_header("Content-Length", str(len(body)))
@@ -182,11 +198,13 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=9400)
     ap.add_argument("--owners", default=None, help="JSON {device index: [namespace, pod, container]}")
     ap.add_argument("--once", action="store_true", help="print one scrape and exit")
+    ap.add_argument("--accessible-only", action="store_true",
+                    help="only the GPUs whose /dev/dri render node this process can open (shared hosts)")
     a = ap.parse_args(argv)
     if a.once:
-        print(exposition(read_devices()), end="")
+        print(exposition(read_devices(accessible_only=a.accessible_only)), end="")
         return 0
-    serve(a.port, a.owners)
+    serve(a.port, a.owners, accessible_only=a.accessible_only)
     return 0
 
 
