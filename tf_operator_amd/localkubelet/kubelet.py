@@ -647,11 +647,14 @@ class LocalKubelet:
 
     def gpu_metrics_text(self, sysfs_root: str | None = None) -> str:
         """cAdvisor-style ``container_accelerator_*`` series for this node's
-        GPUs, attributed to the pods holding them (utils/gpu_metrics.py)."""
+        GPUs, attributed to the pods holding them (utils/gpu_metrics.py).
+        On the real sysfs only the GPUs this node can open are listed (device
+        index i = the i-th of them), not every card of a shared host."""
         from ..utils import gpu_metrics
 
-        return gpu_metrics.exposition(gpu_metrics.read_devices(sysfs_root or gpu_metrics.SYSFS_DRM),
-                                      self.gpu_owners())
+        devs = (gpu_metrics.read_devices(sysfs_root) if sysfs_root
+                else gpu_metrics.read_devices(gpu_metrics.SYSFS_DRM, accessible_only=True))
+        return gpu_metrics.exposition(devs, self.gpu_owners())
 
     async def set_capacity(self, gpus: int):
         """Change the node's allocatable GPUs (fault injection: a device or
