@@ -129,6 +129,25 @@ __device__ __forceinline__ float rowmax32(const f32x16& a, const f32x16& b) {
 }
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
+#ifndef ATTN_WIDE_STORE
+#define ATTN_WIDE_STORE 1
+#endif
+// Epilogue store of one 32x32 accumulator tile's row (guide T21): lane l and
+// l^32 own the same row; `a` / `b` are this lane's packed bf16x4 of column
+// groups 2k and 2k+1 (cols 16k + 8*g' + 4*hh).  One v_permlane32_swap per
+// dword leaves lanes < 32 with cols 16k..16k+7 and lanes >= 32 with
+// 16k+8..16k+15: one 16-B store per lane instead of two 8-B ones.
+__device__ __forceinline__ void store_pair16(bf16_t* row, int col16k, int hh, uint2 a, uint2 b) {
+#if ATTN_WIDE_STORE
+  const auto r0 = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+  const auto r1 = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+  *(uint4*)(row + col16k + 8 * hh) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+#else
+  *(uint2*)(row + col16k + 4 * hh) = a;
+  *(uint2*)(row + col16k + 8 + 4 * hh) = b;
+#endif
+}
+
 // Offset of row (b, h, s) of O / dO: [B, H, S, D] (head-major, like Q) or, with
 // bshd, [B, S, H, D] -- the layout the output projection consumes, so the
 // model needs no transpose copy of O forward or of dO backward.
@@ -337,12 +356,15 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 32 * dt + 8 * g + 4 * hh;
-      uint2 w;
-      w.x = cvt_pk(acc[dt][4 * g + 0] * inv, acc[dt][4 * g + 1] * inv);
-      w.y = cvt_pk(acc[dt][4 * g + 2] * inv, acc[dt][4 * g + 3] * inv);
-      *(uint2*)(orow + d) = w;
+    for (int k = 0; k < 2; ++k) {
+      uint2 w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int g = 2 * k + u;
+        w[u].x = cvt_pk(acc[dt][4 * g + 0] * inv, acc[dt][4 * g + 1] * inv);
+        w[u].y = cvt_pk(acc[dt][4 * g + 2] * inv, acc[dt][4 * g + 3] * inv);
+      }
+      store_pair16(orow, 32 * dt + 16 * k, hh, w[0], w[1]);
     }
   if (hh == 0) LSE[(int64_t)(b * H + h) * S + myq] = (m_run + log2f(l_tot)) * 0.6931471805599453f;
 }
@@ -586,15 +608,18 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 32 * dt + 8 * g + 4 * hh;
-      uint2 a, c;
-      a.x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
-      a.y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
-      c.x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
-      c.y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
-      *(uint2*)(dkr + d) = a;
-      *(uint2*)(dvr + d) = c;
+    for (int k = 0; k < 2; ++k) {
+      uint2 a[2], c[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int g = 2 * k + u;
+        a[u].x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
+        a[u].y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+        c[u].x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
+        c[u].y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+      }
+      store_pair16(dkr, 32 * dt + 16 * k, hh, a[0], a[1]);
+      store_pair16(dvr, 32 * dt + 16 * k, hh, c[0], c[1]);
     }
 }
 
@@ -766,12 +791,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 32 * dt + 8 * g + 4 * hh;
-      uint2 w;
-      w.x = pack2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
-      w.y = pack2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
-      *(uint2*)(qrow + d) = w;
+    for (int k = 0; k < 2; ++k) {
+      uint2 w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int g = 2 * k + u;
+        w[u].x = pack2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
+        w[u].y = pack2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
+      }
+      store_pair16(qrow, 32 * dt + 16 * k, hh, w[0], w[1]);
     }
 }
 
