@@ -79,6 +79,18 @@ def test_dist_mnist_parameter_server(cluster, sync):
     assert "ps" in w0.lower() and "accuracy" in w0
 
 
+def test_tf_smoke_in_graph_replication(cluster):
+    """tf_smoke.py analog: the chief checks a 10x10
+    multiply from every task of Chief + 2 Workers (all-gather); the PS
+    replica never exits and the job still succeeds on the chief."""
+    tpl = payload("smoke")
+    job = tfjob("smoke", {"Chief": rs(1, tpl), "Worker": rs(2, tpl), "PS": rs(1, tpl)},
+                runPolicy={"cleanPodPolicy": "All"})
+    done, logs = _run(cluster, job)
+    assert "Succeeded" in conds(done), (conds(done), logs)
+    assert "smoke ok on 3 task(s)" in logs["smoke-chief-0"], logs["smoke-chief-0"]
+
+
 def test_mnist_with_summaries(cluster, tmp_path):
     job = tfjob("summaries", {"Worker": rs(1, payload("mnist_with_summaries", "--max_steps", 60,
                                                       "--log_dir", tmp_path))})
