@@ -311,3 +311,22 @@ def test_reconcile_span_log_is_structured(cluster, caplog):
     line = json.loads(JsonFormatter().format(recs[0]))
     assert line["msg"] == "reconcile" and line["duration_ms"] >= 0 and line["kind"] == "TFJob"
     c.delete("spans")
+
+
+def test_sdk_watch_table_until_terminal(cluster):
+    """sdk.watch (reference tf_job_watch.py): NAME/STATE/TIME rows from the
+    watch stream, returning when the named job reaches a terminal state."""
+    import io
+
+    from tf_operator_amd.sdk import watch as sdk_watch
+
+    c = cluster.client
+    c.create(tfjob("watched", {"Worker": replica(1, sh("import time; time.sleep(1.0)"))}))
+    out = io.StringIO()
+    state = sdk_watch.watch(c, name="watched", namespace="default", timeout_seconds=60, out=out)
+    assert state == "Succeeded"
+    rows = out.getvalue().splitlines()
+    assert rows[0].split() == ["NAME", "STATE", "TIME"]
+    states = [(r.split() + [""])[1] for r in rows[1:] if r.startswith("watched")]  # "" before any condition
+    assert states[-1] == "Succeeded" and "Created" in states, rows
+    c.delete("watched")
