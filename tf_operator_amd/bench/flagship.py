@@ -163,6 +163,27 @@ def wait_vram_drained(baseline: int | None, timeout: float = 60.0, slack: int = 
     return round(time.monotonic() - t0, 3)
 
 
+def wait_vram_settled(timeout: float = 120.0, window: float = 2.0, tol: int = 1 << 30) -> float:
+    """Block until the node's VRAM counter has stopped falling (moved less
+    than `tol` over the last `window` seconds) and return the seconds waited.
+    A node can still be scrubbing the HBM of a job that ended just before
+    (the previous benchmark run, or whatever used the GPU before this one):
+    a drain baseline taken then would be too high, and every later drain
+    wait would end early."""
+    t0 = time.monotonic()
+    hist = []
+    while time.monotonic() - t0 < timeout:
+        u = vram_used_bytes()
+        if u is None:
+            return 0.0
+        now = time.monotonic()
+        hist = [(t, v) for t, v in hist if now - t <= window] + [(now, u)]
+        if now - t0 >= window and max(v for _, v in hist) - min(v for _, v in hist) < tol:
+            break
+        time.sleep(0.05)
+    return round(time.monotonic() - t0, 3)
+
+
 def _run_job(c, name: str, n: int, command: list[str], timeout: float, env=None,
              vram_baseline: int | None = None) -> dict:
     """Submit one TFJob Worker=n, wait for it to succeed; return the client
@@ -254,6 +275,7 @@ def probe_latency(args, n: int, c=None) -> dict:
     if own:
         c = _cluster(n, args.warm_start == "1")
     samples, err = [], None
+    settle_s = wait_vram_settled()  # a clean drain baseline
     base = vram_used_bytes()
     start_mode = _start_mode(c)
     try:
@@ -273,6 +295,7 @@ def probe_latency(args, n: int, c=None) -> dict:
     out = _summary(samples)
     out["_raw"] = samples
     out["replica_start"] = start_mode
+    out["node_settle_before_probes_s"] = settle_s
     if err:
         out["error"] = err
     return out
@@ -534,6 +557,8 @@ def run_launcher(args) -> int:
         p["error"] = probe["error"]
     p["bench_job_submit_to_first_step_s"] = job["submit_to_first_step_s"]
     p["replica_start"] = start_mode
+    if "node_settle_before_probes_s" in probe:
+        p["node_settle_before_probes_s"] = probe["node_settle_before_probes_s"]
     _attach_probe(out, p)
     print(json.dumps(out), flush=True)
     return 0
