@@ -32,7 +32,12 @@ def use_shipped_miopen_find_db() -> str | None:
     for f in src:
         out = os.path.join(dst, os.path.basename(f))
         if not os.path.exists(out):
-            shutil.copyfile(f, out)
+            # atomic: the replicas of one node start together, and MIOpen must
+            # never read a half-copied db (an existing copy is kept: MIOpen
+            # appends what it finds for other shapes to it)
+            tmp = f"{out}.{os.getpid()}.tmp"
+            shutil.copyfile(f, tmp)
+            os.replace(tmp, out)
     os.environ["MIOPEN_USER_DB_PATH"] = dst
     return dst
 
