@@ -57,6 +57,17 @@ template <>
 __device__ __forceinline__ void stp<float>(float* p, int i, float v) { p[i] = v; }
 template <>
 __device__ __forceinline__ void stp<bf16_t>(bf16_t* p, int i, float v) { p[i] = f2bf(v); }
+// dgamma / dbeta store: gdt 0 = bf16, 1 = fp32; acc: add into what is there
+// (the flat fp32 gradient buffer, main_grad) instead of overwriting
+__device__ __forceinline__ void st_grad(void* p, int gdt, int acc, int i, float v) {
+  if (gdt == 1) {
+    float* q = (float*)p;
+    q[i] = acc ? q[i] + v : v;
+  } else {
+    bf16_t* q = (bf16_t*)p;
+    q[i] = f2bf(acc ? bf2f(q[i]) + v : v);
+  }
+}
 
 // Block geometry: CG = C/8 channel groups across the threads of a row,
 // RPI = 256 / CG rows per block iteration (threads >= RPI*CG idle).
@@ -276,14 +287,15 @@ __global__ __launch_bounds__(BN_THREADS) void bn_bwd_finalize_kernel(const float
                                                                       int C, const float* __restrict__ stats,
                                                                       const P* __restrict__ gamma,
                                                                       float* __restrict__ g, float* __restrict__ k,
-                                                                      P* __restrict__ dgamma, P* __restrict__ dbeta) {
+                                                                      void* __restrict__ dgamma,
+                                                                      void* __restrict__ dbeta, int gdt, int acc) {
   float a, b;  // one workgroup per 8 channels
   if (!bn_sum_partials(ws, nb, C, blockIdx.x * 8, &a, &b)) return;
   const int c = blockIdx.x * 8 + (threadIdx.x & 7);
   g[c] = a;
   g[C + c] = b;
-  if (dbeta) stp(dbeta, c, a);
-  if (dgamma) stp(dgamma, c, b);
+  if (dbeta) st_grad(dbeta, gdt, acc, c, a);
+  if (dgamma) st_grad(dgamma, gdt, acc, c, b);
   const float inv_r = 1.f / (float)R, mean = stats[c], is = stats[C + c];
   const float k1 = (gamma ? ldp(gamma, c) : 1.f) * is;
   k[c] = k1;
@@ -387,11 +399,13 @@ extern "C" int toa_bn_fwd_eval(int dtype, int pdtype, const void* x, const void*
 // mask), else null; dres (may be null) receives dy' for a fused residual
 // mask: 0 no ReLU, 1 ReLU mask from y (the saved output), 2 from x and the
 // saved scale / shift (y unused)
+// dgamma / dbeta: gdtype 0 = bf16, 1 = fp32; accumulate = add into them
 extern "C" int toa_bn_bwd(int dtype, int pdtype, const void* dy, const void* x, const void* y, int mask,
                           const float* stats,
                           const void* gamma, int64_t R, int C, void* dx, void* dres, void* dgamma, void* dbeta,
-                          float* ws, hipStream_t st) {
-  if (!bn_shape_ok(R, C) || mask < 0 || mask > 2 || (mask == 1 && !y)) return (int)hipErrorInvalidValue;
+                          int gdtype, int accumulate, float* ws, hipStream_t st) {
+  if (!bn_shape_ok(R, C) || mask < 0 || mask > 2 || (mask == 1 && !y) || gdtype < 0 || gdtype > 1)
+    return (int)hipErrorInvalidValue;
   const int nb = bn_blocks(R, C);
   float* g = ws + (int64_t)nb * 2 * C;
   float* k = g + 2 * C;
@@ -399,7 +413,7 @@ extern "C" int toa_bn_bwd(int dtype, int pdtype, const void* dy, const void* x, 
     hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, dim3(nb), dim3(BN_THREADS), 0, st, (const T*)dy, (const T*)x,
                        (const T*)y, mask, stats, R, C, ws);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<P>, dim3(C / 8), dim3(BN_THREADS), 0, st,
-                       ws, nb, R, C, stats, (const P*)gamma, g, k, (P*)dgamma, (P*)dbeta);
+                       ws, nb, R, C, stats, (const P*)gamma, g, k, dgamma, dbeta, gdtype, accumulate);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(bn_grid(R * C / 8)), dim3(BN_THREADS), 0, st, (const T*)dy,
                        (const T*)x, (const T*)y, mask, stats, k, R * C / 8, C, (T*)dx, (T*)dres);
   });

@@ -718,6 +718,36 @@ def test_fused_batchnorm_act(N, C, H, W, relu, res, dt):
     assert rel(ye, yef) < tol
 
 
+def test_fused_batchnorm_grads_into_flat_buffer():
+    """With FlatParams-managed gamma / beta, the BN backward kernel adds
+    dgamma / dbeta straight into the fp32 flat gradient buffer (on top of
+    what is there) and fires the bucket hooks; values match the plain path."""
+    _lib()
+    from tf_operator_amd.ops.bn import FusedBatchNorm2d
+    from tf_operator_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(5)
+    C = 64
+    x = torch.randn(4, C, 8, 8, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    dy = torch.randn(4, C, 8, 8, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    ref = FusedBatchNorm2d(C, relu=True).to(DEV, torch.bfloat16)
+    bn = FusedBatchNorm2d(C, relu=True).to(DEV, torch.bfloat16)
+    xr = x.clone().requires_grad_()
+    ref(xr).backward(dy)
+    flat = FlatParams([bn.weight, bn.bias], grad_dtype=torch.float32)
+    fired = []
+    for p in (bn.weight, bn.bias):
+        p._toa_ready = fired.append
+    flat.grad.fill_(0.25)  # accumulate onto what is there
+    xb = x.clone().requires_grad_()
+    bn(xb).backward(dy)
+    torch.cuda.synchronize()
+    assert bn.weight.grad is None and bn.bias.grad is None and len(fired) == 2
+    assert rel(bn.weight.main_grad - 0.25, ref.weight.grad.float()) < 1e-2
+    assert rel(bn.bias.main_grad - 0.25, ref.bias.grad.float()) < 1e-2
+    assert torch.equal(xb.grad, xr.grad)
+
+
 def test_fused_batchnorm_large_mean_variance():
     """Shifted-data variance: a channel with mean 1000 and std 0.5 keeps its
     variance (no E[x^2] - E[x]^2 cancellation)."""

@@ -72,3 +72,27 @@ def test_fused_batchnorm_module_matches_batchnorm2d_on_cpu():
     ref.eval()
     fused.eval()
     assert torch.allclose(fused(x), ref(x).relu(), atol=1e-5)
+
+
+def test_flat_params_keep_channels_last_weights():
+    """A channels-last conv weight stays channels-last as a view of the flat
+    buffer (no per-forward layout copy), its main_grad has the same strides
+    (the channels-last gradient adds without a permute), and the layout
+    names the element order so a checkpoint of the other order is refused."""
+    import torch
+
+    from tf_operator_amd.parallel.flat import FlatParams
+
+    conv = torch.nn.Conv2d(3, 8, 3).to(memory_format=torch.channels_last)
+    lin = torch.nn.Linear(4, 5)
+    w0 = conv.weight.detach().clone()
+    f = FlatParams([conv.weight, conv.bias, lin.weight])
+    assert conv.weight.is_contiguous(memory_format=torch.channels_last) and not conv.weight.is_contiguous()
+    assert torch.equal(conv.weight, w0)
+    assert conv.weight.main_grad.stride() == conv.weight.stride()
+    assert conv.weight.data_ptr() == f.param.data_ptr()  # a view of the flat buffer
+    x = torch.randn(2, 3, 6, 6).to(memory_format=torch.channels_last)
+    conv(x).sum().backward()
+    conv.weight.main_grad.add_(conv.weight.grad)
+    assert torch.equal(conv.weight.main_grad, conv.weight.grad)
+    assert f.layout()[0][0].endswith("@nhwc") and not f.layout()[2][0].endswith("@nhwc")

@@ -105,15 +105,33 @@ class _BatchNormAct(torch.autograd.Function):
         dx2 = torch.empty_like(x2)
         dres2 = torch.empty_like(x2) if ctx.has_res else None
         pdt = _lib.dtype_code(weight) if weight is not None else 1
-        dg = torch.empty(C, device=x.device, dtype=weight.dtype) if weight is not None else None
-        db = torch.empty(C, device=x.device, dtype=bias.dtype) if bias is not None else None
+        # dgamma / dbeta straight into the flat gradient buffer (main_grad,
+        # accumulated by the finalize kernel) when the parameters are managed
+        # by FlatParams: no per-layer temporary, cast and add
+        mg = getattr(weight, "main_grad", None) if weight is not None else None
+        mb = getattr(bias, "main_grad", None) if bias is not None else None
+        into_flat = mg is not None and (bias is None or mb is not None) and mg.dtype in (torch.float32,
+                                                                                          torch.bfloat16)
+        if into_flat:
+            dg, db, gdt, acc = mg, mb, _lib.dtype_code(mg), 1
+            if db is not None and db.dtype != dg.dtype:
+                into_flat = False
+        if not into_flat:
+            dg = torch.empty(C, device=x.device, dtype=weight.dtype) if weight is not None else None
+            db = torch.empty(C, device=x.device, dtype=bias.dtype) if bias is not None else None
+            gdt = _lib.dtype_code(dg if dg is not None else (db if db is not None else x2))
+            acc = 0
         ws = _ws(R, C, x.device)
         _lib.call("toa_bn_bwd", _lib.dtype_code(x2), pdt, _lib.ptr(dy2), _lib.ptr(x2), _lib.ptr(y2), ctx.mask,
                   _lib.ptr(stats),
-                  _lib.ptr(weight), R, C, _lib.ptr(dx2), _lib.ptr(dres2), _lib.ptr(dg), _lib.ptr(db),
+                  _lib.ptr(weight), R, C, _lib.ptr(dx2), _lib.ptr(dres2), _lib.ptr(dg), _lib.ptr(db), gdt, acc,
                   _lib.ptr(ws), _lib.stream(x))
-        gw = deliver_weight_grad(weight, dg) if weight is not None else None
-        gb = deliver_weight_grad(bias, db) if bias is not None else None
+        if into_flat:
+            gw = deliver_weight_grad(weight, None)
+            gb = deliver_weight_grad(bias, None) if bias is not None else None
+        else:
+            gw = deliver_weight_grad(weight, dg) if weight is not None else None
+            gb = deliver_weight_grad(bias, db) if bias is not None else None
         dres = _like(dres2, x) if dres2 is not None else None
         return _like(dx2, x), dres, gw, gb, None, None, None, None, None, None
 

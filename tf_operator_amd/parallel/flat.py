@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import bisect
 import dataclasses
+import os
 
 import torch
 
@@ -73,6 +74,13 @@ class Segment:
     offset: int
     numel: int
     decay: bool
+    nhwc: bool = False  # a channels-last 4D weight: stored N,H,W,C in the flat buffer
+
+
+def _channels_last(p: torch.Tensor) -> bool:
+    if os.environ.get("TOA_FLAT_NHWC") == "0":  # A/B switch: NCHW views, as before
+        return False
+    return p.dim() == 4 and not p.is_contiguous() and p.is_contiguous(memory_format=torch.channels_last)
 
 
 class FlatParams:
@@ -96,17 +104,21 @@ class FlatParams:
         for p in uniq:
             n = p.numel()
             decay = not (no_decay(p) if no_decay else p.dim() == 1)
-            self.segments.append(Segment(names.get(id(p), f"p{len(self.segments)}"), p, off, n, decay))
+            self.segments.append(Segment(names.get(id(p), f"p{len(self.segments)}"), p, off, n, decay,
+                                         _channels_last(p)))
             off += _round_up(n)
         self.numel = max(off, ALIGN)
         gdt = grad_dtype or dtype
         self.param = torch.zeros(self.numel, device=dev, dtype=dtype)
         self.grad = torch.zeros(self.numel, device=dev, dtype=gdt)
         for s in self.segments:
-            view = self.param[s.offset:s.offset + s.numel].view_as(s.param)
+            # channels-last conv weights keep their memory format in the flat
+            # buffers: no per-forward layout copy of the weight, and the
+            # channels-last gradient adds into main_grad without a permute
+            view = self._view(self.param, s)
             view.copy_(s.param.data)
             s.param.data = view
-            s.param.main_grad = self.grad[s.offset:s.offset + s.numel].view_as(s.param)
+            s.param.main_grad = self._view(self.grad, s)
             s.param._toa_uses = seen[id(s.param)]
         self.master = None
         if master:
@@ -214,8 +226,18 @@ class FlatParams:
             "layout": self.layout(),
         }
 
+    @staticmethod
+    def _view(buf: torch.Tensor, s: Segment) -> torch.Tensor:
+        seg = buf[s.offset:s.offset + s.numel]
+        if s.nhwc:
+            n, c, h, w = s.param.shape
+            return seg.view(n, h, w, c).permute(0, 3, 1, 2)
+        return seg.view(s.param.shape)
+
     def layout(self):
-        return [(s.name, s.offset, s.numel) for s in self.segments]
+        # a channels-last segment's element order differs: name it, so a
+        # checkpoint of the other order is refused instead of permuted
+        return [(s.name + ("@nhwc" if s.nhwc else ""), s.offset, s.numel) for s in self.segments]
 
     def check_layout(self, layout):
         if [tuple(x) for x in layout] != self.layout():
