@@ -25,6 +25,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+from tf_operator_amd.bench.flagship import vram_used_bytes, wait_vram_drained, wait_vram_settled  # noqa: E402
 from tf_operator_amd.sdk import container, pod_template  # noqa: E402
 from tf_operator_amd.testing.cluster import LocalCluster  # noqa: E402
 
@@ -51,7 +52,7 @@ def make_job(name, a):
             "spec": {"runPolicy": {"cleanPodPolicy": "All"}, "tfReplicaSpecs": specs}}
 
 
-def one_run(c, i, a):
+def one_run(c, i, a, vram_base=None):
     name = f"lat-{i}"
     t0 = time.time()
     c.client.create(make_job(name, a))
@@ -67,9 +68,11 @@ def one_run(c, i, a):
     t_first = float(rep["first_step_time"])
     c.client.wait_for_job(name, polling_interval=0.2, timeout_seconds=a.timeout)
     c.client.delete(name)
-    c.wait(lambda: not c.pods(labels={"job-name": name}), 60, 0.05, "cleanup")
+    c.wait(lambda: not c.pods(labels={"job-name": name}) and not any(
+        k[1].startswith(name + "-") for k in c.kubelet.running), 60, 0.05, "cleanup")
+    drain = wait_vram_drained(vram_base)  # the next job starts on a drained node (bench/flagship.py)
     out = {"total": t_first - t0, "to_pods": t_pods - t0, "to_spawn": t_spawn - t0,
-           "spawn_to_first": t_first - t_spawn}
+           "spawn_to_first": t_first - t_spawn, "node_drain": drain}
     for k, v in (rep.get("phases") or {}).items():
         out["phase:" + k] = v
     return out
@@ -93,10 +96,11 @@ def main():
     runs = []
     with LocalCluster(gpus=node_gpus, grace_seconds=5.0, warm_python=a.warm) as c:
         if a.warm:
-            c.wait(lambda: c.kubelet._fs_ready is not None and c.kubelet._fs_ready.is_set(), 300,
-                   what="fork server ready")
+            c.wait(c.kubelet.warm_ready, 300, what="fork server ready")
+        wait_vram_settled()
+        base = vram_used_bytes()
         for i in range(a.repeats):
-            r = one_run(c, i, a)
+            r = one_run(c, i, a, base)
             runs.append(r)
             print(json.dumps({"run": i, **{k: round(v, 4) for k, v in r.items()}}), file=sys.stderr, flush=True)
     tot = sorted(r["total"] for r in runs)
