@@ -190,3 +190,43 @@ def test_sharded_optimizer_matches_replicated(tmp_path, world, bucket_mb):
     for a, b in ((p0, p1), (m0, m1)):
         assert float((a - b).abs().max()) <= 1e-2 * float(a.abs().max())
     assert float((v0 - v1).abs().max()) <= 1e-2 * float(v0.abs().max())
+
+
+def _bcast_worker(rank, world, port, same, out):
+    import torch.distributed as dist
+
+    from tf_operator_amd.parallel import ddp
+    from tf_operator_amd.parallel.flat import FlatParams
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(0 if same else rank)
+        ps = [torch.nn.Parameter(torch.randn(n, generator=g)) for n in (100, 7, 333)]
+        flat = FlatParams(ps)
+        calls = []
+        real = dist.broadcast
+        ddp.dist.broadcast = lambda *a, **k: (calls.append(1), real(*a, **k))[1]
+        try:
+            ddp.broadcast_params(flat)
+        finally:
+            ddp.dist.broadcast = real
+        gathered = [torch.empty_like(flat.param) for _ in range(world)]
+        dist.all_gather(gathered, flat.param)
+        if rank == 0:
+            torch.save({"calls": len(calls), "equal": all(torch.equal(x, gathered[0]) for x in gathered),
+                        "master_ok": torch.equal(flat.master, flat.param.float())}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_broadcast_params_only_when_weights_differ(tmp_path, same):
+    """Seeded init gives every rank the same weights: the 16 GB startup
+    broadcast is skipped after a checksum all-reduce; different weights are
+    still broadcast from rank 0."""
+    out = str(tmp_path / "b.pt")
+    mp.spawn(_bcast_worker, args=(2, _free_port(), same, out), nprocs=2, join=True)
+    r = torch.load(out, weights_only=True)
+    assert r["equal"] and r["master_ok"]
+    assert r["calls"] == (0 if same else 1)

@@ -168,9 +168,23 @@ def _is_nccl(group) -> bool:
 
 
 def broadcast_params(flat: FlatParams, src=0, group=None):
-    """Make every rank start from rank `src`'s weights (and master copy)."""
+    """Make every rank start from rank `src`'s weights (and master copy).
+
+    Seeded initialisation usually gives every rank the same weights already:
+    two fp64 checksums (plain and position-weighted) are compared across
+    ranks first, and the broadcast -- 16 GB at Llama-3-8B, part of every
+    job's submit -> first-step -- runs only when they differ."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
+    p = flat.param
+    w = torch.arange(1, p.numel() + 1, device=p.device, dtype=torch.float64) if p.numel() <= (1 << 24) else None
+    s1 = p.sum(dtype=torch.float64)
+    s2 = (p.double() * w).sum() if w is not None else (p[::97].double() * torch.arange(
+        1, p[::97].numel() + 1, device=p.device, dtype=torch.float64)).sum()
+    v = torch.stack([s1, s2, -s1, -s2])
+    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+    if bool(v[0] == -v[2]) and bool(v[1] == -v[3]):
+        return  # identical on every rank (max == min of both checksums)
     dist.broadcast(flat.param, src, group=group)
     flat.master_from_param()
     flat.params_changed()
