@@ -56,7 +56,7 @@ def test_rmsnorm_fwd_bwd(cols, res):
     assert rel(w.grad, wr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("cols", [4096, 512])
+@pytest.mark.parametrize("cols", [4096, 512, 1000, 8192])
 def test_layernorm_fwd_bwd(cols):
     _lib()
     from tf_operator_amd.ops.norm import layer_norm
