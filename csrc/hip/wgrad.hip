@@ -19,9 +19,14 @@
 //   wave:      128 x 64 of C = 8 x 4 v_mfma_f32_16x16x32_bf16 tiles
 //   operands:  swapped (B fragment first) so each lane's accumulator holds 4
 //              consecutive n of one row m -> 8-byte read-modify-write stores
-//   split-K:   `split` workgroups share a tile; partials go to an fp32
-//              workspace and wgrad_reduce_kernel adds them in a fixed order
-//              (deterministic, no float atomics)
+//   split-K:   only the tiles that would leave the last wave of 256 CUs
+//              part-empty are split: the first `full` tiles (whole waves)
+//              run over the whole K and store bf16 directly; the `rem` tail
+//              tiles are cut into `split` K-pieces that fill the last wave.
+//              Their fp32 partials go to a tile-major workspace and
+//              wgrad_tile_reduce_kernel adds them in a fixed order
+//              (deterministic, no float atomics).  Full tiles are launched
+//              first, so the pieces fill in behind them.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -91,10 +96,19 @@ __device__ __forceinline__ int wg_xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// tile index -> (tm, tn): group-M order (8 row tiles per group) for L2 reuse
+// of the B strips
+__device__ __forceinline__ void wg_tile_coords(int tile, int tiles_m, int tiles_n, int* tm, int* tn) {
+  const int per_group = 8 * tiles_n, group = tile / per_group, first_m = group * 8;
+  const int gsz = min(tiles_m - first_m, 8);
+  *tm = first_m + (tile - group * per_group) % gsz;
+  *tn = (tile - group * per_group) / gsz;
+}
+
 __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                           const bf16_t* __restrict__ B, int64_t ldb,
                                                           bf16_t* __restrict__ C, int64_t ldc, float* __restrict__ W,
-                                                          int M, int N, int K, int split, int beta) {
+                                                          int M, int N, int K, int full, int split, int beta) {
   // Four DISTINCT LDS objects, one per stage, and a loop unrolled by four so
   // every access names its buffer statically: hipcc's wait-count pass then
   // knows a ds_read of one stage cannot alias the LDS-DMA still filling
@@ -108,14 +122,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int tiles_m = M / WG_BM, tiles_n = N / WG_BN, tiles = tiles_m * tiles_n;
-  const int wgid = wg_xcd_remap(blockIdx.x, tiles * split);
-  const int s = wgid / tiles, tile = wgid - s * tiles;
-  // group-M order (8 row tiles per group) for L2 reuse of the B strips
-  const int per_group = 8 * tiles_n, group = tile / per_group, first_m = group * 8;
-  const int gsz = min(tiles_m - first_m, 8);
-  const int tm = first_m + (tile - group * per_group) % gsz;
-  const int tn = (tile - group * per_group) / gsz;
-  const int kc = K / split, k_begin = s * kc, np = kc / WG_BK;
+  const int rem = tiles - full;
+  // blocks [0, full): whole-K tiles; [full, full + rem * split): K-pieces of the tail tiles
+  const bool piece = (int)blockIdx.x >= full;
+  int tile, s = 0, j = 0;
+  if (!piece) {
+    tile = wg_xcd_remap(blockIdx.x, full);
+  } else {
+    const int w2 = wg_xcd_remap(blockIdx.x - full, rem * split);
+    s = w2 / rem;
+    j = w2 - s * rem;
+    tile = full + j;
+  }
+  int tm, tn;
+  wg_tile_coords(tile, tiles_m, tiles_n, &tm, &tn);
+  const int kc = piece ? K / split : K, k_begin = s * kc, np = kc / WG_BK;
 
   const bf16_t* Ab = A + (int64_t)k_begin * lda + (int64_t)tm * WG_BM;
   const bf16_t* Bb = B + (int64_t)k_begin * ldb + (int64_t)tn * WG_BN;
@@ -190,7 +211,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
   // epilogue: lane holds C[m][n .. n+3], m = row16 + (lane & 15), n = col16 + 4 (lane >> 4)
   const int mrow = tm * WG_BM + wm * 128 + (lane & 15);
   const int ncol = tn * WG_BN + wn * 64 + 4 * (lane >> 4);
-  if (split == 1) {
+  if (!piece) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -210,77 +231,107 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
         *(uint2*)p = w;
       }
   } else {
-    float* ws = W + (int64_t)s * M * N;
+    // tile-major fp32 partial: [split][rem][256][256]
+    float* ws = W + ((int64_t)s * rem + j) * (WG_BM * WG_BN);
+    const int lrow = wm * 128 + (lane & 15), lcol = wn * 64 + 4 * (lane >> 4);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *(f32x4*)(ws + (int64_t)(mrow + 16 * i) * N + ncol + 16 * j) = acc[i][j];
+      for (int jj = 0; jj < 4; ++jj) *(f32x4*)(ws + (lrow + 16 * i) * WG_BN + lcol + 16 * jj) = acc[i][jj];
   }
 }
 
-// C[m][n] = (beta ? C : 0) + sum_s W[s][m][n], summed in split order
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ W, bf16_t* __restrict__ C,
-                                                           int64_t ldc, int M, int N, int split, int beta) {
-  const int64_t n8 = (int64_t)M * N / 8;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = i * 8, m = e / N, n = e - m * N;
-    bf16_t* p = C + m * ldc + n;
+// Tail tile j of `rem`: C = (beta ? C : 0) + sum_s W[s][j], summed in split order.
+__global__ __launch_bounds__(256) void wgrad_tile_reduce_kernel(const float* __restrict__ W, bf16_t* __restrict__ C,
+                                                                int64_t ldc, int M, int N, int full, int rem,
+                                                                int split, int beta) {
+  const int j = blockIdx.x;
+  int tm, tn;
+  wg_tile_coords(full + j, M / WG_BM, N / WG_BN, &tm, &tn);
+  for (int e = threadIdx.x; e < WG_BM * WG_BN / 8; e += 256) {
+    const int row = e / (WG_BN / 8), col = (e % (WG_BN / 8)) * 8;
+    bf16_t* p = C + (int64_t)(tm * WG_BM + row) * ldc + tn * WG_BN + col;
     float acc[8];
     if (beta) {
       unpack8(ld16(p), acc);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+      for (int q = 0; q < 8; ++q) acc[q] = 0.f;
     }
     for (int s = 0; s < split; ++s) {
-      const f32x4* w = (const f32x4*)(W + (int64_t)s * M * N + e);
+      const f32x4* w = (const f32x4*)(W + ((int64_t)s * rem + j) * (WG_BM * WG_BN) + row * WG_BN + col);
       const f32x4 a = w[0], b = w[1];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[j] += a[j];
-        acc[4 + j] += b[j];
+      for (int q = 0; q < 4; ++q) {
+        acc[q] += a[q];
+        acc[4 + q] += b[q];
       }
     }
     st16(p, pack8(acc));
   }
 }
 
-// Workgroups per tile so the grid fills whole waves of the 256 CUs (one
-// workgroup per CU: 128 KiB LDS) -- K must stay a multiple of 128 * split.
-extern "C" int toa_wgrad_split(int M, int N, int K) {
+static bool wg_split_ok(int K, int s) { return K % (4 * WG_BK * s) == 0 && K / s >= 16 * WG_BK; }
+
+// The launch plan: `full` whole-K tiles (whole waves of the 256 CUs, one
+// workgroup per CU: 128 KiB LDS) and the tail tiles cut into `split` pieces
+// so the last wave is as full as possible.  No tail: split 1.
+static void wg_plan(int M, int N, int K, int* full, int* split) {
   const int tiles = (M / WG_BM) * (N / WG_BN);
+  const int rem = tiles % 256;
+  *full = tiles - rem;
+  *split = 1;
+  if (rem == 0) return;
   int best = 1;
-  double best_eff = 0.0;
-  for (int s = 1; s <= 4; ++s) {
-    if (K % (4 * WG_BK * s) != 0 || K / s < 16 * WG_BK) continue;
-    const int nwg = tiles * s;
-    const int waves = (nwg + 255) / 256;
-    const double eff = (double)nwg / (waves * 256.0);
-    if (eff > best_eff + 0.05) {
-      best_eff = eff;
-      best = s;
-    }
+  for (int s = 2; s <= 4; ++s)
+    if (rem * s <= 256 && wg_split_ok(K, s)) best = s;
+  if (best == 1) {  // nothing to split: the tail runs whole
+    *full = tiles;
+    return;
   }
-  return best;
+  *split = best;
 }
 
-// Bytes of fp32 workspace toa_wgrad needs for `split` > 1.
-extern "C" int64_t toa_wgrad_workspace(int M, int N, int split) {
-  return split > 1 ? (int64_t)split * M * N * 4 : 0;
+// Auto plan's split factor (1 = no split-K at all).
+extern "C" int toa_wgrad_split(int M, int N, int K) {
+  int full, split;
+  wg_plan(M, N, K, &full, &split);
+  return split;
+}
+
+// Bytes of fp32 workspace toa_wgrad needs: split == 0 = the auto plan, else
+// `split` K-pieces for every tile.
+extern "C" int64_t toa_wgrad_workspace(int M, int N, int K, int split) {
+  const int tiles = (M / WG_BM) * (N / WG_BN);
+  int full = 0;
+  if (split == 0) wg_plan(M, N, K, &full, &split);
+  else full = split == 1 ? tiles : 0;
+  return split > 1 ? (int64_t)split * (tiles - full) * WG_BM * WG_BN * 4 : 0;
 }
 
 // dW[M][N] (+)= dY[K][M]^T X[K][N].  M, N multiples of 256, K of 128 * split,
-// row strides multiples of 8 elements, 16-byte aligned bases.
+// row strides multiples of 8 elements, 16-byte aligned bases.  split == 0:
+// the auto plan (whole-K waves + a split tail); split >= 1: every tile cut
+// into `split` K-pieces (1 = none).
 extern "C" int toa_wgrad(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc,
                          float* W, int M, int N, int K, int split, int beta, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % WG_BM || N % WG_BN || split < 1 || K % (4 * WG_BK * split) ||
-      (lda | ldb | ldc) % 8 || (split > 1 && W == nullptr))
+  if (M <= 0 || N <= 0 || K <= 0 || M % WG_BM || N % WG_BN || split < 0 || (lda | ldb | ldc) % 8)
     return (int)hipErrorInvalidValue;
-  const int nwg = (M / WG_BM) * (N / WG_BN) * split;
-  hipLaunchKernelGGL(wgrad_nt_kernel, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K,
+  const int tiles = (M / WG_BM) * (N / WG_BN);
+  int full;
+  if (split == 0) {
+    wg_plan(M, N, K, &full, &split);
+  } else {
+    full = split == 1 ? tiles : 0;
+  }
+  if (K % (4 * WG_BK * split) || (split > 1 && W == nullptr) || (split == 1 && full != tiles))
+    return (int)hipErrorInvalidValue;
+  const int rem = tiles - full;
+  const int nwg = full + (split > 1 ? rem * split : 0);
+  hipLaunchKernelGGL(wgrad_nt_kernel, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
                      split, beta);
-  if (split > 1)
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(toa_stream_grid((int64_t)M * N / 8, 256)), dim3(256), 0, stream, W,
-                       C, ldc, M, N, split, beta);
+  if (split > 1 && rem > 0)
+    hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split,
+                       beta);
   return (int)hipGetLastError();
 }

@@ -235,6 +235,31 @@ def test_wgrad_nt_kernel(N, K, T, beta, split):
     assert err < 1e-2, float(err)
 
 
+@pytest.mark.parametrize("N,K,T,beta,want_split", [(4352, 4096, 4096, 1, 4), (5376, 4096, 3072, 0, 3),
+                                                   (1024, 1024, 2048, 1, 4), (4096, 4096, 2048, 1, 1)])
+def test_wgrad_nt_auto_plan(N, K, T, beta, want_split):
+    """Auto plan (split=None): whole-K tiles for the full waves of 256 CUs,
+    only the tail tiles cut into K-pieces reduced from a tile-major
+    workspace; bit-identical to a uniform-split run's math within bf16."""
+    _lib()
+    from tf_operator_amd.ops import _lib as L
+    from tf_operator_amd.ops import gemm
+
+    assert L.call_ret("toa_wgrad_split", N, K, T) == want_split
+    torch.manual_seed(N + K + T)
+    dy = (torch.rand(T, N, device=DEV) * 2 - 1).to(torch.bfloat16)
+    x = (torch.rand(T, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    g0 = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float() + (g0.float() if beta else 0)
+    g = g0.clone()
+    gemm.wgrad_hip_(g, dy, x, beta=float(beta))
+    err = (g.float() - ref).abs().max() / ref.abs().max()
+    assert err < 1e-2, float(err)
+    g2 = g0.clone()
+    gemm.wgrad_hip_(g2, dy, x, beta=float(beta))
+    assert torch.equal(g, g2)  # deterministic
+
+
 def test_wgrad_routing_matches_hipblaslt():
     """accumulate_mm sends a Linear weight gradient through the HIP kernel;
     the result matches hipBLASLt's addmm_ to bf16 rounding."""

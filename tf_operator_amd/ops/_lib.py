@@ -102,6 +102,9 @@ def _load():
         ws = getattr(lib, "toa_bn_ws_floats", None)
         if ws is not None:
             ws.argtypes, ws.restype = [c_i64, c_int], c_i64
+        ww = getattr(lib, "toa_wgrad_workspace", None)
+        if ww is not None:
+            ww.argtypes, ww.restype = [c_int, c_int, c_int, c_int], c_i64
         _lib = lib
 
 

@@ -127,13 +127,15 @@ def wgrad_hip_ok(g, dy2, x2) -> bool:
 
 
 def wgrad_hip_(g, dy2, x2, beta=1.0, split=None):
-    """g[N,K] (+)= dy2[T,N]^T x2[T,K] on the hand-written MFMA kernel."""
+    """g[N,K] (+)= dy2[T,N]^T x2[T,K] on the hand-written MFMA kernel.
+    split=None: the kernel's auto plan (whole-K waves, only the tail tiles
+    cut into K-pieces); an int: every tile cut into `split` pieces."""
     _lib.use_hip(dy2)
     T, N = dy2.shape
     K = x2.shape[1]
-    if split is None:
-        split = _lib.call_ret("toa_wgrad_split", N, K, T)
-    ws = _workspace(dy2.device, split * N * K * 4) if split > 1 else None
+    split = 0 if split is None else int(split)
+    nbytes = int(_lib.call_ret("toa_wgrad_workspace", N, K, T, split))
+    ws = _workspace(dy2.device, nbytes) if nbytes > 0 else None
     _lib.call("toa_wgrad", _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(g), K, _lib.ptr(ws),
               N, K, T, int(split), int(beta != 0.0), _lib.stream(dy2))
     return g
