@@ -1,6 +1,7 @@
 """Trainer plumbing on the CPU: transposed weight copies (ops/wt.py) stay in
 sync with the weights through optimizer steps, checkpoint loads and the
 rank-0 broadcast, and the data gradient they feed equals dY W."""
+import pytest
 import torch
 
 from tf_operator_amd.models.llama import PRESETS
@@ -96,3 +97,29 @@ def test_flat_params_keep_channels_last_weights():
     conv.weight.main_grad.add_(conv.weight.grad)
     assert torch.equal(conv.weight.main_grad, conv.weight.grad)
     assert f.layout()[0][0].endswith("@nhwc") and not f.layout()[2][0].endswith("@nhwc")
+
+
+@pytest.mark.parametrize("tie", [False, True])
+def test_fresh_gradients_match_zeroed_buffer(monkeypatch, tie):
+    """TOA_FRESH_GRADS (default): no zeroing pass, each parameter's first
+    gradient producer of a step overwrites its flat slice.  Bit-identical to
+    zeroing the buffer, with gradient accumulation (later micro-batches add)
+    and with tied embeddings (lm_head writes first, the embedding scatter adds)."""
+    import torch
+
+    from tf_operator_amd.models.llama import LlamaConfig
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    cfg = LlamaConfig(vocab_size=256, hidden=128, layers=2, heads=4, kv_heads=2, ffn=256, max_seq=64,
+                      tie_embeddings=tie)
+    res = {}
+    for fresh in ("1", "0"):
+        monkeypatch.setenv("TOA_FRESH_GRADS", fresh)
+        torch.manual_seed(0)
+        tr = LlamaTrainer(cfg, torch.device("cpu"), micro_batch=2, seq_len=32, grad_accum=2, lr=1e-3)
+        assert tr.fresh_grads == (fresh == "1") and tr.opt.fuse_zero_grad == (fresh == "0")
+        batches = [tr.synthetic_batch(seed=s) for s in (1, 2)]
+        losses = [float(tr.step(batches)) for _ in range(3)]
+        res[fresh] = (losses, tr.flat.param.clone(), tr.flat.master.clone())
+    assert res["1"][0] == res["0"][0]
+    assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])

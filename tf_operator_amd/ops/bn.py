@@ -25,7 +25,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from .grad import deliver_weight_grad
+from .grad import deliver_weight_grad, take_fresh
 
 
 _MODE = os.environ.get("TOA_BN", "hip")
@@ -116,6 +116,15 @@ class _BatchNormAct(torch.autograd.Function):
             dg, db, gdt, acc = mg, mb, _lib.dtype_code(mg), 1
             if db is not None and db.dtype != dg.dtype:
                 into_flat = False
+            else:  # the step's first producer overwrites (grad.take_fresh)
+                fw = take_fresh(weight)
+                fb = take_fresh(bias) if bias is not None else fw
+                if fw and fb:
+                    acc = 0
+                else:
+                    for p_, f_ in ((weight, fw), (bias, fb if bias is not None else False)):
+                        if f_:
+                            p_.main_grad.zero_()
         if not into_flat:
             dg = torch.empty(C, device=x.device, dtype=weight.dtype) if weight is not None else None
             db = torch.empty(C, device=x.device, dtype=bias.dtype) if bias is not None else None

@@ -5,7 +5,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
-from .grad import deliver_weight_grad
+from .grad import deliver_weight_grad, take_fresh
 
 
 def _scatter_rows(grad, idx, dy2):
@@ -38,6 +38,8 @@ class _EmbeddingFn(torch.autograd.Function):
         idx = tokens.reshape(-1)
         mg = getattr(weight, "main_grad", None)
         if mg is not None:
+            if take_fresh(weight):  # a scatter-add needs zeros under it
+                mg.zero_()
             _scatter_rows(mg, idx, dy2)
             return None, deliver_weight_grad(weight, None)
         g = torch.zeros(ctx.wshape, device=dy.device, dtype=torch.float32)

@@ -13,6 +13,17 @@ from __future__ import annotations
 import torch
 
 
+def take_fresh(param) -> bool:
+    """True (once per step) when param.main_grad still holds the previous
+    step's data (FlatParams.mark_fresh): its first gradient producer then
+    overwrites instead of accumulating.  Producers whose kernel accumulates
+    call this BEFORE launching it, to pick beta = 0 / accumulate = 0."""
+    if param is not None and getattr(param, "_toa_fresh", False):
+        param._toa_fresh = False
+        return True
+    return False
+
+
 def deliver_weight_grad(param: torch.Tensor, grad: torch.Tensor | None):
     """Accumulate `grad` into param.main_grad if present (then return None),
     else return it (cast to the param dtype) for autograd.
@@ -23,7 +34,10 @@ def deliver_weight_grad(param: torch.Tensor, grad: torch.Tensor | None):
     if mg is None:
         return None if grad is None else grad.to(param.dtype).view_as(param)
     if grad is not None:
-        mg.add_(grad.view_as(mg).to(mg.dtype))
+        if take_fresh(param):
+            mg.copy_(grad.view_as(mg))
+        else:
+            mg.add_(grad.view_as(mg).to(mg.dtype))
     hook = getattr(param, "_toa_ready", None)
     if hook is not None:
         hook(param)
@@ -31,16 +45,20 @@ def deliver_weight_grad(param: torch.Tensor, grad: torch.Tensor | None):
 
 
 def accumulate_mm(param: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
-    """param.main_grad += a @ b  (hipBLASLt GEMM with beta=1, no temporary);
+    """param.main_grad += a @ b  (beta = 1, no temporary; = a @ b for the
+    step's first producer, see take_fresh);
     falls back to returning a @ b when the param has no main_grad."""
     mg = getattr(param, "main_grad", None)
     if mg is None:
         return torch.mm(a, b).to(param.dtype).view_as(param)
     mg2 = mg.view(a.shape[0], b.shape[1])
+    fresh = take_fresh(param)
     if a.dim() == 2 and a.stride(0) == 1 and a.t().is_contiguous():
         from . import gemm  # a = dy^T view: the tuned wgrad form
 
-        gemm.wgrad_acc_(mg2, a.t(), b)
+        gemm.wgrad_acc_(mg2, a.t(), b, beta=0.0 if fresh else 1.0)
+    elif fresh:
+        mg2.copy_(torch.mm(a, b))
     elif mg2.dtype == a.dtype:
         mg2.addmm_(a, b)
     else:

@@ -13,7 +13,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .grad import deliver_weight_grad
+from .grad import deliver_weight_grad, take_fresh
 
 
 def _ref_norm(h, w, b, eps, rms):
@@ -108,6 +108,15 @@ class _NormFn(torch.autograd.Function):
             s = _lib.stream(dy2)
             dt = _lib.dtype_code(dy2)
             acc = 1 if w_main is not None else 0
+            if acc:  # the step's first producer overwrites (grad.take_fresh)
+                fw = take_fresh(weight)
+                fb = take_fresh(bias) if b_main is not None else fw
+                if fw and fb:
+                    acc = 0
+                else:
+                    for p_, f_ in ((weight, fw), (bias, fb if b_main is not None else False)):
+                        if f_:
+                            p_.main_grad.zero_()
             if rms:
                 _lib.call("toa_rmsnorm_bwd", dt, _lib.ptr(dy2), _lib.ptr(h), _lib.ptr(weight), _lib.ptr(rstd),
                           _lib.ptr(dh2), _lib.ptr(dx), _lib.ptr(partial), _lib.ptr(dw_t),

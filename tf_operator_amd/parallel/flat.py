@@ -213,6 +213,22 @@ class FlatParams:
     def zero_grad(self):
         self.grad.zero_()
 
+    def mark_fresh(self):
+        """Start a step WITHOUT zeroing the gradient buffer: every parameter's
+        first gradient producer of the step overwrites its main_grad slice
+        instead of accumulating (ops/grad.py take_fresh).  Saves the 2 B /
+        parameter zeroing pass (16 GB at Llama-3-8B)."""
+        for s in self.segments:
+            s.param._toa_fresh = True
+
+    def zero_stale(self):
+        """After backward: zero the main_grad of parameters no producer wrote
+        since mark_fresh() (unused parameters), so they hold no stale data."""
+        for s in self.segments:
+            if getattr(s.param, "_toa_fresh", False):
+                s.param.main_grad.zero_()
+                s.param._toa_fresh = False
+
     def state_dict(self):
         """This rank's fp32 state (compact) and where it belongs in the flat
         buffer.  World-size independent when combined with the other ranks'

@@ -53,6 +53,9 @@ class LlamaTrainer:
         broadcast_params(self.flat)
         if shard_optimizer is None:
             shard_optimizer = os.environ.get("TOA_ZERO", "0") == "1"
+        # fresh gradients: no zeroing pass, each parameter's first producer of
+        # a step overwrites its slice (FlatParams.mark_fresh, ops.grad.take_fresh)
+        self.fresh_grads = os.environ.get("TOA_FRESH_GRADS", "1") != "0"
         # force_collectives: run the bucketed collectives even at world 1 (the
         # RCCL world-1 test drives the real reduce-scatter / all-gather path)
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20),
@@ -68,7 +71,8 @@ class LlamaTrainer:
             if overlap_optimizer is None:
                 overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
             self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
-                                 fuse_zero_grad=True, post_update=self.wt.refresh if self.wt else None)
+                                 fuse_zero_grad=not self.fresh_grads,
+                                 post_update=self.wt.refresh if self.wt else None)
         if self.opt.overlap or self.gather is not None:
             self._hooks = self._install_param_waits()
         self.step_idx = 0
@@ -113,7 +117,9 @@ class LlamaTrainer:
 
     def step(self, batches):
         """batches: list (len grad_accum) of (tokens, targets)."""
-        if not self.opt.grads_zeroed:
+        if self.fresh_grads and not self.opt.overlap:
+            self.flat.mark_fresh()
+        elif not self.opt.grads_zeroed:
             self.flat.zero_grad()
         loss_sum = None
         for i, (tok, tgt) in enumerate(batches):
@@ -124,6 +130,8 @@ class LlamaTrainer:
             self.bucketer.armed = i == len(batches) - 1  # reduce once, after the last micro-batch
             (loss / len(batches)).backward()
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
+        if self.fresh_grads and not self.opt.overlap:
+            self.flat.zero_stale()  # parameters no producer wrote this step
         self.bucketer.armed = True
         self.bucketer.finish()
         self.opt.step(grad_scale=self.bucketer.grad_scale)

@@ -9,6 +9,7 @@ import time
 
 import torch
 
+from ..ops.grad import take_fresh
 from ..ops.optim import FlatAdamW, FlatSGD
 from ..parallel.ddp import GradBucketer, broadcast_params
 from ..parallel.flat import FlatParams
@@ -25,7 +26,10 @@ def attach_autograd_hooks(flat: FlatParams):
         def hook(param):
             if param.grad is None:
                 return
-            param.main_grad.add_(param.grad.view_as(param.main_grad))  # mixed-dtype add: one kernel, no cast copy
+            if take_fresh(param):
+                param.main_grad.copy_(param.grad.view_as(param.main_grad))
+            else:
+                param.main_grad.add_(param.grad.view_as(param.main_grad))
             param.grad = None
             h = getattr(param, "_toa_ready", None)
             if h is not None:
