@@ -1,0 +1,38 @@
+"""Counter subject for the GEMM comparison: the hand-written NT
+weight-gradient kernel and hipBLASLt's TN form (the forward's
+x W^T) at the Llama-3-8B gate|up shape, 5 calls each after a warm-up.
+
+    rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES ... -- python3 scripts/probes/gemm_pmc.py
+    python scripts/pmc_summary.py <out> wgrad_nt_kernel Cijk
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from tf_operator_amd.ops import gemm  # noqa: E402
+
+
+def main():
+    T, N, K = 24576, 28672, 4096
+    torch.manual_seed(0)
+    dy = (torch.rand(T, N, device="cuda") - 0.5).to(torch.bfloat16)
+    x = (torch.rand(T, K, device="cuda") - 0.5).to(torch.bfloat16)
+    g = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+    w = (torch.rand(N, K, device="cuda") - 0.5).to(torch.bfloat16)
+    assert gemm.wgrad_hip_ok(g, dy, x)
+    for _ in range(2):
+        gemm.wgrad_hip_(g, dy, x, beta=0.0)
+        torch.matmul(x, w.t())
+    torch.cuda.synchronize()
+    for _ in range(5):
+        gemm.wgrad_hip_(g, dy, x, beta=0.0)
+    for _ in range(5):
+        torch.matmul(x, w.t())
+    torch.cuda.synchronize()
+    print("ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()
