@@ -260,6 +260,37 @@ def test_wgrad_nt_auto_plan(N, K, T, beta, want_split):
     assert torch.equal(g, g2)  # deterministic
 
 
+@pytest.mark.parametrize("N,K,T,beta,split", [(256, 256, 1024, 0, 1), (512, 768, 2048, 1, 1),
+                                              (4352, 4096, 4096, 1, None), (5376, 4096, 3072, 0, None),
+                                              (1024, 1024, 2048, 1, 2), (28672, 4096, 1024, 0, None)])
+def test_wgrad_nt4_variant(N, K, T, beta, split):
+    """The 4-wave (one wave per SIMD, 32x32x16 MFMA) weight-gradient kernel
+    against an fp32 reference, incl. the split-K tail pieces and a strided
+    dy view."""
+    _lib()
+    from tf_operator_amd.ops import _lib as L
+    from tf_operator_amd.ops import gemm
+
+    torch.manual_seed(N + K + T + 4)
+    big = (torch.rand(T, N + 256, device=DEV) * 2 - 1).to(torch.bfloat16)
+    dy = big[:, 128:128 + N]
+    x = (torch.rand(T, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    g0 = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float() + (g0.float() if beta else 0)
+    assert L.call_ret("toa_wgrad_set_variant", 4) == 0
+    try:
+        g = g0.clone()
+        gemm.wgrad_hip_(g, dy, x, beta=float(beta), split=split)
+        g2 = g0.clone()
+        gemm.wgrad_hip_(g2, dy, x, beta=float(beta), split=split)
+        torch.cuda.synchronize()
+    finally:
+        L.call_ret("toa_wgrad_set_variant", 8)
+    err = (g.float() - ref).abs().max() / ref.abs().max()
+    assert err < 1e-2, float(err)
+    assert torch.equal(g, g2)  # deterministic
+
+
 def test_wgrad_routing_matches_hipblaslt():
     """accumulate_mm sends a Linear weight gradient through the HIP kernel;
     the result matches hipBLASLt's addmm_ to bf16 rounding."""
