@@ -10,6 +10,8 @@
 // (`dist_mnist.py:192` clip+log+mul+reduce_sum cross entropy).
 #include "toa_common.h"
 
+#include <algorithm>
+
 // ---------------------------------------------------------------------------
 // RoPE.  qkv: [T = B*S, (Hq + 2*Hkv) * D] (output of the fused QKV GEMM).
 // Writes q: [B, Hq, S, D], k / v: [B, Hkv*rep, S, D] (rep = kv replication
@@ -195,17 +197,74 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
   }
 }
 
+// Row-structured forms: workgroup per row (grid-strided over rows), threads
+// over the row's 16-B chunks -- no 64-bit divide per chunk -- with
+// non-temporal loads/stores (every byte is touched once; the 1-3 GB streams
+// are far beyond the Infinity Cache).  Selected by toa_set_stream_variant
+// bit 1 (in-process A/B, scripts/stream_ab.py).
+__global__ __launch_bounds__(256) void swiglu_fwd_rows_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ out,
+                                                              int64_t T, int F) {
+  const int fc = F / 8;
+  for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
+    const u32x4* row = (const u32x4*)(gu + t * 2 * F);
+    u32x4* orow = (u32x4*)(out + t * F);
+    for (int c = threadIdx.x; c < fc; c += blockDim.x) {
+      float g[8], up[8], o[8];
+      unpack8(__builtin_nontemporal_load(row + c), g);
+      unpack8(__builtin_nontemporal_load(row + fc + c), up);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * up[j];
+      __builtin_nontemporal_store(pack8(o), orow + c);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_rows_kernel(const bf16_t* __restrict__ dout,
+                                                              const bf16_t* __restrict__ gu, bf16_t* __restrict__ dgu,
+                                                              int64_t T, int F) {
+  const int fc = F / 8;
+  for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
+    const u32x4* row = (const u32x4*)(gu + t * 2 * F);
+    const u32x4* drow = (const u32x4*)(dout + t * F);
+    u32x4* orow = (u32x4*)(dgu + t * 2 * F);
+    for (int c = threadIdx.x; c < fc; c += blockDim.x) {
+      float g[8], up[8], d[8], dg[8], du[8];
+      unpack8(__builtin_nontemporal_load(row + c), g);
+      unpack8(__builtin_nontemporal_load(row + fc + c), up);
+      unpack8(__builtin_nontemporal_load(drow + c), d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float sg = 1.f / (1.f + __expf(-g[j]));
+        const float silu = g[j] * sg;
+        du[j] = d[j] * silu;
+        dg[j] = d[j] * up[j] * sg * (1.f + g[j] * (1.f - sg));
+      }
+      __builtin_nontemporal_store(pack8(dg), orow + c);
+      __builtin_nontemporal_store(pack8(du), orow + fc + c);
+    }
+  }
+}
+
+static inline int rows_grid(int64_t T) { return (int)std::min<int64_t>(std::max<int64_t>(T, 1), 4096); }
+
 extern "C" int toa_swiglu_fwd(const bf16_t* gu, bf16_t* out, int64_t T, int F, hipStream_t stream) {
   if (F % 8 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(toa_stream_grid(T * (F / 8), 256)), dim3(256), 0, stream, gu, out, T, F);
+  if (toa_stream_variant() & 2)
+    hipLaunchKernelGGL(swiglu_fwd_rows_kernel, dim3(rows_grid(T)), dim3(256), 0, stream, gu, out, T, F);
+  else
+    hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(toa_stream_grid(T * (F / 8), 256)), dim3(256), 0, stream, gu, out, T,
+                       F);
   return (int)hipGetLastError();
 }
 
 extern "C" int toa_swiglu_bwd(const bf16_t* dout, const bf16_t* gu, bf16_t* dgu, int64_t T, int F,
                               hipStream_t stream) {
   if (F % 8 != 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(toa_stream_grid(T * (F / 8), 256)), dim3(256), 0, stream, dout, gu, dgu,
-                     T, F);
+  if (toa_stream_variant() & 2)
+    hipLaunchKernelGGL(swiglu_bwd_rows_kernel, dim3(rows_grid(T)), dim3(256), 0, stream, dout, gu, dgu, T, F);
+  else
+    hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(toa_stream_grid(T * (F / 8), 256)), dim3(256), 0, stream, dout, gu,
+                       dgu, T, F);
   return (int)hipGetLastError();
 }
 

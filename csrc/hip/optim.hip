@@ -13,6 +13,8 @@
 // dist_mnist.py:194,208 ; multi_worker_strategy-with-keras.py:56) -- SURVEY K5.
 #include "toa_common.h"
 
+#include <algorithm>
+
 // ---------------------------------------------------------------------------
 // sum of squares of a bf16 (or fp32) vector, two-pass deterministic reduction
 // ---------------------------------------------------------------------------
@@ -76,7 +78,23 @@ extern "C" int toa_sumsq(const void* x, int64_t n, int is_bf16, float* workspace
 // grad may be bf16 or fp32.  n must be a multiple of 8 (flat buffers are
 // padded to 64 elements by the Python side).
 // ---------------------------------------------------------------------------
-template <bool GRAD_BF16>
+// Every stream is touched exactly once per step (28 B / parameter, far
+// beyond the 256 MB Infinity Cache at Llama-3-8B), so NT = 1 issues the
+// loads and stores non-temporal: nothing of the optimizer sweep is kept in
+// L2 / MALL that the next step's GEMMs would have to evict.
+template <typename T>
+__device__ __forceinline__ T ld_s(const T* p, bool nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename T>
+__device__ __forceinline__ void st_s(T* p, T v, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+template <bool GRAD_BF16, bool NT>
 __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ master, bf16_t* __restrict__ param,
                                                          void* __restrict__ grad, int zero_grad, float* __restrict__ m,
                                                          float* __restrict__ v, int64_t n8, float lr, float b1,
@@ -100,10 +118,10 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
        i += (int64_t)gridDim.x * blockDim.x) {
     float g[8], p[8], mm[8], vv[8];
     if (GRAD_BF16) {
-      unpack8(ld16((const bf16_t*)grad + i * 8), g);
+      unpack8(ld_s((const u32x4*)grad + i, NT), g);
       if (zero_grad) st16((bf16_t*)grad + i * 8, u32x4{0, 0, 0, 0});
     } else {
-      f32x4 a = *((const f32x4*)grad + 2 * i), b = *((const f32x4*)grad + 2 * i + 1);
+      f32x4 a = ld_s((const f32x4*)grad + 2 * i, NT), b = ld_s((const f32x4*)grad + 2 * i + 1, NT);
       g[0] = a[0]; g[1] = a[1]; g[2] = a[2]; g[3] = a[3];
       g[4] = b[0]; g[5] = b[1]; g[6] = b[2]; g[7] = b[3];
       if (zero_grad) {
@@ -114,7 +132,8 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
     f32x4* pm = (f32x4*)master + 2 * i;
     f32x4* mv = (f32x4*)m + 2 * i;
     f32x4* vvp = (f32x4*)v + 2 * i;
-    f32x4 p0 = pm[0], p1 = pm[1], m0 = mv[0], m1 = mv[1], v0 = vvp[0], v1 = vvp[1];
+    f32x4 p0 = ld_s(pm, NT), p1 = ld_s(pm + 1, NT), m0 = ld_s(mv, NT), m1 = ld_s(mv + 1, NT),
+          v0 = ld_s(vvp, NT), v1 = ld_s(vvp + 1, NT);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       p[j] = p0[j]; p[j + 4] = p1[j];
@@ -135,9 +154,25 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
       m0[j] = mm[j]; m1[j] = mm[j + 4];
       v0[j] = vv[j]; v1[j] = vv[j + 4];
     }
-    pm[0] = p0; pm[1] = p1; mv[0] = m0; mv[1] = m1; vvp[0] = v0; vvp[1] = v1;
-    if (param != nullptr) st16(param + i * 8, pack8(p));
+    st_s(pm, p0, NT); st_s(pm + 1, p1, NT);
+    st_s(mv, m0, NT); st_s(mv + 1, m1, NT);
+    st_s(vvp, v0, NT); st_s(vvp + 1, v1, NT);
+    if (param != nullptr) st_s((u32x4*)param + i, pack8(p), NT);
   }
+}
+
+// Variant switch for in-process A/B (scripts/stream_ab.py): bit 0 = the
+// non-temporal AdamW, bit 1 = the row-structured non-temporal SwiGLU,
+// bits 8.. = AdamW grid cap / 1024 (0: toa_stream_grid's 2048).  Default
+// from the A/B on MI355X (profiles/r2_stream_ab/): AdamW NT with a 16K-block
+// grid 5.43 -> 5.52 TB/s, SwiGLU rows+NT fwd 0.404 -> 0.373 ms and bwd
+// 0.723 -> 0.653 ms at T = 24576, F = 14336; all arms bit-identical.
+static int g_stream_variant = 1 | 2 | (16 << 8);
+int toa_stream_variant() { return g_stream_variant; }
+extern "C" int toa_set_stream_variant(int v) {
+  const int old = g_stream_variant;
+  g_stream_variant = v;
+  return old;
 }
 
 // grad_flags: bit 0 = grad is bf16 (else fp32); bit 1 = zero the gradient
@@ -151,15 +186,14 @@ static int adamw_launch(float* master, bf16_t* param, void* grad, int grad_flags
   const float bc2 = 1.f - powf(beta2, (float)step);
   const float inv_bc1 = 1.f / bc1, inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   int grid = toa_stream_grid(n8, 256);
+  const int cap = (g_stream_variant >> 8) * 1024;
+  if (cap > 0) grid = (int)std::min<int64_t>(std::max<int64_t>((n8 + 255) / 256, 1), cap);
   const int zero_grad = (grad_flags >> 1) & 1;
-  if (grad_flags & 1)
-    hipLaunchKernelGGL(adamw_flat_kernel<true>, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8,
-                       lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
-                       max_norm, step_dev);
-  else
-    hipLaunchKernelGGL(adamw_flat_kernel<false>, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8,
-                       lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq,
-                       max_norm, step_dev);
+  const bool nt = g_stream_variant & 1;
+  auto k = (grad_flags & 1) ? (nt ? adamw_flat_kernel<true, true> : adamw_flat_kernel<true, false>)
+                            : (nt ? adamw_flat_kernel<false, true> : adamw_flat_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8, lr, beta1, beta2,
+                     eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq, max_norm, step_dev);
   return (int)hipGetLastError();
 }
 

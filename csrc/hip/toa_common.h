@@ -99,6 +99,10 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 
 // Grid size for memory-bound grid-stride kernels: cap at 256 CUs x 8 blocks
 // (CDNA guide G11).
+// Kernel-variant switch for in-process A/B of the streaming kernels
+// (defined in optim.hip, set by toa_set_stream_variant).
+int toa_stream_variant();
+
 static inline int toa_stream_grid(int64_t work_items, int block) {
   int64_t g = (work_items + block - 1) / block;
   if (g > 2048) g = 2048;

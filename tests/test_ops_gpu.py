@@ -98,20 +98,29 @@ def test_rope_qkv_roundtrip():
         assert rel(g.cpu(), gr) < 1e-2
 
 
-def test_swiglu():
-    _lib()
+@pytest.mark.parametrize("F", [1024, 1000, 14336])
+def test_swiglu(F):
+    L = _lib()
     from tf_operator_amd.ops import llm
 
     torch.manual_seed(3)
-    gu = torch.randn(333, 2 * 1024, device=DEV, dtype=torch.bfloat16)
+    gu = torch.randn(333, 2 * F, device=DEV, dtype=torch.bfloat16)
     out = llm.swiglu(gu)
-    ref = torch.nn.functional.silu(gu[:, :1024].float()) * gu[:, 1024:].float()
+    ref = torch.nn.functional.silu(gu[:, :F].float()) * gu[:, F:].float()
     assert rel(out, ref) < 1e-2
-    d = torch.randn(333, 1024, device=DEV, dtype=torch.bfloat16)
+    d = torch.randn(333, F, device=DEV, dtype=torch.bfloat16)
     dgu = llm.swiglu_bwd(d, gu)
     g = gu.float().requires_grad_()
-    (torch.nn.functional.silu(g[:, :1024]) * g[:, 1024:]).backward(d.float())
+    (torch.nn.functional.silu(g[:, :F]) * g[:, F:]).backward(d.float())
     assert rel(dgu, g.grad) < 1e-2
+    # the default row-structured non-temporal kernels are bit-identical to the flat ones
+    old = L.lib().toa_set_stream_variant(0)
+    try:
+        assert torch.equal(llm.swiglu(gu), out)
+        assert torch.equal(llm.swiglu_bwd(d, gu), dgu)
+    finally:
+        L.lib().toa_set_stream_variant(old)
+    assert old & 2, "row-structured SwiGLU is the default"
 
 
 @pytest.mark.parametrize("V", [128256, 1000, 10])
