@@ -12,11 +12,15 @@ rate.  Outputs of every arm are checked bit-identical to arm 0.
 from __future__ import annotations
 
 import argparse
+import os
 import statistics
+import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from tf_operator_amd.ops import _lib
+import torch  # noqa: E402
+
+from tf_operator_amd.ops import _lib  # noqa: E402
 
 
 def timed(fn, reps_out, stream):
