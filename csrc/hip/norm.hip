@@ -128,6 +128,9 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const T* __restrict__ x, 
 #ifndef NORM_KEEP_BELOW
 #define NORM_KEEP_BELOW 8
 #endif
+#ifndef NORM_NT_SINGLE
+#define NORM_NT_SINGLE 1
+#endif
 #ifndef NORM_BWD_WG_PER_CU
 #define NORM_BWD_WG_PER_CU 3
 #endif
@@ -203,11 +206,19 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const T* __restrict__ dy,
         }
         if (dadd != nullptr) {
           float a[8];
-          Vec8<T>::load(dadd + (int64_t)row * cols + ch * 8, a);
+          if (NORM_NT_SINGLE && sizeof(T) == 2)
+            unpack8(__builtin_nontemporal_load((const u32x4*)(dadd + (int64_t)row * cols + ch * 8)), a);
+          else
+            Vec8<T>::load(dadd + (int64_t)row * cols + ch * 8, a);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += a[j];
         }
-        Vec8<T>::store(dx + (int64_t)row * cols + ch * 8, o);
+        // single-use streams (dadd, dx) non-temporal: they leave the L2 to
+        // the h / dy rows the second pass re-reads
+        if (NORM_NT_SINGLE && sizeof(T) == 2)
+          __builtin_nontemporal_store(pack8(o), (u32x4*)(dx + (int64_t)row * cols + ch * 8));
+        else
+          Vec8<T>::store(dx + (int64_t)row * cols + ch * 8, o);
       }
     }
   }
