@@ -825,3 +825,19 @@ def test_fused_batchnorm_large_mean_variance():
     batch_norm_act(x, None, None, rm, rv, training=True, momentum=1.0, relu=False)
     ref = x.float().permute(1, 0, 2, 3).reshape(64, -1).var(1)
     assert float(((rv - ref) / ref).abs().max()) < 1e-3
+
+
+def test_fused_batchnorm_momentum_none_matches_torch():
+    """HIP BN with momentum=None keeps torch's cumulative running average."""
+    _lib()
+    from tf_operator_amd.ops.bn import FusedBatchNorm2d
+
+    torch.manual_seed(6)
+    ref = torch.nn.BatchNorm2d(32, momentum=None).to(DEV)
+    bn = FusedBatchNorm2d(32, momentum=None).to(DEV)
+    for i in range(3):
+        x = (torch.randn(8, 32, 6, 6, device=DEV) * (i + 1) + i).to(memory_format=torch.channels_last)
+        ref(x.float())
+        bn(x)
+    assert rel(bn.running_mean, ref.running_mean) < 1e-4
+    assert rel(bn.running_var, ref.running_var) < 1e-4

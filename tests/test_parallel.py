@@ -230,3 +230,27 @@ def test_broadcast_params_only_when_weights_differ(tmp_path, same):
     r = torch.load(out, weights_only=True)
     assert r["equal"] and r["master_ok"]
     assert r["calls"] == (0 if same else 1)
+
+
+def test_param_checksums_cover_every_element():
+    """the startup-broadcast skip compared a sampled positional
+    checksum.  Now both checksums see every element: swapping two values
+    (plain sum unchanged) or changing one element anywhere changes the hash,
+    identical tensors give identical checksums, at sizes past the old 16M
+    sampling threshold too (chunked)."""
+    from tf_operator_amd.parallel.ddp import param_checksums
+
+    for n in (1000, (1 << 24) + 4099):
+        p = torch.randn(n).to(torch.bfloat16)
+        s1, h = param_checksums(p, chunk=1 << 20)
+        assert param_checksums(p.clone(), chunk=1 << 20) == (s1, h)
+        q = p.clone()
+        i, j = 5, n - 3
+        while torch.equal(q[i], q[j]):
+            j -= 1
+        q[i], q[j] = p[j], p[i]
+        s1q, hq = param_checksums(q, chunk=1 << 20)
+        assert float(s1q) == float(s1) and float(hq) != float(h)
+        r = p.clone()
+        r[(n * 2) // 3] = r[(n * 2) // 3] + 1
+        assert param_checksums(r, chunk=1 << 20)[1] != h

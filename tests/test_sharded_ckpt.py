@@ -232,3 +232,86 @@ def test_llama_train_zero_checkpoint_every(tmp_path, world, zero):
     port = _free_port()
     run(6)  # resumes at step 4 from the world-2 shares, runs to 6
     assert sharded_ckpt.load_latest(root)[0]["step"] == 6
+
+
+def test_stale_partial_of_crashed_attempt_never_commits(tmp_path):
+    """A crashed attempt left ``step_N.partial`` with both ranks' markers.
+    Saving step N again, rank 0 must NOT take the old markers as this
+    attempt's: it waits for rank 1's new share, then commits the new data
+    (stale markers satisfied the wait while peers rewrote)."""
+    root = str(tmp_path)
+    # the crashed attempt: rank 1's share and marker, never committed (its
+    # rank 0 died before the commit)
+    stale = sharded_ckpt.Checkpointer(root, rank=1, world=2, attempt="old", commit_timeout=1.0)
+    stale.save(4, _state(_flat(seed=11)), block=True)
+    assert os.path.exists(os.path.join(root, "step_00000004.partial", "rank00001.json"))
+    new = [_flat(seed=20), _flat(seed=21)]
+    ck0 = sharded_ckpt.Checkpointer(root, rank=0, world=2, attempt="new", commit_timeout=1.0)
+    ck0.save(4, _state(new[0]))
+    with pytest.raises(RuntimeError):  # times out: rank 1's marker is the old attempt's
+        ck0.wait()
+    assert sharded_ckpt.latest_dir(root) is None
+    ck0 = sharded_ckpt.Checkpointer(root, rank=0, world=2, attempt="new", commit_timeout=60)
+    ck1 = sharded_ckpt.Checkpointer(root, rank=1, world=2, attempt="new", commit_timeout=60)
+    ck0.save(4, _state(new[0]))
+    ck1.save(4, _state(new[1]))
+    ck0.wait()
+    ck1.wait()
+    shares = sharded_ckpt.load_latest(root)
+    assert [s["rank"] for s in shares] == [0, 1]
+    for r in range(2):
+        assert torch.equal(torch.from_numpy(shares[r]["flat"]["master"].copy()), new[r].master)
+
+
+def _stream_worker(rank, world, port, root, phase, out):
+    """Synthetic token stream + RNG across a checkpoint (gloo, ZeRO-1)."""
+    from tf_operator_amd.train.data import SyntheticTokens
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = LlamaTrainer("llama-tiny", torch.device("cpu"), micro_batch=2, seq_len=32, lr=1e-3, seed=0,
+                          bucket_mb=0.01, shard_optimizer=True)
+        data = SyntheticTokens(2, 32, tr.cfg.vocab_size, rank=rank)
+        ck = sharded_ckpt.Checkpointer(root, rank, world)
+        ck.sync_attempt()
+        res = {"loss": []}
+        torch.manual_seed(1000 + rank)
+        if phase == "full":
+            for i in range(5):
+                res["loss"].append(float(tr.step([data.next()])))
+                torch.rand(3 + i)  # the step's own (here: stand-in) RNG use
+        elif phase == "save":
+            for i in range(3):
+                res["loss"].append(float(tr.step([data.next()])))
+                torch.rand(3 + i)
+            ck.save(tr.step_idx, trainer_state(tr, data), block=True)
+        else:
+            torch.manual_seed(99)  # a restarted process: different RNG, fresh stream
+            load_trainer_state(tr, sharded_ckpt.load_latest(root), data=data)
+            assert data.cursor == 3 and tr.step_idx == 3
+            for i in range(3, 5):
+                res["loss"].append(float(tr.step([data.next()])))
+                torch.rand(3 + i)
+        res["rand"] = torch.rand(4)
+        torch.save(res, f"{out}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resume_reproduces_losses_rng_and_data(tmp_path):
+    """3 steps + checkpoint + a fresh world-2 job running 2 more steps gives
+    bit-for-bit the losses and the RNG draws of 5 uninterrupted steps (the
+    data cursor and every rank's RNG state travel in the checkpoint)."""
+    root = str(tmp_path / "ck")
+    outs = {}
+    for phase in ("full", "save", "load"):
+        o = str(tmp_path / phase)
+        mp.spawn(_stream_worker, args=(2, _free_port(), root if phase != "full" else str(tmp_path / "x"), phase, o),
+                 nprocs=2, join=True)
+        outs[phase] = [torch.load(f"{o}.{r}", weights_only=True) for r in range(2)]
+    for r in range(2):
+        full, a, b = outs["full"][r], outs["save"][r], outs["load"][r]
+        assert a["loss"] + b["loss"] == full["loss"], r
+        assert torch.equal(b["rand"], full["rand"]), r

@@ -123,3 +123,20 @@ def test_fresh_gradients_match_zeroed_buffer(monkeypatch, tie):
         res[fresh] = (losses, tr.flat.param.clone(), tr.flat.master.clone())
     assert res["1"][0] == res["0"][0]
     assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])
+
+
+def test_fused_batchnorm_momentum_none_is_cumulative_average():
+    """momentum=None means a cumulative moving average in
+    torch.nn.BatchNorm2d (factor 1 / batches seen), not 0.1."""
+    from tf_operator_amd.ops.bn import FusedBatchNorm2d
+
+    torch.manual_seed(0)
+    ref = torch.nn.BatchNorm2d(8, momentum=None)
+    bn = FusedBatchNorm2d(8, momentum=None)
+    for i in range(4):
+        x = torch.randn(4, 8, 5, 5) * (i + 1) + i
+        ref(x)
+        bn(x)
+    assert int(bn.num_batches_tracked) == 4
+    assert torch.allclose(bn.running_mean, ref.running_mean, atol=1e-6)
+    assert torch.allclose(bn.running_var, ref.running_var, atol=1e-5)

@@ -17,6 +17,7 @@ import torch
 from tf_operator_amd.examples.common import pick_device
 from tf_operator_amd.train import dist as tdist
 from tf_operator_amd.train import sharded_ckpt
+from tf_operator_amd.train.data import SyntheticTokens
 from tf_operator_amd.train.llm import LlamaTrainer, load_trainer_state, trainer_state
 from tf_operator_amd.train.runtime import Runtime
 
@@ -31,6 +32,7 @@ def main(argv=None):
     p.add_argument("--checkpoint-every", type=int, default=0)
     p.add_argument("--step-sleep", type=float, default=0.0, help="testing: slow steps down")
     p.add_argument("--report-every", type=int, default=0, help="report samples/sec to the operator every N steps")
+    p.add_argument("--fixed-batch", action="store_true", help="reuse one resident batch (benchmarking)")
     p.add_argument("--zero", choices=("auto", "0", "1"), default="auto",
                    help="ZeRO-1 sharded optimizer; auto = on for world > 1 (bench.py's default)")
     a = p.parse_args(argv)
@@ -61,15 +63,21 @@ def _train(a, rt, info):
     tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr, shard_optimizer=zero)
     rt.mark("model_init")
     ck = sharded_ckpt.Checkpointer(rt.ckpt_dir, rt.rank, rt.world) if rt.ckpt_dir else None
+    if ck is not None:
+        ck.sync_attempt()  # markers of a crashed earlier attempt never commit this run's saves
+    # a resumable stream: batch i of rank r is a function of (seed, r, i), so
+    # the checkpointed cursor continues the uninterrupted run's data exactly
+    data = SyntheticTokens(a.micro_batch, a.seq_len, tr.cfg.vocab_size, rank=rt.rank, device=dev,
+                           fixed=a.fixed_batch)
     shares = sharded_ckpt.load_latest(rt.ckpt_dir)
     if shares is not None:
-        load_trainer_state(tr, shares)  # re-shards a checkpoint of any world size
-        rt.log(f"resumed at step {tr.step_idx} (world {rt.world}) from a world-{shares[0]['world']} checkpoint")
+        load_trainer_state(tr, shares, data=data)  # re-shards a checkpoint of any world size
+        rt.log(f"resumed at step {tr.step_idx} (world {rt.world}) from a world-{shares[0]['world']} checkpoint"
+               f" at data cursor {data.cursor}")
         rt.mark("checkpoint_load")
-    batch = [tr.synthetic_batch(seed=100 + rt.rank)]
     t0, n0 = time.perf_counter(), tr.step_idx
     while tr.step_idx < a.steps:
-        loss = tr.step(batch)
+        loss = tr.step([data.next()])
         if tr.step_idx == n0 + 1:
             if dev.type == "cuda":
                 torch.cuda.synchronize()
@@ -85,11 +93,11 @@ def _train(a, rt, info):
             rt.report(samples_per_sec=a.micro_batch * rt.world * (tr.step_idx - n0 - 1) / max(el, 1e-9),
                       step=tr.step_idx, world=rt.world)
         if ck and a.checkpoint_every and tr.step_idx % a.checkpoint_every == 0:
-            ck.save(tr.step_idx, trainer_state(tr))  # every rank, its own shard; asynchronous
+            ck.save(tr.step_idx, trainer_state(tr, data))  # every rank, its own shard; asynchronous
         if _stop_agreed(rt, dev):
             if ck:
                 t_s = time.time()
-                ck.save(tr.step_idx, trainer_state(tr), block=True)
+                ck.save(tr.step_idx, trainer_state(tr, data), block=True)
                 rt.log(f"preemption checkpoint at step {tr.step_idx} in {time.time() - t_s:.2f}s "
                        f"{ck.last_timing}")
             rt.log(f"preempted at step {tr.step_idx}")
@@ -104,7 +112,7 @@ def _train(a, rt, info):
     if done:
         rt.report(samples_per_sec=a.micro_batch * rt.world * done / dt)
     if ck:
-        ck.save(tr.step_idx, trainer_state(tr), block=True)
+        ck.save(tr.step_idx, trainer_state(tr, data), block=True)
     rt.log(f"done: {tr.step_idx} steps")
 
 

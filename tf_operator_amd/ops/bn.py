@@ -167,10 +167,12 @@ class FusedBatchNorm2d(torch.nn.BatchNorm2d):
 
     def forward(self, x, residual=None):
         training = self.training or self.running_mean is None
-        if self.training and self.num_batches_tracked is not None:
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
             self.num_batches_tracked.add_(1)
+            if self.momentum is None:  # torch: cumulative moving average, factor 1 / batches seen
+                momentum = 1.0 / float(self.num_batches_tracked)
         return batch_norm_act(x, self.weight, self.bias, self.running_mean if not self.training or
                               self.track_running_stats else None,
                               self.running_var if not self.training or self.track_running_stats else None,
-                              training, self.momentum if self.momentum is not None else 0.1, self.eps, self.relu,
-                              residual)
+                              training, momentum, self.eps, self.relu, residual)

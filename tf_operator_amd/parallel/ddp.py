@@ -157,6 +157,14 @@ class GradBucketer:
         self.pending = [b[2] for b in self.buckets]
         self.launched = [False] * len(self.buckets)
 
+    def verify(self):
+        """Synchronous health check of the collectives behind the CURRENT
+        weights (the one-shot kernel's peer-timeout word; ``finish()`` polls
+        it one step late).  Checkpoint paths call this before staging
+        anything, so an update built from stale peer slots is never saved."""
+        if self.ipc is not None:
+            self.ipc.check()
+
     @property
     def grad_scale(self):
         """Factor the optimizer applies to the summed gradients."""
@@ -167,20 +175,38 @@ def _is_nccl(group) -> bool:
     return dist.get_backend(group) == "nccl"
 
 
+_HASH_P = 2147483629  # prime < 2^31: products of two residues fit int64
+
+
+@torch.no_grad()
+def param_checksums(p: torch.Tensor, chunk: int = 1 << 26):
+    """(fp64 sum, positional hash) of a flat tensor, both over every element.
+    The hash is sum_i bits(p_i) * (i mod P + 1) mod P on the raw bit patterns
+    (exact integer arithmetic, so equal only if -- up to a 1/P collision --
+    the same values sit at the same positions; a permutation or two
+    cancelling differences change it).  Chunked: no full-size int64 copy."""
+    flat = p.reshape(-1)
+    bits = flat.view(torch.int16) if flat.element_size() == 2 else flat.view(torch.int32)
+    s1 = flat.sum(dtype=torch.float64)
+    h = torch.zeros((), dtype=torch.int64, device=p.device)
+    for lo in range(0, flat.numel(), chunk):
+        b = bits[lo:lo + chunk].to(torch.int64) & 0xFFFFFFFF
+        idx = torch.arange(lo, lo + b.numel(), device=p.device, dtype=torch.int64) % _HASH_P + 1
+        h = (h + ((b % _HASH_P) * idx % _HASH_P).sum() % _HASH_P) % _HASH_P
+    return s1, h.to(torch.float64)
+
+
 def broadcast_params(flat: FlatParams, src=0, group=None):
     """Make every rank start from rank `src`'s weights (and master copy).
 
     Seeded initialisation usually gives every rank the same weights already:
-    two fp64 checksums (plain and position-weighted) are compared across
-    ranks first, and the broadcast -- 16 GB at Llama-3-8B, part of every
+    two checksums over EVERY element are compared across ranks first (a
+    plain fp64 sum and an exact integer hash of the bit patterns weighted by
+    position), and the broadcast -- 16 GB at Llama-3-8B, part of every
     job's submit -> first-step -- runs only when they differ."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
-    p = flat.param
-    w = torch.arange(1, p.numel() + 1, device=p.device, dtype=torch.float64) if p.numel() <= (1 << 24) else None
-    s1 = p.sum(dtype=torch.float64)
-    s2 = (p.double() * w).sum() if w is not None else (p[::97].double() * torch.arange(
-        1, p[::97].numel() + 1, device=p.device, dtype=torch.float64)).sum()
+    s1, s2 = param_checksums(flat.param)
     v = torch.stack([s1, s2, -s1, -s2])
     dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
     if bool(v[0] == -v[2]) and bool(v[1] == -v[3]):

@@ -122,8 +122,11 @@ class IpcAllReduce:
         """Non-blocking error check, once per step: the sticky device error
         word is copied into pinned host memory behind this step's reduces and
         the copy queued one step earlier is inspected (an event query, no
-        host sync).  A set bit raises, so the peer-loss exit path runs instead
-        of the optimizer consuming sums built from stale peer slots."""
+        host sync).  So a peer timeout in step t is seen in step t+1's
+        finish(): by then step t's optimizer update has consumed sums built
+        from stale peer slots.  The peer-loss exit path runs from there, and
+        nothing of step t is persisted: every checkpoint path first calls
+        :meth:`check` (synchronous) through ``GradBucketer.verify()``."""
         if getattr(self, "broken", False):
             raise RuntimeError("IPC all-reduce already failed; refusing to reuse it")
         if not hasattr(self, "_host_err"):

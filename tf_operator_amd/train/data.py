@@ -90,3 +90,42 @@ class SyntheticBinary:
         idx = torch.arange(self.i, self.i + self.batch) % n
         self.i = (self.i + self.batch) % n
         return self.x[idx].to(self.device), self.y[idx].to(self.device)
+
+
+class SyntheticTokens:
+    """Llama token stream with a resumable position: batch i of rank r is a
+    pure function of (seed, r, i), drawn on the device, so ``state_dict()``
+    (the cursor) is the whole data state a checkpoint needs -- a resumed run
+    reads exactly the batches the uninterrupted run would have read next.
+
+    ``fixed=True`` hands out batch 0 every time (the benchmark's resident
+    batch: no generation work inside the timed step)."""
+
+    def __init__(self, micro_batch, seq_len, vocab, rank=0, seed=100, device="cpu", fixed=False):
+        self.micro_batch, self.seq_len, self.vocab = micro_batch, seq_len, vocab
+        self.rank, self.seed, self.device, self.fixed = rank, seed, torch.device(device), fixed
+        self.cursor = 0
+        self._fixed = None
+
+    def _draw(self, i):
+        g = torch.Generator(device=self.device)
+        g.manual_seed((self.seed * 1000003 + self.rank) * 1000003 + i)
+        tok = torch.randint(0, self.vocab, (self.micro_batch, self.seq_len + 1), device=self.device, generator=g)
+        return tok[:, :-1].contiguous(), tok[:, 1:].contiguous()
+
+    def next(self):
+        if self.fixed:
+            if self._fixed is None:
+                self._fixed = self._draw(0)
+            self.cursor += 1
+            return self._fixed
+        b = self._draw(self.cursor)
+        self.cursor += 1
+        return b
+
+    def state_dict(self):
+        return {"cursor": int(self.cursor), "seed": int(self.seed), "rank": int(self.rank)}
+
+    def load_state_dict(self, sd):
+        if sd:
+            self.cursor = int(sd.get("cursor", 0))

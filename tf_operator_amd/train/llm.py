@@ -154,24 +154,48 @@ def timed_steps(trainer: LlamaTrainer, batches, n, sync=True):
     return time.perf_counter() - t0, loss
 
 
-def trainer_state(tr: LlamaTrainer):
+def rng_state(device) -> dict:
+    """This process's CPU RNG state and, on a GPU, the device generator's
+    (uint8 tensors)."""
+    out = {"cpu": torch.get_rng_state()}
+    if torch.device(device).type == "cuda":
+        out["cuda"] = torch.cuda.get_rng_state(torch.device(device))
+    return out
+
+
+def set_rng_state(st: dict | None, device):
+    if not st:
+        return
+    if st.get("cpu") is not None:
+        torch.set_rng_state(st["cpu"].cpu().to(torch.uint8))
+    if st.get("cuda") is not None and torch.device(device).type == "cuda":
+        torch.cuda.set_rng_state(st["cuda"].cpu().to(torch.uint8), torch.device(device))
+
+
+def trainer_state(tr: LlamaTrainer, data=None):
     """This rank's share of the training state: the fp32 master / moment
     shards it holds (all of them without ZeRO) plus where they belong in the
-    flat buffer.  NOT a collective -- every rank saves its own share
+    flat buffer, the step, this rank's RNG states and (given the data
+    stream) its cursor.  NOT a collective -- every rank saves its own share
     (train/sharded_ckpt.py), and the shares of any world size re-shard on
     load (:func:`load_trainer_state`)."""
     tr.opt.wait_all()
     if tr.gather is not None:
         tr.gather.wait_all()
+    tr.bucketer.verify()  # never persist an update built from a failed one-shot all-reduce
     return {"flat": tr.flat.state_dict(), "opt": tr.opt.state_dict(), "step": tr.step_idx,
-            "rank": tr.bucketer.rank, "world": tr.bucketer.world}
+            "rank": tr.bucketer.rank, "world": tr.bucketer.world, "rng": rng_state(tr.device),
+            "data": data.state_dict() if data is not None else None}
 
 
-def load_trainer_state(tr: LlamaTrainer, st):
+def load_trainer_state(tr: LlamaTrainer, st, data=None):
     """Restore from one state (``trainer_state`` of an unsharded run) or a
     list of per-rank shares of any world size.  Collective when this
-    trainer shards its optimizer: the restored weights are all-gathered."""
+    trainer shards its optimizer: the restored weights are all-gathered.
+    RNG states and the data cursor come from the share this rank saved
+    (same rank index; rank 0's when the world grew)."""
     shards = st if isinstance(st, (list, tuple)) else [st]
+    mine = next((s for s in shards if int(s.get("rank", 0)) == tr.bucketer.rank), shards[0])
     tr.opt.wait_all()
     if tr.gather is not None:
         tr.gather.wait_all()
@@ -183,3 +207,6 @@ def load_trainer_state(tr: LlamaTrainer, st):
     tr.flat.params_changed()
     tr.opt.load_state_dict(shards[0]["opt"])
     tr.step_idx = int(shards[0]["step"])
+    set_rng_state(mine.get("rng"), tr.device)
+    if data is not None and mine.get("data"):
+        data.load_state_dict(mine["data"])

@@ -20,6 +20,16 @@ termination grace period.  Here:
   markers, writes ``manifest.json``, renames the directory to ``step_N`` and
   rewrites ``latest`` -- a crash at any point leaves the previous step as
   ``latest``;
+* **per attempt**: a marker names the save attempt that wrote it (an id
+  every rank of one run shares: :meth:`Checkpointer.sync_attempt`, or the
+  elastic generation / restart count from the environment), and rank 0
+  commits only markers of ITS attempt whose byte counts match the files on
+  disk.  A ``step_N.partial`` left by a crashed earlier attempt therefore
+  never satisfies the wait: its markers name the old attempt, and every
+  rank deletes its own stale marker before it rewrites its files;
+* **RNG and data position**: each rank's marker also carries its CPU/GPU
+  RNG states and data-stream cursor (``trainer_state``), so a resumed run
+  continues the uninterrupted run's random and data sequence exactly;
 * **re-sharding on load**: :func:`load_latest` returns every rank's share as
   read-only ``numpy.memmap`` views (nothing is unpickled), and
   ``FlatParams.load_state_shards`` copies the pieces intersecting this
@@ -31,6 +41,7 @@ file-based, so the save never races the training step's RCCL stream.
 """
 from __future__ import annotations
 
+import base64
 import json
 import os
 import re
@@ -69,6 +80,31 @@ def _fsync_dir(path: str):
         os.close(fd)
 
 
+def _env_attempt() -> str:
+    """An attempt id all ranks of one launch agree on without talking:
+    explicit TOA_CKPT_ATTEMPT, else the elastic generation / restart counts
+    the operator (csrc/core/elastic.cc) and torchrun inject."""
+    if os.environ.get("TOA_CKPT_ATTEMPT"):
+        return os.environ["TOA_CKPT_ATTEMPT"]
+    return "g{}.r{}.t{}".format(os.environ.get("TOA_ELASTIC_GENERATION", "0"),
+                                os.environ.get("TOA_ELASTIC_RESTARTS", "0"),
+                                os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+
+
+def _b64(x) -> str | None:
+    if x is None:
+        return None
+    if torch.is_tensor(x):
+        x = x.cpu().numpy().tobytes()
+    return base64.b64encode(bytes(x)).decode("ascii")
+
+
+def _unb64(s) -> torch.Tensor | None:
+    if s is None:
+        return None
+    return torch.frombuffer(bytearray(base64.b64decode(s)), dtype=torch.uint8).clone()
+
+
 def _write_raw(path: str, arr: np.ndarray, chunk=1 << 28):
     with open(path, "wb", buffering=0) as f:
         mv = memoryview(arr.reshape(-1).view(np.uint8))
@@ -82,9 +118,10 @@ class Checkpointer:
     until the last save is durable (and, on rank 0, committed)."""
 
     def __init__(self, root: str, rank: int = 0, world: int = 1, keep: int = 2, commit_timeout: float = 600.0,
-                 io_threads: int = 3):
+                 io_threads: int = 3, attempt: str | None = None):
         self.root = root
         self.rank, self.world = int(rank), int(world)
+        self.attempt = str(attempt) if attempt is not None else _env_attempt()
         self.keep = keep
         self.commit_timeout = commit_timeout
         self.io_threads = io_threads
@@ -94,6 +131,20 @@ class Checkpointer:
         self._last_step: int | None = None
         self.last_timing: dict = {}
         os.makedirs(root, exist_ok=True)
+
+    def sync_attempt(self, group=None) -> str:
+        """Collective (call once at setup, every rank): adopt a fresh attempt
+        id drawn by rank 0.  Covers restarts the environment does not count
+        (a whole-group container restart under OnFailure)."""
+        import torch.distributed as dist
+
+        if dist.is_initialized() and dist.get_world_size(group) > 1:
+            obj = [f"{self.attempt}.{os.urandom(6).hex()}" if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            self.attempt = obj[0]
+        else:
+            self.attempt = f"{self.attempt}.{os.urandom(6).hex()}"
+        return self.attempt
 
     # ------------------------------------------------------------------ staging
     def _stage(self, name: str, t: torch.Tensor) -> torch.Tensor:
@@ -126,7 +177,8 @@ class Checkpointer:
         meta = {"rank": self.rank, "world": self.world, "step": int(step),
                 "state_ranges": [list(map(int, r)) for r in fl["state_ranges"]], "numel": int(fl["numel"]),
                 "layout": [list(x) for x in fl["layout"]], "opt": state.get("opt") or {},
-                "dtype": {k: "float32" for k in staged}, "extra": extra or {}}
+                "dtype": {k: "float32" for k in staged}, "extra": extra or {}, "attempt": self.attempt,
+                "rng": {k: _b64(v) for k, v in (state.get("rng") or {}).items()}, "data": state.get("data")}
         self._error = None
         self._thread = threading.Thread(target=self._write, args=(int(step), staged, ev, meta, t0),
                                         name=f"ckpt-writer-{self.rank}", daemon=True)
@@ -141,6 +193,12 @@ class Checkpointer:
             t_staged = time.time()
             d = _step_dir(self.root, step, partial=True)
             os.makedirs(d, exist_ok=True)
+            # a crashed earlier attempt's marker must go BEFORE this rank's
+            # files are rewritten (its attempt id already keeps rank 0 from
+            # committing it; this keeps the directory honest too)
+            marker = os.path.join(d, f"rank{self.rank:05d}.json")
+            if os.path.exists(marker):
+                os.remove(marker)
             files = {}
             threads = []
             for k, buf in staged.items():
@@ -154,7 +212,7 @@ class Checkpointer:
                 th.join()
             meta["files"] = files
             meta["bytes"] = int(sum(b.numel() * b.element_size() for b in staged.values()))
-            _atomic_write_text(os.path.join(d, f"rank{self.rank:05d}.json"), json.dumps(meta))
+            _atomic_write_text(marker, json.dumps(meta))
             t_written = time.time()
             if self.rank == 0:
                 self._commit(step, d, meta)
@@ -164,20 +222,45 @@ class Checkpointer:
         except BaseException as e:  # surfaced by wait()
             self._error = e
 
+    def _marker_ok(self, d, path):
+        """A rank's marker counts only if it is this attempt's and every file
+        it names is on disk at the size it records."""
+        try:
+            with open(path) as f:
+                m = json.load(f)
+        except (OSError, ValueError):
+            return None
+        if m.get("attempt") != self.attempt:
+            return None
+        n = sum(hi - lo for lo, hi in m["state_ranges"])
+        for fn in m.get("files", {}).values():
+            try:
+                if os.path.getsize(os.path.join(d, fn)) != 4 * n:
+                    return None
+            except OSError:
+                return None
+        return m
+
     def _commit(self, step, d, meta0):
         deadline = time.monotonic() + self.commit_timeout
         want = [os.path.join(d, f"rank{r:05d}.json") for r in range(self.world)]
-        while not all(os.path.exists(p) for p in want):
+        got = [None] * self.world
+        while True:
+            for r, p in enumerate(want):
+                if got[r] is None and os.path.exists(p):
+                    got[r] = self._marker_ok(d, p)
+            if all(m is not None for m in got):
+                break
             if time.monotonic() > deadline:
-                raise TimeoutError(f"checkpoint step {step}: not every rank finished its share")
+                raise TimeoutError(f"checkpoint step {step}: not every rank finished its share "
+                                   f"(attempt {self.attempt})")
             time.sleep(0.05)
         shards = []
-        for p in want:
-            with open(p) as f:
-                m = json.load(f)
+        for m in got:
             shards.append({"rank": m["rank"], "state_ranges": m["state_ranges"], "files": m["files"],
-                           "bytes": m["bytes"]})
-        manifest = {"format": "toa-sharded-v1", "step": step, "world": self.world, "numel": meta0["numel"],
+                           "bytes": m["bytes"], "rng": m.get("rng") or {}, "data": m.get("data")})
+        manifest = {"format": "toa-sharded-v1", "step": step, "attempt": self.attempt, "world": self.world,
+                    "numel": meta0["numel"],
                     "layout": meta0["layout"], "opt": meta0["opt"], "extra": meta0["extra"], "time": time.time(),
                     "shards": shards}
         _atomic_write_text(os.path.join(d, "manifest.json"), json.dumps(manifest))
@@ -248,5 +331,7 @@ def load_latest(root: str | None):
                 raise ValueError(f"{fn}: {arr.shape[0]} elements, manifest says {n}")
             flat[k] = arr
         out.append({"flat": flat, "opt": man["opt"], "step": man["step"], "rank": sh["rank"],
-                    "world": man["world"], "extra": man.get("extra", {})})
+                    "world": man["world"], "extra": man.get("extra", {}),
+                    "rng": {k: _unb64(v) for k, v in (sh.get("rng") or {}).items() if v is not None},
+                    "data": sh.get("data")})
     return out

@@ -133,6 +133,7 @@ class DPTrainer:
 
     # ------------------------------------------------------------------ checkpoint
     def state(self):
+        self.bucketer.verify()  # never persist an update built from a failed one-shot all-reduce
         st = {"flat": self.flat.state_dict(), "step": self.step_idx}
         if isinstance(self.opt, FlatAdamW):
             st["opt"] = self.opt.state_dict()
