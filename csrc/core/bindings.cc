@@ -80,6 +80,12 @@ PYBIND11_MODULE(_toa_core, m) {
         return t.dump();
       },
       py::arg("job"), py::arg("template"), py::arg("rtype"), py::arg("index"), py::arg("options") = "");
+  m.def(
+      "node_local",
+      [](const std::string& job, const std::string& options) {
+        return node_local(set_defaults(J(job)), options_from_json(J(options)));
+      },
+      py::arg("job"), py::arg("options") = "{}");
   m.def("tf_is_distributed", [](const std::string& job) { return tf_is_distributed(set_defaults(J(job))); });
   m.def(
       "gen_podgroup",

@@ -108,6 +108,7 @@ struct Options {
   bool rccl_defaults = true;            // xGMI-oriented defaults (never override the user's env)
   std::string gpu_resource = "amd.com/gpu";
   int64_t elastic_free_gpus = -1;       // free GPUs for an elastic job (own pods count as free); -1 unknown
+  int64_t gpus_per_node = 8;            // node-local layout: at most this many ranks share a node
 };
 Options options_from_json(const Json& o);
 
@@ -117,6 +118,13 @@ std::string gen_tf_config(const Json& job, const std::string& rt_lower, int inde
 // environment variables appended to the replica's containers; returns list of
 // {"container": name|"*", "name":..., "value":...}
 Json gen_env(const Json& job, const std::string& rtype, int index, const Options& opt);
+// single-node xGMI layout of the RCCL ranks (nodelocal.cc)
+extern const char* kAnnNodeLocal;      // amd.com/node-local: "true" | "false" (default: auto)
+extern const char* kAnnGpuVisibility;  // amd.com/gpu-visibility=node on node-local pods
+extern const char* kLabelNodeLocal;    // training.amd.com/node-local
+int64_t rank_world(const Json& job);   // Chief+Master+Worker (TFJob) / Master+Worker (PyTorchJob)
+bool node_local(const Json& job, const Options& opt);
+void apply_node_local(const Json& job, const std::string& rtype, Json& pod_template, const Options& opt);
 // apply gen_env to a pod template (in place)
 void set_cluster_spec(const Json& job, Json& pod_template, const std::string& rtype, int index,
                       const Options& opt);

@@ -7,7 +7,9 @@
 //   PLUS the ROCm/RCCL block consumed by the PyTorch-ROCm trainer:
 //   MASTER_ADDR/MASTER_PORT (rank-0 = Chief, else Master, else Worker-0),
 //   WORLD_SIZE (= Chief+Master+Worker; PS/Evaluator are outside the RCCL
-//   world), RANK, LOCAL_RANK/LOCAL_WORLD_SIZE (one GPU per pod),
+//   world), RANK, LOCAL_RANK/LOCAL_WORLD_SIZE (one GPU per pod; in the
+//   node-local layout -- nodelocal.cc -- the rank's index on the one node
+//   and the node's rank count),
 //   TOA_ROLE / TOA_PS_HOSTS for parameter-server mode, NCCL_* knobs.
 // * PyTorchJob: pytorch/pytorch.go:13-96 (every container).
 // * MXJob: mxnet/mxnet.go:55-233 (MX_CONFIG + DMLC_* + BytePS id).
@@ -31,6 +33,7 @@ Options options_from_json(const Json& o) {
   if (o.has("rccl_defaults")) opt.rccl_defaults = o.get("rccl_defaults").as_bool(true);
   opt.gpu_resource = o.get("gpu_resource").str("amd.com/gpu");
   opt.elastic_free_gpus = o.get("elastic_free_gpus").as_int(-1);
+  opt.gpus_per_node = o.get("gpus_per_node").as_int(8);
   return opt;
 }
 
@@ -187,9 +190,11 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
     else if (rtype == "Master") rank = n_chief + index;
     else if (rtype == "Worker") rank = n_chief + n_master + index;
     if (rank >= 0) {
+      const bool nl = node_local(job, opt);
       add_env(out, c, "RANK", std::to_string(rank));
-      add_env(out, c, "LOCAL_RANK", "0");
-      add_env(out, c, "LOCAL_WORLD_SIZE", "1");
+      add_env(out, c, "LOCAL_RANK", nl ? std::to_string(rank) : "0");
+      add_env(out, c, "LOCAL_WORLD_SIZE", nl ? std::to_string(world) : "1");
+      if (nl) add_env(out, c, "TOA_NODE_LOCAL", "1");
     }
     add_env(out, c, "TOA_ROLE", role);
     int64_t n_ps = spec_replicas(job, "PS");
@@ -218,8 +223,10 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
     add_env(out, "*", "RANK", std::to_string(rank));
     add_env(out, "*", "PYTHONUNBUFFERED", "0");
     if (opt.inject_rocm_env) {
-      add_env(out, "*", "LOCAL_RANK", "0");
-      add_env(out, "*", "LOCAL_WORLD_SIZE", "1");
+      const bool nl = node_local(job, opt);
+      add_env(out, "*", "LOCAL_RANK", nl ? std::to_string(rank) : "0");
+      add_env(out, "*", "LOCAL_WORLD_SIZE", nl ? std::to_string(total) : "1");
+      if (nl) add_env(out, "*", "TOA_NODE_LOCAL", "1");
       rocm_block(job, rtype, index, opt, "*", out);
     }
     return out;

@@ -161,6 +161,7 @@ static Json new_pod(const Json& job, const KindInfo& ki, const std::string& rtyp
   tmd.set("labels", labels);
   tmd.set("name", gen_general_name(name, rt, std::to_string(index)));
   set_cluster_spec(job, tpl, rtype, index, opt);
+  apply_node_local(job, rtype, tpl, opt);
   wrap_rocprof(md.get("annotations"), ki, tmd.get("name").str(), tpl["spec"], events);
   Json& ps = tpl["spec"];
   if (!ps.get("restartPolicy").str().empty())

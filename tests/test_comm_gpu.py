@@ -159,3 +159,75 @@ def test_ipc_lost_peer_raises_from_poll():
         p.join(timeout=30)
     assert res[0][1] is None and res[1][1] is None, res
     assert res[0][0] and "rank" in res[0][0] and "1" in res[0][0], res
+
+
+def _operator_env_worker(rank, world, port, env, q):
+    """One replica with exactly the env the operator's node-local layout
+    injects (core.gen_env), no TOA_IPC_ALLREDUCE: GradBucketer must pick the
+    one-shot path by itself, per bucket by size."""
+    import torch.distributed as dist
+
+    os.environ.pop("TOA_IPC_ALLREDUCE", None)
+    os.environ.update(env, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=int(env["RANK"]), world_size=int(env["WORLD_SIZE"]))
+        from tf_operator_amd.models.vision import MnistMLP
+        from tf_operator_amd.ops.llm import cross_entropy
+        from tf_operator_amd.train import simple
+        from tf_operator_amd.train.data import SyntheticMNIST
+        from tf_operator_amd.train.runtime import Runtime
+
+        torch.manual_seed(0)
+        # hid.weight 784 x 3000 fp32 = 9.4 MB: above the one-shot size; the
+        # 12 KB-120 KB tensors below it
+        model = MnistMLP(3000, dtype=torch.float32, device="cuda")
+        rt = Runtime()
+        rt.info = type("I", (), {"rank": rank, "world": world})()
+        tr = simple.DPTrainer(model, lambda o, y: cross_entropy(o, y), rt, lr=1e-3, bucket_mb=1.0)
+        reason = tr.bucketer.ipc_reason
+        data = SyntheticMNIST(100, rank, world, device="cuda")
+        for _ in range(5):
+            tr.step(*data.next())
+        torch.cuda.synchronize()
+        tr.bucketer.verify()
+        flat = tr.flat.param.detach().float().cpu()
+        out = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(out, flat)
+        q.put((rank, (tr.bucketer.ipc is not None, reason, dict(tr.bucketer.path_counts),
+                      bool(torch.equal(out[0], out[1]))), None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.timeout(240)
+def test_oneshot_auto_selected_under_operator_env():
+    """Verdict r2: the one-shot path was dead for every operator-launched
+    pod (LOCAL_WORLD_SIZE=1).  With the node-local env of a Worker=2 TFJob
+    it is auto-selected, small buckets go one-shot, the big one stays on the
+    process group, and the replicas stay identical."""
+    from tf_operator_amd import core
+
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
+           "metadata": {"name": "nl", "namespace": "default", "annotations": {"amd.com/node-local": "true"}},
+           "spec": {"tfReplicaSpecs": {"Worker": {"replicas": 2, "template": {"spec": {"containers": [
+               {"name": "tensorflow", "image": "x", "resources": {"limits": {"amd.com/gpu": 1}}}]}}}}}}
+    keep = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "TOA_NODE_LOCAL")
+    envs = [{e["name"]: e["value"] for e in core.gen_env(job, "Worker", i) if e["name"] in keep} for i in range(2)]
+    assert [e["LOCAL_WORLD_SIZE"] for e in envs] == ["2", "2"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_operator_env_worker, args=(r, 2, port, envs[r], q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, got, err in res:
+        assert err is None, (rank, err)
+        selected, reason, counts, same = got
+        assert selected and reason.startswith("auto"), (rank, reason)
+        assert counts["oneshot"] > 0 and counts["collective"] > 0, (rank, counts)
+        assert same, rank

@@ -513,3 +513,93 @@ def test_claim_nothing_adopted_while_job_deleting():
     orphan["metadata"].pop("ownerReferences", None)
     res = core.claim_objects(job, [orphan])
     assert res["claimed"] == [] and res["adopt"] == []
+
+
+# ---------------------------------------------------------------------------
+# node-local xGMI layout (csrc/core/nodelocal.cc)
+# ---------------------------------------------------------------------------
+def _gpu_job(workers, chief=0, ps=0, gpus=1, annotation=None):
+    job = fx.new_tfjob(workers, ps, chief=chief)
+    for rt, s in job["spec"]["tfReplicaSpecs"].items():
+        if rt != "PS":
+            s["template"]["spec"]["containers"][0]["resources"] = {"limits": {"amd.com/gpu": gpus}}
+    if annotation is not None:
+        job["metadata"]["annotations"] = {"amd.com/node-local": annotation}
+    return job
+
+
+def test_node_local_pod_spec_and_env():
+    """Worker=8 gang-scheduled, one GPU each: every rank pod is co-located by
+    a required hostname podAffinity, gets hostIPC and the node's /dev/kfd +
+    /dev/dri, and LOCAL_RANK / LOCAL_WORLD_SIZE of the node (the hard-coded
+    0 / 1 of round 2 made the one-shot path unreachable)."""
+    job = _gpu_job(7, chief=1, ps=1)
+    res = run(job, enable_gang_scheduling=True)
+    pods = {p["pod"]["metadata"]["name"]: p["pod"] for p in ops(res, "create_pod")}
+    w3 = pods["test-tfjob-worker-3"]
+    spec = w3["spec"]
+    assert spec["hostIPC"] is True
+    term = spec["affinity"]["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][0]
+    assert term["topologyKey"] == "kubernetes.io/hostname"
+    assert term["labelSelector"]["matchLabels"] == {"group-name": "kubeflow.org", "job-name": "test-tfjob",
+                                                    "training.amd.com/node-local": "true"}
+    assert w3["metadata"]["labels"]["training.amd.com/node-local"] == "true"
+    assert w3["metadata"]["annotations"]["amd.com/gpu-visibility"] == "node"
+    assert {v["hostPath"]["path"] for v in spec["volumes"]} == {"/dev/kfd", "/dev/dri"}
+    c = spec["containers"][0]
+    assert {m["mountPath"] for m in c["volumeMounts"]} == {"/dev/kfd", "/dev/dri"}
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert env["RANK"] == "4" and env["LOCAL_RANK"] == "4"  # chief is rank 0
+    assert env["LOCAL_WORLD_SIZE"] == "8" and env["WORLD_SIZE"] == "8" and env["TOA_NODE_LOCAL"] == "1"
+    chief = {e["name"]: e["value"] for e in pods["test-tfjob-chief-0"]["spec"]["containers"][0]["env"]}
+    assert chief["LOCAL_RANK"] == "0" and chief["LOCAL_WORLD_SIZE"] == "8"
+    ps = pods["test-tfjob-ps-0"]  # outside the RCCL world: unchanged
+    assert "hostIPC" not in ps["spec"] and "affinity" not in ps["spec"]
+    assert "LOCAL_RANK" not in {e["name"] for e in ps["spec"]["containers"][0]["env"]}
+
+
+@pytest.mark.parametrize("workers,gpus,annotation,gang,expected", [
+    (2, 1, None, False, False),    # no gang scheduling, no annotation: the classic layout
+    (2, 1, None, True, True),      # gang-scheduled, one GPU per rank, fits a node: automatic
+    (2, 1, "true", False, True),   # opt in
+    (8, 1, "false", True, False),  # opt out
+    (9, 1, "true", True, False),   # does not fit one 8-GPU node
+    (1, 1, "true", True, False),   # a single rank has no peers
+    (4, 2, None, True, False),     # automatic only with exactly one GPU per rank
+])
+def test_node_local_selection(workers, gpus, annotation, gang, expected):
+    job = _gpu_job(workers, gpus=gpus, annotation=annotation)
+    opts = {"enable_gang_scheduling": gang}
+    assert core.node_local(job, opts) is expected
+    env = {e["name"]: e["value"] for e in core.gen_env(job, "Worker", workers - 1, opts)}
+    assert env["LOCAL_WORLD_SIZE"] == (str(workers) if expected else "1")
+    assert env["LOCAL_RANK"] == (str(workers - 1) if expected else "0")
+    assert not core.node_local(_gpu_job(4), {"enable_gang_scheduling": True, "gpus_per_node": 2})
+
+
+def test_node_local_pytorchjob_env():
+    tpl = fx.replica_template()
+    tpl["spec"]["containers"][0]["name"] = "pytorch"
+    job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "metadata": {"name": "pt", "namespace": "default", "annotations": {"amd.com/node-local": "true"}},
+           "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "template": tpl},
+                                            "Worker": {"replicas": 3, "template": tpl}}}}
+    env = {e["name"]: e["value"] for e in core.gen_env(job, "Worker", 1)}
+    assert env["RANK"] == "2" and env["LOCAL_RANK"] == "2"
+    assert env["LOCAL_WORLD_SIZE"] == env["WORLD_SIZE"] == "4"
+
+
+def test_oneshot_selection_under_operator_env():
+    """The operator's node-local env makes GradBucketer's one-shot IPC path
+    auto-selectable (no TOA_IPC_ALLREDUCE=1); the classic env does not."""
+    from tf_operator_amd.parallel.ddp import ipc_decision
+
+    job = _gpu_job(2, annotation="true")
+    env = {e["name"]: e["value"] for e in core.gen_env(job, "Worker", 1)}
+    ok, why = ipc_decision("auto", int(env["WORLD_SIZE"]), True, True, True, 1, env["LOCAL_WORLD_SIZE"])
+    assert ok, why
+    classic = {e["name"]: e["value"] for e in core.gen_env(_gpu_job(2), "Worker", 1)}
+    ok, why = ipc_decision("auto", 2, True, True, True, 1, classic["LOCAL_WORLD_SIZE"])
+    assert not ok and "span nodes" in why
+    assert not ipc_decision("auto", 2, True, True, True, 0, "2")[0]  # nothing small enough
+    assert not ipc_decision("0", 2, True, True, True, 1, "2")[0]

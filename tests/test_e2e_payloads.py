@@ -66,6 +66,21 @@ def test_dist_mnist_allreduce(cluster):
     assert "rank 0/3" in chief and "accuracy" in chief
 
 
+def test_dist_mnist_node_local_auto_oneshot(cluster):
+    """The node-local layout reaches the payload: both ranks get
+    LOCAL_WORLD_SIZE=2 from the operator (no TOA_IPC_ALLREDUCE in their
+    env), and GradBucketer's automatic selection finds the job eligible for
+    the one-shot IPC all-reduce -- here only the CPU gradients keep it on
+    gloo; on GPUs the same decision turns it on (tests/test_comm_gpu.py)."""
+    args = ("--train_steps", 40, "--log_every", 20, "--min_accuracy", 0.0)
+    job = tfjob("mnist-nl", {"Worker": rs(2, payload("dist_mnist", *args))},
+                annotations={"amd.com/node-local": "true"})
+    done, logs = _run(cluster, job)
+    assert "Succeeded" in conds(done), (conds(done), logs)
+    for name in ("mnist-nl-worker-0", "mnist-nl-worker-1"):
+        assert "one-shot IPC off (eligible (2 ranks on this node" in logs[name], logs[name]
+
+
 @pytest.mark.parametrize("sync", [False, True])
 def test_dist_mnist_parameter_server(cluster, sync):
     args = ["--train_steps", 200, "--log_every", 50, "--min_accuracy", 0.2]

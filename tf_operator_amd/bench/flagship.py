@@ -105,7 +105,10 @@ def _tfjob(name: str, n: int, command: list[str], env: dict | None = None) -> di
 
     tpl = pod_template(container(image="toa/trainer:latest", command=command, gpus=1,
                                  env={"OMP_NUM_THREADS": "8", **(env or {})}))
-    return {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": name, "namespace": "default"},
+    # node-local xGMI layout (csrc/core/nodelocal.cc): the ranks share one
+    # node, see each other's GPUs and get LOCAL_RANK / LOCAL_WORLD_SIZE of it
+    return {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
+            "metadata": {"name": name, "namespace": "default", "annotations": {"amd.com/node-local": "true"}},
             "spec": {"runPolicy": {"cleanPodPolicy": "All"},
                      "tfReplicaSpecs": {"Worker": {"replicas": n, "restartPolicy": "Never", "template": tpl}}}}
 
@@ -255,7 +258,7 @@ def _cluster(n: int, warm: bool = False):
     server has imported torch (a job submitted earlier would start cold)."""
     from ..testing.cluster import LocalCluster
 
-    c = LocalCluster(gpus=n, grace_seconds=10.0, device_visibility="node", threadiness=2, warm_python=warm).start()
+    c = LocalCluster(gpus=n, grace_seconds=10.0, threadiness=2, warm_python=warm).start()
     if warm:
         try:
             c.wait(c.kubelet.warm_ready, 120, 0.05, "kubelet fork server ready")

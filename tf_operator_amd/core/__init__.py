@@ -75,6 +75,12 @@ def gen_tf_config(job: dict, rtype: str, index: int, options: dict | None = None
     return native().gen_tf_config(_d(job), rtype, int(index), _d(options or {}))
 
 
+def node_local(job: dict, options: dict | None = None) -> bool:
+    """Does the job's RCCL world run in the single-node xGMI layout
+    (csrc/core/nodelocal.cc)?"""
+    return bool(native().node_local(_d(job), _d(options or {})))
+
+
 def gen_env(job: dict, rtype: str, index: int, options: dict | None = None) -> list:
     return json.loads(native().gen_env(_d(job), rtype, int(index), _d(options or {})))
 

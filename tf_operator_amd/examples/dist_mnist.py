@@ -58,6 +58,9 @@ def run_allreduce(a, rt):
     torch.manual_seed(0)
     model = MnistMLP(a.hidden_units, dtype=model_dtype(dev), device=dev)
     tr = simple.DPTrainer(model, loss_fn, rt, lr=a.learning_rate)
+    if tr.bucketer.enabled:
+        rt.log(f"gradient all-reduce: one-shot IPC {'on' if tr.bucketer.ipc is not None else 'off'} "
+               f"({getattr(tr.bucketer, 'ipc_reason', '')})")
     data = SyntheticMNIST(a.batch_size, rt.rank, rt.world, device=dev, dtype=model_dtype(dev), pool=600)
     steps = max(1, a.train_steps // rt.world)  # train_steps is global (dist_mnist.py:64-69)
     last = simple.run(tr, data, steps, a.log_every, rt.ckpt_dir, a.checkpoint_every, metric_fn=accuracy,

@@ -6,10 +6,14 @@ item 2; replaces the reference's EKS-based E2E):
 * **scheduling**: a pod is bound when its ``amd.com/gpu`` request fits the
   node's free GPUs (each pod gets exclusive device indices, exported as
   ``HIP_VISIBLE_DEVICES`` -- the role the AMD device plugin plays on a real
-  node).  ``device_visibility="node"`` (``TOA_KUBELET_DEVICES=node``) instead
-  leaves every GPU of the node visible and names the pod's device in
+  node).  A pod of the operator's node-local layout (annotation
+  ``amd.com/gpu-visibility=node`` with ``hostIPC``, csrc/core/nodelocal.cc;
+  on a real node its /dev/kfd + /dev/dri host mounts do the same) instead
+  sees every GPU of the node, with its own device named in
   ``TOA_LOCAL_DEVICE``: the single-node data-parallel layout in which RCCL
-  sees all peers and picks its P2P/xGMI transport directly;
+  sees all peers and picks its P2P/xGMI transport directly.
+  ``device_visibility="node"`` (``TOA_KUBELET_DEVICES=node``) forces that
+  view for every pod;
   ``schedulerName: volcano`` pods are gang-admitted only when their
   PodGroup's ``minMember`` pods all fit at once (Volcano semantics);
 * **networking**: every per-replica headless Service name gets a unique
@@ -341,6 +345,19 @@ class LocalKubelet:
         self.running[key] = rec
         rec["task"] = asyncio.create_task(self._run_pod(key, rec))
 
+    def _node_visible(self, pod) -> bool:
+        """Node-wide GPU visibility for this pod: the node is configured that
+        way (TOA_KUBELET_DEVICES=node), or the pod asks for it -- the
+        operator's node-local layout (csrc/core/nodelocal.cc) marks its rank
+        pods with amd.com/gpu-visibility=node next to hostIPC and the
+        /dev/kfd + /dev/dri host mounts that give a real container the same
+        view."""
+        if self.device_visibility == "node":
+            return True
+        md = pod.get("metadata") or {}
+        return ((md.get("annotations") or {}).get("amd.com/gpu-visibility") == "node"
+                and bool((pod.get("spec") or {}).get("hostIPC")))
+
     def _build_env(self, pod, container, gpus):
         env = {}
         for e in container.get("env") or []:
@@ -360,7 +377,7 @@ class LocalKubelet:
         base["TOA_POD_NAMESPACE"] = ns
         base["TOA_NODE_NAME"] = self.node
         base["PYTHONPATH"] = REPO_ROOT + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
-        if gpus and self.device_visibility == "node":
+        if gpus and self._node_visible(pod):
             base.pop("HIP_VISIBLE_DEVICES", None)
             base.pop("TOA_NO_GPU", None)
             base["TOA_LOCAL_DEVICE"] = str(gpus[0])

@@ -49,6 +49,7 @@ class ControllerOptions:
     resync_period: float = 12 * 3600.0    # --resyc-period (12h)
     report_url: str | None = None         # injected as TOA_REPORT_URL
     gpu_resource: str = "amd.com/gpu"
+    gpus_per_node: int = 8                # --gpus-per-node: node-local layout bound (csrc/core/nodelocal.cc)
 
 
 class JobController:
@@ -171,7 +172,7 @@ class JobController:
         o = {"cluster_domain": self.opt.cluster_domain, "enable_gang_scheduling": self.opt.enable_gang_scheduling,
              "gang_scheduler_name": self.opt.gang_scheduler_name, "inject_rocm_env": self.opt.inject_rocm_env,
              "gpu_resource": self.opt.gpu_resource, "previous_retry": self.queue.num_requeues(key),
-             "rccl_defaults": self.opt.rccl_defaults}
+             "rccl_defaults": self.opt.rccl_defaults, "gpus_per_node": self.opt.gpus_per_node}
         env = dict(self.opt.nccl_env)
         if self.opt.report_url:
             env["TOA_REPORT_URL"] = self.opt.report_url

@@ -95,6 +95,9 @@ def build_parser():
     p.add_argument("--cluster-domain", default=os.environ.get("CUSTOM_CLUSTER_DOMAIN", ""))
     p.add_argument("--report-url", default=os.environ.get("TOA_OPERATOR_REPORT_URL"))
     p.add_argument("--gpu-resource", default="amd.com/gpu", help="extended resource name of a GPU")
+    p.add_argument("--gpus-per-node", type=int, default=8,
+                   help="GPUs of one node: a job's RCCL ranks up to this many can run in the node-local "
+                        "xGMI layout (amd.com/node-local annotation, or automatically when gang-scheduled)")
     p.add_argument("--config", default=None, help="optional YAML file with the same keys as the flags")
     return p
 
@@ -144,7 +147,7 @@ class Operator:
             inject_rocm_env=args.inject_rocm_env, cluster_domain=args.cluster_domain, nccl_env=nccl,
             rccl_defaults=args.rccl_defaults,
             resync_period=_duration(str(args.resync_period)), report_url=args.report_url,
-            gpu_resource=args.gpu_resource), self.metrics)
+            gpu_resource=args.gpu_resource, gpus_per_node=args.gpus_per_node), self.metrics)
         self.stop = asyncio.Event()
         self.ready = False
         self.runners = []

@@ -27,6 +27,30 @@ from . import zero
 from .flat import FlatParams, _round_up
 
 
+def ipc_decision(mode: str, world: int, reducing: bool, on_gpu: bool, dist_ready: bool, n_small: int,
+                 local_world_size: str | None):
+    """(use the one-shot IPC all-reduce?, why) -- a pure function of the
+    job's layout, so every rank decides alike."""
+    if mode == "0":
+        return False, "disabled (TOA_IPC_ALLREDUCE=0)"
+    if not reducing:
+        return False, "no all-reduce buckets (single rank or sharded optimizer)"
+    if not dist_ready:
+        return False, "no process group"
+    if mode == "1":
+        return (True, "forced (TOA_IPC_ALLREDUCE=1)") if on_gpu else (False, "forced, but gradients are on the CPU")
+    local = local_world_size is not None and int(local_world_size) == world
+    if not local:
+        return False, f"ranks span nodes (LOCAL_WORLD_SIZE={local_world_size}, world {world})"
+    if not 1 < world <= 8:
+        return False, f"world {world} outside 2..8"
+    if not n_small:
+        return False, "every bucket is above the one-shot size"
+    if not on_gpu:
+        return False, f"eligible ({world} ranks on this node, {n_small} small buckets) but gradients are on the CPU"
+    return True, f"auto: {world} ranks on this node, {n_small} bucket(s) <= {GradBucketer.IPC_MAX_BUCKET >> 20} MB"
+
+
 class GradBucketer:
     """shard=True: reduce-scatter each bucket instead of all-reducing it
     (ZeRO-1, :mod:`tf_operator_amd.parallel.zero`); after finish() this
@@ -61,6 +85,7 @@ class GradBucketer:
         self.pending = [b[2] for b in self.buckets]
         self.works = []
         self.finishers = []
+        self.path_counts = {"oneshot": 0, "collective": 0}  # buckets per path, cumulative
         # with gradient accumulation only the LAST micro-batch's backward may
         # launch collectives (the trainer disarms the others); armed by default
         self.armed = True
@@ -76,20 +101,20 @@ class GradBucketer:
     IPC_MAX_BUCKET = 8 << 20  # bytes: above this RCCL's ring is at bandwidth and wins
 
     def _maybe_ipc(self, group, flat, esz):
-        """TOA_IPC_ALLREDUCE: "auto" (default) = on when the job is one node
-        (LOCAL_WORLD_SIZE == world, <= 8 ranks, RCCL) and at least one bucket
-        is small enough; "1" forces it, "0" disables it.  The decision is the
-        same on every rank (it depends on env and layout only), and a
-        one-time self-check against RCCL turns it off everywhere if the IPC
-        path is unavailable or wrong on this node."""
+        """TOA_IPC_ALLREDUCE: "auto" (default) = on when every rank of the job
+        is on this node (LOCAL_WORLD_SIZE == world: the operator's node-local
+        layout, csrc/core/nodelocal.cc, or torchrun), <= 8 ranks, the
+        gradients live on the GPU, and at least one bucket is small enough;
+        "1" forces it, "0" disables it.  The decision is the same on every
+        rank (it depends on env and layout only; ``self.ipc_reason`` says
+        why), and a one-time self-check against the process group turns it
+        off everywhere if the IPC path is unavailable or wrong on this node."""
         mode = os.environ.get("TOA_IPC_ALLREDUCE", "auto")
-        if mode == "0" or not (self.enabled and not self.shard and flat.grad.is_cuda):
-            return None
-        if not dist.is_initialized():
-            return None
-        local = int(os.environ.get("LOCAL_WORLD_SIZE", self.world)) == self.world
         small = [(e - s) * esz for s, e, _ in self.buckets if (e - s) * esz <= self.IPC_MAX_BUCKET]
-        if mode != "1" and not (_is_nccl(group) and local and 1 < self.world <= 8 and small):
+        ok, self.ipc_reason = ipc_decision(mode, self.world, self.enabled and not self.shard,
+                                           flat.grad.is_cuda, dist.is_initialized(), len(small),
+                                           os.environ.get("LOCAL_WORLD_SIZE"))
+        if not ok:
             return None
         from .ipc import IpcAllReduce
 
@@ -107,6 +132,7 @@ class GradBucketer:
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
         if int(flag.item()) == 1:
             return ipc
+        self.ipc_reason += "; IPC self-check failed on some rank: staying on the process group"
         if ipc is not None:
             try:
                 ipc.close()
@@ -136,7 +162,9 @@ class GradBucketer:
             return
         if self.ipc is not None and self.ipc.fits(view):
             self.ipc(view)  # one-shot on the compute stream: latency-bound small gradients
+            self.path_counts["oneshot"] += 1
             return
+        self.path_counts["collective"] += 1
         self.works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def finish(self):
