@@ -155,3 +155,48 @@ extern "C" int toa_allreduce_oneshot(void* const* bufs, void* const* flags, int 
                        (float*)out, n);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Collective traffic emulator (parallel/emulate.py): what one rank's RCCL
+// reduce-scatter / all-gather kernel does to THIS GPU at world N, on a
+// one-GPU box.  RCCL's ring kernel occupies `nblocks` workgroups (one per
+// channel, 256 threads) for the whole collective, streams (N-1)/N of the
+// bucket through HBM, and lasts as long as the xGMI links need for it.  The
+// emulator moves the same bytes (src -> a scratch dst) with the same
+// workgroup count and paces every workgroup to the link rate: a workgroup
+// that covered `done` bytes of its share waits until t0 + done / rate
+// (s_memrealtime, 100 MHz) before its next 64 KiB chunk.  A workgroup that
+// is dispatched late (CUs held by a GEMM) starts its clock late, so the
+// emulated collective stretches exactly as a real one whose peers wait for
+// this rank would.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void emu_xfer_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       int64_t n16, int64_t ticks_per_mib) {
+  const int64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per;
+  const int64_t hi = lo + per < n16 ? lo + per : n16;
+  constexpr int64_t CHUNK = 4096;  // 16-B vectors: 64 KiB per workgroup step
+  const long long t0 = wall_clock64();
+  for (int64_t c = lo; c < hi; c += CHUNK) {
+    const int64_t e = c + CHUNK < hi ? c + CHUNK : hi;
+    for (int64_t i = c + threadIdx.x; i < e; i += 256) dst[i] = src[i];
+    if (ticks_per_mib > 0) {
+      // bytes of this workgroup's share done so far -> earliest allowed time
+      const long long due = t0 + (long long)(((e - lo) * 16 * ticks_per_mib) >> 20);
+      while (wall_clock64() < due) __builtin_amdgcn_s_sleep(8);
+    }
+  }
+}
+
+// Move `nbytes` (multiple of 16) from src to dst on `nblocks` workgroups,
+// paced to `gbps` GB/s for the whole transfer (0 = unpaced).
+extern "C" int toa_emulate_xfer(const void* src, void* dst, int64_t nbytes, int nblocks, double gbps,
+                                hipStream_t stream) {
+  if (nbytes <= 0) return 0;
+  if (nbytes % 16 || nblocks <= 0) return (int)hipErrorInvalidValue;
+  // per-workgroup rate = gbps / nblocks; ticks of the 100 MHz clock per MiB of a share
+  const int64_t ticks_per_mib = gbps > 0 ? (int64_t)(1e8 * (double)(1 << 20) * nblocks / (gbps * 1e9)) : 0;
+  hipLaunchKernelGGL(emu_xfer_kernel, dim3(nblocks), dim3(256), 0, stream, (const u32x4*)src, (u32x4*)dst,
+                     nbytes / 16, ticks_per_mib);
+  return (int)hipGetLastError();
+}

@@ -22,6 +22,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
+#include <string>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -173,10 +175,23 @@ extern "C" int toa_gemm_current_algo(int ta, int tb, int64_t m, int64_t n, int64
 // Time every hipBLASLt solution for a form on the given (scratch) buffers and
 // keep the fastest.  Returns 0 and writes the winner's index / ms, the
 // heuristic default's ms, and the number of candidates timed.
+//
+// exclude_streamk: skip stream-K solutions (kernel names with _SK<n>, n > 0).
+// Those run a persistent grid of one workgroup per CU holding the whole
+// register file, so a collective kernel on another stream gets no CU until
+// the GEMM ends -- or, once resident, delays one of the GEMM's workgroups by
+// the collective's whole duration (profiles/r2_sk_contention,
+// profiles/r3_overlap).  The data-parallel (world > 1) policy tunes without them.
+static bool is_streamk(const std::string& kname) {
+  for (size_t p = kname.find("_SK"); p != std::string::npos; p = kname.find("_SK", p + 1))
+    if (p + 3 < kname.size() && kname[p + 3] >= '1' && kname[p + 3] <= '9') return true;
+  return false;
+}
+
 extern "C" int toa_gemm_tune(int ta, int tb, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
                              const void* B, int64_t ldb, void* C, int64_t ldc, float beta, int out_f32,
                              hipStream_t stream, int* best_index, float* best_ms, float* default_ms,
-                             int* n_timed) {
+                             int* n_timed, int exclude_streamk) {
   Ctx& c = ctx();
   std::lock_guard<std::mutex> g(c.mu);
   if (ensure_handle(c)) return 1;
@@ -221,11 +236,13 @@ extern "C" int toa_gemm_tune(int ta, int tb, int64_t m, int64_t n, int64_t k, co
   std::vector<std::pair<float, size_t>> first;
   for (size_t i = 0; i < all.size(); ++i) {
     if (!supported(c, p, all[i].algo, beta)) continue;
+    if (exclude_streamk && is_streamk(hipblaslt_ext::getKernelNameFromAlgo(c.h, all[i].algo))) continue;
     first.emplace_back(time_it(all[i].algo, 2), i);
   }
   std::sort(first.begin(), first.end());
-  float bms = dms;
-  int bidx = dflt.has_algo ? dflt.index : -1;
+  const bool dflt_ok = dflt.has_algo && !(exclude_streamk && is_streamk(hipblaslt_ext::getKernelNameFromAlgo(c.h, dflt.algo)));
+  float bms = dflt_ok ? dms : 1e30f;
+  int bidx = dflt_ok ? dflt.index : -1;
   hipblasLtMatmulAlgo_t balgo = dflt.algo;
   for (size_t j = 0; j < first.size() && j < 8; ++j) {
     const float ms = time_it(all[first[j].second].algo, 10);
@@ -246,4 +263,22 @@ extern "C" int toa_gemm_tune(int ta, int tb, int64_t m, int64_t n, int64_t k, co
   *default_ms = dms;
   *n_timed = (int)first.size();
   return 0;
+}
+
+// Kernel name of the solution a form runs (resolved on first use); "" if
+// the form was never run.  Returns the name's length.
+extern "C" int toa_gemm_kernel_name(int ta, int tb, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
+                                    int64_t ldc, int beta_nz, int out_f32, char* buf, int buflen) {
+  Ctx& c = ctx();
+  std::lock_guard<std::mutex> g(c.mu);
+  auto it = c.plans.find(Key{ta, tb, m, n, k, lda, ldb, ldc, beta_nz, out_f32});
+  std::string name;
+  if (it != c.plans.end() && it->second.has_algo && c.h != nullptr)
+    name = hipblaslt_ext::getKernelNameFromAlgo(c.h, it->second.algo);
+  if (buf != nullptr && buflen > 0) {
+    const size_t nn = std::min((size_t)buflen - 1, name.size());
+    std::memcpy(buf, name.data(), nn);
+    buf[nn] = 0;
+  }
+  return (int)name.size();
 }

@@ -254,3 +254,33 @@ def test_param_checksums_cover_every_element():
         r = p.clone()
         r[(n * 2) // 3] = r[(n * 2) // 3] + 1
         assert param_checksums(r, chunk=1 << 20)[1] != h
+
+
+def test_emulated_world_runs_rank0_zero1_step(monkeypatch):
+    """TOA_EMULATE_WORLD=4 at world 1 (parallel/emulate.py): the trainer
+    runs rank 0's ZeRO-1 step of a world-4 job -- every bucket goes through
+    one emulated reduce-scatter during backward and one emulated all-gather
+    after the update, AdamW touches only rank 0's quarter of each bucket,
+    and the gradient scale is 1/4."""
+    from tf_operator_amd.parallel import zero
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    monkeypatch.setenv("TOA_EMULATE_WORLD", "4")
+    tr = LlamaTrainer("llama-tiny", torch.device("cpu"), micro_batch=2, seq_len=32, lr=1e-2, bucket_mb=0.05,
+                      shard_optimizer=True)
+    b = tr.bucketer
+    assert b.emu is not None and b.world == 4 and b.rank == 0 and b.shard and b.grad_scale == 0.25
+    assert tr.gather is not None and tr.gather.emu is b.emu
+    nb = len(b.buckets)
+    assert nb > 1
+    before = tr.flat.param.float().clone()
+    tr.step([tr.synthetic_batch()])
+    assert b.emu.calls == 2 * nb  # one reduce-scatter + one all-gather per bucket
+    assert b.path_counts["collective"] == nb
+    changed = (tr.flat.param.float() != before)
+    owned = zero.owned_ranges(b.buckets, 4, 0)
+    mask = torch.zeros_like(changed)
+    for lo, hi in owned:
+        mask[lo:hi] = True
+    assert bool(changed[mask].any()) and not bool(changed[~mask].any())
+    assert tr.flat.master.numel() == sum(hi - lo for lo, hi in owned)

@@ -12,12 +12,23 @@ transposition algebra).  The per-form solution table measured by
 with) and installed once per process; untuned forms use the library
 heuristic.
 
-Default: OFF (``TOA_GEMM=torch``).  Measured on the MI355X (profiles/
-r1_gemm_tuning*.log, r1_gemm_ab_*.log): the per-form winners are 2-22 %
-faster in isolation, hot or cold cache, yet the full Llama-3-8B step is
-~1.3 % SLOWER with them (787.8 vs 777.1 ms, same box, back to back) -- a
-solution picked alone is not the best one in the sustained, power-limited
-sequence of the real step.  ``TOA_GEMM=tuned`` opts in.
+Modes (``TOA_GEMM``):
+
+* ``torch`` (default at world 1): torch.matmul, i.e. hipBLASLt's own
+  heuristic.  Measured on the MI355X (profiles/r1_gemm_tuning*.log,
+  r1_gemm_ab_*.log): per-form winners picked in isolation are 2-22 % faster
+  alone, yet the full Llama-3-8B step was ~1.3 % SLOWER with them -- a
+  solution picked alone is not the best one in the sustained, power-limited
+  sequence of the real step.
+* ``tuned``: the measured per-form table (``gemm_tuning_gfx950.json``).
+* ``nosk``: the fastest solution per form among those that are NOT
+  stream-K (``gemm_tuning_gfx950_nosk.json``, ``scripts/tune_gemm.py
+  --exclude-streamk``).  hipBLASLt's stream-K kernels run one persistent
+  workgroup per CU holding the whole register file: a collective on another
+  stream either gets no CU until the GEMM ends or, once resident, holds
+  back one of the GEMM's workgroups for its whole duration
+  (profiles/r2_sk_contention, profiles/r3_overlap).  This is the policy for
+  data-parallel steps whose reduce-scatter / all-gather overlap the GEMMs.
 """
 from __future__ import annotations
 
@@ -29,9 +40,24 @@ import torch
 
 from . import _lib
 
-TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning_gfx950.json")
+_HERE = os.path.dirname(os.path.abspath(__file__))
+TABLE = os.path.join(_HERE, "gemm_tuning_gfx950.json")
+TABLE_NOSK = os.path.join(_HERE, "gemm_tuning_gfx950_nosk.json")
 _MODE = os.environ.get("TOA_GEMM", "torch")
 _installed = False
+
+
+def mode() -> str:
+    return _MODE
+
+
+def set_mode(m: str):
+    """Select the GEMM policy for this process (before the first GEMM)."""
+    global _MODE, _installed
+    if m not in ("torch", "tuned", "nosk"):
+        raise ValueError(f"unknown GEMM mode {m!r}")
+    _MODE = m
+    _installed = False
 
 
 def hipblaslt_build() -> str:
@@ -48,9 +74,10 @@ def _install():
     if _installed:
         return
     _installed = True
-    if not os.path.exists(TABLE):
+    table = TABLE_NOSK if _MODE == "nosk" else TABLE
+    if not os.path.exists(table):
         return
-    with open(TABLE) as f:
+    with open(table) as f:
         tab = json.load(f)
     if tab.get("hipblaslt") != hipblaslt_build():
         return
@@ -61,7 +88,7 @@ def _install():
 
 
 def _ok(*ts):
-    if _MODE not in ("tuned", "auto") or not _lib.has("toa_gemm"):
+    if _MODE not in ("tuned", "nosk") or not _lib.has("toa_gemm"):
         return False
     for t in ts:
         if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
@@ -174,16 +201,28 @@ def form_keys(T: int, shapes: dict) -> list:
     for name, (K, N) in shapes.items():
         out.append((name, "fwd", (1, 0, N, T, K, K, K, N, 0)))
         out.append((name, "dgrad", (0, 0, K, T, N, K, N, K, 0)))
+        # dgrad on the transposed weight copy (ops/wt.py, the default): the forward's form
+        out.append((name, "dgrad_wt", (1, 0, K, T, N, N, N, K, 0)))
         out.append((name, "wgrad", (0, 1, K, N, T, K, N, K, 1)))
     return out
+
+
+def kernel_name(key) -> str:
+    """hipBLASLt kernel a form currently runs through this layer ("" if none)."""
+    if not _lib.has("toa_gemm_kernel_name"):
+        return ""
+    buf = ctypes.create_string_buffer(512)
+    _lib.call_ret("toa_gemm_kernel_name", *key, 0, buf, 512)
+    return buf.value.decode(errors="replace")
 
 
 def current_algo(key) -> int:
     return _lib.call_ret("toa_gemm_current_algo", *key, 0) if _lib.has("toa_gemm_current_algo") else -1
 
 
-def tune_form(key, device="cuda"):
-    """Time all hipBLASLt solutions for one form on scratch buffers."""
+def tune_form(key, device="cuda", exclude_streamk=False):
+    """Time all hipBLASLt solutions for one form on scratch buffers
+    (optionally only the non-stream-K ones)."""
     ta, tb, m, n, k, lda, ldb, ldc, beta_nz = key
     a_rows, a_cols = (m, k) if not ta else (k, m)   # column-major op(A) source dims
     b_rows, b_cols = (k, n) if not tb else (n, k)
@@ -195,7 +234,7 @@ def tune_form(key, device="cuda"):
     bi, bms, dms, nt = ctypes.c_int(-1), ctypes.c_float(0), ctypes.c_float(0), ctypes.c_int(0)
     rc = _lib.call_ret("toa_gemm_tune", ta, tb, m, n, k, _lib.ptr(A), lda, _lib.ptr(B), ldb, _lib.ptr(C), ldc,
                        float(beta_nz), 0, _lib.stream(C), ctypes.byref(bi), ctypes.byref(bms), ctypes.byref(dms),
-                       ctypes.byref(nt))
+                       ctypes.byref(nt), int(bool(exclude_streamk)))
     if rc != 0:
         raise RuntimeError(f"toa_gemm_tune failed ({rc}) for {key}")
     return bi.value, bms.value, dms.value, nt.value

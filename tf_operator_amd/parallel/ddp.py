@@ -23,7 +23,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from . import zero
+from . import emulate, zero
 from .flat import FlatParams, _round_up
 
 
@@ -57,11 +57,19 @@ class GradBucketer:
     rank holds the summed gradient of ``owned`` only.  Falls back to
     all-reduce when the world size does not divide the buckets."""
 
-    def __init__(self, flat: FlatParams, bucket_bytes=None, group=None, average=True, enabled=None, shard=False):
+    def __init__(self, flat: FlatParams, bucket_bytes=None, group=None, average=True, enabled=None, shard=False,
+                 emulate_world=None):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # TOA_EMULATE_WORLD=N at world 1: run rank 0's world-N step, its
+        # collectives replaced by paced traffic on this GPU (parallel/emulate.py)
+        self.emu = None
+        ew = emulate.world_from_env() if emulate_world is None else int(emulate_world)
+        if self.world == 1 and ew > 1:
+            self.emu = emulate.CommEmulator(ew, flat.grad.device)
+            self.world = ew
         self.enabled = (self.world > 1) if enabled is None else enabled
         self.average = average
         mb = float(os.environ.get("TOA_BUCKET_MB", "512"))
@@ -109,6 +117,9 @@ class GradBucketer:
         rank (it depends on env and layout only; ``self.ipc_reason`` says
         why), and a one-time self-check against the process group turns it
         off everywhere if the IPC path is unavailable or wrong on this node."""
+        if self.emu is not None:
+            self.ipc_reason = "collectives emulated (TOA_EMULATE_WORLD)"
+            return None
         mode = os.environ.get("TOA_IPC_ALLREDUCE", "auto")
         small = [(e - s) * esz for s, e, _ in self.buckets if (e - s) * esz <= self.IPC_MAX_BUCKET]
         ok, self.ipc_reason = ipc_decision(mode, self.world, self.enabled and not self.shard,
@@ -154,6 +165,12 @@ class GradBucketer:
         self.launched[b] = True
         s, e, _ = self.buckets[b]
         view = self.flat.grad[s:e]
+        if self.emu is not None:
+            # a reduce-scatter moves (N-1)/N of the bucket; a ring all-reduce twice that
+            for _ in range(1 if self.shard else 2):
+                self.works.append(self.emu.collective(view))
+            self.path_counts["collective"] += 1
+            return
         if self.shard:
             w, fin = zero.reduce_scatter_(view, self.rank, self.world, self.group)
             self.works.append(w)

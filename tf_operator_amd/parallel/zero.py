@@ -80,8 +80,9 @@ class ParamGather:
     """In-place all-gather of the updated bf16 weights after a sharded
     optimizer step, waited for per bucket by the next forward."""
 
-    def __init__(self, flat, buckets, rank, world, group=None, on_gathered=None):
+    def __init__(self, flat, buckets, rank, world, group=None, on_gathered=None, emulator=None):
         self.flat = flat
+        self.emu = emulator  # parallel/emulate.CommEmulator: paced traffic instead of RCCL (world 1)
         self.ranges = [(b[0], b[1]) for b in buckets]
         self.rank, self.world, self.group = rank, world, group
         self.on_gathered = on_gathered  # fn(lo, hi) on the waiting stream (W^T refresh)
@@ -91,6 +92,9 @@ class ParamGather:
         # flat order is backward order: the forward needs the last bucket first
         for b in reversed(range(len(self.ranges))):
             lo, hi = self.ranges[b]
+            if self.emu is not None:
+                self.works[b] = self.emu.collective(self.flat.param[lo:hi])
+                continue
             self.works[b] = all_gather_(self.flat.param[lo:hi], self.rank, self.world, self.group)
 
     def wait(self, b):

@@ -66,7 +66,7 @@ class LlamaTrainer:
             self.flat.shard_state(self.bucketer.owned)
             self.opt = FlatAdamW(self.flat, lr=lr, owned=self.bucketer.owned)
             self.gather = ParamGather(self.flat, self.bucketer.buckets, self.bucketer.rank, self.bucketer.world,
-                                      on_gathered=self.wt.refresh if self.wt else None)
+                                      on_gathered=self.wt.refresh if self.wt else None, emulator=self.bucketer.emu)
         else:
             if overlap_optimizer is None:
                 overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
