@@ -45,8 +45,10 @@ def _check(r, n):
     assert r["config"]["parallelism"] == f"dp{n}" and r["config"]["global_batch"] == 2 * n
     assert r["replicas_identical"] is True
     assert r["value"] > 0 and r["steps"] == 3 and r["warmup"] == 1
-    assert set(r["startup_phases_s"]) == {"process_start->imports", "imports->dist_init", "dist_init->model_init",
-                                          "model_init->first_step"}
+    phases = {"process_start->imports", "imports->dist_init", "dist_init->model_init", "model_init->first_step"}
+    if r["config"]["launched_by"] == "torchrun":  # rank 0's probe phase is its own field, not part of start-up
+        phases = (phases - {"process_start->imports"}) | {"process_start->probes_done", "probes_done->imports"}
+    assert set(r["startup_phases_s"]) == phases
     lat = r["submit_to_first_step"]
     assert "error" not in lat and r.get("submit_to_first_step_p50_s", 0) > 0, lat
     assert lat["breakdown_p50_s"]["submit_to_pods_created"] < r["submit_to_first_step_p50_s"]
@@ -54,14 +56,22 @@ def _check(r, n):
 
 @pytest.mark.timeout(600)
 def test_bench_launcher_two_workers_through_operator():
-    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1"], cwd=ROOT,
-                       env=_env(), capture_output=True, text=True, timeout=580)
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1", "--cold-probes",
+                        "1"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=580)
     assert p.returncode == 0, p.stderr[-4000:]
     r = _json_line(p.stdout)
     _check(r, 2)
     assert r["config"]["launched_by"] == "operator"
-    assert len(r["submit_to_first_step"]["samples_s"]) == 2  # 1 probe + the benchmark job itself
-    assert r["submit_to_first_step"]["replica_start"].startswith("warm")  # the default
+    lat = r["submit_to_first_step"]
+    assert len(lat["samples_s"]) == 2  # 1 probe + the benchmark job itself
+    assert lat["replica_start"].startswith("warm")  # the default
+    # every probe's own breakdown is in the record, and a cold-process probe set beside the warm one
+    assert [pr["submit_to_first_step_s"] for pr in lat["probes"]] == lat["samples_s"]
+    assert all("replica_phases_s" in pr and "spawn_to_first_step_s" in pr for pr in lat["probes"])
+    assert r["submit_to_first_step_cold_p50_s"] > 0
+    cold = r["submit_to_first_step_cold"]
+    assert cold["replica_start"] == "cold process" and len(cold["probes"]) == 1
+    assert cold["probes"][0]["replica_phases_s"]["process_start->runtime"] > 0.2  # paid its own imports
     assert "ZeRO-1" in r["config"]["optimizer"]
 
 
@@ -70,7 +80,8 @@ def test_bench_launcher_cold_start():
     """--warm-start 0: every replica is a fresh python process (its import
     phase is paid inside submit -> first step); the default forks the
     kubelet's warm interpreter, whose import phase is near zero."""
-    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1", "--warm-start", "0"],
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1", "--warm-start", "0",
+                        "--cold-probes", "0"],
                        cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=580)
     assert p.returncode == 0, p.stderr[-4000:]
     r = _json_line(p.stdout)
@@ -82,7 +93,8 @@ def test_bench_launcher_cold_start():
 @pytest.mark.timeout(600)
 def test_bench_under_torchrun_probes_first():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1"]
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", *TINY, "--latency-probes", "1",
+           "--cold-probes", "0"]
     p = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=580)
     assert p.returncode == 0, p.stderr[-4000:]
     r = _json_line(p.stdout)

@@ -62,6 +62,9 @@ def parser() -> argparse.ArgumentParser:
                     help="sharded optimizer (reduce-scatter / owned-shard AdamW / all-gather); auto = on for N > 1")
     ap.add_argument("--latency-probes", type=int, default=3,
                     help="TFJobs submitted (and timed submit -> first step) before the throughput run; 0 = skip")
+    ap.add_argument("--cold-probes", type=int, default=2,
+                    help="extra probe TFJobs whose replicas start as cold processes (a real kubelet's start), "
+                         "reported as submit_to_first_step_cold_p50_s; 0 = skip")
     ap.add_argument("--probe-timeout", type=float, default=180.0, help="per probe job (s)")
     ap.add_argument("--warm-start", choices=("0", "1"), default="1",
                     help="replicas start as forks of the local kubelet's warm interpreter (torch pre-imported, "
@@ -86,10 +89,11 @@ def main(argv=None, t_proc_start=None) -> int:
     m = "replica" if args.direct else mode()
     if m == "launcher":
         return run_launcher(args)
-    probe = None
+    probe, t_probes_done = None, None
     if m == "torchrun" and args.latency_probes > 0:
         probe = _torchrun_probe_phase(args)
-    return run_replica(args, t_proc_start, probe=probe, launched_by=m)
+        t_probes_done = time.time()
+    return run_replica(args, t_proc_start, probe=probe, launched_by=m, t_probes_done=t_probes_done)
 
 
 # =============================================================================
@@ -100,11 +104,13 @@ def _payload(args) -> list[str]:
             "--seq-len", str(args.seq_len), "--micro-batch", str(args.micro_batch)]
 
 
-def _tfjob(name: str, n: int, command: list[str], env: dict | None = None) -> dict:
+def _tfjob(name: str, n: int, command: list[str], env: dict | None = None, cold: bool = False) -> dict:
     from ..sdk import container, pod_template
 
     tpl = pod_template(container(image="toa/trainer:latest", command=command, gpus=1,
                                  env={"OMP_NUM_THREADS": "8", **(env or {})}))
+    if cold:  # local kubelet: start this pod's replicas as fresh processes, not warm forks
+        tpl.setdefault("metadata", {}).setdefault("annotations", {})["training.amd.com/start"] = "cold"
     # node-local xGMI layout (csrc/core/nodelocal.cc): the ranks share one
     # node, see each other's GPUs and get LOCAL_RANK / LOCAL_WORLD_SIZE of it
     return {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
@@ -188,12 +194,12 @@ def wait_vram_settled(timeout: float = 120.0, window: float = 2.0, tol: int = 1 
 
 
 def _run_job(c, name: str, n: int, command: list[str], timeout: float, env=None,
-             vram_baseline: int | None = None) -> dict:
+             vram_baseline: int | None = None, cold: bool = False) -> dict:
     """Submit one TFJob Worker=n, wait for it to succeed; return the client
     clock from create() to rank 0's first step plus the breakdown."""
     key = ("default", name)
     t0 = time.time()
-    c.client.create(_tfjob(name, n, command, env))
+    c.client.create(_tfjob(name, n, command, env, cold=cold))
     t_pods = c.wait(lambda: len(c.pods(labels={"job-name": name})) >= n and time.time(), timeout, 0.005,
                     f"{name}: pods created")
 
@@ -277,31 +283,42 @@ def probe_latency(args, n: int, c=None) -> dict:
     own = c is None
     if own:
         c = _cluster(n, args.warm_start == "1")
-    samples, err = [], None
+    samples, cold, err = [], [], None
     settle_s = wait_vram_settled()  # a clean drain baseline
     base = vram_used_bytes()
     start_mode = _start_mode(c)
+    plan = [(f"probe-{i}", False, samples) for i in range(args.latency_probes)]
+    plan += [(f"probe-cold-{i}", True, cold) for i in range(getattr(args, "cold_probes", 0))]
     try:
-        for i in range(args.latency_probes):
+        for name, is_cold, into in plan:
             try:
-                s = _run_job(c, f"probe-{i}", n, _payload(args), args.probe_timeout, vram_baseline=base)
+                s = _run_job(c, name, n, _payload(args), args.probe_timeout, vram_baseline=base, cold=is_cold)
             except Exception as e:  # keep the throughput run alive; report why latency is missing
                 err = f"{type(e).__name__}: {str(e)[:2000]}"
                 break
             s.pop("_logs", None)
-            samples.append(s)
-            print(f"[bench] probe {i}: submit->first-step {s['submit_to_first_step_s']:.3f}s", file=sys.stderr,
+            s["replica_start"] = "cold process" if is_cold else start_mode
+            into.append(s)
+            print(f"[bench] {name}: submit->first-step {s['submit_to_first_step_s']:.3f}s", file=sys.stderr,
                   flush=True)
     finally:
         if own:
             c.stop()
     out = _summary(samples)
     out["_raw"] = samples
+    out["_cold"] = cold
     out["replica_start"] = start_mode
     out["node_settle_before_probes_s"] = settle_s
     if err:
         out["error"] = err
     return out
+
+
+def _probe_record(s: dict) -> dict:
+    """One probe's breakdown for the JSON line (the clock and every phase)."""
+    keep = ("submit_to_first_step_s", "submit_to_pods_created_s", "submit_to_processes_spawned_s",
+            "spawn_to_first_step_s", "node_drain_s", "replica_phases_s", "replica_start")
+    return {k: s[k] for k in keep if k in s}
 
 
 def _torchrun_probe_phase(args) -> dict | None:
@@ -372,8 +389,15 @@ def summarize_rccl_log(path: str | None) -> dict | None:
     return {"version": ver, "channel_connections_by_transport": trans, "coll_channels": nch, "log": path}
 
 
-def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_by: str = "replica") -> int:
+def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_by: str = "replica",
+                t_probes_done: float | None = None) -> int:
+    """t_probes_done: under torchrun rank 0 ran the latency probes before
+    this replica started its own work; that phase is reported on its own
+    (``startup_phases_s["process_start->probes_done"]``) and the replica's
+    first_step_s is counted from its end."""
     phases = {"process_start": t_proc_start}
+    if t_probes_done is not None:
+        phases["probes_done"] = t_probes_done
     rccl_log = _rccl_log_setup(args, launched_by)
     # the RCCL defaults the operator injects into every trainer pod
     # (csrc/core/envgen.cc kRcclDefaults), also under torchrun: collective
@@ -451,7 +475,8 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
     samples_s = global_batch * args.steps / dt if dt > 0 else 0.0
     tokens_s = samples_s * args.seq_len
     flops = tr.cfg.flops_per_token(args.seq_len) * tokens_s
-    order = ["process_start", "imports", "dist_init", "model_init", "first_step"]
+    order = ["process_start"] + (["probes_done"] if "probes_done" in phases else []) + [
+        "imports", "dist_init", "model_init", "first_step"]
     startup = {f"{a}->{b}": round(phases[b] - phases[a], 3) for a, b in zip(order, order[1:])}
     on_gpu = dev.type == "cuda"
     rc = 0
@@ -488,7 +513,7 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
             "backend": backend,
             "tokens_per_sec": round(tokens_s, 1),
             "model_tflops_per_gpu": round(flops / n_gpus / 1e12, 1),
-            "first_step_s": round(phases["first_step"] - t_proc_start, 2),
+            "first_step_s": round(phases["first_step"] - phases.get("probes_done", t_proc_start), 2),
             "startup_phases_s": startup,
             "loss": round(loss_v, 4),
             "loss_max_over_ranks": round(loss_max, 4),
@@ -514,9 +539,18 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
 def _attach_probe(out: dict, probe: dict):
     if probe.get("p50_s") is not None:
         out["submit_to_first_step_p50_s"] = probe["p50_s"]
-    out["submit_to_first_step"] = {k: v for k, v in probe.items() if k not in ("p50_s", "_raw")}
+    out["submit_to_first_step"] = {k: v for k, v in probe.items() if k not in ("p50_s", "_raw", "_cold")}
     if probe.get("replica_start"):
         out["submit_to_first_step"]["replica_start"] = probe["replica_start"]
+    # every probe's own breakdown (no logs): an outlier is explained in the record itself
+    out["submit_to_first_step"]["probes"] = [_probe_record(s) for s in probe.get("_raw", [])]
+    cold = probe.get("_cold") or []
+    if cold:
+        cs = _summary(cold)
+        out["submit_to_first_step_cold_p50_s"] = cs["p50_s"]
+        out["submit_to_first_step_cold"] = {"samples_s": cs["samples_s"], "breakdown_p50_s": cs["breakdown_p50_s"],
+                                            "replica_start": "cold process",
+                                            "probes": [_probe_record(s) for s in cold]}
 
 
 # =============================================================================
@@ -559,6 +593,9 @@ def run_launcher(args) -> int:
     if probe.get("error"):
         p["error"] = probe["error"]
     p["bench_job_submit_to_first_step_s"] = job["submit_to_first_step_s"]
+    job["replica_start"] = start_mode
+    p["_raw"] = list(probe.get("_raw", [])) + [job]
+    p["_cold"] = probe.get("_cold", [])
     p["replica_start"] = start_mode
     if "node_settle_before_probes_s" in probe:
         p["node_settle_before_probes_s"] = probe["node_settle_before_probes_s"]
