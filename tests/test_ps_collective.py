@@ -67,16 +67,18 @@ def _proc(rank, workers, servers, mode, port, out):
         else:
             tr = simple.PSTrainer(model, loss_fn, _RT(), workers, servers, mode=mode, lr=LR, bucket_mb=0.0005)
             x, y = _data(rank)
-            for _ in range(STEPS):
-                tr.step(x, y)
-            res = {"param": tr.flat.param.clone(), "nbuckets": len(tr.ps.buckets), "pieces": len(tr.ps.pieces)}
+            losses = [float(tr.step(x, y)[0]) for _ in range(STEPS)]
+            pending = len(tr.ps.pulls)  # sync: the last pull is still in flight when step() returns
+            tr.sync_params()
+            res = {"param": tr.flat.param.clone(), "nbuckets": len(tr.ps.buckets), "pieces": len(tr.ps.pieces),
+                   "losses": losses, "pending_after_step": pending}
         torch.save(res, f"{out}.{rank}")
     finally:
         dist.destroy_process_group()
 
 
-def _run(tmp_path, workers, servers, mode):
-    out = str(tmp_path / "r")
+def _run(tmp_path, workers, servers, mode, tag="r"):
+    out = str(tmp_path / tag)
     mp.spawn(_proc, args=(workers, servers, mode, _free_port(), out), nprocs=workers + servers, join=True)
     return [torch.load(f"{out}.{r}", weights_only=True) for r in range(workers + servers)]
 
@@ -108,6 +110,22 @@ def test_sync_ps_matches_mean_gradient_adam(tmp_path, servers):
         r = res[workers + s]
         assert r["updates"] == STEPS
         assert torch.allclose(r["param"], ref[r["lo"]:r["hi"]], atol=1e-6, rtol=1e-5)
+
+
+def test_sync_ps_async_pull_keeps_loss_trajectory(tmp_path, monkeypatch):
+    """PS=1 Worker=2: the parameter pull issued asynchronously and waited
+    per bucket by the next forward gives exactly the losses and weights of
+    the blocking pull (TOA_PS_BLOCKING_PULL=1), and step() really returns
+    with the pull still in flight."""
+    workers, servers = 2, 1
+    asyn = _run(tmp_path, workers, servers, "sync", tag="a")
+    monkeypatch.setenv("TOA_PS_BLOCKING_PULL", "1")
+    block = _run(tmp_path, workers, servers, "sync", tag="b")
+    for w in range(workers):
+        assert asyn[w]["losses"] == block[w]["losses"], w
+        assert torch.equal(asyn[w]["param"], block[w]["param"]), w
+        assert asyn[w]["pending_after_step"] > 0 and block[w]["pending_after_step"] == 0
+    assert asyn[0]["losses"][-1] < asyn[0]["losses"][0]
 
 
 def test_async_ps_applies_every_push(tmp_path):

@@ -19,8 +19,13 @@ wire is xGMI.
   backward each gradient bucket is ``reduce``-d (SUM) onto the PS owning
   it, bucket by bucket in flat order as the buckets complete -- the same
   backward overlap as the all-reduce path.  The PS applies one AdamW step
-  with the mean and ``broadcast``-s its bf16 shard back.  One collective
-  group per PS (the W workers + that PS).
+  with the mean and ``broadcast``-s its shard back, piece by piece (a
+  bucket's part on that server) in FORWARD order.  The workers issue the
+  matching broadcasts asynchronously at the end of their step and return;
+  the next forward waits per bucket in module pre-hooks
+  (:meth:`CollectivePS.wait_bucket`), so the pull of late layers runs under
+  the compute of early ones (``TOA_PS_BLOCKING_PULL=1``: wait at the end of
+  the step instead).  One collective group per PS (the W workers + that PS).
 * **async**: every worker ``isend``-s its gradient shard to each PS and
   ``irecv``-s the parameters back; each PS polls one pending ``irecv`` per
   worker and applies every gradient as it arrives (stale by whatever the
@@ -119,6 +124,11 @@ class CollectivePS:
         self.groups = [dist.new_group(list(range(self.W)) + [self.W + p]) for p in range(self.P)]
         self.buckets = flat_buckets(flat, bucket_mb)
         self.pieces = bucket_pieces(self.buckets, self.ranges)
+        # the parameter pull, piece by piece in forward order (flat order is
+        # backward order: the forward needs the last bucket first)
+        self.pull_order = sorted(self.pieces, key=lambda t: (-t[0], t[1]))
+        self.pulls = {}
+        self.blocking_pull = os.environ.get("TOA_PS_BLOCKING_PULL", "0") == "1"
         # everyone starts from worker 0's weights
         dist.broadcast(flat.param, 0)
         self.updates = 0
@@ -172,11 +182,16 @@ class CollectivePS:
             while self.next_bucket < len(self.buckets):  # buckets whose params got no gradient
                 self._launch(self.next_bucket)
                 self.next_bucket += 1
-            for w in self.works:
+            for w in self.works:  # the next backward overwrites these gradients
                 w.wait()
-            for p, (lo, hi) in enumerate(self.ranges):
-                dist.broadcast(f.param[lo:hi], self.W + p, group=self.groups[p])
             self._reset()
+            for (b, p, lo, hi) in self.pull_order:
+                self.pulls.setdefault(b, []).append(
+                    dist.broadcast(f.param[lo:hi], self.W + p, group=self.groups[p], async_op=True))
+            if self.blocking_pull:
+                self.wait_params()
+            self.updates += 1
+            return
         else:
             works = []
             for p, (lo, hi) in enumerate(self.ranges):
@@ -186,6 +201,21 @@ class CollectivePS:
                 w.wait()
         self.updates += 1
         f.params_changed()
+
+    def wait_bucket(self, b: int):
+        """Block until bucket b's fresh parameters have arrived (sync mode;
+        RCCL: the current stream waits, the host does not)."""
+        works = self.pulls.pop(b, None)
+        if not works:
+            return
+        for w in works:
+            w.wait()
+        if not self.pulls:
+            self.flat.params_changed()
+
+    def wait_params(self):
+        for b in list(self.pulls):
+            self.wait_bucket(b)
 
     # ------------------------------------------------------------------ server
     @torch.no_grad()
@@ -208,7 +238,11 @@ class CollectivePS:
             for w in works:
                 w.wait()
             self.opt.step(grad_scale=1.0 / self.W)  # SyncReplicas: the mean of W gradients
-            dist.broadcast(f.param[lo:hi], self.rank, group=self.groups[p])
+            # the same pieces, in the same (forward) order as the workers' pulls
+            outs = [dist.broadcast(f.param[a:bb], self.rank, group=self.groups[p], async_op=True)
+                    for (_, pp, a, bb) in self.pull_order if pp == p]
+            for w in outs:
+                w.wait()
             self.updates += 1
 
     def _serve_async(self, steps):

@@ -179,6 +179,24 @@ class PSTrainer:
         attach_autograd_hooks(self.flat)
         self.ps = CollectivePS(self.flat, workers, servers, mode=mode, lr=lr, bucket_mb=bucket_mb)
         self.step_idx = 0
+        # the next forward waits, module by module, only for the buckets holding
+        # its own parameters (the asynchronous parameter pull of sync mode)
+        def waiter(buckets):
+            def hook(mod, args):
+                for b in buckets:
+                    self.ps.wait_bucket(b)
+            return hook
+
+        self._hooks = []
+        for mod in model.modules():
+            bs = sorted({p._toa_bucket for p in mod.parameters(recurse=False) if hasattr(p, "_toa_bucket")})
+            if bs:
+                self._hooks.append(mod.register_forward_pre_hook(waiter(bs)))
+
+    def sync_params(self):
+        """Every parameter current (before reading ``flat.param`` directly:
+        checkpoints, comparisons)."""
+        self.ps.wait_params()
 
     def step(self, x, y):
         self.flat.zero_grad()
