@@ -99,6 +99,20 @@ bool supported(Ctx& c, Plan& p, hipblasLtMatmulAlgo_t& algo, float beta) {
   return ws <= c.ws_size;
 }
 
+// Stream-K solutions (kernel names with _SK<n>, n > 0) run a persistent grid
+// of one workgroup per CU holding the whole register file, so a collective
+// kernel on another stream gets no CU until the GEMM ends -- or, once
+// resident, delays one of the GEMM's workgroups by the collective's whole
+// duration (profiles/r2_sk_contention, profiles/r3_overlap).
+bool is_streamk(const std::string& kname) {
+  for (size_t p = kname.find("_SK"); p != std::string::npos; p = kname.find("_SK", p + 1))
+    if (p + 3 < kname.size() && kname[p + 3] >= '1' && kname[p + 3] <= '9') return true;
+  return false;
+}
+
+// policy: untuned forms take the heuristic's best NON-stream-K solution
+bool g_no_streamk = false;
+
 int resolve(Ctx& c, const Key& k, Plan& p, float beta) {
   if (p.has_algo) return 0;
   auto w = c.wanted.find(k);
@@ -117,12 +131,20 @@ int resolve(Ctx& c, const Key& k, Plan& p, float beta) {
   hipblasLtMatmulPreferenceCreate(&pref);
   uint64_t wsz = c.ws_size;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz, sizeof(wsz));
-  hipblasLtMatmulHeuristicResult_t r[1];
+  hipblasLtMatmulHeuristicResult_t r[16];
   int got = 0;
-  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(c.h, p.desc, p.a, p.b, p.c, p.c, pref, 1, r, &got);
+  hipblasStatus_t st =
+      hipblasLtMatmulAlgoGetHeuristic(c.h, p.desc, p.a, p.b, p.c, p.c, pref, g_no_streamk ? 16 : 1, r, &got);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (st != HIPBLAS_STATUS_SUCCESS || got == 0) return 2;
-  p.algo = r[0].algo;
+  int pick = 0;
+  if (g_no_streamk)
+    for (int i = 0; i < got; ++i)
+      if (!is_streamk(hipblaslt_ext::getKernelNameFromAlgo(c.h, r[i].algo))) {
+        pick = i;
+        break;
+      }
+  p.algo = r[pick].algo;
   p.has_algo = true;
   p.index = hipblaslt_ext::getIndexFromAlgo(p.algo);
   return 0;
@@ -176,18 +198,8 @@ extern "C" int toa_gemm_current_algo(int ta, int tb, int64_t m, int64_t n, int64
 // keep the fastest.  Returns 0 and writes the winner's index / ms, the
 // heuristic default's ms, and the number of candidates timed.
 //
-// exclude_streamk: skip stream-K solutions (kernel names with _SK<n>, n > 0).
-// Those run a persistent grid of one workgroup per CU holding the whole
-// register file, so a collective kernel on another stream gets no CU until
-// the GEMM ends -- or, once resident, delays one of the GEMM's workgroups by
-// the collective's whole duration (profiles/r2_sk_contention,
-// profiles/r3_overlap).  The data-parallel (world > 1) policy tunes without them.
-static bool is_streamk(const std::string& kname) {
-  for (size_t p = kname.find("_SK"); p != std::string::npos; p = kname.find("_SK", p + 1))
-    if (p + 3 < kname.size() && kname[p + 3] >= '1' && kname[p + 3] <= '9') return true;
-  return false;
-}
-
+// exclude_streamk: skip stream-K solutions (is_streamk above); the
+// data-parallel (world > 1) policy tunes without them.
 extern "C" int toa_gemm_tune(int ta, int tb, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
                              const void* B, int64_t ldb, void* C, int64_t ldc, float beta, int out_f32,
                              hipStream_t stream, int* best_index, float* best_ms, float* default_ms,
@@ -281,4 +293,13 @@ extern "C" int toa_gemm_kernel_name(int ta, int tb, int64_t m, int64_t n, int64_
     buf[nn] = 0;
   }
   return (int)name.size();
+}
+
+// Policy for forms without a tuned entry: 1 = the heuristic's best
+// non-stream-K solution (forms already resolved keep theirs).
+extern "C" int toa_gemm_set_no_streamk(int on) {
+  Ctx& c = ctx();
+  std::lock_guard<std::mutex> g(c.mu);
+  g_no_streamk = on != 0;
+  return 0;
 }

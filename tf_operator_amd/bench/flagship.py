@@ -508,6 +508,7 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
                 "launched_by": {"launcher": "operator", "replica": "operator" if os.environ.get("TOA_JOB_NAME")
                                 else "direct", "torchrun": "torchrun"}.get(launched_by, launched_by),
                 "weights": "random-init",
+                "gemm_policy": getattr(tr, "gemm_mode", "torch"),
             },
             "rccl_world": rccl_world,
             "backend": backend,

@@ -23,12 +23,17 @@ Modes (``TOA_GEMM``):
 * ``tuned``: the measured per-form table (``gemm_tuning_gfx950.json``).
 * ``nosk``: the fastest solution per form among those that are NOT
   stream-K (``gemm_tuning_gfx950_nosk.json``, ``scripts/tune_gemm.py
-  --exclude-streamk``).  hipBLASLt's stream-K kernels run one persistent
+  --exclude-streamk``; forms not in the table take the heuristic's best
+  non-stream-K solution).  hipBLASLt's stream-K kernels run one persistent
   workgroup per CU holding the whole register file: a collective on another
   stream either gets no CU until the GEMM ends or, once resident, holds
   back one of the GEMM's workgroups for its whole duration
-  (profiles/r2_sk_contention, profiles/r3_overlap).  This is the policy for
-  data-parallel steps whose reduce-scatter / all-gather overlap the GEMMs.
+  (profiles/r2_sk_contention).  With world-8 ZeRO-1 traffic emulated on
+  one MI355X (profiles/r3_overlap) the collectives cost the stream-K step
+  +6.7 % and the nosk step +3.4 %, at equal step time without traffic.
+* ``auto`` (the default): ``nosk`` when the data-parallel world (real or
+  emulated, parallel/emulate.py) is > 1, else ``torch`` -- resolved by
+  :func:`resolve_auto` when the trainer knows its world.
 """
 from __future__ import annotations
 
@@ -43,7 +48,7 @@ from . import _lib
 _HERE = os.path.dirname(os.path.abspath(__file__))
 TABLE = os.path.join(_HERE, "gemm_tuning_gfx950.json")
 TABLE_NOSK = os.path.join(_HERE, "gemm_tuning_gfx950_nosk.json")
-_MODE = os.environ.get("TOA_GEMM", "torch")
+_MODE = os.environ.get("TOA_GEMM", "auto")
 _installed = False
 
 
@@ -54,10 +59,18 @@ def mode() -> str:
 def set_mode(m: str):
     """Select the GEMM policy for this process (before the first GEMM)."""
     global _MODE, _installed
-    if m not in ("torch", "tuned", "nosk"):
+    if m not in ("auto", "torch", "tuned", "nosk"):
         raise ValueError(f"unknown GEMM mode {m!r}")
     _MODE = m
     _installed = False
+
+
+def resolve_auto(world: int) -> str:
+    """``auto`` -> ``nosk`` for a data-parallel world > 1, else ``torch``
+    (an explicit TOA_GEMM is kept).  Returns the mode in force."""
+    if _MODE == "auto":
+        set_mode("nosk" if world > 1 else "torch")
+    return _MODE
 
 
 def hipblaslt_build() -> str:
@@ -74,6 +87,8 @@ def _install():
     if _installed:
         return
     _installed = True
+    if _lib.has("toa_gemm_set_no_streamk"):
+        _lib.call("toa_gemm_set_no_streamk", int(_MODE == "nosk"))
     table = TABLE_NOSK if _MODE == "nosk" else TABLE
     if not os.path.exists(table):
         return

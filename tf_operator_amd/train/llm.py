@@ -60,6 +60,10 @@ class LlamaTrainer:
         # RCCL world-1 test drives the real reduce-scatter / all-gather path)
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20),
                                      shard=shard_optimizer, enabled=True if force_collectives else None)
+        # GEMM policy: no stream-K kernels when collectives overlap the GEMMs (ops/gemm.py)
+        from ..ops import gemm as _gemm
+
+        self.gemm_mode = _gemm.resolve_auto(self.bucketer.world if self.bucketer.enabled else 1)
         self.gather = None
         if self.bucketer.shard:  # ZeRO-1: reduce-scatter, owned-shard AdamW, in-place all-gather
             # fp32 master / m / v only for the owned shards: 12 B/param x (1 - 1/world) of HBM freed
