@@ -1,0 +1,311 @@
+// Forward / data-gradient GEMM on MFMA (the "TN" form) with fused epilogues:
+//
+//     C[M][N] = sum_k A[m][k] * B[n][k]          (bf16 in, fp32 accumulate)
+//
+// A = X [M][K] (row stride lda), B = W [N][K] (ldb): y = x W^T, and the data
+// gradient on the transposed weight copy (ops/wt.py) has the same form.
+// Both operands are contiguous along the reduction, so every MFMA operand
+// fragment is ONE ds_read_b128 of a row (the weight-gradient kernel,
+// wgrad.hip, needs two transposed reads per fragment).
+//
+//   workgroup: 8 waves (2 M x 4 N), tile 256 x 256, 32 k per phase, 4 LDS
+//              stages filled by global_load_lds two phases ahead, the two
+//              wave rows staggered by one barrier (guide §5 template)
+//   wave:      128 x 64 of C = 8 x 4 v_mfma_f32_16x16x32_bf16 tiles
+//   operands:  swapped (B fragment first): each lane's accumulator holds 4
+//              consecutive n of one row m -> 8-byte stores
+//   grid:      one workgroup per tile, not persistent: a collective kernel
+//              on another stream takes CUs as tiles retire (parallel/zero.py,
+//              profiles/r3_overlap) instead of waiting for the whole GEMM
+//
+// Epilogues (the element-wise work the Llama MLP does around these GEMMs):
+//   TN_PLAIN        C (bf16)
+//   TN_SWIGLU_FWD   gate|up projection: the workgroup's 256 columns are 128
+//                   gate columns [c, c+128) and the SAME 128 up columns
+//                   [F+c, F+c+128) (the B-row map below; W keeps its [gate |
+//                   up] layout), each wave holding 32 gate + 32 up columns of
+//                   the same 32 hidden units, so it writes gu (saved for
+//                   backward) AND s = silu(gate) * up for the down projection
+//                   -- no separate SwiGLU pass re-reading gu
+//   TN_SWIGLU_BWD   data gradient of the down projection: C = ds is never
+//                   stored; the epilogue reads gate / up from gu and writes
+//                   dgu = [ds * up * silu'(gate) | ds * silu(gate)]
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "toa_common.h"
+
+#define TN_BM 256
+#define TN_BN 256
+#define TN_BK 32                   // k per stage (one phase)
+#define TN_ROWB 64                 // one LDS row = 32 bf16 of k
+#define TN_TILE (TN_BM * TN_ROWB)  // 16 KiB per operand per stage
+#define TN_STAGE (2 * TN_TILE)
+#define TN_VMCNT0 0x0F70
+#define TN_VMCNT4 0x0F74
+
+enum { TN_PLAIN = 0, TN_SWIGLU_FWD = 1, TN_SWIGLU_BWD = 2 };
+
+typedef __attribute__((ext_vector_type(8))) short tn_s16x8;
+
+// Chunk c (16 B, 0..3) of LDS row r lives at chunk position c ^ tn_f(r).  A
+// fragment read takes chunk (lane >> 4) of rows r0 + (lane & 15): with the XOR
+// the 16 lanes of every ds_read_b128 lane group hit 16 distinct 16-byte bank
+// slots (plain rows are 2-way).
+__device__ __forceinline__ int tn_f(int r) { return ((r >> 3) & 1) << 1; }
+__device__ __forceinline__ int tn_off(int r, int c) { return r * TN_ROWB + ((c ^ tn_f(r)) << 4); }
+
+// 16x16x32 operand fragment of rows row0..row0+15, all 32 k of the stage:
+// lane l gets image[row0 + (l & 15)][8 (l >> 4) .. +7].
+__device__ __forceinline__ tn_s16x8 tn_frag(const char* img, int row0, int lane) {
+  const int r = row0 + (lane & 15);
+  return *(const tn_s16x8*)(img + tn_off(r, lane >> 4));
+}
+
+// B-row map: tile row t of column tile tn -> row of B.  Plain: tn * 256 + t.
+// SwiGLU forward (f = F, the up half's offset): wave block w = t / 64 holds
+// gate rows c + 32w .. +31 then the same up rows, c = tn * 128.
+// (relative to the column tile's first row: tn * 256, or tn * 128 for SwiGLU)
+__device__ __forceinline__ int tn_brow(int t, int f) {
+  if (f == 0) return t;
+  const int w = t >> 6, u = t & 63;
+  return 32 * w + (u & 31) + (u >= 32 ? f : 0);
+}
+
+// Lane's source element offset (from the tile's first row) for staging LDS
+// row t, chunk (lane & 3) of the image (the swizzle goes on the SOURCE: LDS-DMA
+// writes lane-linearly, guide §5.4 rule 21); `src_row` = the row of the
+// operand, relative to the wave-uniform base.
+__device__ __forceinline__ uint32_t tn_goff(int64_t ld, int t, int src_row, int lane) {
+  const int chunk = (lane & 3) ^ tn_f(t);
+  return (uint32_t)(src_row * ld + 8 * chunk);
+}
+
+// one 16-row (1 KiB) global_load_lds per u: LDS rows 32 wave + 16 u + (lane >> 2);
+// g = wave-uniform base (tile start + k offset): the scalar-base + 32-bit-offset form
+__device__ __forceinline__ void tn_stage(const bf16_t* __restrict__ g, const uint32_t* goff, char* lds_tile, int wave) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    char* dst = lds_tile + (32 * wave + 16 * u) * TN_ROWB;  // wave-uniform
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + goff[u]),
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ int tn_xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// tile index -> (tm, tn): groups of 8 row tiles walk the column tiles, so a
+// group's 8 A strips and the current B strip stay in the XCD's L2
+__device__ __forceinline__ void tn_tile_coords(int tile, int tiles_m, int tiles_n, int* tm, int* tn) {
+  const int per_group = 8 * tiles_n, group = tile / per_group, first_m = group * 8;
+  const int gsz = min(tiles_m - first_m, 8);
+  *tm = first_m + (tile - group * per_group) % gsz;
+  *tn = (tile - group * per_group) / gsz;
+}
+
+__device__ __forceinline__ float tn_silu(float g) { return g / (1.f + __expf(-g)); }
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                         const bf16_t* __restrict__ B, int64_t ldb,
+                                                         bf16_t* __restrict__ C, int64_t ldc,
+                                                         bf16_t* __restrict__ S, int64_t lds_,
+                                                         const bf16_t* __restrict__ GU, int64_t ldgu, int M, int N,
+                                                         int K, int F) {
+  // one LDS object per stage, loop unrolled by four: every access names its
+  // buffer statically (see wgrad.hip: a runtime stage index makes hipcc drain
+  // the LDS-DMA prefetch before every phase's first read)
+  __shared__ __attribute__((aligned(1024))) char sb0[TN_STAGE];
+  __shared__ __attribute__((aligned(1024))) char sb1[TN_STAGE];
+  __shared__ __attribute__((aligned(1024))) char sb2[TN_STAGE];
+  __shared__ __attribute__((aligned(1024))) char sb3[TN_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_m = M / TN_BM, tiles_n = N / TN_BN;
+  int tm, tn;
+  tn_tile_coords(tn_xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, &tm, &tn);
+  const int np = K / TN_BK;
+  const int fmap = EPI == TN_SWIGLU_FWD ? F : 0;
+
+  const bf16_t* Ab = A + (int64_t)tm * TN_BM * lda;
+  const bf16_t* Bb = B + (int64_t)tn * (fmap ? TN_BN / 2 : TN_BN) * ldb;
+  uint32_t ga[2], gb[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int t = 32 * wave + 16 * u + (lane >> 2);
+    ga[u] = tn_goff(lda, t, t, lane);
+    gb[u] = tn_goff(ldb, t, tn_brow(t, fmap), lane);
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool lag = wm == 1;
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // phase p: fragments of stage p (this buffer), LDS-DMA of stage p + 2 into
+  // the buffer stage p - 2 used, wait for this wave's DMA of stage p + 1,
+  // barrier, 32 MFMAs, barrier (the wgrad.hip schedule)
+  auto phase = [&](const char* cur, char* pre, int p) {
+    tn_s16x8 bf[4], af[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = tn_frag(cur + TN_TILE, wn * 64 + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = tn_frag(cur, wm * 128 + 16 * i, lane);
+    const int q = min(p + 2, np - 1);  // past the end: re-fetch into a buffer nobody reads again
+    tn_stage(Ab + q * TN_BK, ga, pre, wave);
+    tn_stage(Bb + q * TN_BK, gb, pre + TN_TILE, wave);
+    __builtin_amdgcn_s_waitcnt(TN_VMCNT4);
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+
+  tn_stage(Ab, ga, sb0, wave);
+  tn_stage(Bb, gb, sb0 + TN_TILE, wave);
+  tn_stage(Ab + TN_BK, ga, sb1, wave);
+  tn_stage(Bb + TN_BK, gb, sb1 + TN_TILE, wave);
+  __builtin_amdgcn_s_waitcnt(TN_VMCNT4);
+  sync();
+  if (lag) sync();
+  for (int p = 0; p < np; p += 4) {
+    phase(sb0, sb2, p);
+    phase(sb1, sb3, p + 1);
+    phase(sb2, sb0, p + 2);
+    phase(sb3, sb1, p + 3);
+  }
+  if (!lag) sync();
+  __builtin_amdgcn_s_waitcnt(TN_VMCNT0);
+
+  // epilogue: acc[i][j] = C[m][n .. n+3], m = row0 + 16 i, n = col0 + 16 j
+  const int m0 = tm * TN_BM + wm * 128 + (lane & 15);
+  const int nl = 4 * (lane >> 4);
+  if (EPI == TN_PLAIN) {
+    const int n0 = tn * TN_BN + wn * 64 + nl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 w;
+        w.x = pack2(acc[i][j][0], acc[i][j][1]);
+        w.y = pack2(acc[i][j][2], acc[i][j][3]);
+        *(uint2*)(C + (int64_t)(m0 + 16 * i) * ldc + n0 + 16 * j) = w;
+      }
+  } else if (EPI == TN_SWIGLU_FWD) {
+    // j = 0, 1: gate units h0 + 16 j; j = 2, 3: the same units' up values
+    const int h0 = tn * (TN_BN / 2) + 32 * wn + nl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16_t* crow = C + (int64_t)(m0 + 16 * i) * ldc;
+      bf16_t* srow = S + (int64_t)(m0 + 16 * i) * lds_;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 g = acc[i][j], u = acc[i][j + 2];
+        uint2 wg, wu, ws;
+        wg.x = pack2(g[0], g[1]);
+        wg.y = pack2(g[2], g[3]);
+        wu.x = pack2(u[0], u[1]);
+        wu.y = pack2(u[2], u[3]);
+        // s from the bf16-rounded gate / up: the values backward re-reads from gu
+        const float g0 = __uint_as_float(wg.x << 16), g1 = __uint_as_float(wg.x & 0xffff0000u);
+        const float g2 = __uint_as_float(wg.y << 16), g3 = __uint_as_float(wg.y & 0xffff0000u);
+        const float u0 = __uint_as_float(wu.x << 16), u1 = __uint_as_float(wu.x & 0xffff0000u);
+        const float u2 = __uint_as_float(wu.y << 16), u3 = __uint_as_float(wu.y & 0xffff0000u);
+        ws.x = pack2(tn_silu(g0) * u0, tn_silu(g1) * u1);
+        ws.y = pack2(tn_silu(g2) * u2, tn_silu(g3) * u3);
+        const int h = h0 + 16 * j;
+        *(uint2*)(crow + h) = wg;
+        *(uint2*)(crow + F + h) = wu;
+        *(uint2*)(srow + h) = ws;
+      }
+    }
+  } else {  // TN_SWIGLU_BWD: C = ds (never stored) -> dgu
+    const int n0 = tn * TN_BN + wn * 64 + nl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bf16_t* gurow = GU + (int64_t)(m0 + 16 * i) * ldgu;
+      bf16_t* drow = C + (int64_t)(m0 + 16 * i) * ldc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = n0 + 16 * j;
+        const uint2 gw = *(const uint2*)(gurow + h), uw = *(const uint2*)(gurow + F + h);
+        float g[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u), __uint_as_float(gw.y << 16),
+                      __uint_as_float(gw.y & 0xffff0000u)};
+        float u[4] = {__uint_as_float(uw.x << 16), __uint_as_float(uw.x & 0xffff0000u), __uint_as_float(uw.y << 16),
+                      __uint_as_float(uw.y & 0xffff0000u)};
+        // ds rounded to bf16 first: the value the unfused path stores
+        float d[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] = bf2f(f2bf(acc[i][j][e]));
+        float dg[4], du[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sg = 1.f / (1.f + __expf(-g[e]));
+          du[e] = d[e] * g[e] * sg;
+          dg[e] = d[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
+        }
+        uint2 wdg, wdu;
+        wdg.x = pack2(dg[0], dg[1]);
+        wdg.y = pack2(dg[2], dg[3]);
+        wdu.x = pack2(du[0], du[1]);
+        wdu.y = pack2(du[2], du[3]);
+        *(uint2*)(drow + h) = wdg;
+        *(uint2*)(drow + F + h) = wdu;
+      }
+    }
+  }
+}
+
+static bool tn_shape_ok(int M, int N, int K, int64_t lda, int64_t ldb) {
+  return M > 0 && N > 0 && K > 0 && M % TN_BM == 0 && N % TN_BN == 0 && K % (4 * TN_BK) == 0 && lda % 8 == 0 &&
+         ldb % 8 == 0;
+}
+
+// C[M][N] = A[M][K] B[N][K]^T.  M, N multiples of 256, K of 128, strides of
+// 8 elements, 16-byte aligned bases.
+extern "C" int toa_gemm_tn(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
+                           int N, int K, hipStream_t stream) {
+  if (!tn_shape_ok(M, N, K, lda, ldb) || ldc % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemm_tn_kernel<TN_PLAIN>, dim3((M / TN_BM) * (N / TN_BN)), dim3(512), 0, stream, A, lda, B, ldb,
+                     C, ldc, (bf16_t*)nullptr, (int64_t)0, (const bf16_t*)nullptr, (int64_t)0, M, N, K, 0);
+  return (int)hipGetLastError();
+}
+
+// gu[M][2F] = X[M][K] Wgu[2F][K]^T (Wgu = [gate; up]) and s[M][F] =
+// silu(gate) * up.  F a multiple of 128.
+extern "C" int toa_gemm_tn_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* Wgu, int64_t ldw, bf16_t* GU,
+                                  int64_t ldgu, bf16_t* S, int64_t lds_, int M, int F, int K, hipStream_t stream) {
+  if (F % (TN_BN / 2) || !tn_shape_ok(M, 2 * F, K, ldx, ldw) || ldgu % 4 || lds_ % 4)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemm_tn_kernel<TN_SWIGLU_FWD>, dim3((M / TN_BM) * (2 * F / TN_BN)), dim3(512), 0, stream, X, ldx,
+                     Wgu, ldw, GU, ldgu, S, lds_, (const bf16_t*)nullptr, (int64_t)0, M, 2 * F, K, F);
+  return (int)hipGetLastError();
+}
+
+// dgu[M][2F] = swiglu'(gu) applied to ds = dY[M][K] WdT[F][K]^T (ds itself is
+// not stored).  F a multiple of 256.
+extern "C" int toa_gemm_tn_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16_t* WdT, int64_t ldw,
+                                      const bf16_t* GU, int64_t ldgu, bf16_t* dGU, int64_t lddgu, int M, int F, int K,
+                                      hipStream_t stream) {
+  if (!tn_shape_ok(M, F, K, ldy, ldw) || ldgu % 4 || lddgu % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemm_tn_kernel<TN_SWIGLU_BWD>, dim3((M / TN_BM) * (F / TN_BN)), dim3(512), 0, stream, dY, ldy,
+                     WdT, ldw, dGU, lddgu, (bf16_t*)nullptr, (int64_t)0, GU, ldgu, M, F, K, F);
+  return (int)hipGetLastError();
+}

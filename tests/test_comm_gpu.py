@@ -184,7 +184,7 @@ def _operator_env_worker(rank, world, port, env, q):
         model = MnistMLP(3000, dtype=torch.float32, device="cuda")
         rt = Runtime()
         rt.info = type("I", (), {"rank": rank, "world": world})()
-        tr = simple.DPTrainer(model, lambda o, y: cross_entropy(o, y), rt, lr=1e-3, bucket_mb=1.0)
+        tr = simple.DPTrainer(model, lambda o, y: cross_entropy(o, y), rt, lr=1e-3, bucket_mb=0.05)
         reason = tr.bucketer.ipc_reason
         data = SyntheticMNIST(100, rank, world, device="cuda")
         for _ in range(5):

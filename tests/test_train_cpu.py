@@ -140,3 +140,36 @@ def test_fused_batchnorm_momentum_none_is_cumulative_average():
     assert int(bn.num_batches_tracked) == 4
     assert torch.allclose(bn.running_mean, ref.running_mean, atol=1e-6)
     assert torch.allclose(bn.running_var, ref.running_var, atol=1e-5)
+
+
+def test_fused_swiglu_mlp_autograd_matches_unfused():
+    """ops.llm.swiglu_mlp under TOA_GEMM=hip (the fused-GEMM autograd
+    function; on the CPU its GEMMs take the library fallbacks) gives the
+    unfused path's output and gradients, weight gradients into main_grad."""
+    from tf_operator_amd.ops import gemm, llm
+    from tf_operator_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(0)
+    T, Hd, F_ = 64, 32, 48
+    x0 = torch.randn(T, Hd)
+    outs = []
+    for mode in ("torch", "hip"):
+        wgu = torch.nn.Parameter(torch.randn(2 * F_, Hd) * 0.2)
+        wd = torch.nn.Parameter(torch.randn(Hd, F_) * 0.2)
+        with torch.no_grad():
+            g = torch.Generator().manual_seed(1)
+            wgu.copy_(torch.randn(2 * F_, Hd, generator=g) * 0.2)
+            wd.copy_(torch.randn(Hd, F_, generator=g) * 0.2)
+        flat = FlatParams([wd, wgu], grad_dtype=torch.float32)
+        old = gemm.mode()
+        gemm.set_mode(mode)
+        try:
+            x = x0.clone().requires_grad_()
+            y = llm.swiglu_mlp(x, wgu, wd)
+            y.backward(torch.ones_like(y))
+        finally:
+            gemm.set_mode(old)
+        outs.append((y.detach(), x.grad, wgu.main_grad.clone(), wd.main_grad.clone()))
+        del flat
+    for a, b in zip(*outs):
+        assert torch.allclose(a.float(), b.float(), rtol=1e-4, atol=1e-5)

@@ -26,7 +26,7 @@ import torch
 
 from ..ops.embedding import Embedding
 from ..ops.linear import linear
-from ..ops.llm import causal_attention, cross_entropy, rope_qkv, rope_tables, swiglu_down
+from ..ops.llm import causal_attention, cross_entropy, rope_qkv, rope_tables, swiglu_mlp
 from ..ops.norm import RMSNorm, add_rms_norm
 
 
@@ -106,8 +106,7 @@ class LlamaBlock(torch.nn.Module):
         o = o.reshape(B * S, cfg.heads * cfg.head_dim)
         a = linear(o, self.wo)
         h, x = self.mlp_norm(h, a)
-        gu = linear(x, self.wgu)
-        delta = swiglu_down(gu, self.wd)
+        delta = swiglu_mlp(x, self.wgu, self.wd)  # SwiGLU fused into the GEMMs under TOA_GEMM=hip
         return h, delta
 
 

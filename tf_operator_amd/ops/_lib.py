@@ -78,6 +78,10 @@ _SIGS = {
     "toa_bn_bwd": [c_int, c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_p,
                    c_p],
     "toa_gemm_set_no_streamk": [c_int],
+    "toa_gemm_tn": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_tn_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_tn_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_attn_set_dkdv_variant": [c_int],
     "toa_emulate_xfer": [c_p, c_p, c_i64, c_int, ctypes.c_double, c_p],
     "toa_gemm_tune": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p, c_p, c_p,
                       c_p, c_p, c_int],

@@ -31,9 +31,16 @@ Modes (``TOA_GEMM``):
   (profiles/r2_sk_contention).  With world-8 ZeRO-1 traffic emulated on
   one MI355X (profiles/r3_overlap) the collectives cost the stream-K step
   +6.7 % and the nosk step +3.4 %, at equal step time without traffic.
-* ``auto`` (the default): ``nosk`` when the data-parallel world (real or
-  emulated, parallel/emulate.py) is > 1, else ``torch`` -- resolved by
-  :func:`resolve_auto` when the trainer knows its world.
+* ``hip``: the hand-written TN kernel (csrc/hip/gemm_tn.hip) for the
+  forward and data-gradient GEMMs whose shapes it takes (M, N multiples of
+  256, K of 128), with the Llama MLP's SwiGLU fused into the gate|up
+  projection's epilogue and its backward into the down projection's data
+  gradient (``ops.llm.swiglu_mlp``); everything else as ``nosk``.
+* ``auto`` (the default): ``nosk``, resolved by :func:`resolve_auto` when
+  the trainer starts.  At world 1 the two are equal in-model (996.5 vs
+  999.2 ms/step, two alternating runs each on one box,
+  profiles/r3_gemm_policy); from world 2 on the collectives overlap the
+  GEMMs and nosk is the one that tolerates it.
 """
 from __future__ import annotations
 
@@ -59,17 +66,19 @@ def mode() -> str:
 def set_mode(m: str):
     """Select the GEMM policy for this process (before the first GEMM)."""
     global _MODE, _installed
-    if m not in ("auto", "torch", "tuned", "nosk"):
+    if m not in ("auto", "torch", "tuned", "nosk", "hip"):
         raise ValueError(f"unknown GEMM mode {m!r}")
     _MODE = m
     _installed = False
 
 
-def resolve_auto(world: int) -> str:
-    """``auto`` -> ``nosk`` for a data-parallel world > 1, else ``torch``
-    (an explicit TOA_GEMM is kept).  Returns the mode in force."""
+def resolve_auto(world: int = 1) -> str:
+    """``auto`` -> ``nosk`` (an explicit TOA_GEMM is kept).  Returns the mode
+    in force.  `world` is kept for the policy record: the choice does not
+    depend on it since world-1 steps measured equal."""
+    del world
     if _MODE == "auto":
-        set_mode("nosk" if world > 1 else "torch")
+        set_mode("nosk")
     return _MODE
 
 
@@ -88,8 +97,8 @@ def _install():
         return
     _installed = True
     if _lib.has("toa_gemm_set_no_streamk"):
-        _lib.call("toa_gemm_set_no_streamk", int(_MODE == "nosk"))
-    table = TABLE_NOSK if _MODE == "nosk" else TABLE
+        _lib.call("toa_gemm_set_no_streamk", int(_MODE in ("nosk", "hip")))
+    table = TABLE_NOSK if _MODE in ("nosk", "hip") else TABLE
     if not os.path.exists(table):
         return
     with open(table) as f:
@@ -103,7 +112,7 @@ def _install():
 
 
 def _ok(*ts):
-    if _MODE not in ("tuned", "nosk") or not _lib.has("toa_gemm"):
+    if _MODE not in ("tuned", "nosk", "hip") or not _lib.has("toa_gemm"):
         return False
     for t in ts:
         if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
@@ -117,7 +126,28 @@ def _gemm(ta, tb, m, n, k, a, lda, b, ldb, c, ldc, beta):
               int(c.dtype == torch.float32), _lib.stream(c))
 
 
+def _tn_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
+    """Operands csrc/hip/gemm_tn.hip takes: bf16 GPU rows with unit column
+    stride, 16-byte aligned, M and N multiples of 256 (n_mult), K of 128."""
+    if _MODE != "hip" or not _lib.has("toa_gemm_tn"):
+        return False
+    if not (x2.is_cuda and x2.dtype == w.dtype == torch.bfloat16 and x2.dim() == 2 and w.dim() == 2):
+        return False
+    if x2.stride(1) != 1 or w.stride(1) != 1 or x2.stride(0) % 8 or w.stride(0) % 8:
+        return False
+    M, K = x2.shape
+    N = w.shape[0]
+    return (M % 256 == 0 and N % n_mult == 0 and K % 128 == 0 and w.shape[1] == K
+            and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _lib.use_hip(x2))
+
+
 def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if _tn_ok(x2, w):
+        M, N = x2.shape[0], w.shape[0]
+        y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
+        _lib.call("toa_gemm_tn", _lib.ptr(x2), x2.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), N, M, N,
+                  x2.shape[1], _lib.stream(x2))
+        return y
     if not _ok(x2, w):
         return torch.matmul(x2, w.t())
     M, K = x2.shape
@@ -138,6 +168,33 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
     _gemm(0, 0, K, M, N, w, w.stride(0), dy2, dy2.stride(0), dx, K, 0.0)
     return dx
+
+
+def swiglu_gate_up(x2: torch.Tensor, wgu: torch.Tensor):
+    """(gu, s) = (x Wgu^T, silu(gate) * up) from ONE hand-written GEMM with
+    the SwiGLU in its epilogue; None when the TN kernel cannot take it."""
+    if not (_tn_ok(x2, wgu) and (wgu.shape[0] // 2) % 128 == 0):
+        return None
+    M, F = x2.shape[0], wgu.shape[0] // 2
+    gu = torch.empty(M, 2 * F, device=x2.device, dtype=x2.dtype)
+    s = torch.empty(M, F, device=x2.device, dtype=x2.dtype)
+    _lib.call("toa_gemm_tn_swiglu", _lib.ptr(x2), x2.stride(0), _lib.ptr(wgu), wgu.stride(0), _lib.ptr(gu), 2 * F,
+              _lib.ptr(s), F, M, F, x2.shape[1], _lib.stream(x2))
+    return gu, s
+
+
+def swiglu_down_dgrad(d2: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor):
+    """dgu = SwiGLU-backward(gu, ds = d2 Wd) from ONE hand-written GEMM on
+    the transposed weight copy (ops/wt.py) with the SwiGLU backward in its
+    epilogue (ds is never stored); None when the TN kernel cannot take it."""
+    wdt = getattr(wd, "_toa_wt", None)
+    if wdt is None or not (_tn_ok(d2, wdt) and gu.is_contiguous() and gu.shape[1] == 2 * wdt.shape[0]):
+        return None
+    M, F = d2.shape[0], wdt.shape[0]
+    dgu = torch.empty_like(gu)
+    _lib.call("toa_gemm_tn_swiglu_bwd", _lib.ptr(d2), d2.stride(0), _lib.ptr(wdt), wdt.stride(0), _lib.ptr(gu),
+              2 * F, _lib.ptr(dgu), 2 * F, M, F, d2.shape[1], _lib.stream(d2))
+    return dgu
 
 
 _WGRAD = os.environ.get("TOA_WGRAD", "hip")

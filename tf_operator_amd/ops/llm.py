@@ -159,6 +159,51 @@ def swiglu_down(gu, wd):
     return _SwiGLUDown.apply(gu, wd)
 
 
+class _SwiGLUMLP(torch.autograd.Function):
+    """out = swiglu(x Wgu^T) Wd^T with the SwiGLU fused into the GEMMs
+    (ops/gemm.py ``swiglu_gate_up`` / ``swiglu_down_dgrad``,
+    csrc/hip/gemm_tn.hip): the gate|up GEMM writes gu and s = silu(gate) *
+    up, and the down projection's data gradient emits dgu directly -- no
+    separate SwiGLU pass over the [T, 2F] activations in either direction.
+    Weight gradients land in the flat buffer as in ``ops.linear``."""
+
+    @staticmethod
+    def forward(ctx, x, wgu, wd):
+        x2 = x.reshape(-1, x.shape[-1])
+        r = gemm.swiglu_gate_up(x2, wgu)
+        gu, s = r if r is not None else (None, None)
+        if gu is None:
+            gu = gemm.linear_fwd(x2, wgu)
+            s = swiglu(gu)
+        ctx.save_for_backward(x, wgu, wd, gu, s)
+        return gemm.linear_fwd(s, wd).view(*x.shape[:-1], wd.shape[0])
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, wgu, wd, gu, s = ctx.saved_tensors
+        d2 = dout.reshape(-1, dout.shape[-1])
+        dwd = accumulate_mm(wd, d2.t(), s)
+        del s
+        dgu = gemm.swiglu_down_dgrad(d2, wd, gu)
+        if dgu is None:
+            dgu = swiglu_bwd(gemm.linear_dgrad(d2, wd), gu)
+        del gu
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = gemm.linear_dgrad(dgu, wgu).view_as(x) if ctx.needs_input_grad[0] else None
+        dwgu = accumulate_mm(wgu, dgu.t(), x2)
+        return dx, dwgu, dwd
+
+
+def swiglu_mlp(x, wgu, wd):
+    """The Llama MLP, x -> swiglu(x Wgu^T) Wd^T, fused where the hand-written
+    GEMM takes the shapes (TOA_GEMM=hip), else the two-GEMM + SwiGLU path."""
+    if gemm.mode() == "hip":
+        return _SwiGLUMLP.apply(x, wgu, wd)
+    from .linear import linear
+
+    return swiglu_down(linear(x, wgu), wd)
+
+
 # ---------------------------------------------------------------------------
 # Cross entropy (mean over non-ignored tokens)
 # ---------------------------------------------------------------------------
