@@ -626,7 +626,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// dK / dV, 4-wave form (the default; TOA_ATTN_DKDV=8 selects the one above).
+// dK / dV, 4-wave form (opt-in, TOA_ATTN_DKDV=4; measured SLOWER than the
+// 8-wave form at the bench shape: dQ + dK/dV 3.61 vs 3.45 ms,
+// profiles/r3_kernels/attn_bwd_ab.log -- one wave per SIMD leaves the
+// LDS-read and exp latencies of each half to the compiler's scheduling, which
+// the 8-wave form hides with the partner wave).
 // Workgroup = 4 waves, one per SIMD with up to 512 registers each, = 128 keys
 // of one (batch, kv head).  Wave w owns keys 32w..32w+31 and BOTH 32-row
 // halves of every 64-row query tile, so its dK^T / dV^T need no cross-wave
@@ -1018,13 +1022,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     }
 }
 
-// dK/dV kernel form: 4 (4-wave, K/V in registers; default) or 8 (8-wave,
-// K/V in LDS); TOA_ATTN_DKDV=8 or toa_attn_set_dkdv_variant for A/B runs.
+// dK/dV kernel form: 8 (8-wave, K/V in LDS; default) or 4 (4-wave, K/V in
+// registers); TOA_ATTN_DKDV=4 or toa_attn_set_dkdv_variant for A/B runs.
 static int g_dkdv_variant = -1;
 static int attn_dkdv_variant() {
   if (g_dkdv_variant < 0) {
     const char* e = getenv("TOA_ATTN_DKDV");
-    g_dkdv_variant = (e && e[0] == '8') ? 8 : 4;
+    g_dkdv_variant = (e && e[0] == '4') ? 4 : 8;
   }
   return g_dkdv_variant;
 }
