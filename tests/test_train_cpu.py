@@ -183,7 +183,8 @@ def test_miopen_find_db_version_gate(monkeypatch, tmp_path, capsys):
 
     assert common.db_miopen_version("gfx950100.HIP.3_5_0_2025-x.ufdb.txt") == (3, 5, 0)
     assert common.db_miopen_version("nothing.txt") is None
-    monkeypatch.delenv("MIOPEN_USER_DB_PATH", raising=False)
+    monkeypatch.setenv("MIOPEN_USER_DB_PATH", "x")  # recorded, so teardown restores the original state
+    monkeypatch.delenv("MIOPEN_USER_DB_PATH")
     monkeypatch.setattr(common, "miopen_version", lambda: (9, 9, 9))
     assert common.use_shipped_miopen_find_db() is None
     assert "WARNING" in capsys.readouterr().err
