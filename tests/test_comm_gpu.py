@@ -231,3 +231,28 @@ def test_oneshot_auto_selected_under_operator_env():
         assert selected and reason.startswith("auto"), (rank, reason)
         assert counts["oneshot"] > 0 and counts["collective"] > 0, (rank, counts)
         assert same, rank
+
+
+def test_emulate_xfer_moves_bytes_at_the_paced_rate():
+    """parallel/emulate.py's stand-in for an RCCL ring kernel: copies every
+    byte, and paced to G GB/s on 32 workgroups it takes about bytes / G
+    (the property the overlap emulation relies on); unpaced it runs at HBM
+    speed."""
+    from tf_operator_amd.ops import _lib
+
+    src = torch.randint(0, 255, (64 << 20,), dtype=torch.uint8, device="cuda")
+    dst = torch.zeros_like(src)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    times = {}
+    for gbps in (0.0, 100.0):
+        dst.zero_()
+        torch.cuda.synchronize()
+        ev[0].record()
+        _lib.call("toa_emulate_xfer", _lib.ptr(src), _lib.ptr(dst), src.numel(), 32, gbps, _lib.stream(src))
+        ev[1].record()
+        torch.cuda.synchronize()
+        times[gbps] = ev[0].elapsed_time(ev[1])
+        assert torch.equal(src, dst), gbps
+    want_ms = src.numel() / 100e9 * 1e3  # 0.67 ms at 100 GB/s
+    assert 0.9 * want_ms <= times[100.0] <= 1.6 * want_ms, times
+    assert times[0.0] < 0.5 * want_ms, times
