@@ -112,3 +112,22 @@ def test_bench_world_mismatch_fails():
     assert p.returncode != 0
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert "FATAL" in p.stderr
+
+
+@pytest.mark.timeout(900)
+def test_bench_under_torchrun_four_ranks():
+    """A larger world rehearsed on gloo (the driver's N = 4 / 8 launches run
+    the same code over RCCL): four ranks under torchrun, ZeRO-1 over four
+    shards, latency probes as a TFJob Worker=4 in the node-local layout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "4", *TINY, "--latency-probes", "1",
+           "--cold-probes", "0"]
+    env = _env()
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=880)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json_line(p.stdout)
+    assert r["n_gpus"] == 4 and r["rccl_world"] == 4 and r["config"]["global_batch"] == 8
+    assert r["replicas_identical"] is True and "ZeRO-1" in r["config"]["optimizer"]
+    assert r["config"]["gemm_policy"] == "nosk"
+    assert r["submit_to_first_step_p50_s"] > 0
