@@ -48,6 +48,10 @@ struct Ctx {
   int device = -1;
   std::map<Key, Plan> plans;
   std::map<Key, int> wanted;  // installed tuned indices, resolved lazily
+  // solution index -> algo, filled by ONE getAlgosFromIndex call for every
+  // installed index (a call per form cost ~30 ms each in the first step)
+  std::map<int, hipblasLtMatmulAlgo_t> by_index;
+  bool by_index_built = false;
   std::mutex mu;
 };
 
@@ -117,11 +121,20 @@ int resolve(Ctx& c, const Key& k, Plan& p, float beta) {
   if (p.has_algo) return 0;
   auto w = c.wanted.find(k);
   if (w != c.wanted.end()) {
-    std::vector<int> idx{w->second};
-    std::vector<hipblasLtMatmulHeuristicResult_t> res;
-    if (hipblaslt_ext::getAlgosFromIndex(c.h, idx, res) == HIPBLAS_STATUS_SUCCESS && !res.empty() &&
-        supported(c, p, res[0].algo, beta)) {
-      p.algo = res[0].algo;
+    if (!c.by_index_built || c.by_index.find(w->second) == c.by_index.end()) {
+      std::vector<int> idx;
+      for (const auto& kv : c.wanted)
+        if (c.by_index.find(kv.second) == c.by_index.end()) idx.push_back(kv.second);
+      std::sort(idx.begin(), idx.end());
+      idx.erase(std::unique(idx.begin(), idx.end()), idx.end());
+      std::vector<hipblasLtMatmulHeuristicResult_t> res;
+      if (!idx.empty() && hipblaslt_ext::getAlgosFromIndex(c.h, idx, res) == HIPBLAS_STATUS_SUCCESS)
+        for (const auto& r : res) c.by_index[hipblaslt_ext::getIndexFromAlgo(const_cast<hipblasLtMatmulAlgo_t&>(r.algo))] = r.algo;
+      c.by_index_built = true;
+    }
+    auto a = c.by_index.find(w->second);
+    if (a != c.by_index.end() && supported(c, p, a->second, beta)) {
+      p.algo = a->second;
       p.has_algo = true;
       p.index = w->second;
       return 0;
