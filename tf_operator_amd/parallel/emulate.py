@@ -25,6 +25,11 @@ as they were), so the loss is meaningless; the TIME is rank 0's.  Compare
 against ``TOA_EMULATE_GBPS=0`` with ``TOA_EMULATE_BYTES=0`` (same step, no
 traffic) to read what the overlap costs.  scripts/overlap_emulation.py runs
 the policies side by side.
+
+Reference parity: the reference's only collective is the payloads' per-step
+gradient all-reduce (``examples/v1/distribution_strategy/keras-API/
+multi_worker_strategy-with-keras.py:76-77, 117-120``); this
+module measures what that step's collectives cost on MI355X at world 8.
 """
 from __future__ import annotations
 
