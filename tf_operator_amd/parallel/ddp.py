@@ -39,7 +39,10 @@ def ipc_decision(mode: str, world: int, reducing: bool, on_gpu: bool, dist_ready
         return False, "no process group"
     if mode == "1":
         return (True, "forced (TOA_IPC_ALLREDUCE=1)") if on_gpu else (False, "forced, but gradients are on the CPU")
-    local = local_world_size is not None and int(local_world_size) == world
+    try:
+        local = local_world_size is not None and int(local_world_size) == world
+    except ValueError:
+        local = False
     if not local:
         return False, f"ranks span nodes (LOCAL_WORLD_SIZE={local_world_size}, world {world})"
     if not 1 < world <= 8:
