@@ -21,6 +21,9 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -38,6 +41,7 @@ struct Plan {
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
   hipblasLtMatmulAlgo_t algo;
   bool has_algo = false;
+  bool ran = false;
   int index = -1;
 };
 
@@ -60,12 +64,34 @@ Ctx& ctx() {
   return c;
 }
 
+// TOA_GEMM_TRACE=1: host time of each first-use phase on stderr (the GEMM
+// layer's share of a job's submit -> first step)
+bool trace_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TOA_GEMM_TRACE");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
+struct PhaseTimer {
+  const char* what;
+  std::chrono::steady_clock::time_point t0;
+  explicit PhaseTimer(const char* w) : what(w), t0(std::chrono::steady_clock::now()) {}
+  ~PhaseTimer() {
+    if (what != nullptr && trace_on())
+      std::fprintf(stderr, "[toa_gemm] %s %.2f ms\n", what,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+
 hipblasOperation_t op_of(int t) { return t ? HIPBLAS_OP_T : HIPBLAS_OP_N; }
 
 int ensure_handle(Ctx& c) {
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (c.h != nullptr && c.device == dev) return 0;
+  PhaseTimer t("hipblasLtCreate+workspace");
   if (hipblasLtCreate(&c.h) != HIPBLAS_STATUS_SUCCESS) return 1;
   c.ws_size = 256ull << 20;  // 256 MB: stream-K / split-K solutions need room
   if (hipMalloc(&c.ws, c.ws_size) != hipSuccess) {
@@ -127,12 +153,18 @@ int resolve(Ctx& c, const Key& k, Plan& p, float beta) {
         if (c.by_index.find(kv.second) == c.by_index.end()) idx.push_back(kv.second);
       std::sort(idx.begin(), idx.end());
       idx.erase(std::unique(idx.begin(), idx.end()), idx.end());
+      // Most of this call's ~0.47 s is loading the chosen solutions' code
+      // objects; a typed getAllAlgos lookup only moves that into
+      // matmulIsAlgoSupported (0.27 + 0.36 s, profiles/r3_first), so
+      // toa_gemm_prewarm() takes it off the first step instead.
       std::vector<hipblasLtMatmulHeuristicResult_t> res;
+      PhaseTimer t(idx.empty() ? nullptr : "getAlgosFromIndex");
       if (!idx.empty() && hipblaslt_ext::getAlgosFromIndex(c.h, idx, res) == HIPBLAS_STATUS_SUCCESS)
         for (const auto& r : res) c.by_index[hipblaslt_ext::getIndexFromAlgo(const_cast<hipblasLtMatmulAlgo_t&>(r.algo))] = r.algo;
       c.by_index_built = true;
     }
     auto a = c.by_index.find(w->second);
+    PhaseTimer t("matmulIsAlgoSupported");
     if (a != c.by_index.end() && supported(c, p, a->second, beta)) {
       p.algo = a->second;
       p.has_algo = true;
@@ -140,6 +172,7 @@ int resolve(Ctx& c, const Key& k, Plan& p, float beta) {
       return 0;
     }
   }
+  PhaseTimer t("heuristic");
   hipblasLtMatmulPreference_t pref;
   hipblasLtMatmulPreferenceCreate(&pref);
   uint64_t wsz = c.ws_size;
@@ -166,6 +199,8 @@ int resolve(Ctx& c, const Key& k, Plan& p, float beta) {
 int run(Ctx& c, Plan& p, hipblasLtMatmulAlgo_t& algo, const void* A, const void* B, void* C, float beta,
         hipStream_t s) {
   const float alpha = 1.f;
+  PhaseTimer t(p.ran ? nullptr : "first hipblasLtMatmul");
+  p.ran = true;
   return hipblasLtMatmul(c.h, p.desc, &alpha, A, p.a, B, p.b, &beta, C, p.c, C, p.c, &algo, c.ws, c.ws_size, s) ==
                  HIPBLAS_STATUS_SUCCESS
              ? 0
@@ -315,4 +350,22 @@ extern "C" int toa_gemm_set_no_streamk(int on) {
   std::lock_guard<std::mutex> g(c.mu);
   g_no_streamk = on != 0;
   return 0;
+}
+
+// Resolve every installed form's plan now (handle + workspace, ONE batched
+// index lookup, per-form support checks) instead of inside the first step.
+// Host-side work only -- no kernel runs -- so ops/gemm.py calls it from a
+// helper thread while the model's weights are being initialised.  Returns
+// the number of installed forms that resolved.
+extern "C" int toa_gemm_prewarm() {
+  Ctx& c = ctx();
+  std::lock_guard<std::mutex> g(c.mu);
+  if (ensure_handle(c)) return -1;
+  PhaseTimer t("prewarm");
+  int ok = 0;
+  for (const auto& kv : c.wanted) {
+    Plan& p = plan_for(c, kv.first);
+    if (resolve(c, kv.first, p, std::get<8>(kv.first) ? 1.f : 0.f) == 0) ++ok;
+  }
+  return ok;
 }

@@ -2,7 +2,9 @@
 step): each Llama-3-8B forward / dgrad form called once, then again, under
 one GEMM policy, in a fresh process.
 
-    python scripts/gemm_first_call.py --mode nosk|torch [--tokens 24576]
+    python scripts/gemm_first_call.py --mode nosk|torch [--tokens 24576] [--prewarm]
+
+TOA_GEMM_TRACE=1 adds the GEMM layer's per-phase host times on stderr.
 """
 import argparse
 import json
@@ -22,13 +24,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="nosk")
     ap.add_argument("--tokens", type=int, default=24576)
+    ap.add_argument("--prewarm", action="store_true", help="gemm.prewarm() first (timed separately)")
     a = ap.parse_args()
     torch.cuda.init()
     torch.empty(1, device="cuda")
     torch.cuda.synchronize()
     gemm.set_mode(a.mode)
     T = a.tokens
-    out = {"mode": a.mode, "first_ms": {}, "second_ms": {}}
+    out = {"mode": a.mode, "prewarm": a.prewarm, "first_ms": {}, "second_ms": {}}
+    if a.prewarm:
+        t0 = time.perf_counter()
+        gemm.prewarm(background=False)
+        out["prewarm_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
     t_all = time.perf_counter()
     for name, (K, N) in FORMS.items():
         for kind, (kk, nn) in (("fwd", (K, N)), ("dgrad_wt", (N, K))):

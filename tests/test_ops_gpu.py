@@ -604,6 +604,31 @@ def test_tuned_gemm_forms(M, K, N):
     assert rel(gemm.linear_fwd(x, w), x.float() @ w.float().t()) < 1e-2
 
 
+def test_gemm_prewarm_resolves_table():
+    """gemm.prewarm() on its helper thread resolves every installed nosk
+    table entry to the table's solution before any GEMM runs."""
+    _lib()
+    import json
+
+    from tf_operator_amd.ops import gemm
+
+    gemm.set_mode("nosk")
+    try:
+        with open(gemm.TABLE_NOSK) as f:
+            tab = json.load(f)
+        th = gemm.prewarm(DEV)
+        assert th is not None
+        th.join(timeout=60)
+        assert not th.is_alive()
+        if tab.get("hipblaslt") != gemm.hipblaslt_build():
+            pytest.skip("nosk table measured with another hipBLASLt build")
+        for e in tab["entries"]:
+            key = (e["ta"], e["tb"], e["m"], e["n"], e["k"], e["lda"], e["ldb"], e["ldc"], e["beta_nz"])
+            assert gemm.current_algo(key) == e["index"], key
+    finally:
+        gemm.set_mode("auto")
+
+
 @pytest.mark.parametrize("B,H,Hk,S", [(2, 4, 2, 384), (1, 8, 2, 1024)])
 def test_flash_attention_bshd_output_layout(B, H, Hk, S):
     """O written / dO read as [B, S, H, D] (no transpose copies in the model)

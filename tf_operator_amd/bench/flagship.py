@@ -412,6 +412,9 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
     from ..train.runtime import Runtime
 
     phases["imports"] = time.time()
+    from ..ops import gemm as _gemm
+
+    _gemm.prewarm_early()  # GEMM plans resolve while the process group and the model come up
     rt = Runtime()
     info = tdist.init()
     rt.info = info

@@ -36,6 +36,9 @@ def main(argv=None):
     p.add_argument("--zero", choices=("auto", "0", "1"), default="auto",
                    help="ZeRO-1 sharded optimizer; auto = on for world > 1 (bench.py's default)")
     a = p.parse_args(argv)
+    from tf_operator_amd.ops import gemm
+
+    gemm.prewarm_early()  # GEMM plans resolve while the process group and the model come up
     rt = Runtime()
     rt.install_preemption_handler()
     info = rt.init_dist()

@@ -78,6 +78,7 @@ _SIGS = {
     "toa_bn_bwd": [c_int, c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_i64, c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_p,
                    c_p],
     "toa_gemm_set_no_streamk": [c_int],
+    "toa_gemm_prewarm": [],
     "toa_gemm_tn": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_tn_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_tn_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],

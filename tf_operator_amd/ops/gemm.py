@@ -47,6 +47,7 @@ from __future__ import annotations
 import ctypes
 import json
 import os
+import threading
 
 import torch
 
@@ -109,6 +110,54 @@ def _install():
         if e.get("index", -1) >= 0:
             _lib.call("toa_gemm_set_algo", e["ta"], e["tb"], e["m"], e["n"], e["k"], e["lda"], e["ldb"], e["ldc"],
                       e["beta_nz"], e.get("out_f32", 0), e["index"])
+
+
+_prewarm_thread = None
+
+
+def prewarm(device=None, background: bool = True):
+    """Resolve the installed table's plans (hipBLASLt handle, solution
+    lookup, support checks: ~0.47 s of host work, mostly code-object loading,
+    at the first GEMM -- profiles/r3_first) ahead of the first step.  With
+    `background` it runs on a helper thread -- ctypes drops the GIL, so the
+    caller initialises the process group and the model meanwhile -- and the
+    thread is returned (the GEMM layer's lock orders the first real GEMM
+    after it).  Idempotent; None when the policy uses no table."""
+    global _prewarm_thread
+    if _MODE not in ("tuned", "nosk", "hip") or not _lib.has("toa_gemm_prewarm"):
+        return None
+    if _prewarm_thread is not None:
+        return _prewarm_thread
+    _install()
+    dev = None if device is None else torch.device(device).index
+    dev = torch.cuda.current_device() if dev is None else dev
+
+    def work():
+        torch.cuda.set_device(dev)
+        _lib.call_ret("toa_gemm_prewarm")
+
+    if not background:
+        work()
+        return None
+    _prewarm_thread = threading.Thread(target=work, name="toa-gemm-prewarm", daemon=True)
+    _prewarm_thread.start()
+    return _prewarm_thread
+
+
+def prewarm_early():
+    """Start :func:`prewarm` at process start, on this replica's GPU
+    (LOCAL_RANK), before the process group and the model exist.  No-op off
+    the GPU, for the ``torch`` policy, or without the HIP library."""
+    if not torch.cuda.is_available():
+        return None
+    resolve_auto()
+    try:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+    except ValueError:
+        local = 0
+    if local >= torch.cuda.device_count():
+        return None
+    return prewarm(torch.device("cuda", local))
 
 
 def _ok(*ts):

@@ -37,6 +37,14 @@ class LlamaTrainer:
         self.micro_batch = micro_batch
         self.seq_len = seq_len
         self.grad_accum = grad_accum
+        # GEMM policy: no stream-K kernels, so collectives can overlap the
+        # GEMMs (ops/gemm.py).  Its plans resolve on a helper thread while
+        # the weights initialise (~0.47 s of code-object loading that would
+        # otherwise sit in the first step, profiles/r3_first).
+        from ..ops import gemm as _gemm
+
+        self.gemm_mode = _gemm.resolve_auto()
+        self._gemm_prewarm = _gemm.prewarm(device) if torch.device(device).type == "cuda" else None
         with torch.device(device):
             model = Llama(cfg, device=device)
         model.init_weights(seed)
@@ -60,10 +68,6 @@ class LlamaTrainer:
         # RCCL world-1 test drives the real reduce-scatter / all-gather path)
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20),
                                      shard=shard_optimizer, enabled=True if force_collectives else None)
-        # GEMM policy: no stream-K kernels when collectives overlap the GEMMs (ops/gemm.py)
-        from ..ops import gemm as _gemm
-
-        self.gemm_mode = _gemm.resolve_auto(self.bucketer.world if self.bucketer.enabled else 1)
         self.gather = None
         if self.bucketer.shard:  # ZeRO-1: reduce-scatter, owned-shard AdamW, in-place all-gather
             # fp32 master / m / v only for the owned shards: 12 B/param x (1 - 1/world) of HBM freed
