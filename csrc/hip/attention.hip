@@ -1022,6 +1022,507 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Backward with dS through HBM (TOA_ATTN_BWD=ds): the dK/dV kernel already
+// forms dS = P * (dP - delta) for every (32-query, 32-key) block at or below
+// the diagonal; the dS form's dK/dV kernel also stores them (bf16, 2 KB per
+// block: the lane's 8-byte (key, 4-query) pieces, piece sigma = 2 g' + hh of
+// key k at sigma * 256 + k * 8 bytes, so each store instruction writes 512
+// contiguous bytes; the blocks of one (batch, head) packed lower-triangular:
+// block (qi, ki) at qi (qi + 1) / 2 + ki).  dQ = scale * dS K is
+// then a plain GEMM over those blocks -- the split form's dQ kernel recomputes
+// S and dP for it (3 of the backward's 7 executed S^2 D products; this form
+// executes 5).  The dS round trip is 2 x 3.2 GB at the Llama-3-8B shape; the
+// GEMM streams it once.  delta = rowsum(dO * O) moves to its own pass, since
+// the dK/dV kernel now runs first.
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                         const float* __restrict__ LSE, float* __restrict__ NDELTA,
+                                                         float* __restrict__ NLSE2, int rows, int H, int S,
+                                                         int o_bshd) {
+  constexpr int LPR = D / 8;  // lanes per row, 16 B each
+  const int row = blockIdx.x * (256 / LPR) + (int)threadIdx.x / LPR;
+  const int c = threadIdx.x % LPR;
+  if (row >= rows) return;  // whole LPR-lane groups leave together
+  const int s = row % S, bh = row / S;
+  const int64_t off = o_off<D>(bh / H, bh % H, s, H, S, o_bshd) + c * 8;
+  float a[8], g[8];
+  unpack8(ld16(O + off), a);
+  unpack8(ld16(dO + off), g);
+  float part = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part = fmaf(a[j], g[j], part);
+#pragma unroll
+  for (int m = LPR / 2; m >= 1; m >>= 1) part += __shfl_xor(part, m, LPR);
+  if (c == 0) {
+    NDELTA[row] = -part;              // the dP accumulators' initial value
+    NLSE2[row] = -(LSE[row] * LOG2E);  // the exp2 argument's addend
+  }
+}
+
+template <int D>
+struct DQG {
+  static constexpr int KT = TK * AG<D>::ROWB;  // one 64-key K tile
+  static constexpr int DSW = 4096;             // per wave and tile: two 32 x 32 dS blocks
+  static constexpr int STAGE = KT + 8 * DSW;   // 48 KB (D = 128) / 40 KB (D = 64)
+  static constexpr int NKP = KT / 1024 / 8;    // K LDS-DMA pieces per wave and tile
+};
+
+// dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for one (batch, head) and a
+// 256-row query block: 8 waves x 32 query rows, 64-key tiles, v_mfma 32x32x16
+// with the accumulator of the split dQ kernel (query on the lane, so its
+// epilogue is reused).  Everything reaches LDS by LDS-DMA in a 3-slot ring
+// (guide §5 "Pipelining across barriers": counted vmcnt, raw s_barrier, one
+// distinct LDS object per slot so no read waits on another slot's DMA):
+//  * the K tile, shared by the 8 waves, in the rt_off image (source-swizzled);
+//    the A operand comes out of it by transposed reads, as in the split kernel;
+//  * each wave's own two dS blocks, copied verbatim; a transposed read of a
+//    block's (key, 4-query) pieces gives the B operand (query on the lane, 4
+//    keys per read; the key order matches the K^T read's, as in the split
+//    kernel).
+template <int D>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __restrict__ K,
+                                                              const bf16_t* __restrict__ dS, bf16_t* __restrict__ dQ,
+                                                              int B, int H, int Hk, int S, float scale) {
+  using G = AG<D>;
+  constexpr int ROWB = G::ROWB, NCH = G::NCH, ND = G::ND;
+  constexpr int KT = DQG<D>::KT, NKP = DQG<D>::NKP;
+  __shared__ __attribute__((aligned(1024))) char s0[DQG<D>::STAGE];
+  __shared__ __attribute__((aligned(1024))) char s1[DQG<D>::STAGE];
+  __shared__ __attribute__((aligned(1024))) char s2[DQG<D>::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = S / FWD_QB;
+  int qb, h, b;
+  fwd_block_coords(blockIdx.x, nqb, B, H, Hk, &qb, &h, &b);
+  const int hk = h / (H / Hk);
+  const int nb = S >> 5;
+  const int qi = qb * 8 + wave;    // this wave's 32-row query block
+  const int tdiag = qi >> 1;       // its last 64-key tile
+  const int ntiles = (qb + 1) * 4;  // the workgroup's causal key range
+  const bf16_t* kbase = K + ((int64_t)(b * Hk + hk) * S) * D;
+  const bf16_t* dsrow = dS + (((int64_t)(b * H + h) * (nb * (nb + 1) / 2) + (int64_t)qi * (qi + 1) / 2) << 10);
+
+  // K tile pieces: wave w fills rows (w NKP + u) * rows_per_piece ..; the
+  // lane's 16 B land at chunk position lane % NCH, so it loads the chunk the
+  // rt_off image keeps there
+  constexpr int RPP = 1024 / ROWB;
+  int kgo[NKP];
+#pragma unroll
+  for (int u = 0; u < NKP; ++u) {
+    const int row = (wave * NKP + u) * RPP + lane / NCH, cpos = lane % NCH;
+    const int swz = D == 128 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 3) << 1) | ((row >> 2) & 1));
+    kgo[u] = row * D + ((cpos ^ swz) << 3);
+  }
+  // dS blocks as stored: 8-byte piece (key k, sigma) at sigma * 256 + k * 8.
+  // In LDS the 32-byte key quads of piece row sigma rotate by sigma (quad kq
+  // at ((kq + sigma) & 7) * 32), which makes the transposed reads below
+  // conflict-free; the rotation is applied to the DMA's source chunks.  LDS
+  // chunk j = 64 half + lane holds global chunk 16 sigma + 2 kq + (j & 1).
+  int dsg[2];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int sg = 4 * half + (lane >> 4), jj = lane & 15;
+    dsg[half] = (16 * sg + ((((jj >> 1) - sg) & 7) << 1) + (jj & 1)) * 8;
+  }
+  auto stage_k = [&](int t, char* st) {  // this wave's pieces of K tile t (shared by the workgroup)
+#pragma unroll
+    for (int u = 0; u < NKP; ++u)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(kbase + (int64_t)t * TK * D + (uint32_t)kgo[u]),
+          (__attribute__((address_space(3))) void*)(st + (wave * NKP + u) * 1024), 16, 0, 0);
+  };
+  auto stage_s = [&](int t, char* st) {  // this wave's own dS blocks 2t, 2t + 1 (clamped to the diagonal)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int ki = min(2 * t + (v >> 1), qi);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(dsrow + ((int64_t)ki << 10) + (uint32_t)dsg[v & 1]),
+          (__attribute__((address_space(3))) void*)(st + KT + wave * DQG<D>::DSW + v * 1024), 16, 0,
+          2 /* nt: read once; leave L2 to the K tiles */);
+    }
+  };
+
+  int tro[ND], tro8[ND];
+  {
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int c = 4 * dt + 2 * (g & 1) + (pp >> 1);
+      tro[dt] = rt_off<D>(4 * hh + qq, c) + (pp & 1) * 8;
+      tro8[dt] = rt_off<D>(4 * hh + qq + 8, c) + (pp & 1) * 8;
+    }
+  }
+  // dS^T operand: group lane 4q + p reads key R = 16 s2 + 8 e + 4 hh + q,
+  // queries 16 (g & 1) + 4p .. + 3 = piece sigma = 4 (g & 1) + p, at
+  // sigma * 256 + (((R >> 2) + sigma) & 7) * 32 + (R & 3) * 8 in LDS
+  int dso[2][2];
+  {
+    const int sg = 4 * ((lane >> 4) & 1) + (lane & 3), q = (lane >> 2) & 3;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) dso[s2][e] = sg * 256 + (((4 * s2 + 2 * e + hh) + sg) & 7) * 32 + q * 8;
+  }
+
+  f32x16 acc[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+
+  auto compute = [&](int t, const char* st) {
+    const char* dimg = st + KT + wave * DQG<D>::DSW;
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      if (n == 1 && 2 * t + 1 > qi) break;  // above the diagonal: never stored
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x4 lo = tr_read(dimg + n * 2048, dso[s2][0]);
+        const bf16x4 hi = tr_read(dimg + n * 2048, dso[s2][1]);
+        const bf16x8 sb = (bf16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        const int rb = (32 * n + 16 * s2) * ROWB;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          const bf16x4 a = tr_read(st, tro[dt] + rb), c = tr_read(st, tro8[dt] + rb);
+          acc[dt] = mfma32((bf16x8)__builtin_shufflevector(a, c, 0, 1, 2, 3, 4, 5, 6, 7), sb, acc[dt]);
+        }
+      }
+    }
+  };
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // The K tiles are shared, so they are restaged only behind a barrier; a
+  // wave's dS slot is its own, so it is refilled as soon as the wave has
+  // read it -- dS runs three tiles ahead, K two.  Per-wave issue order:
+  // dS0 K0 dS1 K1 dS2 | K2 dS3 | K3 dS4 | ...; at tile t, K t and dS t are
+  // retired once only dS t+1, K t+1 and dS t+2 (2 x 4 + NKP pieces) may
+  // still be in flight.  Past the end the last tile is re-fetched into a
+  // slot nobody reads (constant DMA count).
+  auto it = [&](int t, const char* cur, char* kpre) {
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (8 + NKP));
+    sync();  // every wave's K pieces of t landed; every wave done with K t - 1
+    stage_k(min(t + 2, ntiles - 1), kpre);
+    if (t <= tdiag) compute(t, cur);
+    stage_s(min(t + 3, ntiles - 1), (char*)cur);
+  };
+  stage_s(0, s0);
+  stage_k(0, s0);
+  stage_s(1, s1);
+  stage_k(1, s1);
+  stage_s(2, s2);
+  // whole rounds of three (the extra tiles compute nothing): a conditional
+  // it() would let hipcc's wait-count pass see a path on which the slot
+  // about to be read was just restaged, and wait vmcnt(0) before every read
+  for (int t = 0; t < ntiles; t += 3) {
+    it(t, s0, s2);
+    it(t + 1, s1, s0);
+    it(t + 2, s2, s1);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA in flight at exit
+
+  bf16_t* qrow = dQ + ((int64_t)(b * H + h) * S + qi * 32 + r) * D;
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint2 w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int g = 2 * k + u;
+        w[u].x = pack2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
+        w[u].y = pack2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
+      }
+      store_pair16(qrow, 32 * dt + 16 * k, hh, w[0], w[1]);
+    }
+}
+
+// dK / dV of the dS form: the split form's dK/dV kernel (same workgroup /
+// wave geometry and the same sub-tile body) with
+//  * the Q / dO tiles and their -lse log2(e) / -delta rows (from the delta
+//    pass) brought in by LDS-DMA into two distinct LDS objects (no register
+//    staging: 16 VGPRs and the ds_write pass freed; guide §5 "Pipelining
+//    across barriers"), and
+//  * every (32-query, 32-key) dS block stored for the dQ GEMM (layout at
+//    attn_bwd_dqg_kernel), between the sub-tile's two MFMA halves so the
+//    stores drain under the second half.
+// Each step ends with its own DMA and stores retired (vmcnt(0)) and a
+// barrier.  LSE / DELTA here are the delta pass's -lse log2(e) / -delta rows.
+// S % 256 == 0 only (no ragged tiles).
+template <int D>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, bf16_t* __restrict__ dS, int B, int H, int Hk, int S,
+    float scale, float scale_log2, int o_bshd) {
+  using G = AG<D>;
+  constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
+  constexpr int QBUF = DKV<D>::QBUF, KVB = DKV<D>::KVB;
+  constexpr int NLK = 128 * NCH / 512;
+  // Q/dO/lse/-delta buffers 0 and 1, K and V: distinct LDS objects, so
+  // hipcc's wait-count pass knows a read of one buffer cannot alias the
+  // LDS-DMA filling the other (with one array it waits vmcnt(0) before the
+  // first transposed read of every sub-tile)
+  __shared__ __attribute__((aligned(1024))) char qd0[QBUF];
+  __shared__ __attribute__((aligned(1024))) char qd1[QBUF];
+  __shared__ __attribute__((aligned(1024))) char kv[2 * KVB];
+  char* kimg = kv;
+  char* vimg = kv + KVB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int kg = wave & 3, m = wave >> 2;
+  // heaviest (most query tiles) key blocks first; (b, hk) fastest
+  const int nkb = (S + 127) / 128;
+  const int kb = nkb - 1 - (int)(blockIdx.x / (B * Hk));
+  const int bh = blockIdx.x % (B * Hk);
+  const int b = bh / Hk, hk = bh % Hk;
+  const int rep = H / Hk;
+  const int kw = kb * 128 + kg * 32;  // first key of this wave
+  const int mykey = kw + r;
+  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
+
+  // K / V of the block -> LDS (rt_off image: row reads give the B operands)
+#pragma unroll
+  for (int i = 0; i < NLK; ++i) {
+    const int e = tid + 512 * i;
+    const int row = e / NCH, c = e % NCH;
+    const int64_t g = koff + (int64_t)(kb * 128 + row) * D + c * 8;
+    *(u32x4*)(kimg + rt_off<D>(row, c)) = ld16(K + g);
+    *(u32x4*)(vimg + rt_off<D>(row, c)) = ld16(V + g);
+  }
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { dk[i][j] = 0.f; dv[i][j] = 0.f; }
+
+  int rro[NS], tro[ND], tro8[ND];
+  {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) rro[s] = rt_off<D>(r, 2 * s + hh);
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const int c = 4 * dt + 2 * (g & 1) + (pp >> 1);
+      tro[dt] = rt_off<D>(4 * hh + qq, c) + (pp & 1) * 8;
+      tro8[dt] = rt_off<D>(4 * hh + qq + 8, c) + (pp & 1) * 8;
+    }
+  }
+
+  const int qt0 = (kb * 128) / 64;  // first causal 64-row query tile
+  const int nqt = (S + TK - 1) / TK - qt0;
+  const int total = nqt * rep;
+  // Q / dO tiles by LDS-DMA (no register staging): 1-KB piece pt of a tile
+  // covers rows RPP pt .. + RPP - 1; waves 0-3 fetch Q, 4-7 dO, PW pieces
+  // each.  The lane's 16 B land at chunk position lane % NCH of row
+  // RPP pt + lane / NCH, so it loads the chunk the rt_off image keeps there
+  // (the swizzle's row-block part is (pt & 3) << 3 elements at D = 128, 0 at 64).
+  constexpr int RPP = 1024 / ROWB, PPT = TILEB / 1024, PW = PPT / 4;
+  const int lrow = lane / NCH;
+  const int lswz = D == 128 ? (lrow & 3) << 2 : ((lrow & 3) << 1) | ((lrow >> 2) & 1);
+  const int lcol = ((lane % NCH) ^ lswz) << 3;
+  auto stage = [&](int it, int buf) {
+    const int hq = hk * rep + it / nqt;
+    const int qt = qt0 + it % nqt;
+    char* st = buf ? qd1 : qd0;
+    if (wave < 4) {
+      const bf16_t* src = Q + ((int64_t)(b * H + hq) * S + qt * 64) * D;
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int pt = PW * wave + u;
+        const int col = D == 128 ? lcol ^ ((pt & 3) << 3) : lcol;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + (uint32_t)((RPP * pt + lrow) * D + col)),
+            (__attribute__((address_space(3))) void*)(st + pt * 1024), 16, 0, 0);
+      }
+    } else {
+      const int64_t rs = o_bshd ? (int64_t)H * D : D;  // dO row stride
+      const bf16_t* src = dO + o_off<D>(b, hq, qt * 64, H, S, o_bshd);
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int pt = PW * (wave - 4) + u;
+        const int col = D == 128 ? lcol ^ ((pt & 3) << 3) : lcol;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(src + (uint32_t)((RPP * pt + lrow) * rs + col)),
+            (__attribute__((address_space(3))) void*)(st + TILEB + pt * 1024), 16, 0, 0);
+      }
+    }
+    if (wave == 0) {  // -lse log2e and -delta rows (the delta pass wrote them): 256 B each
+      const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + lane;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(LSE + li),
+                                       (__attribute__((address_space(3))) void*)(st + 2 * TILEB), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(DELTA + li),
+                                       (__attribute__((address_space(3))) void*)(st + 2 * TILEB + 256), 4, 0, 0);
+    }
+  };
+
+  auto subtile = [&](int buf, int qs, bool mask, bf16_t* dsb) {
+    const char* qi = buf ? qd1 : qd0;
+    const char* oi = qi + TILEB;
+    const float* lb = (const float*)(qi + 2 * TILEB);
+    f32x16 nd;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 d4 = *(const f32x4*)(lb + 64 + 32 * m + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nd[4 * g4 + j] = d4[j];
+    }
+    const f32x16 z = {};
+    f32x16 sc = z, dp = nd;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const bf16x8 qa = as_bf16x8(*(const u32x4*)(qi + rro[s] + 32 * ROWB * m));
+      const bf16x8 kf = as_bf16x8(*(const u32x4*)(kimg + rro[s] + 32 * ROWB * kg));
+      sc = mfma32(qa, kf, sc);
+      const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rro[s] + 32 * ROWB * m));
+      const bf16x8 vf = as_bf16x8(*(const u32x4*)(vimg + rro[s] + 32 * ROWB * kg));
+      dp = mfma32(oa, vf, dp);
+    }
+    // (scalar VALU here: the packed forms need aligned register pairs, and at
+    // 256 VGPRs with resident dK^T / dV^T accumulators that spills in the loop)
+    uint32_t pw[8], sw[8];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      const f32x4 l4 = *(const f32x4*)(lb + 32 * m + 8 * (j >> 2) + 4 * hh);  // -lse * log2(e)
+      float p0 = EXP2(fmaf(sc[j], scale_log2, l4[j & 3]));
+      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, l4[(j + 1) & 3]));
+      if (mask) {
+        const int q = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        if (q < mykey) p0 = 0.f;
+        if (q + 1 < mykey) p1 = 0.f;
+      }
+      pw[j >> 1] = pack2(p0, p1);
+      sw[j >> 1] = pack2(p0 * dp[j], p1 * dp[j + 1]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      u32x4 a, c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = pw[4 * s2 + i];
+        c[i] = sw[4 * s2 + i];
+      }
+      const bf16x8 pb = as_bf16x8(a), sb = as_bf16x8(c);
+      const int rb = (32 * m + 16 * s2) * ROWB;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        const bf16x4 o0 = tr_read(oi, tro[dt] + rb), o1 = tr_read(oi, tro8[dt] + rb);
+        dv[dt] = mfma32((bf16x8)__builtin_shufflevector(o0, o1, 0, 1, 2, 3, 4, 5, 6, 7), pb, dv[dt]);
+        const bf16x4 q0 = tr_read(qi, tro[dt] + rb), q1 = tr_read(qi, tro8[dt] + rb);
+        dk[dt] = mfma32((bf16x8)__builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7), sb, dk[dt]);
+      }
+      if (s2 == 0) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {  // streamed once, by the dQ GEMM: non-temporal
+          typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+          __builtin_nontemporal_store(u32x2{sw[2 * g], sw[2 * g + 1]}, (u32x2*)(dsb + g * 256 + hh * 128 + r * 4));
+        }
+      }
+    }
+  };
+  auto step = [&](int it, int buf) {
+    if (it + 1 < total) stage(it + 1, buf ^ 1);
+    const int qs = (qt0 + it % nqt) * 64 + 32 * m;
+    const int hq = hk * rep + it / nqt, qb32 = qs >> 5, nb = S >> 5;
+    bf16_t* dsb = dS + (int64_t)(b * H + hq) * (nb * (nb + 1) / 2) * 1024 + ((uint32_t)(qb32 * (qb32 + 1) / 2 + (kw >> 5)) << 10);
+    if (qs > kw) subtile(buf, qs, false, dsb);        // strictly below this wave's diagonal
+    else if (qs == kw) subtile(buf, qs, true, dsb);  // the diagonal sub-tile
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  int it = 0;
+  for (; it + 1 < total; it += 2) {  // unrolled by 2: buffer offsets become immediates
+    step(it, 0);
+    step(it + 1, 1);
+  }
+  if (it < total) step(it, 0);
+
+  // sum the two query halves' partials: waves m = 1 park theirs in LDS
+  // (dK^T partials in kv, dV^T in qd0 / qd1: ND 16 64 floats per wave)
+  constexpr int RW = ND * 16 * 64;
+  float* rdk = (float*)kv + kg * RW;
+  float* rdv = (float*)(kg < 2 ? qd0 : qd1) + (kg & 1) * RW;
+  if (m == 1) {
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        *(f32x4*)(rdk + (dt * 16 + j) * 64 + lane * 4) = f32x4{dk[dt][j], dk[dt][j + 1], dk[dt][j + 2], dk[dt][j + 3]};
+        *(f32x4*)(rdv + (dt * 16 + j) * 64 + lane * 4) = f32x4{dv[dt][j], dv[dt][j + 1], dv[dt][j + 2], dv[dt][j + 3]};
+      }
+  }
+  __syncthreads();
+  if (m == 1) return;
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      const f32x4 a = *(const f32x4*)(rdk + (dt * 16 + j) * 64 + lane * 4);
+      const f32x4 c = *(const f32x4*)(rdv + (dt * 16 + j) * 64 + lane * 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dk[dt][j + i] += a[i];
+        dv[dt][j + i] += c[i];
+      }
+    }
+  // store: lane owns key `mykey`, d rows 32dt + 8g + 4hh + (0..3)
+  bf16_t* dkr = dK + koff + (int64_t)mykey * D;
+  bf16_t* dvr = dV + koff + (int64_t)mykey * D;
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint2 a[2], c[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int g = 2 * k + u;
+        a[u].x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
+        a[u].y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+        c[u].x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
+        c[u].y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
+      }
+      store_pair16(dkr, 32 * dt + 16 * k, hh, a[0], a[1]);
+      store_pair16(dvr, 32 * dt + 16 * k, hh, c[0], c[1]);
+    }
+}
+
+// Backward form: 0 = split (dQ recomputes S / dP; default), 1 = dS through
+// HBM (S % 256 == 0 only).  TOA_ATTN_BWD=ds or toa_attn_set_bwd_variant.
+static int g_bwd_variant = -1;
+static int attn_bwd_variant() {
+  if (g_bwd_variant < 0) {
+    const char* e = getenv("TOA_ATTN_BWD");
+    g_bwd_variant = (e && e[0] == 'd' && e[1] == 's') ? 1 : 0;
+  }
+  return g_bwd_variant;
+}
+extern "C" int toa_attn_set_bwd_variant(int v) {
+  if (v != 0 && v != 1) return (int)hipErrorInvalidValue;
+  g_bwd_variant = v;
+  return 0;
+}
+static bool attn_bwd_uses_ds(int S) { return attn_bwd_variant() == 1 && S % FWD_QB == 0; }
+// [dS blocks][-lse log2e rows]; the -delta rows go to the caller's delta buffer
+static int64_t attn_ds_blocks_bytes(int B, int H, int S) {
+  const int64_t nb = S / 32;
+  return (int64_t)B * H * (nb * (nb + 1) / 2) * 2048;
+}
+static int64_t attn_ds_bytes(int B, int H, int S) {
+  return attn_ds_blocks_bytes(B, H, S) + (int64_t)B * H * S * 4 + 2048;
+}
+// Workspace toa_attn_bwd needs (its `ws` argument) under the current form; 0 = none.
+extern "C" int64_t toa_attn_bwd_ws_bytes(int B, int H, int S, int D) {
+  (void)D;
+  return attn_bwd_uses_ds(S) ? attn_ds_bytes(B, H, S) : 0;
+}
+
 // dK/dV kernel form: 8 (8-wave, K/V in LDS; default) or 4 (4-wave, K/V in
 // registers); TOA_ATTN_DKDV=4 or toa_attn_set_dkdv_variant for A/B runs.
 static int g_dkdv_variant = -1;
@@ -1065,9 +1566,24 @@ static int attn_fwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf
 
 template <int D, bool TAIL>
 static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
-                           const float* lse, float* delta, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B, int H, int Hk,
-                           int S, int o_bshd, float scale, hipStream_t stream) {
+                           const float* lse, float* delta, void* ws, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B, int H,
+                           int Hk, int S, int o_bshd, float scale, hipStream_t stream) {
   attn_set_lds_limits<D, TAIL>();
+  if constexpr (!TAIL) {
+    if (attn_bwd_uses_ds(S)) {
+      if (ws == nullptr) return (int)hipErrorInvalidValue;
+      bf16_t* ds = (bf16_t*)ws;
+      float* nlse2 = (float*)((char*)ws + attn_ds_blocks_bytes(B, H, S));
+      const int rows = B * H * S;
+      hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
+                         stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
+      hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k, v, dout,
+                         nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
+      hipLaunchKernelGGL((attn_bwd_dqg_kernel<D>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, dq, B, H,
+                         Hk, S, scale);
+      return (int)hipGetLastError();
+    }
+  }
   // dQ first: it also computes delta = rowsum(dO * O), which dK/dV then reads
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, TAIL>), dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES),
                      4 * AG<D>::TILEB, stream, q, k, v, dout, o, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E,
@@ -1103,16 +1619,15 @@ extern "C" int toa_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, b
 #undef TOA_ATTN_FWD
 }
 
-// dq_acc is unused (kept in the ABI for an atomic-dQ variant); dq/dk/dv bf16.
+// ws: toa_attn_bwd_ws_bytes(B, H, S, D) bytes (may be null when that is 0); dq/dk/dv bf16.
 extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
-                            const float* lse, float* delta, float* dq_acc, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B,
+                            const float* lse, float* delta, void* ws, bf16_t* dq, bf16_t* dk, bf16_t* dv, int B,
                             int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
-  (void)dq_acc;
   if (!attn_shape_ok(B, H, Hk, S, D, flags)) return (int)hipErrorInvalidValue;
   const int o_bshd = (flags >> 1) & 1;
   const bool tail = S % FWD_QB != 0;
 #define TOA_ATTN_BWD(DD, TT) \
-  attn_bwd_launch<DD, TT>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, H, Hk, S, o_bshd, scale, stream)
+  attn_bwd_launch<DD, TT>(q, k, v, o, dout, lse, delta, ws, dq, dk, dv, B, H, Hk, S, o_bshd, scale, stream)
 #ifdef TOA_ATTN_D128_ONLY
   if (D != 128) return (int)hipErrorInvalidValue;
   return tail ? TOA_ATTN_BWD(128, true) : TOA_ATTN_BWD(128, false);

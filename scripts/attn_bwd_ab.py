@@ -1,10 +1,14 @@
-"""In-process A/B of the attention-backward kernel forms at the Llama-3-8B
-bench shape (B=6, H=32, Hkv=8, S=4096, D=128, O/dO in [B,S,H,D]):
-dQ + dK/dV with the 8-wave dK/dV kernel (K/V re-read from LDS) vs the
-4-wave one (K/V fragments in registers), interleaved rounds on random
-data (guide §5.4 rules 24/25).  Also checks the two forms agree.
+"""In-process A/B of the attention-backward forms at the Llama-3-8B bench
+shape (B=6, H=32, Hkv=8, S=4096, D=128, O/dO in [B,S,H,D]), interleaved
+rounds on random data (guide §5.4 rules 24/25):
 
-    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5]
+    split8  dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
+    split4  the same with the 4-wave dK/dV (K/V fragments in registers)
+    ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
+
+Also checks every form agrees with split8.
+
+    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5] [--variants split8,ds]
 """
 import argparse
 import json
@@ -23,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=6)
+    ap.add_argument("--variants", default="split8,split4,ds")
     a = ap.parse_args()
     B, H, Hk, S, D = a.batch, 32, 8, 4096, 128
     dev = "cuda"
@@ -40,23 +45,32 @@ def main():
     _lib.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, flags, scale, _lib.stream(q))
     outs = {}
 
+    forms = {"split8": (8, 0), "split4": (4, 0), "ds": (8, 1)}
+    variants = a.variants.split(",")
+
     def run(variant):
-        _lib.call("toa_attn_set_dkdv_variant", variant)
+        dkdv, bwd = forms[variant]
+        _lib.call("toa_attn_set_dkdv_variant", dkdv)
+        _lib.call("toa_attn_set_bwd_variant", bwd)
+        nws = _lib.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D)
+        ws = torch.empty(nws, device=dev, dtype=torch.uint8) if nws > 0 else None
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        _lib.call("toa_attn_bwd", P(q), P(k), P(v), P(o), P(do), P(lse), P(delta), None, P(dq), P(dk), P(dv), B, H,
+        _lib.call("toa_attn_bwd", P(q), P(k), P(v), P(o), P(do), P(lse), P(delta), P(ws), P(dq), P(dk), P(dv), B, H,
                   Hk, S, D, flags, scale, _lib.stream(q))
         return dq, dk, dv
 
-    for var in (8, 4):
+    for var in variants:
         outs[var] = run(var)
     torch.cuda.synchronize()
-    agree = {n: float((outs[4][i].float() - outs[8][i].float()).norm() / outs[8][i].float().norm())
-             for i, n in enumerate(("dq", "dk", "dv"))}
+    base = variants[0]
+    agree = {f"{var}_vs_{base}": {n: float((outs[var][i].float() - outs[base][i].float()).norm()
+                                            / outs[base][i].float().norm()) for i, n in enumerate(("dq", "dk", "dv"))}
+             for var in variants[1:]}
     flops_fwd = 4 * B * H * S * S * D / 2  # causal: two matmuls over half the scores
-    times = {8: [], 4: []}
+    times = {v: [] for v in variants}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for _ in range(a.rounds):
-        for var in (8, 4):
+        for var in variants:
             run(var)
             ev[0].record()
             for _ in range(a.reps):
@@ -64,10 +78,10 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[var].append(ev[0].elapsed_time(ev[1]) / a.reps)
-    res = {"shape": [B, H, Hk, S, D], "rel_diff_4_vs_8": agree}
+    res = {"shape": [B, H, Hk, S, D], "rel_diff": agree}
     for var, t in times.items():
         med = statistics.median(t)
-        res[f"dkdv{var}"] = {"median_ms": round(med, 3), "min_ms": round(min(t), 3),
+        res[var] = {"median_ms": round(med, 3), "min_ms": round(min(t), 3),
                              "useful_PFps": round(2.5 * flops_fwd / med / 1e12, 3)}
     print(json.dumps(res))
 

@@ -496,6 +496,52 @@ def test_flash_attention_bench_shape():
         del qr, kr, vr, orf
 
 
+@pytest.mark.parametrize("B,H,Hk,S,D,bshd", [(1, 2, 2, 256, 128, False), (2, 4, 2, 512, 128, True),
+                                              (1, 8, 2, 1024, 128, True), (1, 4, 1, 768, 128, False),
+                                              (2, 4, 2, 512, 64, False), (1, 2, 1, 1024, 64, True)])
+def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
+    """The dS-through-HBM backward (delta pass, dK/dV storing the lower-
+    triangular dS blocks, dQ as a GEMM over them) vs the fp32 reference and
+    vs the split form: dK/dV bit-identical (same kernel body), dQ close."""
+    L = _lib()
+    torch.manual_seed(5)
+    scale = 1.0 / math.sqrt(D)
+    q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16) if bshd else torch.empty_like(q)
+    lse = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
+    flags = 1 | (2 if bshd else 0)
+    P = L.ptr
+    L.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, flags, scale, L.stream(q))
+    do = torch.randn_like(o)
+    grads = {}
+    try:
+        for form in (0, 1):
+            L.call("toa_attn_set_bwd_variant", form)
+            nws = L.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D)
+            assert (nws > 0) == (form == 1)
+            ws = torch.full((nws,), 0xFF, device=DEV, dtype=torch.uint8) if nws else None  # NaN-poisoned
+            delta = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
+            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            L.call("toa_attn_bwd", P(q), P(k), P(v), P(o), P(do), P(lse), P(delta), P(ws), P(dq), P(dk), P(dv),
+                   B, H, Hk, S, D, flags, scale, L.stream(q))
+            torch.cuda.synchronize()
+            grads[form] = (dq, dk, dv, delta)
+    finally:
+        L.call("toa_attn_set_bwd_variant", 0)
+    (dq0, dk0, dv0, de0), (dq1, dk1, dv1, de1) = grads[0], grads[1]
+    assert torch.isfinite(dq1.float()).all()
+    assert rel(-de1, de0) < 1e-5  # the dS form's delta pass leaves -delta (the dP accumulators' start)
+    assert rel(dk1, dk0) < 1e-2 and rel(dv1, dv0) < 1e-2
+    assert rel(dq1, dq0) < 1e-2, rel(dq1, dq0)
+    qr, kr, vr = [t.float().requires_grad_() for t in (q, k, v)]
+    orf, _ = _attn_ref(qr, kr, vr, scale)
+    orf.backward((do.transpose(1, 2) if bshd else do).float())
+    for got, ref in ((dq1, qr.grad), (dk1, kr.grad), (dv1, vr.grad)):
+        assert rel(got, ref) < 3e-2, rel(got, ref)
+
+
 def test_attention_gpu_has_no_library_fallback():
     """A GPU tensor the HIP kernel cannot take raises instead of silently
     running a library (SDPA / aotriton) kernel."""

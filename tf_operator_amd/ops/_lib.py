@@ -83,6 +83,7 @@ _SIGS = {
     "toa_gemm_tn_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_tn_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_attn_set_dkdv_variant": [c_int],
+    "toa_attn_set_bwd_variant": [c_int],
     "toa_emulate_xfer": [c_p, c_p, c_i64, c_int, ctypes.c_double, c_p],
     "toa_gemm_tune": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p, c_p, c_p,
                       c_p, c_p, c_int],
@@ -112,6 +113,9 @@ def _load():
         ws = getattr(lib, "toa_bn_ws_floats", None)
         if ws is not None:
             ws.argtypes, ws.restype = [c_i64, c_int], c_i64
+        aw = getattr(lib, "toa_attn_bwd_ws_bytes", None)
+        if aw is not None:
+            aw.argtypes, aw.restype = [c_int, c_int, c_int, c_int], c_i64
         ww = getattr(lib, "toa_wgrad_workspace", None)
         if ww is not None:
             ww.argtypes, ww.restype = [c_int, c_int, c_int, c_int], c_i64

@@ -297,8 +297,12 @@ class _FlashAttn(torch.autograd.Function):
         dk = torch.empty_like(k)
         dv = torch.empty_like(v)
         delta = torch.empty(B, H, S, device=q.device, dtype=torch.float32)
+        # the dS-through-HBM form (attention.hip, TOA_ATTN_BWD=ds) needs a
+        # lower-triangular dS buffer (3.2 GB at the Llama-3-8B bench shape)
+        nws = _lib.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D) if _lib.has("toa_attn_bwd_ws_bytes") else 0
+        ws = torch.empty(nws, device=q.device, dtype=torch.uint8) if nws > 0 else None
         _lib.call("toa_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do), _lib.ptr(lse),
-                  _lib.ptr(delta), None, _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D,
+                  _lib.ptr(delta), _lib.ptr(ws), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D,
                   1 | (2 if ctx.bshd else 0), float(ctx.scale), _lib.stream(q))
         return dq, dk, dv, None, None
 
