@@ -23,9 +23,11 @@
 // wave's last row are skipped wave-uniformly; blocks are launched
 // heaviest-first for load balance.
 //
-// Backward = two kernels: dQ (which also computes delta = rowsum(dO*O)),
-// then dK/dV (workgroup per 128-key block, sweeping the GQA group's query
-// heads).  No float atomics: deterministic.
+// Backward (S % 256 == 0, default): a delta pass, dK/dV (workgroup per
+// 128-key block, sweeping the GQA group's query heads) which also stores dS,
+// and dQ as a GEMM over the stored dS; otherwise two kernels: dQ (which also
+// computes delta = rowsum(dO*O)), then dK/dV.  No float atomics:
+// deterministic.
 //
 // Ragged S (S % 64 != 0): every row index that feeds a LOAD is clamped to
 // S - 1, so tiles past the end re-read the last row instead of branching
@@ -1026,10 +1028,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dq_kernel(
 // Backward with dS through HBM (TOA_ATTN_BWD=ds): the dK/dV kernel already
 // forms dS = P * (dP - delta) for every (32-query, 32-key) block at or below
 // the diagonal; the dS form's dK/dV kernel also stores them (bf16, 2 KB per
-// block: the lane's 8-byte (key, 4-query) pieces, piece sigma = 2 g' + hh of
-// key k at sigma * 256 + k * 8 bytes, so each store instruction writes 512
-// contiguous bytes; the blocks of one (batch, head) packed lower-triangular:
-// block (qi, ki) at qi (qi + 1) / 2 + ki).  dQ = scale * dS K is
+// block of 16-byte (key, 8-query) chunks, chunk (k, g') at g' * 512 + k * 16
+// bytes, so each store instruction writes 1 KB contiguous; the blocks of one
+// (batch, head) packed lower-triangular: block (qi, ki) at qi (qi + 1) / 2 + ki).  dQ = scale * dS K is
 // then a plain GEMM over those blocks -- the split form's dQ kernel recomputes
 // S and dP for it (3 of the backward's 7 executed S^2 D products; this form
 // executes 5).  The dS round trip is 2 x 3.2 GB at the Llama-3-8B shape; the
@@ -1116,16 +1117,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     const int swz = D == 128 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 3) << 1) | ((row >> 2) & 1));
     kgo[u] = row * D + ((cpos ^ swz) << 3);
   }
-  // dS blocks as stored: 8-byte piece (key k, sigma) at sigma * 256 + k * 8.
-  // In LDS the 32-byte key quads of piece row sigma rotate by sigma (quad kq
-  // at ((kq + sigma) & 7) * 32), which makes the transposed reads below
-  // conflict-free; the rotation is applied to the DMA's source chunks.  LDS
-  // chunk j = 64 half + lane holds global chunk 16 sigma + 2 kq + (j & 1).
+  // dS blocks as stored: 16-byte chunk (key k, queries 8g' .. + 7) at
+  // g' * 512 + k * 16.  In LDS the keys of chunk row g' rotate by 4g' (chunk
+  // (k, g') at g' * 512 + ((k + 4g') & 31) * 16), which makes the transposed
+  // reads below conflict-free; the rotation is applied to the DMA's source
+  // chunks: LDS chunk j = 64 half + lane holds (k = ((j & 31) - 4g') & 31, g' = j >> 5).
   int dsg[2];
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
-    const int sg = 4 * half + (lane >> 4), jj = lane & 15;
-    dsg[half] = (16 * sg + ((((jj >> 1) - sg) & 7) << 1) + (jj & 1)) * 8;
+    const int gq = 2 * half + (lane >> 5);
+    dsg[half] = (32 * gq + (((lane & 31) - 4 * gq) & 31)) * 8;
   }
   auto stage_k = [&](int t, char* st) {  // this wave's pieces of K tile t (shared by the workgroup)
 #pragma unroll
@@ -1156,15 +1157,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     }
   }
   // dS^T operand: group lane 4q + p reads key R = 16 s2 + 8 e + 4 hh + q,
-  // queries 16 (g & 1) + 4p .. + 3 = piece sigma = 4 (g & 1) + p, at
-  // sigma * 256 + (((R >> 2) + sigma) & 7) * 32 + (R & 3) * 8 in LDS
+  // queries 16 (g & 1) + 4p .. + 3 = half (p & 1) of chunk g' = 2 (g & 1) + (p >> 1)
   int dso[2][2];
   {
-    const int sg = 4 * ((lane >> 4) & 1) + (lane & 3), q = (lane >> 2) & 3;
+    const int gq = 2 * ((lane >> 4) & 1) + ((lane & 3) >> 1), q = (lane >> 2) & 3;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) dso[s2][e] = sg * 256 + (((4 * s2 + 2 * e + hh) + sg) & 7) * 32 + q * 8;
+      for (int e = 0; e < 2; ++e)
+        dso[s2][e] = gq * 512 + ((16 * s2 + 8 * e + 4 * hh + q + 4 * gq) & 31) * 16 + (lane & 1) * 8;
   }
 
   f32x16 acc[ND];
@@ -1254,7 +1255,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
 // Each step ends with its own DMA and stores retired (vmcnt(0)) and a
 // barrier.  LSE / DELTA here are the delta pass's -lse log2(e) / -delta rows.
 // S % 256 == 0 only (no ragged tiles).
-template <int D>
+template <int D, bool STORE = true>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -1416,11 +1417,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
         const bf16x4 q0 = tr_read(qi, tro[dt] + rb), q1 = tr_read(qi, tro8[dt] + rb);
         dk[dt] = mfma32((bf16x8)__builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7), sb, dk[dt]);
       }
-      if (s2 == 0) {
+      if (STORE && s2 == 0) {  // chunk (key r, queries 8g' .. + 7), g' = 2k + hh, at g' * 512 + r * 16 bytes
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {  // streamed once, by the dQ GEMM: non-temporal
-          typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
-          __builtin_nontemporal_store(u32x2{sw[2 * g], sw[2 * g + 1]}, (u32x2*)(dsb + g * 256 + hh * 128 + r * 4));
+        for (int k = 0; k < 2; ++k) {
+          const auto x = __builtin_amdgcn_permlane32_swap(sw[4 * k], sw[4 * k + 2], false, false);
+          const auto y = __builtin_amdgcn_permlane32_swap(sw[4 * k + 1], sw[4 * k + 3], false, false);
+          // streamed once, by the dQ GEMM: non-temporal
+          __builtin_nontemporal_store(u32x4{x[0], y[0], x[1], y[1]}, (u32x4*)(dsb + (2 * k + hh) * 256 + r * 8));
         }
       }
     }
@@ -1493,22 +1496,30 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     }
 }
 
-// Backward form: 0 = split (dQ recomputes S / dP; default), 1 = dS through
-// HBM (S % 256 == 0 only).  TOA_ATTN_BWD=ds or toa_attn_set_bwd_variant.
+// Backward form: 1 = dS through HBM (default where S % 256 == 0: the
+// Llama-3-8B step 987.9 -> 978.1 ms, profiles/r3_attn_ds), 0 = split (dQ
+// recomputes S / dP; ragged S always).  TOA_ATTN_BWD=split|ds, or
+// toa_attn_set_bwd_variant (-1: back to the environment's choice).
 static int g_bwd_variant = -1;
 static int attn_bwd_variant() {
   if (g_bwd_variant < 0) {
     const char* e = getenv("TOA_ATTN_BWD");
-    g_bwd_variant = (e && e[0] == 'd' && e[1] == 's') ? 1 : 0;
+    g_bwd_variant = (e && e[0] == 's' && e[1] == 'p') ? 0 : 1;
   }
   return g_bwd_variant;
 }
+// 2 (A/B only): the split form's dQ kernel, then the delta pass and the dS
+// form's dK/dV kernel without its dS stores -- prices the LDS-DMA staging
 extern "C" int toa_attn_set_bwd_variant(int v) {
-  if (v != 0 && v != 1) return (int)hipErrorInvalidValue;
+  if (v == -1) {
+    g_bwd_variant = -1;
+    return 0;
+  }
+  if (v < 0 || v > 2) return (int)hipErrorInvalidValue;
   g_bwd_variant = v;
   return 0;
 }
-static bool attn_bwd_uses_ds(int S) { return attn_bwd_variant() == 1 && S % FWD_QB == 0; }
+static bool attn_bwd_uses_ds(int S) { return attn_bwd_variant() >= 1 && S % FWD_QB == 0; }
 // [dS blocks][-lse log2e rows]; the -delta rows go to the caller's delta buffer
 static int64_t attn_ds_blocks_bytes(int B, int H, int S) {
   const int64_t nb = S / 32;
@@ -1575,6 +1586,16 @@ static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
       bf16_t* ds = (bf16_t*)ws;
       float* nlse2 = (float*)((char*)ws + attn_ds_blocks_bytes(B, H, S));
       const int rows = B * H * S;
+      if (attn_bwd_variant() == 2) {
+        hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), dim3((S / FWD_QB) * H * B), dim3(64 * FWD_WAVES),
+                           4 * AG<D>::TILEB, stream, q, k, v, dout, o, lse, delta, dq, B, H, Hk, S, scale,
+                           scale * LOG2E, o_bshd);
+        hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
+                           stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
+        hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, false>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k,
+                           v, dout, nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
+        return (int)hipGetLastError();
+      }
       hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
                          stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
       hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k, v, dout,

@@ -5,6 +5,8 @@ rounds on random data (guide §5.4 rules 24/25):
     split8  dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
     split4  the same with the 4-wave dK/dV (K/V fragments in registers)
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
+    gl      split dQ + delta pass + the ds form's LDS-DMA dK/dV without stores
+            (prices the staging alone)
 
 Also checks every form agrees with split8.
 
@@ -45,7 +47,7 @@ def main():
     _lib.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, flags, scale, _lib.stream(q))
     outs = {}
 
-    forms = {"split8": (8, 0), "split4": (4, 0), "ds": (8, 1)}
+    forms = {"split8": (8, 0), "split4": (4, 0), "ds": (8, 1), "gl": (8, 2)}
     variants = a.variants.split(",")
 
     def run(variant):
@@ -83,6 +85,7 @@ def main():
         med = statistics.median(t)
         res[var] = {"median_ms": round(med, 3), "min_ms": round(min(t), 3),
                              "useful_PFps": round(2.5 * flops_fwd / med / 1e12, 3)}
+    _lib.call("toa_attn_set_bwd_variant", -1)
     print(json.dumps(res))
 
 

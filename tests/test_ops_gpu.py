@@ -529,7 +529,7 @@ def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
             torch.cuda.synchronize()
             grads[form] = (dq, dk, dv, delta)
     finally:
-        L.call("toa_attn_set_bwd_variant", 0)
+        L.call("toa_attn_set_bwd_variant", -1)
     (dq0, dk0, dv0, de0), (dq1, dk1, dv1, de1) = grads[0], grads[1]
     assert torch.isfinite(dq1.float()).all()
     assert rel(-de1, de0) < 1e-5  # the dS form's delta pass leaves -delta (the dP accumulators' start)
