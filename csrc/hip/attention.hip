@@ -409,7 +409,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int H, int Hk, int S, float scale,
-    float scale_log2, int o_bshd) {
+    float scale_log2, int o_bshd, int light_first) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
   constexpr int QBUF = DKV<D>::QBUF, KVB = DKV<D>::KVB;
@@ -421,9 +421,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int kg = wave & 3, m = wave >> 2;
-  // heaviest (most query tiles) key blocks first; (b, hk) fastest
+  // (b, hk) fastest
   const int nkb = (S + 127) / 128;
-  const int kb = nkb - 1 - (int)(blockIdx.x / (B * Hk));
+  // heaviest first: key block kb sees S / 64 - 2 kb query tiles, so kb = 0
+  // leads (largest-first keeps the last wave of workgroups short: a
+  // simulated 800 vs 912 tile-units makespan at the bench shape)
+  const int kbi = (int)(blockIdx.x / (B * Hk));
+  const int kb = light_first ? nkb - 1 - kbi : kbi;
   const int bh = blockIdx.x % (B * Hk);
   const int b = bh / Hk, hk = bh % Hk;
   const int rep = H / Hk;
@@ -657,7 +661,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int H, int Hk, int S, float scale,
-    float scale_log2, int o_bshd) {
+    float scale_log2, int o_bshd, int light_first) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
   constexpr int QBUF = DKV4<D>::QBUF;
@@ -665,9 +669,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];  // [Q/dO/lse/-delta buffer 0][buffer 1]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  // heaviest (most query tiles) key blocks first; (b, hk) fastest
+  // (b, hk) fastest
   const int nkb = (S + 127) / 128;
-  const int kb = nkb - 1 - (int)(blockIdx.x / (B * Hk));
+  // heaviest first: key block kb sees S / 64 - 2 kb query tiles, so kb = 0
+  // leads (largest-first keeps the last wave of workgroups short: a
+  // simulated 800 vs 912 tile-units makespan at the bench shape)
+  const int kbi = (int)(blockIdx.x / (B * Hk));
+  const int kb = light_first ? nkb - 1 - kbi : kbi;
   const int bh = blockIdx.x % (B * Hk);
   const int b = bh / Hk, hk = bh % Hk;
   const int rep = H / Hk;
@@ -1260,7 +1268,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, bf16_t* __restrict__ dS, int B, int H, int Hk, int S,
-    float scale, float scale_log2, int o_bshd) {
+    float scale, float scale_log2, int o_bshd, int light_first) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
   constexpr int QBUF = DKV<D>::QBUF, KVB = DKV<D>::KVB;
@@ -1277,9 +1285,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int kg = wave & 3, m = wave >> 2;
-  // heaviest (most query tiles) key blocks first; (b, hk) fastest
+  // (b, hk) fastest
   const int nkb = (S + 127) / 128;
-  const int kb = nkb - 1 - (int)(blockIdx.x / (B * Hk));
+  // heaviest first: key block kb sees S / 64 - 2 kb query tiles, so kb = 0
+  // leads (largest-first keeps the last wave of workgroups short: a
+  // simulated 800 vs 912 tile-units makespan at the bench shape)
+  const int kbi = (int)(blockIdx.x / (B * Hk));
+  const int kb = light_first ? nkb - 1 - kbi : kbi;
   const int bh = blockIdx.x % (B * Hk);
   const int b = bh / Hk, hk = bh % Hk;
   const int rep = H / Hk;
@@ -1496,6 +1508,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     }
 }
 
+// dK/dV key-block launch order: heaviest first (default) or, for A/B,
+// lightest first (TOA_ATTN_KB_ORDER=light / toa_attn_set_kb_order(1)).
+static int g_kb_light = -1;
+static int attn_kb_light_first() {
+  if (g_kb_light < 0) {
+    const char* e = getenv("TOA_ATTN_KB_ORDER");
+    g_kb_light = (e && e[0] == 'l') ? 1 : 0;
+  }
+  return g_kb_light;
+}
+extern "C" int toa_attn_set_kb_order(int light_first) {
+  g_kb_light = light_first < 0 ? -1 : (light_first ? 1 : 0);
+  return 0;
+}
+
 // Backward form: 1 = dS through HBM (default where S % 256 == 0: the
 // Llama-3-8B step 987.9 -> 978.1 ms, profiles/r3_attn_ds), 0 = split (dQ
 // recomputes S / dP; ragged S always).  TOA_ATTN_BWD=split|ds, or
@@ -1593,13 +1620,13 @@ static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
         hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
                            stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
         hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, false>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k,
-                           v, dout, nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
+                           v, dout, nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
         return (int)hipGetLastError();
       }
       hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
                          stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
       hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k, v, dout,
-                         nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
+                         nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
       hipLaunchKernelGGL((attn_bwd_dqg_kernel<D>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, dq, B, H,
                          Hk, S, scale);
       return (int)hipGetLastError();
@@ -1611,10 +1638,10 @@ static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
                      o_bshd);
   if (attn_dkdv_variant() == 8)
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, TAIL>), dim3(((S + 127) / 128) * B * Hk), dim3(512), DKV<D>::LDS,
-                       stream, q, k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
+                       stream, q, k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
   else
     hipLaunchKernelGGL((attn_bwd_dkdv4_kernel<D, TAIL>), dim3(((S + 127) / 128) * B * Hk), dim3(256), DKV4<D>::LDS,
-                       stream, q, k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
+                       stream, q, k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
   return (int)hipGetLastError();
 }
 

@@ -7,6 +7,7 @@ rounds on random data (guide §5.4 rules 24/25):
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
     gl      split dQ + delta pass + the ds form's LDS-DMA dK/dV without stores
             (prices the staging alone)
+    *_light the same with the dK/dV key blocks launched lightest first
 
 Also checks every form agrees with split8.
 
@@ -47,11 +48,14 @@ def main():
     _lib.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, flags, scale, _lib.stream(q))
     outs = {}
 
-    forms = {"split8": (8, 0), "split4": (4, 0), "ds": (8, 1), "gl": (8, 2)}
+    # (dK/dV waves, backward form, key blocks lightest-first)
+    forms = {"split8": (8, 0, 0), "split4": (4, 0, 0), "ds": (8, 1, 0), "gl": (8, 2, 0),
+             "split8_light": (8, 0, 1), "ds_light": (8, 1, 1)}
     variants = a.variants.split(",")
 
     def run(variant):
-        dkdv, bwd = forms[variant]
+        dkdv, bwd, light = forms[variant]
+        _lib.call("toa_attn_set_kb_order", light)
         _lib.call("toa_attn_set_dkdv_variant", dkdv)
         _lib.call("toa_attn_set_bwd_variant", bwd)
         nws = _lib.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D)
@@ -86,6 +90,7 @@ def main():
         res[var] = {"median_ms": round(med, 3), "min_ms": round(min(t), 3),
                              "useful_PFps": round(2.5 * flops_fwd / med / 1e12, 3)}
     _lib.call("toa_attn_set_bwd_variant", -1)
+    _lib.call("toa_attn_set_kb_order", -1)
     print(json.dumps(res))
 
 
