@@ -373,6 +373,208 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
   if (hh == 0) LSE[(int64_t)(b * H + h) * S + myq] = (m_run + log2f(l_tot)) * 0.6931471805599453f;
 }
 
+// Forward with LDS-DMA staging (S % 256 == 0; the default): the same
+// body as attn_fwd_kernel, the K / V tiles brought in by global_load_lds
+// into two distinct LDS objects instead of register staging + ds_write
+// (the change that took the dK/dV kernel from 2.19 to 1.97 ms).
+template <int D>
+__global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+                                                          const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+                                                          float* __restrict__ LSE, int B, int H, int Hk, int S,
+                                                          float scale_log2, int o_bshd) {
+  using G = AG<D>;
+  constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
+  constexpr bool TAIL = false;
+  // two (K tile + V tile) buffers, distinct LDS objects (a read of one then
+  // never waits on the LDS-DMA filling the other)
+  __shared__ __attribute__((aligned(1024))) char kv0[2 * TILEB];
+  __shared__ __attribute__((aligned(1024))) char kv1[2 * TILEB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = (S + FWD_QB - 1) / FWD_QB;
+  int qb, h, b;
+  fwd_block_coords(blockIdx.x, nqb, B, H, Hk, &qb, &h, &b);
+  const int hk = h / (H / Hk);
+  const int64_t qoff = ((int64_t)(b * H + h) * S) * D;
+  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
+  const int q0 = qb * FWD_QB + wave * 32;  // first row of this wave
+  const bool live = q0 < S;                // wave has at least one real row
+  const int myq = q0 + r;                  // the query row this lane owns (>= S: padding)
+  const int myq_ld = TAIL ? min(myq, S - 1) : myq;
+  const int kend = min(S, (qb + 1) * FWD_QB);
+  const int ntiles = (kend + TK - 1) / TK;
+  const int t_diag = live ? (q0 + 31) / TK : -1;  // this wave's last (masked) tile
+
+  // Q fragments: Q[myq][16s + 8hh .. +7], s = 0..NS-1
+  bf16x8 qf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    qf[s] = live ? as_bf16x8(ld16(Q + qoff + (int64_t)myq_ld * D + 16 * s + 8 * hh)) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+
+  // lane-constant LDS read offsets (buffer / half / k-step parts are immediates)
+  int kro[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) kro[s] = k_off<D>(r, 2 * s + hh);
+  // V^T: key = 32n + 16s' + 4hh + qq (+8), column block 32dt + 16(g&1) + 4pp
+  int vro[ND];
+  {
+    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) vro[dt] = v_off<D>(4 * hh + qq, 4 * dt + 2 * (g & 1) + (pp >> 1)) + (pp & 1) * 8;
+  }
+
+  f32x16 acc[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  // K / V tiles by LDS-DMA: 1-KB piece pt of a tile covers keys RPP pt ..
+  // + RPP - 1; waves 0-3 fetch K, 4-7 V, PW pieces each; the lane's 16 B land
+  // at chunk position lane % NCH of key RPP pt + lane / NCH, so it loads the
+  // chunk the k_off / v_off image keeps there
+  constexpr int RPP = 1024 / ROWB, PW = TILEB / 1024 / 4;
+  const int lkey = lane / NCH, lpos = lane % NCH;
+  const int kcol = (lpos ^ (lkey & (NCH - 1))) << 3;  // k_off at D = 64; at 128 XOR (4 (pt & 3)) << 3 per piece
+  const int vcol = (lpos ^ ((lkey & 3) << (D == 128 ? 2 : 1))) << 3;
+  auto stage = [&](int t, int buf) {
+    char* st = buf ? kv1 : kv0;
+    const bf16_t* base = (wave < 4 ? K : V) + koff + (int64_t)t * TK * D;
+    if (wave < 4) {
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int pt = PW * wave + u;
+        const int col = D == 128 ? kcol ^ ((4 * (pt & 3)) << 3) : kcol;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(base + (uint32_t)((RPP * pt + lkey) * D + col)),
+            (__attribute__((address_space(3))) void*)(st + pt * 1024), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int pt = PW * (wave - 4) + u;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(base + (uint32_t)((RPP * pt + lkey) * D + vcol)),
+            (__attribute__((address_space(3))) void*)(st + TILEB + pt * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  auto compute = [&](int t, int buf, bool mask) {
+    const char* kb = buf ? kv1 : kv0;
+    const char* vb = kb + TILEB;
+    // ---- S^T = K Q^T : two 32-key halves (first MFMA of each chain starts from 0)
+    f32x16 sc[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const f32x16 z = {};
+      sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[0] + 32 * ROWB * n)), qf[0], z);
+#pragma unroll
+      for (int s = 1; s < NS; ++s)
+        sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[s] + 32 * ROWB * n)), qf[s], sc[n]);
+    }
+    // ---- causal mask (diagonal tile only) and row max of the raw scores
+    if (mask) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int key = t * TK + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          if (key > myq) sc[n][j] = -INFINITY;
+        }
+    }
+    float mx = rowmax32(sc[0], sc[1]);
+    mx = xhalf_max(mx) * scale_log2;
+    // T13: rescale O / l only when some row's max grew by more than THR
+    if (__any(mx > m_run + RESCALE_THR)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = (m_run == -INFINITY) ? 0.f : EXP2(m_run - m_new);
+      l_run *= alpha;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+    }
+    // ---- P = exp2(s*c - m) packed straight into the PV B operand
+    f32x2 ls;
+    const f32x2 c2 = {scale_log2, scale_log2}, nm2 = {-m_run, -m_run};
+    uint32_t pw[2][8];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        f32x2 x = pk_fma(f32x2{sc[n][j], sc[n][j + 1]}, c2, nm2);
+        x[0] = EXP2(x[0]);
+        x[1] = EXP2(x[1]);
+        ls = (n == 0 && j == 0) ? x : ls + x;
+        pw[n][j >> 1] = cvt_pk(x[0], x[1]);
+      }
+    l_run += ls[0] + ls[1];
+    // ---- O^T += V^T P^T (k permutation of the accumulator handled by the V^T read order)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        u32x4 w;
+        w[0] = pw[n][4 * s + 0];
+        w[1] = pw[n][4 * s + 1];
+        w[2] = pw[n][4 * s + 2];
+        w[3] = pw[n][4 * s + 3];
+        const bf16x8 pf = as_bf16x8(w);
+        const int kb0 = (32 * n + 16 * s) * ROWB;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          const bf16x4 va = tr_read(vb, vro[dt] + kb0);
+          const bf16x4 vbv = tr_read(vb, vro[dt] + kb0 + 8 * ROWB);
+          const bf16x8 vf = __builtin_shufflevector(va, vbv, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[dt] = mfma32(vf, pf, acc[dt]);
+        }
+      }
+  };
+  auto step = [&](int t, int buf) {
+    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
+    if (t < t_diag) compute(t, buf, false);
+    else if (t == t_diag) compute(t, buf, true);
+    // my DMA retired, then everyone's (the next step reads buf ^ 1 and restages buf)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+
+  stage(0, 0);
+  // Q loads and the first tile's DMA retired before the loop
+#pragma unroll
+  for (int s = 0; s < NS; ++s) asm volatile("" ::"v"(qf[s]));
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  int t = 0;
+  for (; t + 1 < ntiles; t += 2) {  // unrolled by 2: buffer offsets become immediates
+    step(t, 0);
+    step(t + 1, 1);
+  }
+  if (t < ntiles) step(t, 0);
+
+  if (!live) return;
+  // ---- epilogue: O = O^T / l  (lane owns query row myq; d rows from the C map)
+  const float l_tot = xhalf_sum(l_run);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  bf16_t* orow = O + o_off<D>(b, h, myq, H, S, o_bshd);
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint2 w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int g = 2 * k + u;
+        w[u].x = cvt_pk(acc[dt][4 * g + 0] * inv, acc[dt][4 * g + 1] * inv);
+        w[u].y = cvt_pk(acc[dt][4 * g + 2] * inv, acc[dt][4 * g + 3] * inv);
+      }
+      store_pair16(orow, 32 * dt + 16 * k, hh, w[0], w[1]);
+    }
+  if (hh == 0) LSE[(int64_t)(b * H + h) * S + myq] = (m_run + log2f(l_tot)) * 0.6931471805599453f;
+}
+
+
 // One image for row reads (ds_read_b128, 32x32x16 A/B operand) AND
 // transposed reads (ds_read_b64_tr_b16): guide T10 layout (b),
 // D = 128: chunk' = chunk ^ (((row & 3) << 2) | ((row >> 2) & 3));
@@ -1592,11 +1794,36 @@ static void attn_set_lds_limits() {
   done = true;
 }
 
+// Forward form: 1 = LDS-DMA staged K/V (default where S % 256 == 0: 0.868 ->
+// 0.811 ms at the bench shape, bit-identical, profiles/r3_attn_ds), 0 =
+// register staged (ragged S always).  TOA_ATTN_FWD=reg|gl or
+// toa_attn_set_fwd_variant (-1: back to the environment's choice).
+static int g_fwd_variant = -1;
+static int attn_fwd_variant() {
+  if (g_fwd_variant < 0) {
+    const char* e = getenv("TOA_ATTN_FWD");
+    g_fwd_variant = (e && e[0] == 'r' && e[1] == 'e') ? 0 : 1;
+  }
+  return g_fwd_variant;
+}
+extern "C" int toa_attn_set_fwd_variant(int v) {
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
+  g_fwd_variant = v;
+  return 0;
+}
+
 template <int D, bool TAIL>
 static int attn_fwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int H,
                            int Hk, int S, int o_bshd, float scale, hipStream_t stream) {
   attn_set_lds_limits<D, TAIL>();
   const int nqb = (S + FWD_QB - 1) / FWD_QB;
+  if constexpr (!TAIL) {
+    if (attn_fwd_variant() == 1) {
+      hipLaunchKernelGGL((attn_fwd_gl_kernel<D>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o, lse,
+                         B, H, Hk, S, scale * LOG2E, o_bshd);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((attn_fwd_kernel<D, TAIL>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 4 * AG<D>::TILEB, stream, q, k, v,
                      o, lse, B, H, Hk, S, scale * LOG2E, o_bshd);
   return (int)hipGetLastError();

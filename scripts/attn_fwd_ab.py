@@ -1,0 +1,73 @@
+"""In-process A/B of the attention-forward forms at the Llama-3-8B bench
+shape (B=6, H=32, Hkv=8, S=4096, D=128, O in [B,S,H,D]), interleaved rounds
+on random data (guide §5.4 rules 24/25):
+
+    reg  K/V tiles staged through registers + ds_write (attn_fwd_kernel)
+    gl   K/V tiles by LDS-DMA into two distinct LDS objects (attn_fwd_gl_kernel)
+
+and the max |difference| of O / lse between them (same arithmetic: 0 expected).
+
+    python scripts/attn_fwd_ab.py [--rounds 6] [--reps 10]
+"""
+import argparse
+import json
+import math
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from tf_operator_amd.ops import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=6)
+    a = ap.parse_args()
+    B, H, Hk, S, D = a.batch, 32, 8, 4096, 128
+    torch.manual_seed(0)
+    q = torch.randn(B, H, S, D, device="cuda").to(torch.bfloat16)
+    k = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
+    v = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
+    P = _lib.ptr
+    forms = {"reg": 0, "gl": 1}
+    outs = {}
+
+    def run(form):
+        _lib.call("toa_attn_set_fwd_variant", forms[form])
+        o = torch.empty(B, S, H, D, device="cuda", dtype=torch.bfloat16)
+        lse = torch.empty(B, H, S, device="cuda", dtype=torch.float32)
+        _lib.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, 1 | 2, 1.0 / math.sqrt(D),
+                  _lib.stream(q))
+        return o, lse
+
+    for f in forms:
+        outs[f] = run(f)
+    torch.cuda.synchronize()
+    diff = {"o": float((outs["gl"][0].float() - outs["reg"][0].float()).abs().max()),
+            "lse": float((outs["gl"][1] - outs["reg"][1]).abs().max())}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    times = {f: [] for f in forms}
+    for _ in range(a.rounds):
+        for f in forms:
+            run(f)
+            ev[0].record()
+            for _ in range(a.reps):
+                run(f)
+            ev[1].record()
+            torch.cuda.synchronize()
+            times[f].append(ev[0].elapsed_time(ev[1]) / a.reps)
+    _lib.call("toa_attn_set_fwd_variant", -1)
+    flops = 4 * B * H * S * S * D / 2
+    res = {"shape": [B, H, Hk, S, D], "max_abs_diff_gl_vs_reg": diff}
+    for f, t in times.items():
+        med = statistics.median(t)
+        res[f] = {"median_ms": round(med, 4), "min_ms": round(min(t), 4), "PFps": round(flops / med / 1e12, 3)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

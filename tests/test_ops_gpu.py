@@ -542,6 +542,31 @@ def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
         assert rel(got, ref) < 3e-2, rel(got, ref)
 
 
+@pytest.mark.parametrize("B,H,Hk,S,D,bshd", [(1, 4, 2, 512, 128, True), (2, 8, 2, 1024, 128, False),
+                                              (1, 4, 1, 768, 64, True)])
+def test_flash_attention_fwd_forms_identical(B, H, Hk, S, D, bshd):
+    """The LDS-DMA-staged forward (default at S % 256 == 0) and the
+    register-staged one run the same arithmetic: O and lse bit-identical."""
+    L = _lib()
+    torch.manual_seed(9)
+    q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    outs = []
+    try:
+        for form in (0, 1):
+            L.call("toa_attn_set_fwd_variant", form)
+            o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16) if bshd else torch.empty_like(q)
+            lse = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
+            L.call("toa_attn_fwd", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(lse), B, H, Hk, S, D,
+                   1 | (2 if bshd else 0), 1.0 / math.sqrt(D), L.stream(q))
+            outs.append((o, lse))
+        torch.cuda.synchronize()
+    finally:
+        L.call("toa_attn_set_fwd_variant", -1)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 def test_attention_gpu_has_no_library_fallback():
     """A GPU tensor the HIP kernel cannot take raises instead of silently
     running a library (SDPA / aotriton) kernel."""
