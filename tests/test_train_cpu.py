@@ -191,3 +191,19 @@ def test_miopen_find_db_version_gate(monkeypatch, tmp_path, capsys):
     monkeypatch.setattr(common, "miopen_version", lambda: (3, 5, 0))
     monkeypatch.setattr(common.tempfile, "gettempdir", lambda: str(tmp_path))
     assert common.use_shipped_miopen_find_db() is not None
+
+
+def test_gemm_prewarm_is_a_noop_off_the_gpu(monkeypatch):
+    """The GEMM layer's prewarm (ops/gemm.py) starts no thread and touches no
+    device when there is nothing to resolve: on the CPU, and for the torch
+    policy (no installed table)."""
+    assert gemm.prewarm_early() is None  # no GPU in this process
+    old = gemm.mode()
+    try:
+        gemm.set_mode("torch")
+        assert gemm.prewarm("cpu") is None
+    finally:
+        gemm.set_mode(old)
+    tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device("cpu"), micro_batch=1, seq_len=16)
+    assert tr._gemm_prewarm is None
+    assert tr.gemm_mode in ("nosk", "torch", "tuned", "hip")
