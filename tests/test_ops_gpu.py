@@ -498,7 +498,9 @@ def test_flash_attention_bench_shape():
 
 @pytest.mark.parametrize("B,H,Hk,S,D,bshd", [(1, 2, 2, 256, 128, False), (2, 4, 2, 512, 128, True),
                                               (1, 8, 2, 1024, 128, True), (1, 4, 1, 768, 128, False),
-                                              (2, 4, 2, 512, 64, False), (1, 2, 1, 1024, 64, True)])
+                                              (2, 4, 2, 512, 64, False), (1, 2, 1, 1024, 64, True),
+                                              # long sequence: 256 x 257 / 2 dS blocks per head
+                                              (1, 4, 2, 8192, 128, True)])
 def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
     """The dS-through-HBM backward (delta pass, dK/dV storing the lower-
     triangular dS blocks, dQ as a GEMM over them) vs the fp32 reference and
