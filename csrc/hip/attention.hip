@@ -1272,6 +1272,30 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
   }
 }
 
+// RoPE backward on a lane's accumulator tiles, in place (the fused
+// rope + attention backward, toa_attn_bwd_rope): element j of tile dt is
+// d = 32 dt + 8 (j / 4) + 4 hh + j % 4, its rotation partner d + D / 2 sits in
+// tile dt + ND / 2 of the same lane; dx1 = dy1 c + dy2 s, dx2 = dy2 c - dy1 s
+// with c / s = cos / sin[position][d], after scaling by `scale`.
+template <int D>
+__device__ __forceinline__ void rope_bwd_acc(f32x16 (&a)[D / 32], const float* __restrict__ cs,
+                                             const float* __restrict__ sn, int hh, float scale) {
+  constexpr int HALF = D / 64;
+#pragma unroll
+  for (int dt = 0; dt < HALF; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 c = *(const f32x4*)(cs + 32 * dt + 8 * g + 4 * hh);
+      const f32x4 sv = *(const f32x4*)(sn + 32 * dt + 8 * g + 4 * hh);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y1 = a[dt][4 * g + e] * scale, y2 = a[dt + HALF][4 * g + e] * scale;
+        a[dt][4 * g + e] = y1 * c[e] + y2 * sv[e];
+        a[dt + HALF][4 * g + e] = y2 * c[e] - y1 * sv[e];
+      }
+    }
+}
+
 template <int D>
 struct DQG {
   static constexpr int KT = TK * AG<D>::ROWB;  // one 64-key K tile
@@ -1292,10 +1316,12 @@ struct DQG {
 //    block's (key, 4-query) pieces gives the B operand (query on the lane, 4
 //    keys per read; the key order matches the K^T read's, as in the split
 //    kernel).
-template <int D>
+template <int D, bool ROPE = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __restrict__ K,
                                                               const bf16_t* __restrict__ dS, bf16_t* __restrict__ dQ,
-                                                              int B, int H, int Hk, int S, float scale) {
+                                                              int B, int H, int Hk, int S, float scale,
+                                                              const float* __restrict__ cosv = nullptr,
+                                                              const float* __restrict__ sinv = nullptr, int H3 = 0) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, ND = G::ND;
   constexpr int KT = DQG<D>::KT, NKP = DQG<D>::NKP;
@@ -1437,7 +1463,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA in flight at exit
 
-  bf16_t* qrow = dQ + ((int64_t)(b * H + h) * S + qi * 32 + r) * D;
+  const int myq = qi * 32 + r;
+  bf16_t* qrow = dQ + ((int64_t)(b * H + h) * S + myq) * D;
+  float osc = scale;
+  if constexpr (ROPE) {  // rotate back and write the q part of d(qkv) row (b, myq)
+    rope_bwd_acc<D>(acc, cosv + (int64_t)myq * (D / 2), sinv + (int64_t)myq * (D / 2), hh, scale);
+    qrow = dQ + ((int64_t)b * S + myq) * H3 * D + h * D;
+    osc = 1.f;
+  }
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -1446,8 +1479,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int g = 2 * k + u;
-        w[u].x = pack2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
-        w[u].y = pack2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
+        w[u].x = pack2(acc[dt][4 * g + 0] * osc, acc[dt][4 * g + 1] * osc);
+        w[u].y = pack2(acc[dt][4 * g + 2] * osc, acc[dt][4 * g + 3] * osc);
       }
       store_pair16(qrow, 32 * dt + 16 * k, hh, w[0], w[1]);
     }
@@ -1465,12 +1498,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
 // Each step ends with its own DMA and stores retired (vmcnt(0)) and a
 // barrier.  LSE / DELTA here are the delta pass's -lse log2(e) / -delta rows.
 // S % 256 == 0 only (no ragged tiles).
-template <int D, bool STORE = true>
+template <int D, bool STORE = true, bool ROPE = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, bf16_t* __restrict__ dS, int B, int H, int Hk, int S,
-    float scale, float scale_log2, int o_bshd, int light_first) {
+    float scale, float scale_log2, int o_bshd, int light_first,
+    const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr, int H3 = 0) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
   constexpr int QBUF = DKV<D>::QBUF, KVB = DKV<D>::KVB;
@@ -1692,6 +1726,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
   // store: lane owns key `mykey`, d rows 32dt + 8g + 4hh + (0..3)
   bf16_t* dkr = dK + koff + (int64_t)mykey * D;
   bf16_t* dvr = dV + koff + (int64_t)mykey * D;
+  float ksc = scale;
+  if constexpr (ROPE) {  // rotate dK back; dK / dV go to the k / v parts of d(qkv) row (b, mykey)
+    rope_bwd_acc<D>(dk, cosv + (int64_t)mykey * (D / 2), sinv + (int64_t)mykey * (D / 2), hh, scale);
+    bf16_t* row = dK + ((int64_t)b * S + mykey) * H3 * D;
+    dkr = row + (H + hk) * D;
+    dvr = row + (H + Hk + hk) * D;
+    ksc = 1.f;
+  }
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
@@ -1700,8 +1742,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int g = 2 * k + u;
-        a[u].x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
-        a[u].y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
+        a[u].x = pack2(dk[dt][4 * g + 0] * ksc, dk[dt][4 * g + 1] * ksc);
+        a[u].y = pack2(dk[dt][4 * g + 2] * ksc, dk[dt][4 * g + 3] * ksc);
         c[u].x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
         c[u].y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
       }
@@ -1911,4 +1953,46 @@ extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   return tail ? TOA_ATTN_BWD(64, true) : TOA_ATTN_BWD(64, false);
 #endif
 #undef TOA_ATTN_BWD
+}
+
+// Fused RoPE + attention backward (the dS form only: S % 256 == 0, packed
+// K/V = one copy per kv head): d(qkv) [B*S, (H + 2 Hk) * D] straight from the
+// dQ GEMM's and the dK/dV kernel's epilogues, rotated back with cos / sin
+// [S, D / 2] -- no dq / dk / dv tensors and no RoPE backward pass (the
+// inverse of toa_rope_fwd).  hipErrorNotSupported when the dS form is off or
+// the shape is not one it takes; the caller then runs toa_attn_bwd +
+// toa_rope_bwd.  ws: toa_attn_bwd_ws_bytes(B, H, S, D) bytes.
+extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,
+                                 const bf16_t* dout, const float* lse, float* delta, void* ws, const float* cosv,
+                                 const float* sinv, bf16_t* dqkv, int B, int H, int Hk, int S, int D, int flags,
+                                 float scale, hipStream_t stream) {
+  if (!attn_shape_ok(B, H, Hk, S, D, flags)) return (int)hipErrorInvalidValue;
+  if (!attn_bwd_uses_ds(S) || attn_bwd_variant() != 1) return (int)hipErrorNotSupported;
+  if (ws == nullptr || dqkv == nullptr || cosv == nullptr || sinv == nullptr) return (int)hipErrorInvalidValue;
+  const int o_bshd = (flags >> 1) & 1;
+  const int H3 = H + 2 * Hk;
+  bf16_t* ds = (bf16_t*)ws;
+  float* nlse2 = (float*)((char*)ws + attn_ds_blocks_bytes(B, H, S));
+  const int rows = B * H * S;
+#define TOA_ATTN_BWD_ROPE(DD)                                                                                    \
+  do {                                                                                                           \
+    hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 256 / (DD / 8) - 1) / (256 / (DD / 8))), dim3(256), \
+                       0, stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);                               \
+    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<DD, true, true>), dim3((S / 128) * B * Hk), dim3(512), 0,       \
+                       stream, q, k, v, dout, nlse2, delta, dqkv, dqkv, ds, B, H, Hk, S, scale, scale * LOG2E,  \
+                       o_bshd, attn_kb_light_first(), cosv, sinv, H3);                                          \
+    hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \
+                       dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                                \
+  } while (0)
+#ifdef TOA_ATTN_D128_ONLY
+  if (D != 128) return (int)hipErrorInvalidValue;
+  TOA_ATTN_BWD_ROPE(128);
+#else
+  if (D == 128)
+    TOA_ATTN_BWD_ROPE(128);
+  else
+    TOA_ATTN_BWD_ROPE(64);
+#endif
+#undef TOA_ATTN_BWD_ROPE
+  return (int)hipGetLastError();
 }

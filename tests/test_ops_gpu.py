@@ -569,6 +569,34 @@ def test_flash_attention_fwd_forms_identical(B, H, Hk, S, D, bshd):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("B,H,Hk,S,D", [(2, 8, 2, 512, 128), (1, 4, 1, 1024, 64), (1, 4, 2, 300, 128)])
+def test_rope_attention_matches_two_nodes(B, H, Hk, S, D):
+    """rope_attention (one autograd node; the backward writes d(qkv) from
+    the attention kernels' epilogues where the dS form runs, S % 256 == 0,
+    else attention backward + RoPE backward) against rope_qkv +
+    causal_attention: same O, d(qkv) equal up to where bf16 rounding happens."""
+    _lib()
+    from tf_operator_amd.ops import llm
+
+    torch.manual_seed(3)
+    cos, sin = llm.rope_tables(S, D, device=DEV)
+    qkv = torch.randn(B * S, (H + 2 * Hk) * D, device=DEV, dtype=torch.bfloat16)
+    a = qkv.clone().requires_grad_()
+    b = qkv.clone().requires_grad_()
+    o1 = llm.rope_attention(a, cos, sin, B, S, H, Hk, D)
+    q, k, v = llm.rope_qkv(b, cos, sin, B, S, H, Hk, D, 1)
+    o2 = llm.causal_attention(q, k, v, out_layout="bshd")
+    assert torch.equal(o1, o2)
+    do = torch.randn_like(o1)
+    o1.backward(do)
+    o2.backward(do)
+    torch.cuda.synchronize()
+    assert rel(a.grad, b.grad) < 1e-2, rel(a.grad, b.grad)
+    # per part (q / k / v) too: a wrong column block would hide in the total
+    for lo, hi in ((0, H * D), (H * D, (H + Hk) * D), ((H + Hk) * D, (H + 2 * Hk) * D)):
+        assert rel(a.grad[:, lo:hi], b.grad[:, lo:hi]) < 1e-2, (lo, hi)
+
+
 def test_attention_gpu_has_no_library_fallback():
     """A GPU tensor the HIP kernel cannot take raises instead of silently
     running a library (SDPA / aotriton) kernel."""

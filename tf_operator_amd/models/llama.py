@@ -5,8 +5,8 @@ Llama-3-8B bf16).  Per layer the forward is:
 
     (h, x) = add_rms_norm(h_prev, delta_prev)      HIP, residual add fused
     qkv    = x @ Wqkv^T                             hipBLASLt (fused Q|K|V weight)
-    q,k,v  = rope_qkv(qkv)                          HIP, RoPE + head-major relayout
-    o      = causal_attention(q, k, v)              HIP flash attention (packed GQA)
+    o      = rope_attention(qkv)                    HIP RoPE + head-major relayout, flash attention
+                                                    (packed GQA); backward writes d(qkv) directly
     a      = o^T @ Wo^T                             hipBLASLt
     (h, x) = add_rms_norm(h, a)                     HIP
     gu     = x @ Wgu^T                              hipBLASLt (fused gate|up weight)
@@ -26,7 +26,7 @@ import torch
 
 from ..ops.embedding import Embedding
 from ..ops.linear import linear
-from ..ops.llm import causal_attention, cross_entropy, rope_qkv, rope_tables, swiglu_mlp
+from ..ops.llm import causal_attention, cross_entropy, rope_attention, rope_qkv, rope_tables, swiglu_mlp
 from ..ops.norm import RMSNorm, add_rms_norm
 
 
@@ -98,11 +98,14 @@ class LlamaBlock(torch.nn.Module):
         else:
             h, x = self.attn_norm(h, delta)
         qkv = linear(x, self.wqkv)
-        rep = cfg.heads // cfg.kv_heads
-        if cfg.kv_layout in ("packed", "auto"):  # the attention kernel reads packed GQA K/V natively
-            rep = 1
-        q, k, v = rope_qkv(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim, rep)
-        o = causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]: no transpose copy
+        if cfg.kv_layout in ("packed", "auto"):
+            # the attention kernel reads packed GQA K/V natively; RoPE and
+            # attention are one autograd node whose backward writes d(qkv)
+            o = rope_attention(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim)  # [B, S, H, D]
+        else:
+            rep = cfg.heads // cfg.kv_heads
+            q, k, v = rope_qkv(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim, rep)
+            o = causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]: no transpose copy
         o = o.reshape(B * S, cfg.heads * cfg.head_dim)
         a = linear(o, self.wo)
         h, x = self.mlp_norm(h, a)

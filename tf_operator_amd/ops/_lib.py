@@ -86,6 +86,8 @@ _SIGS = {
     "toa_attn_set_bwd_variant": [c_int],
     "toa_attn_set_kb_order": [c_int],
     "toa_attn_set_fwd_variant": [c_int],
+    "toa_attn_bwd_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
+                          c_int, c_f, c_p],
     "toa_emulate_xfer": [c_p, c_p, c_i64, c_int, ctypes.c_double, c_p],
     "toa_gemm_tune": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p, c_p, c_p,
                       c_p, c_p, c_int],

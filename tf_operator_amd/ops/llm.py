@@ -290,21 +290,100 @@ class _FlashAttn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        B, H, S, D = q.shape
-        Hk = k.shape[1]
+        return (*_attn_bwd(q, k, v, o, lse, do.contiguous(), ctx.scale, ctx.bshd), None, None)
+
+
+def _attn_ws(B, H, S, D, device):
+    """Workspace of the dS-through-HBM backward form (attention.hip, the
+    default where S % 256 == 0): the lower-triangular dS blocks, 3.2 GB at the
+    Llama-3-8B bench shape.  None when the form in force needs none."""
+    nws = _lib.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D) if _lib.has("toa_attn_bwd_ws_bytes") else 0
+    return torch.empty(nws, device=device, dtype=torch.uint8) if nws > 0 else None
+
+
+def _attn_bwd(q, k, v, o, lse, do, scale, bshd):
+    B, H, S, D = q.shape
+    Hk = k.shape[1]
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    delta = torch.empty(B, H, S, device=q.device, dtype=torch.float32)
+    ws = _attn_ws(B, H, S, D, q.device)
+    _lib.call("toa_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do), _lib.ptr(lse),
+              _lib.ptr(delta), _lib.ptr(ws), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D,
+              1 | (2 if bshd else 0), float(scale), _lib.stream(q))
+    return dq, dk, dv
+
+
+# TOA_ATTN_ROPE_FUSED=0: RoPE backward as its own pass even where the fused
+# epilogues could take it (A/B)
+_ROPE_FUSED_BWD = os.environ.get("TOA_ATTN_ROPE_FUSED", "1") != "0"
+
+
+class _RopeAttn(torch.autograd.Function):
+    """RoPE + causal attention as one autograd node (packed K/V, one copy
+    per kv head).  Forward: toa_rope_fwd, then the flash-attention forward.
+    Backward: d(qkv) straight from the attention backward's epilogues,
+    rotated back there (toa_attn_bwd_rope: no dq / dk / dv tensors, no RoPE
+    backward pass); where that form is off (ragged S, TOA_ATTN_BWD=split)
+    the attention backward + toa_rope_bwd."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, scale, bshd):
+        qkv = qkv.contiguous()
+        q = torch.empty(B, Hq, S, D, device=qkv.device, dtype=qkv.dtype)
+        k = torch.empty(B, Hkv, S, D, device=qkv.device, dtype=qkv.dtype)
+        v = torch.empty(B, Hkv, S, D, device=qkv.device, dtype=qkv.dtype)
+        _lib.call("toa_rope_fwd", _lib.ptr(qkv), _lib.ptr(cos), _lib.ptr(sin), _lib.ptr(q), _lib.ptr(k), _lib.ptr(v),
+                  B, S, Hq, Hkv, D, 1, _lib.stream(qkv))
+        o = torch.empty(B, S, Hq, D, device=q.device, dtype=q.dtype) if bshd else torch.empty_like(q)
+        lse = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
+        _lib.call("toa_attn_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(lse), B, Hq, Hkv, S, D,
+                  1 | (2 if bshd else 0), float(scale), _lib.stream(q))
+        ctx.save_for_backward(q, k, v, o, lse, cos, sin)
+        ctx.scale, ctx.bshd = scale, bshd
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, cos, sin = ctx.saved_tensors
+        B, Hq, S, D = q.shape
+        Hkv = k.shape[1]
         do = do.contiguous()
-        dq = torch.empty_like(q)
-        dk = torch.empty_like(k)
-        dv = torch.empty_like(v)
-        delta = torch.empty(B, H, S, device=q.device, dtype=torch.float32)
-        # the dS-through-HBM form (attention.hip, TOA_ATTN_BWD=ds) needs a
-        # lower-triangular dS buffer (3.2 GB at the Llama-3-8B bench shape)
-        nws = _lib.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D) if _lib.has("toa_attn_bwd_ws_bytes") else 0
-        ws = torch.empty(nws, device=q.device, dtype=torch.uint8) if nws > 0 else None
-        _lib.call("toa_attn_bwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do), _lib.ptr(lse),
-                  _lib.ptr(delta), _lib.ptr(ws), _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), B, H, Hk, S, D,
-                  1 | (2 if ctx.bshd else 0), float(ctx.scale), _lib.stream(q))
-        return dq, dk, dv, None, None
+        dqkv = torch.empty(B * S, (Hq + 2 * Hkv) * D, device=q.device, dtype=q.dtype)
+        flags = 1 | (2 if ctx.bshd else 0)
+        ws = _attn_ws(B, Hq, S, D, q.device)
+        if ws is not None and _ROPE_FUSED_BWD and _lib.has("toa_attn_bwd_rope"):
+            delta = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
+            rc = _lib.call_ret("toa_attn_bwd_rope", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do),
+                               _lib.ptr(lse), _lib.ptr(delta), _lib.ptr(ws), _lib.ptr(cos), _lib.ptr(sin),
+                               _lib.ptr(dqkv), B, Hq, Hkv, S, D, flags, float(ctx.scale), _lib.stream(q))
+            if rc == 0:
+                return dqkv, None, None, None, None, None, None, None, None, None
+            if rc != 801:  # hipErrorNotSupported: take the two-pass path below
+                raise RuntimeError(f"toa_attn_bwd_rope failed with hipError {rc}")
+        del ws
+        dq, dk, dv = _attn_bwd(q, k, v, o, lse, do, ctx.scale, ctx.bshd)
+        _lib.call("toa_rope_bwd", _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), _lib.ptr(cos), _lib.ptr(sin),
+                  _lib.ptr(dqkv), B, S, Hq, Hkv, D, 1, _lib.stream(q))
+        return dqkv, None, None, None, None, None, None, None, None, None
+
+
+def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, scale=None, out_layout="bshd"):
+    """RoPE (Llama rotate-half, cos / sin [S, D/2]) on the fused QKV
+    projection [B*S, (Hq + 2 Hkv) D], then causal attention with packed GQA:
+    O as [B, S, Hq, D] (out_layout="bshd") or [B, Hq, S, D].  On the GPU one
+    autograd node (_RopeAttn) whose backward writes d(qkv) directly; on the
+    CPU rope_qkv + causal_attention."""
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if qkv.is_cuda:
+        if not (qkv.dtype == torch.bfloat16 and D in ATTN_HEAD_DIMS and _lib.has("toa_attn_fwd")
+                and _lib.has("toa_rope_fwd")):
+            raise RuntimeError(f"HIP rope + flash attention needs bf16 and head_dim in {ATTN_HEAD_DIMS} "
+                               f"(got {qkv.dtype}, head_dim {D}; library: {_lib.load_error() or 'ok'})")
+        if Hq % Hkv:
+            raise ValueError(f"query heads {Hq} not a multiple of kv heads {Hkv}")
+        return _RopeAttn.apply(qkv, cos, sin, B, S, Hq, Hkv, D, scale, out_layout == "bshd")
+    q, k, v = rope_qkv(qkv, cos, sin, B, S, Hq, Hkv, D, 1)
+    return causal_attention(q, k, v, scale, out_layout)
 
 
 def _attention_reference(q, k, v, scale):
