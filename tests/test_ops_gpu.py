@@ -730,6 +730,35 @@ def test_gemm_prewarm_resolves_table():
         gemm.set_mode("auto")
 
 
+def test_gemm_runs_on_tn_kernel_while_prewarm_pending(monkeypatch):
+    """While the hipBLASLt table is still being resolved (a live prewarm
+    thread), forward GEMMs of TN-compatible shapes run on the hand-written
+    kernel instead of blocking on the library; results match fp32."""
+    _lib()
+    import threading
+
+    from tf_operator_amd.ops import gemm
+
+    release = threading.Event()
+    th = threading.Thread(target=release.wait, daemon=True)
+    th.start()
+    monkeypatch.setattr(gemm, "_prewarm_thread", th)
+    try:
+        assert gemm._prewarm_pending()
+        torch.manual_seed(1)
+        x = torch.randn(512, 384, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(768, 384, device=DEV, dtype=torch.bfloat16) / 384 ** 0.5
+        assert gemm._tn_shape_ok(x, w)
+        y = gemm.linear_fwd(x, w)
+        assert rel(y, x.float() @ w.float().t()) < 1e-2
+        xo = torch.randn(100, 384, device=DEV, dtype=torch.bfloat16)  # not TN-compatible: the library path
+        assert not gemm._tn_shape_ok(xo, w)
+        assert rel(gemm.linear_fwd(xo, w), xo.float() @ w.float().t()) < 1e-2
+    finally:
+        release.set()
+        th.join()
+
+
 @pytest.mark.parametrize("B,H,Hk,S", [(2, 4, 2, 384), (1, 8, 2, 1024)])
 def test_flash_attention_bshd_output_layout(B, H, Hk, S):
     """O written / dO read as [B, S, H, D] (no transpose copies in the model)

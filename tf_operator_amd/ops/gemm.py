@@ -175,10 +175,10 @@ def _gemm(ta, tb, m, n, k, a, lda, b, ldb, c, ldc, beta):
               int(c.dtype == torch.float32), _lib.stream(c))
 
 
-def _tn_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
+def _tn_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
     """Operands csrc/hip/gemm_tn.hip takes: bf16 GPU rows with unit column
     stride, 16-byte aligned, M and N multiples of 256 (n_mult), K of 128."""
-    if _MODE != "hip" or not _lib.has("toa_gemm_tn"):
+    if not _lib.has("toa_gemm_tn"):
         return False
     if not (x2.is_cuda and x2.dtype == w.dtype == torch.bfloat16 and x2.dim() == 2 and w.dim() == 2):
         return False
@@ -190,8 +190,25 @@ def _tn_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
             and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _lib.use_hip(x2))
 
 
+def _tn_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
+    return _MODE == "hip" and _tn_shape_ok(x2, w, n_mult)
+
+
+# TOA_GEMM_TN_FIRST=0: the first step waits for the hipBLASLt table instead
+_TN_FIRST = os.environ.get("TOA_GEMM_TN_FIRST", "1") != "0"
+
+
+def _prewarm_pending() -> bool:
+    """True while the helper thread is still resolving the hipBLASLt table
+    (~0.47 s of code-object loading from process start): the first step's
+    forward / data-gradient GEMMs then run on the hand-written TN kernel
+    instead of waiting for the library (profiles/r3_first)."""
+    th = _prewarm_thread
+    return _TN_FIRST and th is not None and th.is_alive()
+
+
 def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    if _tn_ok(x2, w):
+    if _tn_ok(x2, w) or (_prewarm_pending() and _tn_shape_ok(x2, w)):
         M, N = x2.shape[0], w.shape[0]
         y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
         _lib.call("toa_gemm_tn", _lib.ptr(x2), x2.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), N, M, N,
