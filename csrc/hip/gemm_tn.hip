@@ -109,6 +109,91 @@ __device__ __forceinline__ void tn_tile_coords(int tile, int tiles_m, int tiles_
 
 __device__ __forceinline__ float tn_silu(float g) { return g / (1.f + __expf(-g)); }
 
+// Epilogue shared by both main loops: acc[i][j] holds C[m][n .. n+3] of the
+// wave's 128 x 64 block, m = wave row 0 + 16 i + (lane & 15), n = wave column 0
+// + 16 j + 4 (lane >> 4).
+template <int EPI>
+__device__ __forceinline__ void tn_epilogue(f32x4 (&acc)[8][4], int tm, int tn, int wm, int wn, int lane,
+                                            bf16_t* __restrict__ C, int64_t ldc, bf16_t* __restrict__ S,
+                                            int64_t lds_, const bf16_t* __restrict__ GU, int64_t ldgu, int F) {
+  const int m0 = tm * TN_BM + wm * 128 + (lane & 15);
+  const int nl = 4 * (lane >> 4);
+  if (EPI == TN_PLAIN) {
+    const int n0 = tn * TN_BN + wn * 64 + nl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint2 w;
+        w.x = pack2(acc[i][j][0], acc[i][j][1]);
+        w.y = pack2(acc[i][j][2], acc[i][j][3]);
+        *(uint2*)(C + (int64_t)(m0 + 16 * i) * ldc + n0 + 16 * j) = w;
+      }
+  } else if (EPI == TN_SWIGLU_FWD) {
+    // j = 0, 1: gate units h0 + 16 j; j = 2, 3: the same units' up values
+    const int h0 = tn * (TN_BN / 2) + 32 * wn + nl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16_t* crow = C + (int64_t)(m0 + 16 * i) * ldc;
+      bf16_t* srow = S + (int64_t)(m0 + 16 * i) * lds_;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4 g = acc[i][j], u = acc[i][j + 2];
+        uint2 wg, wu, ws;
+        wg.x = pack2(g[0], g[1]);
+        wg.y = pack2(g[2], g[3]);
+        wu.x = pack2(u[0], u[1]);
+        wu.y = pack2(u[2], u[3]);
+        // s from the bf16-rounded gate / up: the values backward re-reads from gu
+        const float g0 = __uint_as_float(wg.x << 16), g1 = __uint_as_float(wg.x & 0xffff0000u);
+        const float g2 = __uint_as_float(wg.y << 16), g3 = __uint_as_float(wg.y & 0xffff0000u);
+        const float u0 = __uint_as_float(wu.x << 16), u1 = __uint_as_float(wu.x & 0xffff0000u);
+        const float u2 = __uint_as_float(wu.y << 16), u3 = __uint_as_float(wu.y & 0xffff0000u);
+        ws.x = pack2(tn_silu(g0) * u0, tn_silu(g1) * u1);
+        ws.y = pack2(tn_silu(g2) * u2, tn_silu(g3) * u3);
+        const int h = h0 + 16 * j;
+        *(uint2*)(crow + h) = wg;
+        *(uint2*)(crow + F + h) = wu;
+        *(uint2*)(srow + h) = ws;
+      }
+    }
+  } else {  // TN_SWIGLU_BWD: C = ds (never stored) -> dgu
+    const int n0 = tn * TN_BN + wn * 64 + nl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bf16_t* gurow = GU + (int64_t)(m0 + 16 * i) * ldgu;
+      bf16_t* drow = C + (int64_t)(m0 + 16 * i) * ldc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = n0 + 16 * j;
+        const uint2 gw = *(const uint2*)(gurow + h), uw = *(const uint2*)(gurow + F + h);
+        float g[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u), __uint_as_float(gw.y << 16),
+                      __uint_as_float(gw.y & 0xffff0000u)};
+        float u[4] = {__uint_as_float(uw.x << 16), __uint_as_float(uw.x & 0xffff0000u), __uint_as_float(uw.y << 16),
+                      __uint_as_float(uw.y & 0xffff0000u)};
+        // ds rounded to bf16 first: the value the unfused path stores
+        float d[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d[e] = bf2f(f2bf(acc[i][j][e]));
+        float dg[4], du[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sg = 1.f / (1.f + __expf(-g[e]));
+          du[e] = d[e] * g[e] * sg;
+          dg[e] = d[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
+        }
+        uint2 wdg, wdu;
+        wdg.x = pack2(dg[0], dg[1]);
+        wdg.y = pack2(dg[2], dg[3]);
+        wdu.x = pack2(du[0], du[1]);
+        wdu.y = pack2(du[2], du[3]);
+        *(uint2*)(drow + h) = wdg;
+        *(uint2*)(drow + F + h) = wdu;
+      }
+    }
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                          const bf16_t* __restrict__ B, int64_t ldb,
@@ -194,83 +279,172 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restric
   if (!lag) sync();
   __builtin_amdgcn_s_waitcnt(TN_VMCNT0);
 
-  // epilogue: acc[i][j] = C[m][n .. n+3], m = row0 + 16 i, n = col0 + 16 j
-  const int m0 = tm * TN_BM + wm * 128 + (lane & 15);
-  const int nl = 4 * (lane >> 4);
-  if (EPI == TN_PLAIN) {
-    const int n0 = tn * TN_BN + wn * 64 + nl;
+  tn_epilogue<EPI>(acc, tm, tn, wm, wn, lane, C, ldc, S, lds_, GU, ldgu, F);
+}
+
+// ---------------------------------------------------------------------------
+// Full-line form (the default): LDS rows of 64 k = 128 B, so every LDS-DMA
+// piece is 8 rows x one whole 128-B line of each (the 32-k kernel above
+// fetches 16 half lines per piece: twice the TA / L2 requests per byte --
+// guide §5 "Projection GEMM at M = 256" item 3, and what hipBLASLt's
+// MT256x256x64 does).  Two 64-KiB stages hold two 64-k tiles.  The phases
+// stay 32 k deep (12 ds_read_b128 + 32 MFMAs per wave, two barriers, wave
+// rows staggered by one barrier: the schedule the weight-gradient kernel
+// measured best): phase (t, h) computes k-half h of tile t, and the first
+// half-phase of tile t issues tile t + 1's whole DMA into the other stage
+// (8 pieces per wave), which the second half-phase waits for.
+//
+//   RAW: tile t + 1 is waited (vmcnt(0), every issuing wave) before phase
+//        (t, 1)'s first barrier and first read in phase (t + 1, 0).
+//   WAR: the DMA of phase (t, 0) overwrites the stage tile t - 1 was read
+//        from in phase (t - 1, 1); the lagging wave row issues those reads
+//        one barrier later than the leading row issues the DMA, so phase
+//        (., 1) retires its own reads (lgkmcnt(0)) before its first barrier.
+//
+// Swizzle: 16-B chunk c of LDS row r sits at chunk c ^ ((r >> 1) & 7); the 16
+// lanes of each ds_read_b128 lane group then read 16 distinct 16-B bank slots
+// (2 rows per 256-B bank row), for either k half.
+#define TN64_ROWB 128
+#define TN64_TILE (TN_BM * TN64_ROWB)  // 32 KiB per operand per stage
+#define TN64_STAGE (2 * TN64_TILE)
+#define TN_WAIT_ALL 0x0070             // vmcnt(0) lgkmcnt(0)
+
+__device__ __forceinline__ int tn64_off(int r, int c) { return r * TN64_ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
+
+// lane's source offset (elements, from the operand tile's first row) for
+// LDS row t, chunk position (lane & 7)
+__device__ __forceinline__ uint32_t tn64_goff(int64_t ld, int t, int src_row, int lane) {
+  const int chunk = (lane & 7) ^ ((t >> 1) & 7);
+  return (uint32_t)(src_row * ld + 8 * chunk);
+}
+
+// one operand's 256-row tile: 32 pieces of 8 rows, 4 per wave (rows 32 wave +
+// 8 u + (lane >> 3))
+__device__ __forceinline__ void tn64_stage(const bf16_t* __restrict__ g, const uint32_t* goff, char* lds_tile,
+                                           int wave) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    char* dst = lds_tile + (32 * wave + 8 * u) * TN64_ROWB;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + goff[u]),
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_tn64_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                           const bf16_t* __restrict__ B, int64_t ldb,
+                                                           bf16_t* __restrict__ C, int64_t ldc,
+                                                           bf16_t* __restrict__ S, int64_t lds_,
+                                                           const bf16_t* __restrict__ GU, int64_t ldgu, int M, int N,
+                                                           int K, int F) {
+  // two distinct LDS objects, every access names its stage statically
+  __shared__ __attribute__((aligned(1024))) char sb0[TN64_STAGE];
+  __shared__ __attribute__((aligned(1024))) char sb1[TN64_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_m = M / TN_BM, tiles_n = N / TN_BN;
+  int tm, tn;
+  tn_tile_coords(tn_xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, &tm, &tn);
+  const int nt = K / 64;
+  const int fmap = EPI == TN_SWIGLU_FWD ? F : 0;
+
+  const bf16_t* Ab = A + (int64_t)tm * TN_BM * lda;
+  const bf16_t* Bb = B + (int64_t)tn * (fmap ? TN_BN / 2 : TN_BN) * ldb;
+  uint32_t ga[4], gb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = 32 * wave + 8 * u + (lane >> 3);
+    ga[u] = tn64_goff(lda, t, t, lane);
+    gb[u] = tn64_goff(ldb, t, tn_brow(t, fmap), lane);
+  }
+  // fragment offsets: rows row0 + (lane & 15), chunk 4 h + (lane >> 4); row0
+  // is a multiple of 16, so the swizzle term depends on the lane only
+  const int fr = lane & 15;
+  const int foff0 = fr * TN64_ROWB + (((lane >> 4) ^ ((fr >> 1) & 7)) << 4);
+  const int foff1 = fr * TN64_ROWB + (((4 + (lane >> 4)) ^ ((fr >> 1) & 7)) << 4);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool lag = wm == 1;
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // one 32-k phase: fragments of k-half h of `cur`; h == 0 issues tile t + 1
+  // into `nxt` (past the end: tile t again, into the stage nobody reads any
+  // more), h == 1 waits for it and retires its own reads
+  auto phase = [&](const char* cur, char* nxt, int t, int h) {
+    const int foff = h ? foff1 : foff0;
+    tn_s16x8 bf[4], af[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *(const tn_s16x8*)(cur + TN64_TILE + (wn * 64 + 16 * j) * TN64_ROWB + foff);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *(const tn_s16x8*)(cur + (wm * 128 + 16 * i) * TN64_ROWB + foff);
+    if (h == 0) {
+      const int q = min(t + 1, nt - 1) * 64;
+      tn64_stage(Ab + q, ga, nxt, wave);
+      tn64_stage(Bb + q, gb, nxt + TN64_TILE, wave);
+    } else {
+      __builtin_amdgcn_s_waitcnt(TN_WAIT_ALL);
+    }
+    sync();
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint2 w;
-        w.x = pack2(acc[i][j][0], acc[i][j][1]);
-        w.y = pack2(acc[i][j][2], acc[i][j][3]);
-        *(uint2*)(C + (int64_t)(m0 + 16 * i) * ldc + n0 + 16 * j) = w;
-      }
-  } else if (EPI == TN_SWIGLU_FWD) {
-    // j = 0, 1: gate units h0 + 16 j; j = 2, 3: the same units' up values
-    const int h0 = tn * (TN_BN / 2) + 32 * wn + nl;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      bf16_t* crow = C + (int64_t)(m0 + 16 * i) * ldc;
-      bf16_t* srow = S + (int64_t)(m0 + 16 * i) * lds_;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const f32x4 g = acc[i][j], u = acc[i][j + 2];
-        uint2 wg, wu, ws;
-        wg.x = pack2(g[0], g[1]);
-        wg.y = pack2(g[2], g[3]);
-        wu.x = pack2(u[0], u[1]);
-        wu.y = pack2(u[2], u[3]);
-        // s from the bf16-rounded gate / up: the values backward re-reads from gu
-        const float g0 = __uint_as_float(wg.x << 16), g1 = __uint_as_float(wg.x & 0xffff0000u);
-        const float g2 = __uint_as_float(wg.y << 16), g3 = __uint_as_float(wg.y & 0xffff0000u);
-        const float u0 = __uint_as_float(wu.x << 16), u1 = __uint_as_float(wu.x & 0xffff0000u);
-        const float u2 = __uint_as_float(wu.y << 16), u3 = __uint_as_float(wu.y & 0xffff0000u);
-        ws.x = pack2(tn_silu(g0) * u0, tn_silu(g1) * u1);
-        ws.y = pack2(tn_silu(g2) * u2, tn_silu(g3) * u3);
-        const int h = h0 + 16 * j;
-        *(uint2*)(crow + h) = wg;
-        *(uint2*)(crow + F + h) = wu;
-        *(uint2*)(srow + h) = ws;
-      }
-    }
-  } else {  // TN_SWIGLU_BWD: C = ds (never stored) -> dgu
-    const int n0 = tn * TN_BN + wn * 64 + nl;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const bf16_t* gurow = GU + (int64_t)(m0 + 16 * i) * ldgu;
-      bf16_t* drow = C + (int64_t)(m0 + 16 * i) * ldc;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int h = n0 + 16 * j;
-        const uint2 gw = *(const uint2*)(gurow + h), uw = *(const uint2*)(gurow + F + h);
-        float g[4] = {__uint_as_float(gw.x << 16), __uint_as_float(gw.x & 0xffff0000u), __uint_as_float(gw.y << 16),
-                      __uint_as_float(gw.y & 0xffff0000u)};
-        float u[4] = {__uint_as_float(uw.x << 16), __uint_as_float(uw.x & 0xffff0000u), __uint_as_float(uw.y << 16),
-                      __uint_as_float(uw.y & 0xffff0000u)};
-        // ds rounded to bf16 first: the value the unfused path stores
-        float d[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) d[e] = bf2f(f2bf(acc[i][j][e]));
-        float dg[4], du[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float sg = 1.f / (1.f + __expf(-g[e]));
-          du[e] = d[e] * g[e] * sg;
-          dg[e] = d[e] * u[e] * sg * (1.f + g[e] * (1.f - sg));
-        }
-        uint2 wdg, wdu;
-        wdg.x = pack2(dg[0], dg[1]);
-        wdg.y = pack2(dg[2], dg[3]);
-        wdu.x = pack2(du[0], du[1]);
-        wdu.y = pack2(du[2], du[3]);
-        *(uint2*)(drow + h) = wdg;
-        *(uint2*)(drow + F + h) = wdu;
-      }
-    }
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+
+  tn64_stage(Ab, ga, sb0, wave);
+  tn64_stage(Bb, gb, sb0 + TN64_TILE, wave);
+  __builtin_amdgcn_s_waitcnt(TN_WAIT_ALL);
+  sync();
+  if (lag) sync();
+  for (int t = 0; t < nt; t += 2) {
+    phase(sb0, sb1, t, 0);
+    phase(sb0, sb1, t, 1);
+    phase(sb1, sb0, t + 1, 0);
+    phase(sb1, sb0, t + 1, 1);
   }
+  if (!lag) sync();
+  __builtin_amdgcn_s_waitcnt(TN_WAIT_ALL);
+  tn_epilogue<EPI>(acc, tm, tn, wm, wn, lane, C, ldc, S, lds_, GU, ldgu, F);
+}
+
+// main loop: 1 = full-line 64-k stages (default), 0 = the 32-k kernel;
+// TOA_GEMM_TN_BK=32 selects the latter, toa_gemm_tn_set_variant for A/B
+static int g_tn_variant = -1;
+static int tn_variant() {
+  if (g_tn_variant < 0) {
+    const char* e = getenv("TOA_GEMM_TN_BK");
+    g_tn_variant = (e && e[0] == '3') ? 0 : 1;
+  }
+  return g_tn_variant;
+}
+extern "C" int toa_gemm_tn_set_variant(int v) {
+  g_tn_variant = v < 0 ? -1 : (v ? 1 : 0);
+  return 0;
+}
+
+template <int EPI>
+static void tn_launch(dim3 grid, hipStream_t stream, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
+                      bf16_t* C, int64_t ldc, bf16_t* S, int64_t lds_, const bf16_t* GU, int64_t ldgu, int M, int N,
+                      int K, int F) {
+  if (tn_variant())
+    hipLaunchKernelGGL(gemm_tn64_kernel<EPI>, grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
+                       N, K, F);
+  else
+    hipLaunchKernelGGL(gemm_tn_kernel<EPI>, grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
+                       N, K, F);
 }
 
 static bool tn_shape_ok(int M, int N, int K, int64_t lda, int64_t ldb) {
@@ -283,8 +457,8 @@ static bool tn_shape_ok(int M, int N, int K, int64_t lda, int64_t ldb) {
 extern "C" int toa_gemm_tn(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int M,
                            int N, int K, hipStream_t stream) {
   if (!tn_shape_ok(M, N, K, lda, ldb) || ldc % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_tn_kernel<TN_PLAIN>, dim3((M / TN_BM) * (N / TN_BN)), dim3(512), 0, stream, A, lda, B, ldb,
-                     C, ldc, (bf16_t*)nullptr, (int64_t)0, (const bf16_t*)nullptr, (int64_t)0, M, N, K, 0);
+  tn_launch<TN_PLAIN>(dim3((M / TN_BM) * (N / TN_BN)), stream, A, lda, B, ldb, C, ldc, nullptr, 0, nullptr, 0, M, N,
+                      K, 0);
   return (int)hipGetLastError();
 }
 
@@ -294,8 +468,8 @@ extern "C" int toa_gemm_tn_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* Wg
                                   int64_t ldgu, bf16_t* S, int64_t lds_, int M, int F, int K, hipStream_t stream) {
   if (F % (TN_BN / 2) || !tn_shape_ok(M, 2 * F, K, ldx, ldw) || ldgu % 4 || lds_ % 4)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_tn_kernel<TN_SWIGLU_FWD>, dim3((M / TN_BM) * (2 * F / TN_BN)), dim3(512), 0, stream, X, ldx,
-                     Wgu, ldw, GU, ldgu, S, lds_, (const bf16_t*)nullptr, (int64_t)0, M, 2 * F, K, F);
+  tn_launch<TN_SWIGLU_FWD>(dim3((M / TN_BM) * (2 * F / TN_BN)), stream, X, ldx, Wgu, ldw, GU, ldgu, S, lds_, nullptr, 0,
+                           M, 2 * F, K, F);
   return (int)hipGetLastError();
 }
 
@@ -305,7 +479,7 @@ extern "C" int toa_gemm_tn_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16_
                                       const bf16_t* GU, int64_t ldgu, bf16_t* dGU, int64_t lddgu, int M, int F, int K,
                                       hipStream_t stream) {
   if (!tn_shape_ok(M, F, K, ldy, ldw) || ldgu % 4 || lddgu % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_tn_kernel<TN_SWIGLU_BWD>, dim3((M / TN_BM) * (F / TN_BN)), dim3(512), 0, stream, dY, ldy,
-                     WdT, ldw, dGU, lddgu, (bf16_t*)nullptr, (int64_t)0, GU, ldgu, M, F, K, F);
+  tn_launch<TN_SWIGLU_BWD>(dim3((M / TN_BM) * (F / TN_BN)), stream, dY, ldy, WdT, ldw, dGU, lddgu, nullptr, 0, GU, ldgu,
+                           M, F, K, F);
   return (int)hipGetLastError();
 }

@@ -2,7 +2,8 @@
 Llama-3-8B forward / data-gradient forms (T = 24576 tokens), in-process
 interleaved rounds on random operands (guide §5.4 rules 24/25):
 
-    tn        toa_gemm_tn (plain epilogue)
+    tn        toa_gemm_tn (plain epilogue), full-line 64-k main loop (default)
+    tn32      the same with the 32-k main loop (toa_gemm_tn_set_variant(0))
     blt_nosk  hipBLASLt, the non-stream-K table (ops/gemm.py ``nosk``)
     blt_heur  hipBLASLt heuristic (torch.matmul; stream-K kernels)
 
@@ -55,6 +56,11 @@ def main():
                 _lib.call("toa_gemm_tn", _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn, T, nn, kk,
                           _lib.stream(x))
 
+            def tn32():
+                _lib.call("toa_gemm_tn_set_variant", 0)
+                tn()
+                _lib.call("toa_gemm_tn_set_variant", -1)
+
             def nosk():
                 gemm.set_mode("nosk")
                 gemm.linear_fwd(x, w)
@@ -62,9 +68,9 @@ def main():
             def heur():
                 torch.matmul(x, w.t())
 
-            ts = {"tn": [], "blt_nosk": [], "blt_heur": []}
+            ts = {"tn": [], "tn32": [], "blt_nosk": [], "blt_heur": []}
             for _ in range(a.rounds):
-                for k2, f in (("tn", tn), ("blt_nosk", nosk), ("blt_heur", heur)):
+                for k2, f in (("tn", tn), ("tn32", tn32), ("blt_nosk", nosk), ("blt_heur", heur)):
                     ts[k2].append(timer(f, a.reps))
             ref = (x.float() @ w.float().t())
             tn()

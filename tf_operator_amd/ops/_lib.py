@@ -82,6 +82,7 @@ _SIGS = {
     "toa_gemm_tn": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_tn_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_tn_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_tn_set_variant": [c_int],
     "toa_attn_set_dkdv_variant": [c_int],
     "toa_attn_set_bwd_variant": [c_int],
     "toa_attn_set_kb_order": [c_int],
