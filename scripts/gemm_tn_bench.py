@@ -4,6 +4,9 @@ interleaved rounds on random operands (guide §5.4 rules 24/25):
 
     tn        toa_gemm_tn (plain epilogue), full-line 64-k main loop (default)
     tn32      the same with the 32-k main loop (toa_gemm_tn_set_variant(0))
+    tn4w      one wave per SIMD, 128 x 128 per wave (toa_gemm_tn_set_variant(2))
+    tnrot     tn with a per-tile k rotation (toa_gemm_tn_set_variant(3))
+    tnpad     tn on operands with row stride K + 64 (L2-channel probe)
     blt_nosk  hipBLASLt, the non-stream-K table (ops/gemm.py ``nosk``)
     blt_heur  hipBLASLt heuristic (torch.matmul; stream-K kernels)
 
@@ -68,9 +71,30 @@ def main():
             def heur():
                 torch.matmul(x, w.t())
 
-            ts = {"tn": [], "tn32": [], "blt_nosk": [], "blt_heur": []}
+            def tn4w():
+                _lib.call("toa_gemm_tn_set_variant", 2)
+                tn()
+                _lib.call("toa_gemm_tn_set_variant", -1)
+
+            def tnrot():
+                _lib.call("toa_gemm_tn_set_variant", 3)
+                tn()
+                _lib.call("toa_gemm_tn_set_variant", -1)
+
+            xp = torch.empty(T, kk + 64, device="cuda", dtype=torch.bfloat16)[:, :kk]
+            xp.copy_(x)
+            wp = torch.empty(nn, kk + 64, device="cuda", dtype=torch.bfloat16)[:, :kk]
+            wp.copy_(w)
+
+            def tnpad():
+                _lib.call("toa_gemm_tn", _lib.ptr(xp), kk + 64, _lib.ptr(wp), kk + 64, _lib.ptr(y), nn, T, nn, kk,
+                          _lib.stream(x))
+
+            arms = (("tn", tn), ("tn32", tn32), ("tn4w", tn4w), ("tnrot", tnrot), ("tnpad", tnpad),
+                    ("blt_nosk", nosk), ("blt_heur", heur))
+            ts = {k2: [] for k2, _ in arms}
             for _ in range(a.rounds):
-                for k2, f in (("tn", tn), ("tn32", tn32), ("blt_nosk", nosk), ("blt_heur", heur)):
+                for k2, f in arms:
                     ts[k2].append(timer(f, a.reps))
             ref = (x.float() @ w.float().t())
             tn()
@@ -82,7 +106,7 @@ def main():
                                               for k2, v in ts.items()}
             out["forms"][f"{name}.{kind}"]["tn_rel_err"] = round(err, 5)
             print(json.dumps({f"{name}.{kind}": out["forms"][f"{name}.{kind}"]}), flush=True)
-            del x, w, y, ref
+            del x, w, y, ref, xp, wp
     # fused MLP ends at the gate|up and down shapes
     F_, Hd = 14336, 4096
     x = torch.randn(T, Hd, device="cuda").to(torch.bfloat16)

@@ -33,7 +33,7 @@ def main():
     for _ in range(5):
         torch.matmul(x, w.t())
     y = torch.empty(T, N, device="cuda", dtype=torch.bfloat16)
-    for v in (1, 0):
+    for v in (1, 0, 2):
         _lib.call("toa_gemm_tn_set_variant", v)
         for _ in range(7):
             _lib.call("toa_gemm_tn", _lib.ptr(x), K, _lib.ptr(w), K, _lib.ptr(y), N, T, N, K, _lib.stream(x))

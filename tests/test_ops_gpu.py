@@ -998,13 +998,14 @@ def test_fused_batchnorm_momentum_none_matches_torch():
     assert rel(bn.running_var, ref.running_var) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [1, 0])
+@pytest.mark.parametrize("variant", [1, 0, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 1536, 4096), (768, 512, 256)])
 def test_gemm_tn_matches_fp32(M, N, K, variant):
     """csrc/hip/gemm_tn.hip plain epilogue: y = x w^T vs fp32 torch, with an
     asymmetric non-square operand (guide §3: catch a transposed C write) and
-    padded row strides; both main loops (1 = full-line 64-k stages, the
-    default; 0 = 32-k stages)."""
+    padded row strides; every main loop (1 = full-line 64-k stages, 8 waves,
+    the default; 0 = 32-k stages; 2 = one wave per SIMD, 128 x 128 per wave;
+    3 = 1 with a per-tile k rotation)."""
     L = _lib()
     torch.manual_seed(M + N + K)
     xb = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K]
@@ -1022,22 +1023,23 @@ def test_gemm_tn_matches_fp32(M, N, K, variant):
 
 @pytest.mark.parametrize("M,N,K", [(512, 512, 128), (2048, 1024, 4096)])
 def test_gemm_tn_main_loops_bit_identical(M, N, K):
-    """The 64-k full-line main loop sums the same 32-k MFMA chunks in the same
-    order as the 32-k one, so the two agree bit for bit (a staging race or a
-    wrong swizzle shows up as a difference)."""
+    """Every main loop sums the same 32-k MFMA chunks in the same order, so
+    they agree bit for bit (a staging race or a wrong swizzle shows up as a
+    difference)."""
     L = _lib()
     torch.manual_seed(K)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
     ys = []
-    for v in (0, 1, 1):
+    for v in (0, 1, 2, 1, 2):
         y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         L.call("toa_gemm_tn_set_variant", v)
         L.call("toa_gemm_tn", L.ptr(x), K, L.ptr(w), K, L.ptr(y), N, M, N, K, L.stream(y))
         ys.append(y)
     L.call("toa_gemm_tn_set_variant", -1)
     torch.cuda.synchronize()
-    assert torch.equal(ys[0], ys[1]) and torch.equal(ys[1], ys[2])
+    for y in ys[1:]:
+        assert torch.equal(ys[0], y)
 
 
 @pytest.mark.parametrize("M,F,K", [(256, 128, 128), (512, 384, 256), (1024, 1024, 1024)])
