@@ -330,7 +330,7 @@ __device__ __forceinline__ void tn64_stage(const bf16_t* __restrict__ g, const u
   }
 }
 
-template <int EPI, bool ROT>
+template <int EPI, int MODE>
 __global__ __launch_bounds__(512, 1) void gemm_tn64_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                            const bf16_t* __restrict__ B, int64_t ldb,
                                                            bf16_t* __restrict__ C, int64_t ldc,
@@ -350,7 +350,10 @@ __global__ __launch_bounds__(512, 1) void gemm_tn64_kernel(const bf16_t* __restr
   // ROT: every tile starts its k loop at its own tile offset, so the
   // workgroups in flight fetch different k windows (their rows are K * 2
   // bytes apart: in lockstep, all of them would hit the same L2 channels)
-  const int rot = ROT ? (tm * 5 + tn * 3) % nt : 0;
+  // MODE 2: tile t + 1's DMA goes out between phase (t, 0)'s MFMAs instead of
+  // ahead of its barrier (the MFMA segment has idle issue slots; ahead of the
+  // barrier, 8 pieces' issue can outlast the partner wave's MFMAs)
+  const int rot = MODE == 1 ? (tm * 5 + tn * 3) % nt : 0;
   const int fmap = EPI == TN_SWIGLU_FWD ? F : 0;
 
   const bf16_t* Ab = A + (int64_t)tm * TN_BM * lda;
@@ -390,21 +393,36 @@ __global__ __launch_bounds__(512, 1) void gemm_tn64_kernel(const bf16_t* __restr
     for (int j = 0; j < 4; ++j) bf[j] = *(const tn_s16x8*)(cur + TN64_TILE + (wn * 64 + 16 * j) * TN64_ROWB + foff);
 #pragma unroll
     for (int i = 0; i < 8; ++i) af[i] = *(const tn_s16x8*)(cur + (wm * 128 + 16 * i) * TN64_ROWB + foff);
-    if (h == 0) {
-      int q = min(t + 1, nt - 1) + rot;
-      q = (q >= nt ? q - nt : q) * 64;
+    int q = min(t + 1, nt - 1) + rot;
+    q = (q >= nt ? q - nt : q) * 64;
+    if (h == 0 && MODE != 2) {
       tn64_stage(Ab + q, ga, nxt, wave);
       tn64_stage(Bb + q, gb, nxt + TN64_TILE, wave);
-    } else {
+    } else if (h == 1) {
       __builtin_amdgcn_s_waitcnt(TN_WAIT_ALL);
     }
     sync();
     __builtin_amdgcn_s_setprio(1);
+    if (h == 0 && MODE == 2) {
+      // fragments must have landed before the first MFMA
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      tn64_stage(Ab + q, ga, nxt, wave);
+      tn64_stage(Bb + q, gb, nxt + TN64_TILE, wave);
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    if (h == 0 && MODE == 2) {
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM (LDS-DMA)
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     sync();
   };
@@ -569,17 +587,18 @@ __global__ __launch_bounds__(256, 1) void gemm_tn4w_kernel(const bf16_t* __restr
 
 // main loop: 1 = full-line 64-k stages, 8 waves (default), 0 = the 32-k
 // kernel, 2 = one wave per SIMD (plain epilogue only; the SwiGLU epilogues
-// stay on 1), 3 = 1 with a per-tile k rotation.  TOA_GEMM_TN_VARIANT selects; toa_gemm_tn_set_variant for A/B
+// stay on 1), 3 = 1 with a per-tile k rotation, 4 = 1 with the DMA between
+// the MFMAs.  TOA_GEMM_TN_VARIANT selects; toa_gemm_tn_set_variant for A/B
 static int g_tn_variant = -1;
 static int tn_variant() {
   if (g_tn_variant < 0) {
     const char* e = getenv("TOA_GEMM_TN_VARIANT");
-    g_tn_variant = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 1;
+    g_tn_variant = (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 1;
   }
   return g_tn_variant;
 }
 extern "C" int toa_gemm_tn_set_variant(int v) {
-  g_tn_variant = (v < 0 || v > 3) ? -1 : v;
+  g_tn_variant = (v < 0 || v > 4) ? -1 : v;
   return 0;
 }
 
@@ -590,11 +609,14 @@ static void tn_launch(dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld
   const int v = tn_variant();
   if (v == 2 && EPI == TN_PLAIN)
     hipLaunchKernelGGL(gemm_tn4w_kernel, grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, M, N, K);
+  else if (v == 4)
+    hipLaunchKernelGGL((gemm_tn64_kernel<EPI, 2>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU,
+                       ldgu, M, N, K, F);
   else if (v == 3)
-    hipLaunchKernelGGL((gemm_tn64_kernel<EPI, true>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU,
+    hipLaunchKernelGGL((gemm_tn64_kernel<EPI, 1>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU,
                        ldgu, M, N, K, F);
   else if (v)
-    hipLaunchKernelGGL((gemm_tn64_kernel<EPI, false>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
+    hipLaunchKernelGGL((gemm_tn64_kernel<EPI, 0>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
                        N, K, F);
   else
     hipLaunchKernelGGL(gemm_tn_kernel<EPI>, grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,

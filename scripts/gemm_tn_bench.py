@@ -7,6 +7,7 @@ interleaved rounds on random operands (guide §5.4 rules 24/25):
     tn4w      one wave per SIMD, 128 x 128 per wave (toa_gemm_tn_set_variant(2))
     tnrot     tn with a per-tile k rotation (toa_gemm_tn_set_variant(3))
     tnpad     tn on operands with row stride K + 64 (L2-channel probe)
+    tndm      tn with the LDS-DMA issued between the MFMAs (variant 4)
     blt_nosk  hipBLASLt, the non-stream-K table (ops/gemm.py ``nosk``)
     blt_heur  hipBLASLt heuristic (torch.matmul; stream-K kernels)
 
@@ -81,6 +82,11 @@ def main():
                 tn()
                 _lib.call("toa_gemm_tn_set_variant", -1)
 
+            def tndm():
+                _lib.call("toa_gemm_tn_set_variant", 4)
+                tn()
+                _lib.call("toa_gemm_tn_set_variant", -1)
+
             xp = torch.empty(T, kk + 64, device="cuda", dtype=torch.bfloat16)[:, :kk]
             xp.copy_(x)
             wp = torch.empty(nn, kk + 64, device="cuda", dtype=torch.bfloat16)[:, :kk]
@@ -90,7 +96,7 @@ def main():
                 _lib.call("toa_gemm_tn", _lib.ptr(xp), kk + 64, _lib.ptr(wp), kk + 64, _lib.ptr(y), nn, T, nn, kk,
                           _lib.stream(x))
 
-            arms = (("tn", tn), ("tn32", tn32), ("tn4w", tn4w), ("tnrot", tnrot), ("tnpad", tnpad),
+            arms = (("tn", tn), ("tn32", tn32), ("tn4w", tn4w), ("tnrot", tnrot), ("tnpad", tnpad), ("tndm", tndm),
                     ("blt_nosk", nosk), ("blt_heur", heur))
             ts = {k2: [] for k2, _ in arms}
             for _ in range(a.rounds):
