@@ -194,7 +194,7 @@ __device__ __forceinline__ void tn_epilogue(f32x4 (&acc)[8][4], int tm, int tn, 
   }
 }
 
-template <int EPI>
+template <int EPI, int DIST>
 __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                          const bf16_t* __restrict__ B, int64_t ldb,
                                                          bf16_t* __restrict__ C, int64_t ldc,
@@ -239,19 +239,26 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restric
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  // phase p: fragments of stage p (this buffer), LDS-DMA of stage p + 2 into
-  // the buffer stage p - 2 used, wait for this wave's DMA of stage p + 1,
-  // barrier, 32 MFMAs, barrier (the wgrad.hip schedule)
+  // phase p: fragments of stage p (this buffer), LDS-DMA of stage p + DIST
+  // into the buffer stage p + DIST - 4 used, wait for this wave's DMA of stage
+  // p + 1, barrier, 32 MFMAs, barrier (the wgrad.hip schedule).  DIST = 3
+  // gives each stage two phases of flight instead of one; the buffer it
+  // refills was read in phase p - 1, by the lagging wave row one barrier
+  // after the leading row, so every phase retires its reads (lgkmcnt(0))
+  // before its first barrier.
   auto phase = [&](const char* cur, char* pre, int p) {
     tn_s16x8 bf[4], af[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bf[j] = tn_frag(cur + TN_TILE, wn * 64 + 16 * j, lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) af[i] = tn_frag(cur, wm * 128 + 16 * i, lane);
-    const int q = min(p + 2, np - 1);  // past the end: re-fetch into a buffer nobody reads again
+    const int q = min(p + DIST, np - 1);  // past the end: re-fetch into a buffer nobody reads again
     tn_stage(Ab + q * TN_BK, ga, pre, wave);
     tn_stage(Bb + q * TN_BK, gb, pre + TN_TILE, wave);
-    __builtin_amdgcn_s_waitcnt(TN_VMCNT4);
+    if (DIST == 2)
+      __builtin_amdgcn_s_waitcnt(TN_VMCNT4);
+    else
+      __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) lgkmcnt(0)
     sync();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -267,14 +274,27 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(const bf16_t* __restric
   tn_stage(Bb, gb, sb0 + TN_TILE, wave);
   tn_stage(Ab + TN_BK, ga, sb1, wave);
   tn_stage(Bb + TN_BK, gb, sb1 + TN_TILE, wave);
-  __builtin_amdgcn_s_waitcnt(TN_VMCNT4);
+  if (DIST == 3) {
+    tn_stage(Ab + 2 * TN_BK, ga, sb2, wave);
+    tn_stage(Bb + 2 * TN_BK, gb, sb2 + TN_TILE, wave);
+    __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): stage 0 landed
+  } else {
+    __builtin_amdgcn_s_waitcnt(TN_VMCNT4);
+  }
   sync();
   if (lag) sync();
   for (int p = 0; p < np; p += 4) {
-    phase(sb0, sb2, p);
-    phase(sb1, sb3, p + 1);
-    phase(sb2, sb0, p + 2);
-    phase(sb3, sb1, p + 3);
+    if (DIST == 2) {
+      phase(sb0, sb2, p);
+      phase(sb1, sb3, p + 1);
+      phase(sb2, sb0, p + 2);
+      phase(sb3, sb1, p + 3);
+    } else {
+      phase(sb0, sb3, p);
+      phase(sb1, sb0, p + 1);
+      phase(sb2, sb1, p + 2);
+      phase(sb3, sb2, p + 3);
+    }
   }
   if (!lag) sync();
   __builtin_amdgcn_s_waitcnt(TN_VMCNT0);
@@ -588,17 +608,17 @@ __global__ __launch_bounds__(256, 1) void gemm_tn4w_kernel(const bf16_t* __restr
 // main loop: 1 = full-line 64-k stages, 8 waves (default), 0 = the 32-k
 // kernel, 2 = one wave per SIMD (plain epilogue only; the SwiGLU epilogues
 // stay on 1), 3 = 1 with a per-tile k rotation, 4 = 1 with the DMA between
-// the MFMAs.  TOA_GEMM_TN_VARIANT selects; toa_gemm_tn_set_variant for A/B
+// the MFMAs, 5 = 0 with the DMA three stages ahead.  TOA_GEMM_TN_VARIANT selects; toa_gemm_tn_set_variant for A/B
 static int g_tn_variant = -1;
 static int tn_variant() {
   if (g_tn_variant < 0) {
     const char* e = getenv("TOA_GEMM_TN_VARIANT");
-    g_tn_variant = (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : 1;
+    g_tn_variant = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 1;
   }
   return g_tn_variant;
 }
 extern "C" int toa_gemm_tn_set_variant(int v) {
-  g_tn_variant = (v < 0 || v > 4) ? -1 : v;
+  g_tn_variant = (v < 0 || v > 5) ? -1 : v;
   return 0;
 }
 
@@ -618,8 +638,11 @@ static void tn_launch(dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld
   else if (v)
     hipLaunchKernelGGL((gemm_tn64_kernel<EPI, 0>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
                        N, K, F);
+  else if (v == 5)
+    hipLaunchKernelGGL((gemm_tn_kernel<EPI, 3>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu,
+                       M, N, K, F);
   else
-    hipLaunchKernelGGL(gemm_tn_kernel<EPI>, grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
+    hipLaunchKernelGGL((gemm_tn_kernel<EPI, 2>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
                        N, K, F);
 }
 
