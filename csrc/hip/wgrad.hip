@@ -106,6 +106,7 @@ __device__ __forceinline__ void wg_tile_coords(int tile, int tiles_m, int tiles_
   *tn = (tile - group * per_group) / gsz;
 }
 
+template <int DIST>
 __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                           const bf16_t* __restrict__ B, int64_t ldb,
                                                           bf16_t* __restrict__ C, int64_t ldc, float* __restrict__ W,
@@ -157,7 +158,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
   // first read of phase p+1 (both rows wait before their first barrier of
   // a phase: exact for the lagging row, one barrier early for the leading
   // one), and restages a buffer only two phases after its last read (4
-  // buffers: the lagging row finished it by then).
+  // buffers: the lagging row finished it by then).  DIST = 3: the DMA runs
+  // three phases ahead (vmcnt(8)) into the buffer read in phase p - 1, so
+  // each phase retires its own reads (lgkmcnt(0)) before its first barrier.
   const bool lag = wm == 1;
   int ga[2], gb[2];
 #pragma unroll
@@ -178,10 +181,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
     for (int i = 0; i < 8; ++i) af[i] = wg_frag(cur, 0, wm * 128 + 16 * i, lane);
     // past the end the last stage is re-fetched into a buffer nobody reads
     // again: keeps the DMA count per phase constant (no branches, vmcnt(4))
-    const int q = min(p + 2, np - 1);
+    const int q = min(p + DIST, np - 1);
     wg_stage(Ab + (int64_t)q * WG_BK * lda, ga, pre, wave);
     wg_stage(Bb + (int64_t)q * WG_BK * ldb, gb, pre + WG_TILE, wave);
-    __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // my DMA of phase p+1 retired
+    if (DIST == 2)
+      __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // my DMA of phase p+1 retired
+    else
+      __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) lgkmcnt(0)
     sync();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -197,14 +203,27 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
   wg_stage(Bb, gb, sb0 + WG_TILE, wave);
   wg_stage(Ab + (int64_t)WG_BK * lda, ga, sb1, wave);
   wg_stage(Bb + (int64_t)WG_BK * ldb, gb, sb1 + WG_TILE, wave);
-  __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // phase 0's DMA retired
+  if (DIST == 3) {
+    wg_stage(Ab + (int64_t)2 * WG_BK * lda, ga, sb2, wave);
+    wg_stage(Bb + (int64_t)2 * WG_BK * ldb, gb, sb2 + WG_TILE, wave);
+    __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): phase 0's DMA retired
+  } else {
+    __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // phase 0's DMA retired
+  }
   sync();
   if (lag) sync();
   for (int p = 0; p < np; p += 4) {
-    phase(sb0, sb2, p);
-    phase(sb1, sb3, p + 1);
-    phase(sb2, sb0, p + 2);
-    phase(sb3, sb1, p + 3);
+    if (DIST == 2) {
+      phase(sb0, sb2, p);
+      phase(sb1, sb3, p + 1);
+      phase(sb2, sb0, p + 2);
+      phase(sb3, sb1, p + 3);
+    } else {
+      phase(sb0, sb3, p);
+      phase(sb1, sb0, p + 1);
+      phase(sb2, sb1, p + 2);
+      phase(sb3, sb2, p + 3);
+    }
   }
   if (!lag) sync();
   __builtin_amdgcn_s_waitcnt(WG_VMCNT0);  // no LDS-DMA left in flight at exit
@@ -490,18 +509,20 @@ static void wg_plan(int M, int N, int K, int* full, int* split) {
   *split = best;
 }
 
-// Kernel variant: 8 (waves, default) or 4 (TOA_WGRAD_4W=1); settable for
-// in-process A/B runs.
+// Kernel variant: 8 (waves, default), 4 (TOA_WGRAD_4W=1) or 3 (8 waves with
+// the DMA three phases ahead, TOA_WGRAD_VARIANT=3); settable for in-process
+// A/B runs.
 static int g_wg_variant = -1;
 static int wg_variant() {
   if (g_wg_variant < 0) {
     const char* e = getenv("TOA_WGRAD_4W");
-    g_wg_variant = (e && e[0] == '1') ? 4 : 8;
+    const char* v = getenv("TOA_WGRAD_VARIANT");
+    g_wg_variant = (e && e[0] == '1') ? 4 : (v && v[0] == '3') ? 3 : 8;
   }
   return g_wg_variant;
 }
 extern "C" int toa_wgrad_set_variant(int waves) {
-  if (waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
+  if (waves != 3 && waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
   g_wg_variant = waves;
   return 0;
 }
@@ -545,8 +566,11 @@ extern "C" int toa_wgrad(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t 
   if (wg_variant() == 4)
     hipLaunchKernelGGL(wgrad_nt4_kernel, dim3(nwg), dim3(256), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
                        split, beta);
+  else if (wg_variant() == 3)
+    hipLaunchKernelGGL(wgrad_nt_kernel<3>, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
+                       split, beta);
   else
-    hipLaunchKernelGGL(wgrad_nt_kernel, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
+    hipLaunchKernelGGL(wgrad_nt_kernel<2>, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
                        split, beta);
   if (split > 1 && rem > 0)
     hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split,

@@ -1,7 +1,7 @@
 """In-process A/B of the weight-gradient kernel variants at the Llama-3-8B
 shapes (T = 6 x 4096 tokens): the 8-wave kernel against the 4-wave
-(one wave per SIMD, 32x32x16 MFMA) one, switched with
-toa_wgrad_set_variant.  Interleaved rounds, median ms; the two results
+(one wave per SIMD, 32x32x16 MFMA) one and the 8-wave one with its DMA
+three phases ahead (variant 3), switched with toa_wgrad_set_variant.  Interleaved rounds, median ms; the two results
 compared.
 
     python scripts/wgrad_variant_ab.py
@@ -20,6 +20,7 @@ from tf_operator_amd.ops import gemm  # noqa: E402
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
           "lm_head": (128256, 4096)}
 T = 24576
+VARIANTS = tuple(int(v) for v in os.environ.get("WGRAD_AB_VARIANTS", "8,3").split(","))
 
 
 def main():
@@ -29,17 +30,17 @@ def main():
         dy = (torch.rand(T, N, device="cuda") * 2 - 1).to(torch.bfloat16)
         x = (torch.rand(T, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         outs = {}
-        for v in (8, 4):
+        for v in VARIANTS:
             assert L.call_ret("toa_wgrad_set_variant", v) == 0
             g = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
             gemm.wgrad_hip_(g, dy, x, beta=0.0)
             outs[v] = g
         torch.cuda.synchronize()
-        diff = float((outs[8].float() - outs[4].float()).abs().max())
-        times = {8: [], 4: []}
+        diff = {v: float((outs[8].float() - outs[v].float()).abs().max()) for v in VARIANTS if v != 8}
+        times = {v: [] for v in VARIANTS}
         g = outs[8]
         for _ in range(7):
-            for v in (8, 4):
+            for v in VARIANTS:
                 L.call_ret("toa_wgrad_set_variant", v)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
@@ -56,7 +57,8 @@ def main():
         del dy, x, outs, g
         torch.cuda.empty_cache()
     L.call_ret("toa_wgrad_set_variant", 8)
-    step = {v: round(sum(res[n][v]["ms"] * (1 if n == "lm_head" else 32) for n in SHAPES), 2) for v in ("8w", "4w")}
+    step = {f"{v}w": round(sum(res[n][f"{v}w"]["ms"] * (1 if n == "lm_head" else 32) for n in SHAPES), 2)
+            for v in VARIANTS}
     print(json.dumps({"wgrad_ms_per_step": step}))
 
 

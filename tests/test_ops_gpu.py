@@ -272,10 +272,11 @@ def test_wgrad_nt_auto_plan(N, K, T, beta, want_split):
 @pytest.mark.parametrize("N,K,T,beta,split", [(256, 256, 1024, 0, 1), (512, 768, 2048, 1, 1),
                                               (4352, 4096, 4096, 1, None), (5376, 4096, 3072, 0, None),
                                               (1024, 1024, 2048, 1, 2), (28672, 4096, 1024, 0, None)])
-def test_wgrad_nt4_variant(N, K, T, beta, split):
+@pytest.mark.parametrize("variant", [4, 3])
+def test_wgrad_nt4_variant(N, K, T, beta, split, variant):
     """The 4-wave (one wave per SIMD, 32x32x16 MFMA) weight-gradient kernel
-    against an fp32 reference, incl. the split-K tail pieces and a strided
-    dy view."""
+    and the 8-wave one with its DMA three phases ahead (variant 3) against
+    an fp32 reference, incl. the split-K tail pieces and a strided dy view."""
     _lib()
     from tf_operator_amd.ops import _lib as L
     from tf_operator_amd.ops import gemm
@@ -286,7 +287,7 @@ def test_wgrad_nt4_variant(N, K, T, beta, split):
     x = (torch.rand(T, K, device=DEV) * 2 - 1).to(torch.bfloat16)
     g0 = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
     ref = dy.float().t() @ x.float() + (g0.float() if beta else 0)
-    assert L.call_ret("toa_wgrad_set_variant", 4) == 0
+    assert L.call_ret("toa_wgrad_set_variant", variant) == 0
     try:
         g = g0.clone()
         gemm.wgrad_hip_(g, dy, x, beta=float(beta), split=split)
