@@ -605,20 +605,138 @@ __global__ __launch_bounds__(256, 1) void gemm_tn4w_kernel(const bf16_t* __restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// Full lines AND a deeper prefetch (variant 6): the 160 KiB of LDS as a ring
+// of five 32-KiB operand slots, each one operand's 64-k tile (256 rows x 128
+// B, the full-line image of gemm_tn64_kernel).  Operand tiles go through the
+// ring in the order A0 B0 A1 B1 A2 ..., slot = position % 5, so 2.5 tiles are
+// resident: the two being read, the next one, and half of the one after.
+// Phase (t, 0) issues B(t+1) and A(t+2) into the slots tile t - 1 freed;
+// phase (t, 1) retires A(t+1) and B(t+1) (vmcnt(4): only A(t+2) may stay in
+// flight) and its own reads (the lagging wave row reads tile t - 1's slots
+// one barrier after the leading row refills them) before its first barrier.
+// B gets the full-line kernel's two phases from issue to first read, A four.
+// The slot pattern repeats every 5 tiles: the loop body is 5 tiles, and the
+// K % 320 remainder runs the first tiles of the same body.
+// ---------------------------------------------------------------------------
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_tn5_kernel(const bf16_t* __restrict__ A, int64_t lda,
+                                                          const bf16_t* __restrict__ B, int64_t ldb,
+                                                          bf16_t* __restrict__ C, int64_t ldc,
+                                                          bf16_t* __restrict__ S, int64_t lds_,
+                                                          const bf16_t* __restrict__ GU, int64_t ldgu, int M, int N,
+                                                          int K, int F) {
+  __shared__ __attribute__((aligned(1024))) char r0[TN64_TILE];
+  __shared__ __attribute__((aligned(1024))) char r1[TN64_TILE];
+  __shared__ __attribute__((aligned(1024))) char r2[TN64_TILE];
+  __shared__ __attribute__((aligned(1024))) char r3[TN64_TILE];
+  __shared__ __attribute__((aligned(1024))) char r4[TN64_TILE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_m = M / TN_BM, tiles_n = N / TN_BN;
+  int tm, tn;
+  tn_tile_coords(tn_xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, &tm, &tn);
+  const int nt = K / 64;
+  const int fmap = EPI == TN_SWIGLU_FWD ? F : 0;
+
+  const bf16_t* Ab = A + (int64_t)tm * TN_BM * lda;
+  const bf16_t* Bb = B + (int64_t)tn * (fmap ? TN_BN / 2 : TN_BN) * ldb;
+  uint32_t ga[4], gb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = 32 * wave + 8 * u + (lane >> 3);
+    ga[u] = tn64_goff(lda, t, t, lane);
+    gb[u] = tn64_goff(ldb, t, tn_brow(t, fmap), lane);
+  }
+  const int fr = lane & 15;
+  const int foff0 = fr * TN64_ROWB + (((lane >> 4) ^ ((fr >> 1) & 7)) << 4);
+  const int foff1 = fr * TN64_ROWB + (((4 + (lane >> 4)) ^ ((fr >> 1) & 7)) << 4);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool lag = wm == 1;
+  auto sync = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // phase (t, h): fragments of k-half h from slots (ai, bi); h == 0 issues
+  // B(t+1) into `nb` and A(t+2) into `na` (past the end: the last tile again,
+  // into slots nobody reads any more)
+  auto phase = [&](const char* ai, const char* bi, char* nb, char* na, int t, int h) {
+    const int foff = h ? foff1 : foff0;
+    tn_s16x8 bf[4], af[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *(const tn_s16x8*)(bi + (wn * 64 + 16 * j) * TN64_ROWB + foff);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *(const tn_s16x8*)(ai + (wm * 128 + 16 * i) * TN64_ROWB + foff);
+    if (h == 0) {
+      tn64_stage(Bb + min(t + 1, nt - 1) * 64, gb, nb, wave);
+      tn64_stage(Ab + min(t + 2, nt - 1) * 64, ga, na, wave);
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0074);  // vmcnt(4) lgkmcnt(0)
+    }
+    sync();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    sync();
+  };
+  // tile t = 5 g + j reads A from slot 2j % 5, B from (2j + 1) % 5 and
+  // refills (2j + 3) % 5 with B(t+1), (2j + 4) % 5 with A(t+2)
+#define TN5_TILE(AI, BI, NB, NA, T) \
+  phase(AI, BI, NB, NA, T, 0);      \
+  phase(AI, BI, NB, NA, T, 1);
+
+  tn64_stage(Ab, ga, r0, wave);
+  tn64_stage(Bb, gb, r1, wave);
+  tn64_stage(Ab + min(1, nt - 1) * 64, ga, r2, wave);
+  __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): A0, B0 landed
+  sync();
+  if (lag) sync();
+  const int ng = nt / 5, rem = nt - 5 * ng;
+  int t = 0;
+  for (int g = 0; g < ng; ++g, t += 5) {
+    TN5_TILE(r0, r1, r3, r4, t)
+    TN5_TILE(r2, r3, r0, r1, t + 1)
+    TN5_TILE(r4, r0, r2, r3, t + 2)
+    TN5_TILE(r1, r2, r4, r0, t + 3)
+    TN5_TILE(r3, r4, r1, r2, t + 4)
+  }
+  if (rem > 0) { TN5_TILE(r0, r1, r3, r4, t) }
+  if (rem > 1) { TN5_TILE(r2, r3, r0, r1, t + 1) }
+  if (rem > 2) { TN5_TILE(r4, r0, r2, r3, t + 2) }
+  if (rem > 3) { TN5_TILE(r1, r2, r4, r0, t + 3) }
+#undef TN5_TILE
+  if (!lag) sync();
+  __builtin_amdgcn_s_waitcnt(TN_WAIT_ALL);
+  tn_epilogue<EPI>(acc, tm, tn, wm, wn, lane, C, ldc, S, lds_, GU, ldgu, F);
+}
+
 // main loop: 1 = full-line 64-k stages, 8 waves (default), 0 = the 32-k
 // kernel, 2 = one wave per SIMD (plain epilogue only; the SwiGLU epilogues
 // stay on 1), 3 = 1 with a per-tile k rotation, 4 = 1 with the DMA between
-// the MFMAs, 5 = 0 with the DMA three stages ahead.  TOA_GEMM_TN_VARIANT selects; toa_gemm_tn_set_variant for A/B
+// the MFMAs, 5 = 0 with the DMA three stages ahead, 6 = full lines in a
+// five-slot ring (gemm_tn5_kernel).  TOA_GEMM_TN_VARIANT selects; toa_gemm_tn_set_variant for A/B
 static int g_tn_variant = -1;
 static int tn_variant() {
   if (g_tn_variant < 0) {
     const char* e = getenv("TOA_GEMM_TN_VARIANT");
-    g_tn_variant = (e && e[0] >= '0' && e[0] <= '5') ? e[0] - '0' : 1;
+    g_tn_variant = (e && e[0] >= '0' && e[0] <= '6') ? e[0] - '0' : 1;
   }
   return g_tn_variant;
 }
 extern "C" int toa_gemm_tn_set_variant(int v) {
-  g_tn_variant = (v < 0 || v > 5) ? -1 : v;
+  g_tn_variant = (v < 0 || v > 6) ? -1 : v;
   return 0;
 }
 
@@ -637,6 +755,9 @@ static void tn_launch(dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld
                        ldgu, M, N, K, F);
   else if (v)
     hipLaunchKernelGGL((gemm_tn64_kernel<EPI, 0>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
+                       N, K, F);
+  else if (v == 6)
+    hipLaunchKernelGGL(gemm_tn5_kernel<EPI>, grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu, M,
                        N, K, F);
   else if (v == 5)
     hipLaunchKernelGGL((gemm_tn_kernel<EPI, 3>), grid, dim3(512), 0, stream, A, lda, B, ldb, C, ldc, S, lds_, GU, ldgu,

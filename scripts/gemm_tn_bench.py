@@ -9,6 +9,7 @@ interleaved rounds on random operands (guide §5.4 rules 24/25):
     tnpad     tn on operands with row stride K + 64 (L2-channel probe)
     tndm      tn with the LDS-DMA issued between the MFMAs (variant 4)
     tn32d3    tn32 with the DMA three 32-k stages ahead (variant 5)
+    tn5       full lines in a five-slot ring (variant 6)
     blt_nosk  hipBLASLt, the non-stream-K table (ops/gemm.py ``nosk``)
     blt_heur  hipBLASLt heuristic (torch.matmul; stream-K kernels)
 
@@ -93,6 +94,11 @@ def main():
                 tn()
                 _lib.call("toa_gemm_tn_set_variant", -1)
 
+            def tn5():
+                _lib.call("toa_gemm_tn_set_variant", 6)
+                tn()
+                _lib.call("toa_gemm_tn_set_variant", -1)
+
             xp = torch.empty(T, kk + 64, device="cuda", dtype=torch.bfloat16)[:, :kk]
             xp.copy_(x)
             wp = torch.empty(nn, kk + 64, device="cuda", dtype=torch.bfloat16)[:, :kk]
@@ -102,7 +108,7 @@ def main():
                 _lib.call("toa_gemm_tn", _lib.ptr(xp), kk + 64, _lib.ptr(wp), kk + 64, _lib.ptr(y), nn, T, nn, kk,
                           _lib.stream(x))
 
-            arms = (("tn", tn), ("tn32", tn32), ("tn4w", tn4w), ("tnrot", tnrot), ("tnpad", tnpad), ("tndm", tndm), ("tn32d3", tn32d3),
+            arms = (("tn", tn), ("tn32", tn32), ("tn4w", tn4w), ("tnrot", tnrot), ("tnpad", tnpad), ("tndm", tndm), ("tn32d3", tn32d3), ("tn5", tn5),
                     ("blt_nosk", nosk), ("blt_heur", heur))
             ts = {k2: [] for k2, _ in arms}
             for _ in range(a.rounds):

@@ -999,7 +999,7 @@ def test_fused_batchnorm_momentum_none_matches_torch():
     assert rel(bn.running_var, ref.running_var) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [1, 0, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 0, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 1536, 4096), (768, 512, 256)])
 def test_gemm_tn_matches_fp32(M, N, K, variant):
     """csrc/hip/gemm_tn.hip plain epilogue: y = x w^T vs fp32 torch, with an
@@ -1007,7 +1007,7 @@ def test_gemm_tn_matches_fp32(M, N, K, variant):
     padded row strides; every main loop (1 = full-line 64-k stages, 8 waves,
     the default; 0 = 32-k stages; 2 = one wave per SIMD, 128 x 128 per wave;
     3 = 1 with a per-tile k rotation; 4 = 1 with the DMA between the MFMAs;
-    5 = 0 with the DMA three stages ahead)."""
+    5 = 0 with the DMA three stages ahead; 6 = full lines, five-slot ring)."""
     L = _lib()
     torch.manual_seed(M + N + K)
     xb = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K]
@@ -1023,7 +1023,7 @@ def test_gemm_tn_matches_fp32(M, N, K, variant):
     assert rel(y, ref) < 1e-2, rel(y, ref)
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 512, 128), (2048, 1024, 4096)])
+@pytest.mark.parametrize("M,N,K", [(512, 512, 128), (2048, 1024, 4096), (512, 768, 640), (256, 512, 1152)])
 def test_gemm_tn_main_loops_bit_identical(M, N, K):
     """Every main loop sums the same 32-k MFMA chunks in the same order, so
     they agree bit for bit (a staging race or a wrong swizzle shows up as a
@@ -1033,7 +1033,7 @@ def test_gemm_tn_main_loops_bit_identical(M, N, K):
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
     ys = []
-    for v in (0, 1, 2, 4, 5, 1, 2, 4, 5):
+    for v in (0, 1, 2, 4, 5, 6, 1, 2, 4, 5, 6):
         y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         L.call("toa_gemm_tn_set_variant", v)
         L.call("toa_gemm_tn", L.ptr(x), K, L.ptr(w), K, L.ptr(y), N, M, N, K, L.stream(y))
