@@ -1296,6 +1296,34 @@ __device__ __forceinline__ void rope_bwd_acc(f32x16 (&a)[D / 32], const float* _
     }
 }
 
+// the same with the lane's cos / sin values loaded beforehand (rope_cs_load)
+template <int D>
+__device__ __forceinline__ void rope_cs_load(f32x4 (&c)[D / 64][4], f32x4 (&sv)[D / 64][4],
+                                             const float* __restrict__ cs, const float* __restrict__ sn, int hh) {
+#pragma unroll
+  for (int dt = 0; dt < D / 64; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      c[dt][g] = *(const f32x4*)(cs + 32 * dt + 8 * g + 4 * hh);
+      sv[dt][g] = *(const f32x4*)(sn + 32 * dt + 8 * g + 4 * hh);
+    }
+}
+template <int D>
+__device__ __forceinline__ void rope_bwd_acc(f32x16 (&a)[D / 32], const f32x4 (&c)[D / 64][4],
+                                             const f32x4 (&sv)[D / 64][4], float scale) {
+  constexpr int HALF = D / 64;
+#pragma unroll
+  for (int dt = 0; dt < HALF; ++dt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y1 = a[dt][4 * g + e] * scale, y2 = a[dt + HALF][4 * g + e] * scale;
+        a[dt][4 * g + e] = y1 * c[dt][g][e] + y2 * sv[dt][g][e];
+        a[dt + HALF][4 * g + e] = y2 * c[dt][g][e] - y1 * sv[dt][g][e];
+      }
+}
+
 template <int D>
 struct DQG {
   static constexpr int KT = TK * AG<D>::ROWB;  // one 64-key K tile
@@ -1316,7 +1344,7 @@ struct DQG {
 //    block's (key, 4-query) pieces gives the B operand (query on the lane, 4
 //    keys per read; the key order matches the K^T read's, as in the split
 //    kernel).
-template <int D, bool ROPE = false>
+template <int D, bool ROPE = false, bool PRE = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __restrict__ K,
                                                               const bf16_t* __restrict__ dS, bf16_t* __restrict__ dQ,
                                                               int B, int H, int Hk, int S, float scale,
@@ -1409,6 +1437,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
   for (int i = 0; i < ND; ++i)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  // PRE: the epilogue's cos / sin rows loaded ahead of the main loop, so
+  // their latency hides under it instead of following it
+  f32x4 rcs[D / 64][4], rsn[D / 64][4];
+  if constexpr (ROPE && PRE)
+    rope_cs_load<D>(rcs, rsn, cosv + (int64_t)(qi * 32 + r) * (D / 2), sinv + (int64_t)(qi * 32 + r) * (D / 2), hh);
 
   auto compute = [&](int t, const char* st) {
     const char* dimg = st + KT + wave * DQG<D>::DSW;
@@ -1467,7 +1500,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
   bf16_t* qrow = dQ + ((int64_t)(b * H + h) * S + myq) * D;
   float osc = scale;
   if constexpr (ROPE) {  // rotate back and write the q part of d(qkv) row (b, myq)
-    rope_bwd_acc<D>(acc, cosv + (int64_t)myq * (D / 2), sinv + (int64_t)myq * (D / 2), hh, scale);
+    if constexpr (PRE)
+      rope_bwd_acc<D>(acc, rcs, rsn, scale);
+    else
+      rope_bwd_acc<D>(acc, cosv + (int64_t)myq * (D / 2), sinv + (int64_t)myq * (D / 2), hh, scale);
     qrow = dQ + ((int64_t)b * S + myq) * H3 * D + h * D;
     osc = 1.f;
   }
@@ -1762,6 +1798,20 @@ static int attn_kb_light_first() {
   }
   return g_kb_light;
 }
+// dQ GEMM of the RoPE-fused backward: cos / sin loaded before the main loop
+// (opt-in TOA_ATTN_ROPE_PREFETCH=1 / toa_attn_set_rope_prefetch, -1 = environment)
+static int g_rope_pre = -1;
+static int attn_rope_prefetch() {
+  if (g_rope_pre < 0) {
+    const char* e = getenv("TOA_ATTN_ROPE_PREFETCH");
+    g_rope_pre = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_rope_pre;
+}
+extern "C" int toa_attn_set_rope_prefetch(int v) {
+  g_rope_pre = v < 0 ? -1 : (v ? 1 : 0);
+  return 0;
+}
 extern "C" int toa_attn_set_kb_order(int light_first) {
   g_kb_light = light_first < 0 ? -1 : (light_first ? 1 : 0);
   return 0;
@@ -1981,8 +2031,12 @@ extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t*
     hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<DD, true, true>), dim3((S / 128) * B * Hk), dim3(512), 0,       \
                        stream, q, k, v, dout, nlse2, delta, dqkv, dqkv, ds, B, H, Hk, S, scale, scale * LOG2E,  \
                        o_bshd, attn_kb_light_first(), cosv, sinv, H3);                                          \
-    hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \
-                       dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                                \
+    if (attn_rope_prefetch())                                                                                   \
+      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, \
+                         k, ds, dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                       \
+    else                                                                                                         \
+      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,   \
+                         ds, dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                          \
   } while (0)
 #ifdef TOA_ATTN_D128_ONLY
   if (D != 128) return (int)hipErrorInvalidValue;
