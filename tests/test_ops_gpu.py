@@ -598,6 +598,36 @@ def test_rope_attention_matches_two_nodes(B, H, Hk, S, D):
         assert rel(a.grad[:, lo:hi], b.grad[:, lo:hi]) < 1e-2, (lo, hi)
 
 
+@pytest.mark.parametrize("D", [128, 64])
+def test_rope_attention_backward_prefetch_variant_bit_identical(D):
+    """The RoPE-fused dQ GEMM with its cos / sin rows loaded before the main
+    loop (toa_attn_set_rope_prefetch(1)) writes the same d(qkv) as the
+    epilogue-load form."""
+    _lib()
+    from tf_operator_amd.ops import _lib as L
+    from tf_operator_amd.ops import llm
+
+    B, H, Hk, S = 1, 8, 2, 512
+    torch.manual_seed(5)
+    cos, sin = llm.rope_tables(S, D, device=DEV)
+    qkv = torch.randn(B * S, (H + 2 * Hk) * D, device=DEV, dtype=torch.bfloat16)
+    do = None
+    grads = []
+    try:
+        for pre in (0, 1):
+            L.call("toa_attn_set_rope_prefetch", pre)
+            a = qkv.clone().requires_grad_()
+            o = llm.rope_attention(a, cos, sin, B, S, H, Hk, D)
+            if do is None:
+                do = torch.randn_like(o)
+            o.backward(do)
+            grads.append(a.grad)
+        torch.cuda.synchronize()
+    finally:
+        L.call("toa_attn_set_rope_prefetch", -1)
+    assert torch.equal(grads[0], grads[1])
+
+
 def test_attention_gpu_has_no_library_fallback():
     """A GPU tensor the HIP kernel cannot take raises instead of silently
     running a library (SDPA / aotriton) kernel."""
