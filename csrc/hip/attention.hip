@@ -1799,12 +1799,14 @@ static int attn_kb_light_first() {
   return g_kb_light;
 }
 // dQ GEMM of the RoPE-fused backward: cos / sin loaded before the main loop
-// (opt-in TOA_ATTN_ROPE_PREFETCH=1 / toa_attn_set_rope_prefetch, -1 = environment)
+// (default; TOA_ATTN_ROPE_PREFETCH=0 / toa_attn_set_rope_prefetch(0) loads them in
+// the epilogue: 2.792 vs 2.782 ms per backward, bit-identical,
+// profiles/r3_attn_pmc/ab_rope_prefetch.log)
 static int g_rope_pre = -1;
 static int attn_rope_prefetch() {
   if (g_rope_pre < 0) {
     const char* e = getenv("TOA_ATTN_ROPE_PREFETCH");
-    g_rope_pre = (e && e[0] == '1') ? 1 : 0;
+    g_rope_pre = (e && e[0] == '0') ? 0 : 1;
   }
   return g_rope_pre;
 }
