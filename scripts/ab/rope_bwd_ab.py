@@ -1,10 +1,15 @@
 """In-process A/B of the RoPE-fused attention backward (toa_attn_bwd_rope:
 delta pass + dK/dV storing dS + dQ GEMM writing d(qkv)) at the Llama-3-8B
-bench shape, with the dQ GEMM's cos / sin rows loaded before its main loop
-(prefetch, toa_attn_set_rope_prefetch(1)) or in its epilogue (0).
-Interleaved rounds on random data; checks the two agree bit for bit.
+bench shape, A/B of one switch (--switch):
 
-    python scripts/ab/rope_bwd_ab.py [--rounds 8] [--reps 5]
+    prefetch  the dQ GEMM's cos / sin rows loaded before its main loop (1) or
+              in its epilogue (0)           toa_attn_set_rope_prefetch
+    stagger   (rejected, removed) the dK/dV kernel's two query-half wave rows
+              staggered by one segment: profiles/r3_attn_pmc/ab_dkdv_stagger_rejected.log
+
+Interleaved rounds on random data; checks the two arms agree bit for bit.
+
+    python scripts/ab/rope_bwd_ab.py [--switch prefetch] [--rounds 8] [--reps 5]
 """
 import argparse
 import json
@@ -22,7 +27,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--switch", default="prefetch", choices=("prefetch",))
     a = ap.parse_args()
+    setter = {"prefetch": "toa_attn_set_rope_prefetch"}[a.switch]
     B, H, Hk, S, D = 6, 32, 8, 4096, 128
     dev = "cuda"
     torch.manual_seed(0)
@@ -45,7 +52,7 @@ def main():
     outs = {}
 
     def run(pre):
-        _lib.call("toa_attn_set_rope_prefetch", pre)
+        _lib.call(setter, pre)
         dqkv = torch.empty(B * S, (H + 2 * Hk) * D, device=dev, dtype=torch.bfloat16)
         _lib.call("toa_attn_bwd_rope", P(q), P(k), P(v), P(o), P(do), P(lse), P(delta), P(ws), P(cos), P(sin),
                   P(dqkv), B, H, Hk, S, D, flags, scale, st)
@@ -66,10 +73,10 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[pre].append(ev[0].elapsed_time(ev[1]) / a.reps)
-    _lib.call("toa_attn_set_rope_prefetch", -1)
-    print(json.dumps({"bit_identical": same, "prefetch_ms": round(statistics.median(times[1]), 4),
-                      "epilogue_load_ms": round(statistics.median(times[0]), 4),
-                      "prefetch_min": round(min(times[1]), 4), "epilogue_load_min": round(min(times[0]), 4)}))
+    _lib.call(setter, -1)
+    print(json.dumps({"switch": a.switch, "bit_identical": same, "on_ms": round(statistics.median(times[1]), 4),
+                      "off_ms": round(statistics.median(times[0]), 4), "on_min": round(min(times[1]), 4),
+                      "off_min": round(min(times[0]), 4)}))
 
 
 if __name__ == "__main__":

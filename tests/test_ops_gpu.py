@@ -598,11 +598,12 @@ def test_rope_attention_matches_two_nodes(B, H, Hk, S, D):
         assert rel(a.grad[:, lo:hi], b.grad[:, lo:hi]) < 1e-2, (lo, hi)
 
 
+@pytest.mark.parametrize("setter", ["toa_attn_set_rope_prefetch"])
 @pytest.mark.parametrize("D", [128, 64])
-def test_rope_attention_backward_prefetch_variant_bit_identical(D):
-    """The RoPE-fused dQ GEMM with its cos / sin rows loaded before the main
-    loop (toa_attn_set_rope_prefetch(1)) writes the same d(qkv) as the
-    epilogue-load form."""
+def test_rope_attention_backward_prefetch_variant_bit_identical(D, setter):
+    """The RoPE-fused backward's variants write the same d(qkv): the dQ GEMM
+    with its cos / sin rows loaded before the main loop
+    (toa_attn_set_rope_prefetch) against its epilogue-load form."""
     _lib()
     from tf_operator_amd.ops import _lib as L
     from tf_operator_amd.ops import llm
@@ -615,7 +616,7 @@ def test_rope_attention_backward_prefetch_variant_bit_identical(D):
     grads = []
     try:
         for pre in (0, 1):
-            L.call("toa_attn_set_rope_prefetch", pre)
+            L.call(setter, pre)
             a = qkv.clone().requires_grad_()
             o = llm.rope_attention(a, cos, sin, B, S, H, Hk, D)
             if do is None:
@@ -624,7 +625,7 @@ def test_rope_attention_backward_prefetch_variant_bit_identical(D):
             grads.append(a.grad)
         torch.cuda.synchronize()
     finally:
-        L.call("toa_attn_set_rope_prefetch", -1)
+        L.call(setter, -1)
     assert torch.equal(grads[0], grads[1])
 
 
