@@ -52,7 +52,30 @@ SVC_RE = re.compile(r"([a-z0-9]([-a-z0-9]*[a-z0-9])?)\.([a-z0-9]([-a-z0-9]*[a-z0
 REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+_PORT_RNG = None
+
+
 def _free_port():
+    """A currently free localhost port for a service.  Drawn at random from
+    [20000, 32000), below the kernel's ephemeral range: a port handed out by
+    bind(0) is the next one the kernel gives ANY process, so two local
+    clusters on one host (parallel test workers) would otherwise tend to get
+    the same just-released port between this check and the replica's bind."""
+    global _PORT_RNG
+    if _PORT_RNG is None:
+        import random
+
+        _PORT_RNG = random.Random(os.getpid() ^ time.time_ns())
+    for _ in range(64):
+        p = _PORT_RNG.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     p = s.getsockname()[1]
