@@ -321,6 +321,95 @@ static int norm_fwd_launch(const void* x, const void* res, void* h_out, const vo
 
 // number of workgroups the backward uses (=> partial rows); caller sizes the
 // partial workspace as nb * cols * (RMS ? 1 : 2) floats.
+// RMSNorm backward, one row per workgroup (bf16, cols a multiple of 2048, at
+// most 8192): the row's 4 waves each own a contiguous quarter of the columns
+// (CPL 16-byte chunks per lane), so h and dy stay in registers between the
+// two halves of the row (no second read) and the weight, the same for every
+// row, is loaded once.  The row sum crosses the waves through LDS, double
+// buffered so one barrier per row suffices (row k + 2 rewrites row k's slot
+// only after every wave has passed row k + 1's barrier, i.e. read row k's).
+// Each wave's dW partials cover its own columns: written straight to
+// partial[blockIdx.x][cols] for col_reduce_kernel, no LDS reduction.
+template <int CPL>
+__global__ __launch_bounds__(256) void rms_bwd_row_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
+                                                          const bf16_t* __restrict__ w,
+                                                          const float* __restrict__ rstd_in,
+                                                          const bf16_t* __restrict__ dadd, bf16_t* __restrict__ dx,
+                                                          float* __restrict__ partial, int rows, int cols) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col0 = wid * (cols >> 2);  // this wave's quarter
+  float wv[CPL][8], dw[CPL][8];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    Vec8<bf16_t>::load(w + col0 + (c * 64 + lane) * 8, wv[c]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw[c][j] = 0.f;
+  }
+  const float inv_cols = 1.f / (float)cols;
+  int par = 0;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x, par ^= 1) {
+    const float rstd = rstd_in[row];
+    const int64_t base = (int64_t)row * cols + col0;
+    float xh[CPL][8], g[CPL][8];
+    float s1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      float d[8];
+      Vec8<bf16_t>::load(h + base + (c * 64 + lane) * 8, xh[c]);
+      Vec8<bf16_t>::load(dy + base + (c * 64 + lane) * 8, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xh[c][j] *= rstd;
+        g[c][j] = d[j] * wv[c][j];
+        s1 = fmaf(g[c][j], xh[c][j], s1);
+        dw[c][j] = fmaf(d[j], xh[c][j], dw[c][j]);
+      }
+    }
+    s1 = wave_sum(s1);
+    if (lane == 0) red[par][wid] = s1;
+    __syncthreads();
+    s1 = (red[par][0] + red[par][1] + red[par][2] + red[par][3]) * inv_cols;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int64_t off = base + (c * 64 + lane) * 8;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (g[c][j] - xh[c][j] * s1) * rstd;
+      if (dadd != nullptr) {
+        float a[8];
+        unpack8(__builtin_nontemporal_load((const u32x4*)(dadd + off)), a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += a[j];
+      }
+      __builtin_nontemporal_store(pack8(o), (u32x4*)(dx + off));
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    float* pp = partial + (int64_t)blockIdx.x * cols + col0 + (c * 64 + lane) * 8;
+    *(f32x4*)pp = f32x4{dw[c][0], dw[c][1], dw[c][2], dw[c][3]};
+    *((f32x4*)pp + 1) = f32x4{dw[c][4], dw[c][5], dw[c][6], dw[c][7]};
+  }
+}
+
+// RMSNorm backward form for bf16 rows of 2048-multiple width up to 8192: 1 =
+// one row per workgroup (rms_bwd_row_kernel, the default), 0 = one row per
+// wave with a second read (norm_bwd_kernel).  TOA_NORM_BWD_ROW=0|1,
+// toa_norm_set_bwd_row for A/B (-1 = the environment's choice).
+static int g_norm_bwd_row = -1;
+static int norm_bwd_row() {
+  if (g_norm_bwd_row < 0) {
+    const char* e = getenv("TOA_NORM_BWD_ROW");
+    g_norm_bwd_row = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_norm_bwd_row;
+}
+extern "C" int toa_norm_set_bwd_row(int v) {
+  g_norm_bwd_row = v < 0 ? -1 : (v ? 1 : 0);
+  return 0;
+}
+
 extern "C" int toa_norm_bwd_blocks(int rows, int cols) {
   // ~154 VGPRs at <= 4096 columns: 3 workgroups (12 waves) resident per CU on 256 CUs
   int nb = (rows + 3) / 4;
@@ -336,9 +425,25 @@ static int norm_bwd_launch(const void* dy, const void* h, const void* w, const f
   int chv = pick_ch(cols);
   int nb = toa_norm_bwd_blocks(rows, cols);
   size_t lds = (size_t)4 * 512 * sizeof(float) * (RMS ? 1 : 2);
-  TOA_NORM_DISPATCH(chv, hipLaunchKernelGGL((norm_bwd_kernel<T, CH, RMS>), dim3(nb), dim3(256), lds, s,
-                                            (const T*)dy, (const T*)h, (const T*)w, mean, rstd, (const T*)dadd,
-                                            (T*)dx, partial, rows, cols));
+  if (RMS && sizeof(T) == 2 && cols % 2048 == 0 && cols <= 8192 && norm_bwd_row()) {
+    const bf16_t *dy16 = (const bf16_t*)dy, *h16 = (const bf16_t*)h, *w16 = (const bf16_t*)w,
+                 *a16 = (const bf16_t*)dadd;
+    bf16_t* dx16 = (bf16_t*)dx;
+    switch (cols / 2048) {
+      case 1: hipLaunchKernelGGL(rms_bwd_row_kernel<1>, dim3(nb), dim3(256), 0, s, dy16, h16, w16, rstd, a16, dx16,
+                                 partial, rows, cols); break;
+      case 2: hipLaunchKernelGGL(rms_bwd_row_kernel<2>, dim3(nb), dim3(256), 0, s, dy16, h16, w16, rstd, a16, dx16,
+                                 partial, rows, cols); break;
+      case 3: hipLaunchKernelGGL(rms_bwd_row_kernel<3>, dim3(nb), dim3(256), 0, s, dy16, h16, w16, rstd, a16, dx16,
+                                 partial, rows, cols); break;
+      default: hipLaunchKernelGGL(rms_bwd_row_kernel<4>, dim3(nb), dim3(256), 0, s, dy16, h16, w16, rstd, a16,
+                                  dx16, partial, rows, cols); break;
+    }
+  } else {
+    TOA_NORM_DISPATCH(chv, hipLaunchKernelGGL((norm_bwd_kernel<T, CH, RMS>), dim3(nb), dim3(256), lds, s,
+                                              (const T*)dy, (const T*)h, (const T*)w, mean, rstd, (const T*)dadd,
+                                              (T*)dx, partial, rows, cols));
+  }
   dim3 rg((cols + 63) / 64);
   if (dw != nullptr)
     hipLaunchKernelGGL(col_reduce_kernel, rg, dim3(512), 0, s, partial, nb, cols, dw, dw_bf16, accumulate);
