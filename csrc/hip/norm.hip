@@ -307,11 +307,98 @@ static inline int pick_ch(int cols) {
     default: return (int)hipErrorInvalidValue; \
   }
 
+// RMSNorm form for bf16 rows of 2048-multiple width up to 8192: 1 = one row
+// per workgroup (rms_fwd_row_kernel / rms_bwd_row_kernel, the default), 0 =
+// one row per wave (norm_fwd_kernel / norm_bwd_kernel).  TOA_NORM_ROW=0|1,
+// toa_norm_set_row for A/B (-1 = the environment's choice).
+static int g_norm_row = -1;
+static int norm_row_form() {
+  if (g_norm_row < 0) {
+    const char* e = getenv("TOA_NORM_ROW");
+    g_norm_row = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_norm_row;
+}
+extern "C" int toa_norm_set_row(int v) {
+  g_norm_row = v < 0 ? -1 : (v ? 1 : 0);
+  return 0;
+}
+
+// RMSNorm forward (+ residual add), one row per workgroup (bf16, cols a
+// multiple of 2048, at most 8192): each wave a contiguous quarter of the row,
+// the sum of squares across the waves through a double-buffered LDS pair (one
+// barrier per row), the weight loaded once per workgroup, and h rounded to
+// bf16 in registers (the value backward re-reads) instead of re-loaded from
+// the store just made.  Grid-stride over rows.
+template <int CPL>
+__global__ __launch_bounds__(256) void rms_fwd_row_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                          bf16_t* __restrict__ h_out, const bf16_t* __restrict__ w,
+                                                          bf16_t* __restrict__ y, float* __restrict__ rstd_out,
+                                                          int rows, int cols, float eps) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int col0 = wid * (cols >> 2);
+  float wv[CPL][8];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) Vec8<bf16_t>::load(w + col0 + (c * 64 + lane) * 8, wv[c]);
+  const float inv_cols = 1.f / (float)cols;
+  int par = 0;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x, par ^= 1) {
+    const int64_t base = (int64_t)row * cols + col0;
+    float v[CPL][8];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int64_t off = base + (c * 64 + lane) * 8;
+      Vec8<bf16_t>::load(x + off, v[c]);
+      if (res != nullptr) {
+        float r[8];
+        Vec8<bf16_t>::load(res + off, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += r[j];
+        const u32x4 hv = pack8(v[c]);
+        st16(h_out + off, hv);
+        unpack8(hv, v[c]);  // the rounded values: what backward reads back
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s = fmaf(v[c][j], v[c][j], s);
+    }
+    s = wave_sum(s);
+    if (lane == 0) red[par][wid] = s;
+    __syncthreads();
+    const float rstd = rsqrtf((red[par][0] + red[par][1] + red[par][2] + red[par][3]) * inv_cols + eps);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[c][j] * rstd * wv[c][j];
+      Vec8<bf16_t>::store(y + base + (c * 64 + lane) * 8, o);
+    }
+    if (threadIdx.x == 0) rstd_out[row] = rstd;
+  }
+}
+
 template <typename T, bool RMS>
 static int norm_fwd_launch(const void* x, const void* res, void* h_out, const void* w, const void* b, void* y,
                            float* mean, float* rstd, int rows, int cols, float eps, hipStream_t s) {
   if (cols % 8 != 0) return (int)hipErrorInvalidValue;
   int chv = pick_ch(cols);
+  if (RMS && sizeof(T) == 2 && cols % 2048 == 0 && cols <= 8192 && norm_row_form()) {
+    const int nb = rows < 256 * 8 ? rows : 256 * 8;  // 8 workgroups per CU, grid-stride over rows
+    const bf16_t *x16 = (const bf16_t*)x, *r16 = (const bf16_t*)res, *w16 = (const bf16_t*)w;
+    bf16_t *h16 = (bf16_t*)h_out, *y16 = (bf16_t*)y;
+    switch (cols / 2048) {
+      case 1: hipLaunchKernelGGL(rms_fwd_row_kernel<1>, dim3(nb), dim3(256), 0, s, x16, r16, h16, w16, y16, rstd, rows,
+                                 cols, eps); break;
+      case 2: hipLaunchKernelGGL(rms_fwd_row_kernel<2>, dim3(nb), dim3(256), 0, s, x16, r16, h16, w16, y16, rstd, rows,
+                                 cols, eps); break;
+      case 3: hipLaunchKernelGGL(rms_fwd_row_kernel<3>, dim3(nb), dim3(256), 0, s, x16, r16, h16, w16, y16, rstd, rows,
+                                 cols, eps); break;
+      default: hipLaunchKernelGGL(rms_fwd_row_kernel<4>, dim3(nb), dim3(256), 0, s, x16, r16, h16, w16, y16, rstd,
+                                  rows, cols, eps); break;
+    }
+    return (int)hipGetLastError();
+  }
   dim3 grid((rows + 3) / 4), block(256);
   TOA_NORM_DISPATCH(chv, hipLaunchKernelGGL((norm_fwd_kernel<T, CH, RMS>), grid, block, 0, s, (const T*)x,
                                             (const T*)res, (T*)h_out, (const T*)w, (const T*)b, (T*)y, mean, rstd,
@@ -319,8 +406,6 @@ static int norm_fwd_launch(const void* x, const void* res, void* h_out, const vo
   return (int)hipGetLastError();
 }
 
-// number of workgroups the backward uses (=> partial rows); caller sizes the
-// partial workspace as nb * cols * (RMS ? 1 : 2) floats.
 // RMSNorm backward, one row per workgroup (bf16, cols a multiple of 2048, at
 // most 8192): the row's 4 waves each own a contiguous quarter of the columns
 // (CPL 16-byte chunks per lane), so h and dy stay in registers between the
@@ -393,23 +478,8 @@ __global__ __launch_bounds__(256) void rms_bwd_row_kernel(const bf16_t* __restri
   }
 }
 
-// RMSNorm backward form for bf16 rows of 2048-multiple width up to 8192: 1 =
-// one row per workgroup (rms_bwd_row_kernel, the default), 0 = one row per
-// wave with a second read (norm_bwd_kernel).  TOA_NORM_BWD_ROW=0|1,
-// toa_norm_set_bwd_row for A/B (-1 = the environment's choice).
-static int g_norm_bwd_row = -1;
-static int norm_bwd_row() {
-  if (g_norm_bwd_row < 0) {
-    const char* e = getenv("TOA_NORM_BWD_ROW");
-    g_norm_bwd_row = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_norm_bwd_row;
-}
-extern "C" int toa_norm_set_bwd_row(int v) {
-  g_norm_bwd_row = v < 0 ? -1 : (v ? 1 : 0);
-  return 0;
-}
-
+// number of workgroups the backward uses (=> partial rows); caller sizes the
+// partial workspace as nb * cols * (RMS ? 1 : 2) floats.
 extern "C" int toa_norm_bwd_blocks(int rows, int cols) {
   // ~154 VGPRs at <= 4096 columns: 3 workgroups (12 waves) resident per CU on 256 CUs
   int nb = (rows + 3) / 4;
@@ -425,7 +495,7 @@ static int norm_bwd_launch(const void* dy, const void* h, const void* w, const f
   int chv = pick_ch(cols);
   int nb = toa_norm_bwd_blocks(rows, cols);
   size_t lds = (size_t)4 * 512 * sizeof(float) * (RMS ? 1 : 2);
-  if (RMS && sizeof(T) == 2 && cols % 2048 == 0 && cols <= 8192 && norm_bwd_row()) {
+  if (RMS && sizeof(T) == 2 && cols % 2048 == 0 && cols <= 8192 && norm_row_form()) {
     const bf16_t *dy16 = (const bf16_t*)dy, *h16 = (const bf16_t*)h, *w16 = (const bf16_t*)w,
                  *a16 = (const bf16_t*)dadd;
     bf16_t* dx16 = (bf16_t*)dx;

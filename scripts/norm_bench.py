@@ -7,7 +7,7 @@ reduce).
 
 --libs: single-source builds of norm.hip (scripts/ab/build_variants.py) timed
 interleaved in one process; default: the in-tree libtoa_hip.so, with the
-backward's two forms interleaved (toa_norm_set_bwd_row: "row" = one row per
+backward's two forms interleaved (toa_norm_set_row: "row" = one row per
 workgroup, the default; "wave" = one row per wave with a second read).
 """
 from __future__ import annotations
@@ -50,8 +50,8 @@ def main():
         for n in ("toa_rmsnorm_fwd", "toa_rmsnorm_bwd", "toa_norm_bwd_blocks"):
             getattr(L, n).argtypes = _lib._SIGS[n]
             getattr(L, n).restype = ctypes.c_int
-        if not a.libs and hasattr(L, "toa_norm_set_bwd_row"):
-            L.toa_norm_set_bwd_row.argtypes = [ctypes.c_int]
+        if not a.libs and hasattr(L, "toa_norm_set_row"):
+            L.toa_norm_set_row.argtypes = [ctypes.c_int]
             libs["row"] = (L, 1)
             libs["wave"] = (L, 0)
         else:
@@ -60,7 +60,7 @@ def main():
     for rnd in range(3):
         for name, (L, form) in libs.items():
             if form is not None:
-                L.toa_norm_set_bwd_row(form)
+                L.toa_norm_set_row(form)
             r = run(a, L)
             results.setdefault(name, []).append(r)
             print(json.dumps({"lib": name, "round": rnd, **r}), flush=True)

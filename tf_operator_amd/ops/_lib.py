@@ -87,7 +87,7 @@ _SIGS = {
     "toa_attn_set_bwd_variant": [c_int],
     "toa_attn_set_kb_order": [c_int],
     "toa_attn_set_rope_prefetch": [c_int],
-    "toa_norm_set_bwd_row": [c_int],
+    "toa_norm_set_row": [c_int],
     "toa_attn_set_fwd_variant": [c_int],
     "toa_attn_bwd_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
                           c_int, c_f, c_p],
