@@ -56,6 +56,38 @@ def test_rmsnorm_fwd_bwd(cols, res):
     assert rel(w.grad, wr.grad) < 2e-2
 
 
+@pytest.mark.parametrize("cols", [2048, 4096, 6144, 8192])
+def test_rmsnorm_row_and_wave_forms_agree(cols):
+    """The one-row-per-workgroup RMSNorm kernels (default for bf16 rows of
+    2048-8192 columns) against the one-row-per-wave ones
+    (toa_norm_set_row(0)): same h and y (bit for bit: same per-element
+    arithmetic), dx and dW to summation-order rounding."""
+    L = _lib()
+    from tf_operator_amd.ops.norm import add_rms_norm
+
+    torch.manual_seed(cols)
+    rows = 301
+    x = torch.randn(rows, cols, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(rows, cols, device=DEV, dtype=torch.bfloat16)
+    w0 = (1 + 0.1 * torch.randn(cols, device=DEV)).to(torch.bfloat16)
+    dy, dh = torch.randn_like(x), torch.randn_like(x)
+    outs = []
+    try:
+        for form in (1, 0):
+            L.call("toa_norm_set_row", form)
+            a, b = x.clone().requires_grad_(), r.clone().requires_grad_()
+            w = w0.clone().requires_grad_()
+            h, y = add_rms_norm(a, b, w, 1e-5)
+            torch.autograd.backward([h, y], [dh, dy])
+            outs.append((h.detach(), y.detach(), a.grad, w.grad))
+        torch.cuda.synchronize()
+    finally:
+        L.call("toa_norm_set_row", -1)
+    (h1, y1, dx1, dw1), (h0, y0, dx0, dw0) = outs
+    assert torch.equal(h1, h0)
+    assert rel(y1, y0) < 1e-2 and rel(dx1, dx0) < 1e-2 and rel(dw1, dw0) < 1e-3
+
+
 @pytest.mark.parametrize("cols", [4096, 512, 1000, 8192])
 def test_layernorm_fwd_bwd(cols):
     _lib()
