@@ -1,0 +1,486 @@
+"""Functional emulator for the gfx950 instruction subset the assembly
+generators in this directory emit (csrc/asm/gemm_gen.py).
+
+It runs ONE workgroup of a generated kernel on the CPU: 4 wave64s in
+lockstep between barriers, scalar/vector register files, the 160 KiB LDS,
+buffer resources over numpy "global memory", LDS-DMA, ds_read_b128 and
+v_mfma_f32_16x16x32_bf16 with the CDNA4 fragment layout.  Memory operations
+complete immediately, so it checks ADDRESSING and data flow (every byte that
+lands in LDS, every fragment a lane reads, every output element) -- not the
+timing of waits, which the schedule's vmcnt / barrier placement is reasoned
+about in the generator's docstring.  Any buffer access outside its
+resource's num_records raises, so a bounds bug fails the CPU test instead of
+being silently zero-filled on the GPU.
+
+Used by tests/test_asm_gemm.py; no GPU, no assembler needed.
+"""
+from __future__ import annotations
+
+import re
+import struct
+
+import numpy as np
+
+M32 = 0xFFFFFFFF
+
+
+def f2u(x):
+    return np.asarray(x, dtype=np.float32).view(np.uint32)
+
+
+def u2f(x):
+    return np.asarray(x, dtype=np.uint32).view(np.float32)
+
+
+def bf16_rne(f32: np.ndarray) -> np.ndarray:
+    """fp32 -> bf16 bits (uint32 holding 16 bits), round to nearest even."""
+    u = f2u(f32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) & 0xFFFF
+    return r.astype(np.uint32)
+
+
+class Memory:
+    """Flat 64-bit address space made of named numpy byte buffers."""
+
+    def __init__(self):
+        self.bufs: list[tuple[int, np.ndarray]] = []
+        self.next = 1 << 32
+
+    def add(self, arr: np.ndarray) -> int:
+        b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        base = self.next
+        self.bufs.append((base, b))
+        self.next += ((b.size + (1 << 20)) >> 20 << 20) + (1 << 20)
+        return base
+
+    def add_at(self, base: int, arr: np.ndarray) -> int:
+        """Map `arr` at a given address (mirror a real device pointer)."""
+        b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        self.bufs.append((int(base), b))
+        return int(base)
+
+    def locate(self, addr: np.ndarray, nbytes: int):
+        for base, b in self.bufs:
+            if base <= int(addr.min()) and int(addr.max()) + nbytes <= base + b.size:
+                return base, b
+        raise IndexError(f"address range {hex(int(addr.min()))}..{hex(int(addr.max()))} outside every buffer")
+
+
+_REG = re.compile(r"^([vsa])(?:\[(\d+):(\d+)\]|(\d+))$")
+
+
+class Wave:
+    def __init__(self, wid: int, nvgpr=512):
+        self.s = np.zeros(110, dtype=np.uint64)      # held as u64, masked to 32
+        self.v = np.zeros((nvgpr, 64), dtype=np.uint32)   # v0..255, a0..255 at 256..
+        self.scc = 0
+        self.m0 = 0
+        self.vcc = 0
+        self.pc = 0
+        self.done = False
+        self.wid = wid
+
+
+class Emu:
+    def __init__(self, asm_text: str, kernel: str):
+        self.prog, self.labels = self._parse(asm_text, kernel)
+
+    # ------------------------------------------------------------ parsing
+    @staticmethod
+    def _parse(text: str, kernel: str):
+        lines = text.splitlines()
+        start = lines.index(f"{kernel}:")
+        prog, labels = [], {}
+        for ln in lines[start + 1:]:
+            t = ln.split(";")[0].strip()
+            if not t:
+                continue
+            if t.startswith(".size"):
+                break
+            if t.endswith(":"):
+                labels[t[:-1]] = len(prog)
+                continue
+            if t.startswith("."):
+                continue
+            op, _, rest = t.partition(" ")
+            args = [x.strip() for x in rest.split(",")] if rest else []
+            # trailing modifiers ("offen lds", "offset:32") live in the last arg
+            mods = []
+            if args:
+                parts = args[-1].split()
+                args[-1] = parts[0]
+                mods = parts[1:]
+            prog.append((op, args, mods))
+        return prog, labels
+
+    # ------------------------------------------------------------ operands
+    def _reg(self, w: Wave, tok: str):
+        m = _REG.match(tok)
+        if not m:
+            return None
+        kind = m.group(1)
+        lo = int(m.group(2) if m.group(2) is not None else m.group(4))
+        hi = int(m.group(3)) if m.group(3) is not None else lo
+        return kind, lo, hi
+
+    def sget(self, w: Wave, tok: str) -> int:
+        if tok == "m0":
+            return w.m0
+        r = self._reg(w, tok)
+        if r is not None:
+            assert r[0] == "s" and r[1] == r[2], tok
+            return int(w.s[r[1]]) & M32
+        return self._lit(tok)
+
+    @staticmethod
+    def _lit(tok: str) -> int:
+        if re.match(r"^-?\d+\.\d*(e-?\d+)?$", tok):
+            return int(f2u(np.float32(float(tok))))
+        v = int(tok, 0)
+        return v & M32
+
+    def sset(self, w: Wave, tok: str, val: int):
+        if tok == "m0":
+            w.m0 = val & M32
+            return
+        r = self._reg(w, tok)
+        assert r and r[0] == "s" and r[1] == r[2], tok
+        w.s[r[1]] = val & M32
+
+    def vget(self, w: Wave, tok: str) -> np.ndarray:
+        r = self._reg(w, tok)
+        if r is None:
+            return np.full(64, self.sget(w, tok), dtype=np.uint32) if not tok.startswith(("v", "a")) else None
+        kind, lo, hi = r
+        if kind == "s":
+            return np.full(64, int(w.s[lo]) & M32, dtype=np.uint32)
+        base = 256 if kind == "a" else 0
+        assert lo == hi, tok
+        return w.v[base + lo].copy()
+
+    def vrange(self, w: Wave, tok: str):
+        kind, lo, hi = self._reg(w, tok)
+        base = 256 if kind == "a" else 0
+        return base + lo, base + hi + 1
+
+    def vset(self, w: Wave, tok: str, val):
+        lo, hi = self.vrange(w, tok)
+        assert hi == lo + 1, tok
+        w.v[lo] = np.asarray(val).astype(np.uint32) & M32
+
+    # ------------------------------------------------------------ run
+    def run(self, kernarg: bytes, wg_id: int, mem: Memory, nthreads=256, lds_bytes=160 * 1024):
+        self.mem = mem
+        self.lds = np.zeros(lds_bytes, dtype=np.uint8)
+        self.kernarg = kernarg
+        waves = [Wave(i) for i in range(nthreads // 64)]
+        for w in waves:
+            w.s[2] = wg_id
+            w.v[0] = np.arange(64, dtype=np.uint32) + 64 * w.wid
+        steps = 0
+        while not all(w.done for w in waves):
+            for w in waves:           # each wave to its next barrier (or the end)
+                while not w.done:
+                    steps += 1
+                    if steps > 50_000_000:
+                        raise RuntimeError("emulator step limit")
+                    if self.step(w) == "barrier":
+                        break
+        return steps
+
+    def step(self, w: Wave):
+        op, args, mods = self.prog[w.pc]
+        w.pc += 1
+        h = getattr(self, "op_" + op, None)
+        if h is None:
+            raise NotImplementedError(op)
+        return h(w, args, mods)
+
+    # ------------------------------------------------------------ SALU
+    def op_s_load_dwordx16(self, w, a, m):
+        self._sload(w, a, 16)
+
+    def op_s_load_dwordx4(self, w, a, m):
+        self._sload(w, a, 4)
+
+    def _sload(self, w, a, n):
+        kind, lo, hi = self._reg(w, a[0])
+        off = self._lit(a[2])
+        vals = struct.unpack_from(f"<{n}I", self.kernarg, off)
+        for i, x in enumerate(vals):
+            w.s[lo + i] = x
+
+    def op_s_mov_b32(self, w, a, m):
+        self.sset(w, a[0], self.sget(w, a[1]))
+
+    def op_s_add_u32(self, w, a, m):
+        r = self.sget(w, a[1]) + self.sget(w, a[2])
+        w.scc = int(r > M32)
+        self.sset(w, a[0], r)
+
+    def op_s_addc_u32(self, w, a, m):
+        r = self.sget(w, a[1]) + self.sget(w, a[2]) + w.scc
+        w.scc = int(r > M32)
+        self.sset(w, a[0], r)
+
+    def op_s_sub_u32(self, w, a, m):
+        x, y = self.sget(w, a[1]), self.sget(w, a[2])
+        w.scc = int(y > x)
+        self.sset(w, a[0], x - y)
+
+    def op_s_sub_i32(self, w, a, m):
+        self.sset(w, a[0], self.sget(w, a[1]) - self.sget(w, a[2]))
+
+    def op_s_mul_i32(self, w, a, m):
+        self.sset(w, a[0], self.sget(w, a[1]) * self.sget(w, a[2]))
+
+    def op_s_mul_hi_u32(self, w, a, m):
+        self.sset(w, a[0], (self.sget(w, a[1]) * self.sget(w, a[2])) >> 32)
+
+    def op_s_lshl_b32(self, w, a, m):
+        r = (self.sget(w, a[1]) << (self.sget(w, a[2]) & 31)) & M32
+        w.scc = int(r != 0)
+        self.sset(w, a[0], r)
+
+    def op_s_lshr_b32(self, w, a, m):
+        r = self.sget(w, a[1]) >> (self.sget(w, a[2]) & 31)
+        w.scc = int(r != 0)
+        self.sset(w, a[0], r)
+
+    def op_s_and_b32(self, w, a, m):
+        r = self.sget(w, a[1]) & self.sget(w, a[2])
+        w.scc = int(r != 0)
+        self.sset(w, a[0], r)
+
+    def op_s_xor_b32(self, w, a, m):
+        r = self.sget(w, a[1]) ^ self.sget(w, a[2])
+        w.scc = int(r != 0)
+        self.sset(w, a[0], r)
+
+    def op_s_min_u32(self, w, a, m):
+        x, y = self.sget(w, a[1]), self.sget(w, a[2])
+        w.scc = int(x < y)
+        self.sset(w, a[0], min(x, y))
+
+    @staticmethod
+    def _i32(x):
+        return x - (1 << 32) if x & 0x80000000 else x
+
+    def op_s_cmp_eq_u32(self, w, a, m):
+        w.scc = int(self.sget(w, a[0]) == self.sget(w, a[1]))
+
+    def op_s_cmp_lg_u32(self, w, a, m):
+        w.scc = int(self.sget(w, a[0]) != self.sget(w, a[1]))
+
+    def op_s_cmp_gt_u32(self, w, a, m):
+        w.scc = int(self.sget(w, a[0]) > self.sget(w, a[1]))
+
+    def op_s_cmp_lt_u32(self, w, a, m):
+        w.scc = int(self.sget(w, a[0]) < self.sget(w, a[1]))
+
+    def op_s_cmp_ge_u32(self, w, a, m):
+        w.scc = int(self.sget(w, a[0]) >= self.sget(w, a[1]))
+
+    def op_s_cmp_lt_i32(self, w, a, m):
+        w.scc = int(self._i32(self.sget(w, a[0])) < self._i32(self.sget(w, a[1])))
+
+    def op_s_cselect_b32(self, w, a, m):
+        self.sset(w, a[0], self.sget(w, a[1]) if w.scc else self.sget(w, a[2]))
+
+    def op_s_cbranch_scc0(self, w, a, m):
+        if not w.scc:
+            w.pc = self.labels[a[0]]
+
+    def op_s_cbranch_scc1(self, w, a, m):
+        if w.scc:
+            w.pc = self.labels[a[0]]
+
+    def op_s_branch(self, w, a, m):
+        w.pc = self.labels[a[0]]
+
+    def op_s_waitcnt(self, w, a, m):
+        pass
+
+    def op_s_nop(self, w, a, m):
+        pass
+
+    def op_s_setprio(self, w, a, m):
+        pass
+
+    def op_s_barrier(self, w, a, m):
+        return "barrier"
+
+    def op_s_endpgm(self, w, a, m):
+        w.done = True
+        return "barrier"
+
+    # ------------------------------------------------------------ VALU
+    def _vbin(self, w, a, fn):
+        self.vset(w, a[0], fn(self.vget(w, a[1]), self.vget(w, a[2])))
+
+    def op_v_mov_b32(self, w, a, m):
+        self.vset(w, a[0], self.vget(w, a[1]))
+
+    def op_v_cvt_f32_u32(self, w, a, m):
+        self.vset(w, a[0], f2u(self.vget(w, a[1]).astype(np.float32)))
+
+    def op_v_cvt_u32_f32(self, w, a, m):
+        f = u2f(self.vget(w, a[1]))
+        self.vset(w, a[0], np.clip(np.trunc(f), 0, M32).astype(np.uint64).astype(np.uint32))
+
+    def op_v_rcp_iflag_f32(self, w, a, m):
+        self.vset(w, a[0], f2u(np.float32(1.0) / u2f(self.vget(w, a[1]))))
+
+    op_v_rcp_f32 = op_v_rcp_iflag_f32
+
+    def op_v_mul_f32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: f2u(u2f(x) * u2f(y)))
+
+    def op_v_add_f32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: f2u(u2f(x) + u2f(y)))
+
+    def op_v_sub_f32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: f2u(u2f(x) - u2f(y)))
+
+    def op_v_fma_f32(self, w, a, m):
+        x, y, z = (u2f(self.vget(w, t)).astype(np.float64) for t in a[1:4])
+        self.vset(w, a[0], f2u((x * y + z).astype(np.float32)))
+
+    def op_v_exp_f32(self, w, a, m):
+        self.vset(w, a[0], f2u(np.exp2(u2f(self.vget(w, a[1]))).astype(np.float32)))
+
+    def op_v_readfirstlane_b32(self, w, a, m):
+        self.sset(w, a[0], int(self.vget(w, a[1])[0]))
+
+    def op_v_lshrrev_b32(self, w, a, m):
+        self._vbin(w, a, lambda s, x: x >> (s & 31))
+
+    def op_v_lshlrev_b32(self, w, a, m):
+        self._vbin(w, a, lambda s, x: (x.astype(np.uint64) << (s & 31)).astype(np.uint64) & M32)
+
+    def op_v_and_b32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: x & y)
+
+    def op_v_xor_b32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: x ^ y)
+
+    def op_v_add_u32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: (x.astype(np.uint64) + y) & M32)
+
+    def op_v_mul_lo_u32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: (x.astype(np.uint64) * y) & M32)
+
+    def op_v_mul_u32_u24(self, w, a, m):
+        self._vbin(w, a, lambda x, y: ((x & 0xFFFFFF).astype(np.uint64) * (y & 0xFFFFFF)) & M32)
+
+    def op_v_lshl_add_u32(self, w, a, m):
+        x, s, y = (self.vget(w, t) for t in a[1:4])
+        self.vset(w, a[0], ((x.astype(np.uint64) << (s & 31)) + y) & M32)
+
+    def op_v_accvgpr_write_b32(self, w, a, m):
+        self.vset(w, a[0], self.vget(w, a[1]))
+
+    def op_v_accvgpr_read_b32(self, w, a, m):
+        self.vset(w, a[0], self.vget(w, a[1]))
+
+    def op_v_cvt_pk_bf16_f32(self, w, a, m):
+        lo = bf16_rne(u2f(self.vget(w, a[1])))
+        hi = bf16_rne(u2f(self.vget(w, a[2])))
+        self.vset(w, a[0], lo | (hi << 16))
+
+    def op_v_mfma_f32_16x16x32_bf16(self, w, a, m):
+        d0, d1 = self.vrange(w, a[0])
+        a0, a1 = self.vrange(w, a[1])
+        b0, b1 = self.vrange(w, a[2])
+        c0, c1 = self.vrange(w, a[3])
+        assert d1 - d0 == 4 and a1 - a0 == 4 and b1 - b0 == 4 and c1 - c0 == 4
+
+        def elems(r0):  # [64 lanes, 8] bf16 -> f32
+            regs = w.v[r0:r0 + 4].T  # [64, 4] u32
+            lo = (regs & 0xFFFF) << 16
+            hi = regs & 0xFFFF0000
+            out = np.empty((64, 8), dtype=np.uint32)
+            out[:, 0::2] = lo
+            out[:, 1::2] = hi
+            return u2f(out)
+
+        ea, eb = elems(a0), elems(b0)
+        A = np.zeros((16, 32), np.float32)
+        B = np.zeros((32, 16), np.float32)
+        for l in range(64):
+            A[l & 15, 8 * (l >> 4): 8 * (l >> 4) + 8] = ea[l]
+            B[8 * (l >> 4): 8 * (l >> 4) + 8, l & 15] = eb[l]
+        D = A.astype(np.float64) @ B.astype(np.float64)
+        C = u2f(w.v[c0:c0 + 4]).astype(np.float64)     # [4, 64]
+        out = np.empty((4, 64), np.float64)
+        for l in range(64):
+            for r in range(4):
+                out[r, l] = C[r, l] + D[(l >> 4) * 4 + r, l & 15]
+        w.v[d0:d0 + 4] = f2u(out.astype(np.float32))
+
+    # ------------------------------------------------------------ memory
+    def _buffer_addr(self, w, a, mods, nbytes):
+        voff = self.vget(w, a[0]).astype(np.uint64)
+        kind, lo, hi = self._reg(w, a[1])
+        srd = [int(w.s[lo + i]) & M32 for i in range(4)]
+        base = srd[0] | ((srd[1] & 0xFFFF) << 32)
+        nrec = srd[2]
+        soff = self.sget(w, a[2])
+        ioff = 0
+        for md in mods:
+            if md.startswith("offset:"):
+                ioff = int(md.split(":")[1])
+        off = voff + soff + ioff
+        if int(off.max()) + nbytes > nrec:
+            raise IndexError(f"buffer access past num_records ({int(off.max())} + {nbytes} > {nrec})")
+        return base + off
+
+    def _gread(self, addr, nbytes):
+        base, buf = self.mem.locate(addr, nbytes)
+        rel = (addr - base).astype(np.int64)
+        return np.stack([buf[rel + i] for i in range(nbytes)], axis=1)  # [64, nbytes]
+
+    def _gwrite(self, addr, data):
+        nbytes = data.shape[1]
+        base, buf = self.mem.locate(addr, nbytes)
+        rel = (addr - base).astype(np.int64)
+        for i in range(nbytes):
+            buf[rel + i] = data[:, i]
+
+    def op_buffer_load_dwordx4(self, w, a, mods):
+        assert "lds" in mods and "offen" in mods, "only the LDS-DMA form is emulated"
+        addr = self._buffer_addr(w, a, mods, 16)
+        data = self._gread(addr, 16)
+        dst = w.m0 + 16 * np.arange(64)
+        if dst.max() + 16 > self.lds.size:
+            raise IndexError("LDS-DMA past the LDS")
+        for l in range(64):
+            self.lds[dst[l]:dst[l] + 16] = data[l]
+
+    def op_buffer_load_dwordx2(self, w, a, mods):
+        addr = self._buffer_addr(w, a[1:], mods, 8)
+        data = self._gread(addr, 8).view(np.uint32).reshape(64, 2)
+        lo, hi = self.vrange(w, a[0])
+        w.v[lo:hi] = data.T
+
+    def op_buffer_store_dword(self, w, a, mods):
+        addr = self._buffer_addr(w, a[1:], mods, 4)
+        lo, hi = self.vrange(w, a[0])
+        self._gwrite(addr, np.ascontiguousarray(w.v[lo]).view(np.uint8).reshape(64, 4))
+
+    def op_buffer_store_dwordx2(self, w, a, mods):
+        addr = self._buffer_addr(w, a[1:], mods, 8)
+        lo, hi = self.vrange(w, a[0])
+        data = np.ascontiguousarray(w.v[lo:hi].T).view(np.uint8).reshape(64, 8)
+        self._gwrite(addr, data)
+
+    def op_ds_read_b128(self, w, a, mods):
+        addr = self.vget(w, a[1]).astype(np.int64)
+        for md in mods:
+            if md.startswith("offset:"):
+                addr = addr + int(md.split(":")[1])
+        if addr.max() + 16 > self.lds.size:
+            raise IndexError("ds_read past the LDS")
+        lo, hi = self.vrange(w, a[0])
+        data = np.stack([self.lds[x:x + 16] for x in addr]).view(np.uint32).reshape(64, 4)
+        w.v[lo:hi] = data.T

@@ -1,0 +1,841 @@
+#!/usr/bin/env python3
+"""Generator of the hand-written gfx950 (CDNA4) assembly GEMM kernels.
+
+    python csrc/asm/gemm_gen.py OUT.s
+
+Emits one code object source with the forward / data-gradient GEMM of the
+training step in the "TN" form (both operands contiguous along the
+reduction), written instruction by instruction rather than through hipcc:
+
+    C[m][n] = sum_k X[m][k] * W[n][k]      bf16 in, fp32 accumulate
+
+Why assembly: the one-wave-per-SIMD schedule that gives the lowest energy
+per MFMA (128 x 128 of C per wave, a third fewer LDS bytes per MFMA than
+128 x 64) needs its latency hidden by software pipelining -- fragment reads
+for the next k-step issued between the current k-step's MFMAs, the global
+prefetch two tiles ahead, accumulators that never leave the AGPRs.  hipcc
+did not hold that schedule (round 3: `gemm_tn4w_kernel` shuttled
+accumulators and waited `vmcnt(0)`, 0.96-1.02 PF/s; docs/kernels.md).
+
+Structure (every number below is what the generator emits):
+
+  workgroup   256 threads = 4 waves (one per SIMD), tile 256 x 256, BK = 64
+  wave        (wm, wn) = (wave & 1, wave >> 1): 128 rows of X x 128 rows of W
+              = 8 x 8 tiles of v_mfma_f32_16x16x32_bf16, 256 AGPR accumulators
+  LDS         two stages of 65 KiB (X half, W half).  A half is 32 "lines" of
+              1040 B (1024 B of data + 16 B pad): line i of the wave-row block
+              holds tile rows i, i+16, ..., i+112 (128 B = 64 k each), so the
+              16 lanes of a fragment read (rows 16f + lane&15) fall on 16
+              distinct 16-B bank slots (1040 B = 260 dwords = 4 banks apart)
+  staging     LDS-DMA (`buffer_load_dwordx4 ... lds`): one instruction per
+              wave fills one line = 8 rows x 128 B (8 whole cache lines), the
+              swizzle-free image needs no source permutation.  16 DMA
+              instructions per wave per 64-k tile, bounded by the buffer
+              resource (num_records): an address past the tensor reads 0
+  pipeline    tile t+2 is staged into the stage tile t just vacated (two
+              stages, prefetch distance two), k-step halves of 32:
+                phase 1: 64 MFMAs on sub-step 0 fragments; between them the
+                         sub-step 1 fragment reads of the same stage, then a
+                         barrier per operand half after which that half's
+                         DMA for tile t+2 starts
+                phase 2: 64 MFMAs on sub-step 1; the rest of the DMA, one
+                         counted vmcnt (tile t+1 landed) + barrier, then the
+                         next tile's sub-step 0 fragment reads
+              three barriers per 64-k tile, vmcnt never 0 inside the loop
+  epilogue    accumulators -> bf16 (v_cvt_pk_bf16_f32) -> buffer stores, each
+              lane 4 consecutive columns of one row (the W fragment is the
+              MFMA's A operand); fused variants:
+                plain        C
+                swiglu_fwd   gate|up projection: the workgroup's 256 W rows are
+                             128 gate rows and the SAME 128 up rows (W keeps
+                             its [gate; up] layout); writes gu and
+                             s = silu(gate) * up
+                swiglu_bwd   down-projection data gradient: ds is never stored;
+                             reads gu, writes dgu = [ds*up*silu'(g) | ds*silu(g)]
+  grid        one workgroup per tile, XCD-aware: the 8 XCDs get contiguous
+              ranges of the tile order, which walks groups of 8 row tiles
+              across the column tiles (a group's X strips + the current W
+              strip stay in the XCD's L2)
+
+Reference anchor: SURVEY.md K1/K2/K19 and section 7.1 item 5 (MFMA tiles with
+fused epilogues); the reference itself has no kernels
+(/root/reference/examples/v1/dist-mnist/dist_mnist.py:188-189 is the GEMM +
+bias + activation these generalise).  This file is not derived from any
+library source: the schedule class (4 waves x 128 x 128, prefetch distance
+two) is the one docs/kernels.md and profiles/r3_tn_pmc measured as the
+energy-efficient form on MI355X.
+"""
+from __future__ import annotations
+
+import sys
+
+LINE = 1040              # one LDS line: 8 tile rows x 128 B + 16 B pad
+HALF = 32 * LINE         # 256 rows of one operand = 33280 B
+STAGE = 2 * HALF         # X half + W half = 66560 B
+LDS_BYTES = 2 * STAGE    # 133120 B
+KARG_BYTES = 80
+
+# kernarg layout (byte offsets; mirrored by csrc/hip/gemm_asm.hip)
+KARG = {
+    "X": 0, "W": 8, "C": 16, "S": 24,
+    "ldx": 32, "ldw": 36, "ldc": 40, "lds": 44,
+    "ktiles": 48, "tiles_m": 52, "tiles_n": 56, "xq": 60, "xr": 64,
+    "per_group": 68, "fw": 72, "fc": 76,
+}
+
+EPIS = ("plain", "swiglu_fwd", "swiglu_bwd")
+
+# ---------------------------------------------------------------- registers
+# SGPRs: s[0:1] kernarg pointer, s2 workgroup id (the descriptor's order)
+S_ARGS = 4          # s[4:23]: the 80 B of kernarg
+S_X, S_W, S_C, S_S = 4, 6, 8, 10
+S_LDX, S_LDW, S_LDC, S_LDS = 12, 13, 14, 15
+S_KT, S_TM_N, S_TN_N, S_XQ = 16, 17, 18, 19
+S_XR, S_PG, S_FW, S_FC = 20, 21, 22, 23
+S_TILE, S_TM, S_TN = 24, 25, 26
+S_T0, S_T1, S_T2, S_T3 = 27, 28, 29, 30
+SRD_X, SRD_W, SRD_C, SRD_S = 32, 36, 40, 44
+S_M0X, S_M0XT, S_M0W, S_M0WT = 48, 49, 50, 51
+S_LOOP = 52
+S_SOX = 53          # s53..s59: X DMA row offsets, instructions 1..7
+S_SOW = 60          # s60..s66: W DMA row offsets
+S_E0, S_E1 = 67, 68  # epilogue scratch
+S_Q, S_R = 69, 70   # division results
+N_SGPR = 72
+
+# VGPRs
+V_TID = 132
+V_DX, V_DW = 1, 133        # DMA lane offsets (bytes)
+V_RX, V_RW = 2, 3          # LDS fragment-read bases
+V_RXT, V_RWT = 134, 135    # stage toggles (xor masks)
+V_FX0, V_FX1 = 4, 36       # X fragments, sub-steps 0 / 1 (8 x 4 VGPRs each)
+V_FW0, V_FW1 = 68, 100     # W fragments
+V_T = 136                  # 136..139 scratch
+V_E = 140                  # 140..255 epilogue scratch
+
+UNIT_GATE_ROWS = 64        # swiglu_fwd: W rows per wave column per half
+
+
+class Asm:
+    def __init__(self, prefix: str = ""):
+        self.out: list[str] = []
+        self.nlab = 0
+        self.prefix = prefix
+        self.abort = f"L_{prefix}abort"
+        self.stage_exit = f"L_{prefix}stage_exit"
+
+    def __call__(self, s: str):
+        self.out.append("  " + s)
+
+    def label(self, name: str):
+        self.out.append(name + ":")
+
+    def fresh(self, stem: str) -> str:
+        self.nlab += 1
+        return f"L_{self.prefix}{stem}_{self.nlab}"
+
+    def raw(self, s: str):
+        self.out.append(s)
+
+
+def vr(base: int, n: int = 1) -> str:
+    return f"v{base}" if n == 1 else f"v[{base}:{base + n - 1}]"
+
+
+def sr(base: int, n: int = 1) -> str:
+    return f"s{base}" if n == 1 else f"s[{base}:{base + n - 1}]"
+
+
+def ar(base: int, n: int = 1) -> str:
+    return f"a{base}" if n == 1 else f"a[{base}:{base + n - 1}]"
+
+
+# ---------------------------------------------------------------- helpers
+def udiv(a: Asm, q: int, r: int, num: int, den: int):
+    """s_q = s_num / s_den, s_r = s_num % s_den (unsigned, both < 2^24):
+    float reciprocal estimate on the VALU, then one exact correction step
+    each way on the SALU."""
+    # Explicit wait states (hipcc inserts these; hand-written code must):
+    # a transcendental's result forwarded to the next VALU, and a VALU
+    # result read by v_readfirstlane, both need padding on gfx950 -- without
+    # the second, v_readfirstlane returned the PRE-conversion float bits
+    # (measured: tile coordinate 0x3fc00000 = 1.5 for 3 / 2; the probe kernel).
+    a(f"v_cvt_f32_u32 {vr(V_T)}, {sr(den)}")
+    a(f"v_cvt_f32_u32 {vr(V_T + 1)}, {sr(num)}")
+    a("s_nop 4")
+    a(f"v_rcp_iflag_f32 {vr(V_T)}, {vr(V_T)}")
+    a("s_nop 4")
+    a(f"v_mul_f32 {vr(V_T)}, {vr(V_T)}, {vr(V_T + 1)}")
+    a("s_nop 4")
+    a(f"v_cvt_u32_f32 {vr(V_T)}, {vr(V_T)}")
+    a("s_nop 4")
+    a(f"v_readfirstlane_b32 {sr(q)}, {vr(V_T)}")
+    a("s_nop 4")
+    a(f"s_mul_i32 {sr(r)}, {sr(q)}, {sr(den)}")
+    a(f"s_sub_i32 {sr(r)}, {sr(num)}, {sr(r)}")
+    l1, l2 = a.fresh("div"), a.fresh("div")
+    a(f"s_cmp_lt_i32 {sr(r)}, 0")
+    a(f"s_cbranch_scc0 {l1}")
+    a(f"s_sub_u32 {sr(q)}, {sr(q)}, 1")
+    a(f"s_add_u32 {sr(r)}, {sr(r)}, {sr(den)}")
+    a.label(l1)
+    a(f"s_cmp_ge_u32 {sr(r)}, {sr(den)}")
+    a(f"s_cbranch_scc0 {l2}")
+    a(f"s_add_u32 {sr(q)}, {sr(q)}, 1")
+    a(f"s_sub_u32 {sr(r)}, {sr(r)}, {sr(den)}")
+    a.label(l2)
+
+
+def srd(a: Asm, dst: int, base_lo: int, off_lo: int, off_hi: int, nrec: int):
+    """dst[0:3] = buffer resource at 64-bit s[base] + (off_hi:off_lo),
+    num_records s[nrec] bytes, raw (stride 0), 32-bit dword data format."""
+    a(f"s_add_u32 {sr(dst)}, {sr(base_lo)}, {sr(off_lo)}")
+    a(f"s_addc_u32 {sr(dst + 1)}, {sr(base_lo + 1)}, {sr(off_hi)}")
+    a(f"s_mov_b32 {sr(dst + 2)}, {sr(nrec)}")
+    a(f"s_mov_b32 {sr(dst + 3)}, 0x20000")
+
+
+def mul64(a: Asm, lo: int, hi: int, x: int, y: int):
+    """(s_hi:s_lo) = s_x * s_y (unsigned 32 x 32 -> 64)."""
+    a(f"s_mul_hi_u32 {sr(hi)}, {sr(x)}, {sr(y)}")
+    a(f"s_mul_i32 {sr(lo)}, {sr(x)}, {sr(y)}")
+
+
+# ---------------------------------------------------------------- prologue
+def prologue(a: Asm, epi: str):
+    a(f"s_load_dwordx16 {sr(S_ARGS, 16)}, s[0:1], 0x0")
+    a(f"s_load_dwordx4 {sr(S_ARGS + 16, 4)}, s[0:1], 0x40")
+    a("s_mov_b32 m0, 0")
+    a(f"v_mov_b32 {vr(V_TID)}, v0")
+    a("s_waitcnt lgkmcnt(0)")
+    # defensive: an argument block the host launcher never packs ends the
+    # workgroup before any memory access (2 <= ktiles <= 65536, s2 < nwg)
+    a(f"s_cmp_lt_u32 {sr(S_KT)}, 2")
+    a(f"s_cbranch_scc1 {a.abort}")
+    a(f"s_cmp_gt_u32 {sr(S_KT)}, 65536")
+    a(f"s_cbranch_scc1 {a.abort}")
+    a(f"s_mul_i32 {sr(S_T0)}, {sr(S_TM_N)}, {sr(S_TN_N)}")
+    a(f"s_cmp_ge_u32 s2, {sr(S_T0)}")
+    a(f"s_cbranch_scc1 {a.abort}")
+    a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_XQ)}, 3")
+    a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_XR)}")
+    a(f"s_cmp_lg_u32 {sr(S_T1)}, {sr(S_T0)}")
+    a(f"s_cbranch_scc1 {a.abort}")
+    # --- XCD remap: blocks b, b+8, ... share an XCD; give each XCD a
+    # contiguous range of the tile order (bijective for any nwg)
+    a(f"s_and_b32 {sr(S_T0)}, s2, 7")                 # xcd
+    a(f"s_lshr_b32 {sr(S_T1)}, s2, 3")                # b / 8
+    a(f"s_add_u32 {sr(S_T2)}, {sr(S_XQ)}, 1")         # q + 1
+    a(f"s_mul_i32 {sr(S_T3)}, {sr(S_T0)}, {sr(S_T2)}")  # xcd * (q+1)
+    a(f"s_mul_i32 {sr(S_TILE)}, {sr(S_XR)}, {sr(S_T2)}")  # r * (q+1)
+    a(f"s_sub_u32 {sr(S_T2)}, {sr(S_T0)}, {sr(S_XR)}")  # xcd - r
+    a(f"s_mul_i32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_XQ)}")  # (xcd - r) * q
+    a(f"s_add_u32 {sr(S_TILE)}, {sr(S_TILE)}, {sr(S_T2)}")
+    a(f"s_cmp_lt_u32 {sr(S_T0)}, {sr(S_XR)}")
+    a(f"s_cselect_b32 {sr(S_TILE)}, {sr(S_T3)}, {sr(S_TILE)}")
+    a(f"s_add_u32 {sr(S_TILE)}, {sr(S_TILE)}, {sr(S_T1)}")
+    # --- tile -> (tm, tn): groups of 8 row tiles walk the column tiles
+    udiv(a, S_Q, S_R, S_TILE, S_PG)                   # group, within
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, 3")         # first_m
+    a(f"s_sub_u32 {sr(S_T1)}, {sr(S_TM_N)}, {sr(S_T0)}")
+    a(f"s_min_u32 {sr(S_T1)}, {sr(S_T1)}, 8")         # gsz
+    a(f"s_mov_b32 {sr(S_T2)}, {sr(S_R)}")
+    udiv(a, S_Q, S_R, S_T2, S_T1)                     # within / gsz, within % gsz
+    a(f"s_add_u32 {sr(S_TM)}, {sr(S_T0)}, {sr(S_R)}")
+    a(f"s_mov_b32 {sr(S_TN)}, {sr(S_Q)}")
+
+    # --- buffer resources at the tile's first row / column
+    # X: rows tm*256 .. +255, every k
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
+    mul64(a, S_T2, S_T3, S_T0, S_LDX)
+    a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDX)}, 8")       # 256 rows
+    srd(a, SRD_X, S_X, S_T2, S_T3, S_T1)
+    # W: rows tn*256 (tn*128 for the gate|up projection)
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TN)}, {7 if epi == 'swiglu_fwd' else 8}")
+    mul64(a, S_T2, S_T3, S_T0, S_LDW)
+    a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDW)}, 8")
+    if epi == "swiglu_fwd":
+        a(f"s_lshr_b32 {sr(S_T1)}, {sr(S_T1)}, 1")    # 128 rows of each half
+        a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_FW)}")  # + the up half's offset
+    srd(a, SRD_W, S_W, S_T2, S_T3, S_T1)
+    # C (and S): rows tm*256, columns tn*256 (tn*128 for the gate|up epilogue)
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
+    mul64(a, S_T2, S_T3, S_T0, S_LDC)
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TN)}, {8 if epi == 'swiglu_fwd' else 9}")  # column bytes
+    a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_T0)}")
+    a(f"s_addc_u32 {sr(S_T3)}, {sr(S_T3)}, 0")
+    a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDC)}, 8")
+    srd(a, SRD_C, S_C, S_T2, S_T3, S_T1)
+    if epi != "plain":
+        a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
+        mul64(a, S_T2, S_T3, S_T0, S_LDS)
+        a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TN)}, {8 if epi == 'swiglu_fwd' else 9}")
+        a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_T0)}")
+        a(f"s_addc_u32 {sr(S_T3)}, {sr(S_T3)}, 0")
+        a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 8")
+        srd(a, SRD_S, S_S, S_T2, S_T3, S_T1)
+
+    # --- DMA lane offsets.  Wave w's instruction j fills LDS line w + 4j of
+    # the half: rows (w + 4(j%4)) + 16*(lane>>3) [+ 128 for j >= 4], k chunk
+    # lane & 7.  Per-lane part -> V_DX / V_DW, per-instruction part -> s[SO*].
+    v = V_T
+    a(f"v_lshrrev_b32 {vr(v)}, 6, {vr(V_TID)}")            # w
+    a(f"v_and_b32 {vr(v + 1)}, 63, {vr(V_TID)}")           # lane
+    a(f"v_lshrrev_b32 {vr(v + 2)}, 3, {vr(v + 1)}")        # lane >> 3
+    a(f"v_and_b32 {vr(v + 3)}, 7, {vr(v + 1)}")            # lane & 7
+    a(f"v_lshlrev_b32 {vr(v + 3)}, 4, {vr(v + 3)}")        # chunk bytes
+    # X: row = w + 16 (lane >> 3)
+    a(f"v_lshl_add_u32 {vr(V_DX)}, {vr(v + 2)}, 4, {vr(v)}")
+    a(f"v_mul_lo_u32 {vr(V_DX)}, {vr(V_DX)}, {sr(S_LDX)}")
+    a(f"v_add_u32 {vr(V_DX)}, {vr(V_DX)}, {vr(v + 3)}")
+    if epi == "swiglu_fwd":
+        # row = w + 16 ((lane>>3) & 3) [+ F rows when lane >> 5]
+        a(f"v_and_b32 {vr(V_DW)}, 3, {vr(v + 2)}")
+        a(f"v_lshl_add_u32 {vr(V_DW)}, {vr(V_DW)}, 4, {vr(v)}")
+        a(f"v_mul_lo_u32 {vr(V_DW)}, {vr(V_DW)}, {sr(S_LDW)}")
+        a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v + 3)}")
+        a(f"v_lshrrev_b32 {vr(v + 2)}, 2, {vr(v + 2)}")    # 0 / 1: gate / up
+        a(f"v_mul_lo_u32 {vr(v + 2)}, {vr(v + 2)}, {sr(S_FW)}")
+        a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v + 2)}")
+    else:
+        a(f"v_lshl_add_u32 {vr(V_DW)}, {vr(v + 2)}, 4, {vr(v)}")
+        a(f"v_mul_lo_u32 {vr(V_DW)}, {vr(V_DW)}, {sr(S_LDW)}")
+        a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v + 3)}")
+    for j in range(1, 8):
+        rows_x = 4 * (j % 4) + 128 * (j // 4)
+        rows_w = 4 * (j % 4) + (UNIT_GATE_ROWS if epi == "swiglu_fwd" else 128) * (j // 4)
+        a(f"s_mul_i32 {sr(S_SOX + j - 1)}, {sr(S_LDX)}, {rows_x}")
+        a(f"s_mul_i32 {sr(S_SOW + j - 1)}, {sr(S_LDW)}, {rows_w}")
+    # --- LDS-DMA bases (M0): wave w at line w of the stage's half
+    a("s_nop 4")
+    a(f"v_readfirstlane_b32 {sr(S_T0)}, {vr(v)}")          # w
+    a("s_nop 4")
+    a(f"s_mul_i32 {sr(S_M0X)}, {sr(S_T0)}, {LINE}")
+    a(f"s_add_u32 {sr(S_M0XT)}, {sr(S_M0X)}, {STAGE}")
+    a(f"s_xor_b32 {sr(S_M0XT)}, {sr(S_M0XT)}, {sr(S_M0X)}")
+    a(f"s_add_u32 {sr(S_M0W)}, {sr(S_M0X)}, {HALF}")
+    a(f"s_add_u32 {sr(S_M0WT)}, {sr(S_M0W)}, {STAGE}")
+    a(f"s_xor_b32 {sr(S_M0WT)}, {sr(S_M0WT)}, {sr(S_M0W)}")
+    # --- fragment read bases: line (lane & 15), chunk (lane >> 4), wave half
+    a(f"v_and_b32 {vr(v + 2)}, 15, {vr(v + 1)}")
+    a(f"v_mul_u32_u24 {vr(v + 2)}, {LINE}, {vr(v + 2)}")
+    a(f"v_lshrrev_b32 {vr(v + 3)}, 4, {vr(v + 1)}")
+    a(f"v_lshl_add_u32 {vr(v + 2)}, {vr(v + 3)}, 4, {vr(v + 2)}")
+    a(f"v_and_b32 {vr(v + 3)}, 1, {vr(v)}")                # wm
+    a(f"v_mul_u32_u24 {vr(v + 3)}, {16 * LINE}, {vr(v + 3)}")
+    a(f"v_add_u32 {vr(V_RX)}, {vr(v + 2)}, {vr(v + 3)}")
+    a(f"v_lshrrev_b32 {vr(v + 3)}, 1, {vr(v)}")            # wn
+    a(f"v_mul_u32_u24 {vr(v + 3)}, {16 * LINE}, {vr(v + 3)}")
+    a(f"v_add_u32 {vr(V_RW)}, {vr(v + 2)}, {vr(v + 3)}")
+    a(f"v_add_u32 {vr(V_RW)}, {HALF}, {vr(V_RW)}")
+    a(f"v_add_u32 {vr(V_RXT)}, {STAGE}, {vr(V_RX)}")
+    a(f"v_xor_b32 {vr(V_RXT)}, {vr(V_RXT)}, {vr(V_RX)}")
+    a(f"v_add_u32 {vr(V_RWT)}, {STAGE}, {vr(V_RW)}")
+    a(f"v_xor_b32 {vr(V_RWT)}, {vr(V_RWT)}, {vr(V_RW)}")
+    # --- zero the accumulators
+    for i in range(256):
+        a(f"v_accvgpr_write_b32 {ar(i)}, 0")
+
+
+# ---------------------------------------------------------------- main loop
+def dma(a: Asm, half: str, j: int) -> list[str]:
+    """Instructions for DMA piece j (0..7) of the X or W half: set M0 to the
+    line, one buffer_load_dwordx4 ... lds."""
+    srd_, vo, so, m0 = (SRD_X, V_DX, S_SOX, S_M0X) if half == "x" else (SRD_W, V_DW, S_SOW, S_M0W)
+    out = []
+    if j == 0:
+        out.append(f"s_mov_b32 m0, {sr(m0)}")
+    else:
+        out.append(f"s_add_u32 m0, m0, {4 * LINE}")
+    # gfx9 hazard: an LDS-DMA reads M0 one wait state after the SALU write
+    # (LLVM's checkReadM0Hazards; hipcc always separates the two)
+    out.append("s_nop 0")
+    soff = "0" if j == 0 else sr(so + j - 1)
+    out.append(f"buffer_load_dwordx4 {vr(vo)}, {sr(srd_, 4)}, {soff} offen lds")
+    return out
+
+
+def advance(half: str) -> list[str]:
+    s = SRD_X if half == "x" else SRD_W
+    return [f"s_add_u32 {sr(s)}, {sr(s)}, 128", f"s_addc_u32 {sr(s + 1)}, {sr(s + 1)}, 0"]
+
+
+def frag_read(kind: str, f: int, sub: int) -> str:
+    base = V_RX if kind == "x" else V_RW
+    dst = (V_FX0 if sub == 0 else V_FX1) if kind == "x" else (V_FW0 if sub == 0 else V_FW1)
+    off = 128 * f + 64 * sub
+    return f"ds_read_b128 {vr(dst + 4 * f, 4)}, {vr(base)} offset:{off}"
+
+
+def mfma(i: int, j: int, sub: int) -> str:
+    fw = (V_FW0 if sub == 0 else V_FW1) + 4 * i
+    fx = (V_FX0 if sub == 0 else V_FX1) + 4 * j
+    acc = 4 * (8 * i + j)
+    return f"v_mfma_f32_16x16x32_bf16 {ar(acc, 4)}, {vr(fw, 4)}, {vr(fx, 4)}, {ar(acc, 4)}"
+
+
+def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0):
+    """One 64-k tile: 128 MFMAs with the reads / DMA / waits placed in the
+    gaps after MFMA n (n = 0..127; 0..63 phase 1, 64..127 phase 2)."""
+    slots: dict[int, list[str]] = {n: [] for n in range(128)}
+    # phase 1: sub-step 1 fragment reads of this stage (X then W)
+    for j in range(8):
+        slots[2 * j].append(frag_read("x", j, 1))
+    if with_dma:
+        slots[15] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]      # X half of this stage free
+    for i in range(8):
+        slots[17 + 2 * i].append(frag_read("w", i, 1))
+    if with_dma:
+        for j in range(8):
+            slots[16 + 4 * j] += dma(a, "x", j)
+        slots[47] += advance("x")
+        slots[47] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]      # W half free
+        for j in range(8):
+            slots[48 + 4 * j] += dma(a, "w", j)                 # 48..76
+        slots[78] += advance("w")
+        slots[78] += [f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}",
+                      f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}"]
+        if trace_base:
+            slots[47] += trace_mark(trace_base + 1)
+            slots[78] += trace_mark(trace_base + 2)
+    if next_reads:
+        # the next tile (staged one iteration ago) has landed: own DMA by the
+        # counted wait, everyone's by the barrier
+        slots[79] += [f"s_waitcnt vmcnt({vm_after_dma})", "s_barrier",
+                      f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
+                      f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
+        for j in range(8):
+            slots[80 + 2 * j].append(frag_read("x", j, 0))
+        for i in range(8):
+            slots[96 + 2 * i].append(frag_read("w", i, 0))
+        slots[126].append("s_waitcnt lgkmcnt(0)")
+        if trace_base:
+            slots[79] += trace_mark(trace_base + 3)
+    if trace_base:
+        slots[127] += trace_mark(trace_base + 4)
+    for n in range(128):
+        sub, m = divmod(n, 64)
+        i, j = divmod(m, 8)
+        if n == 64:
+            # phase 2 consumes the sub-step 1 fragments read in phase 1
+            a("s_waitcnt lgkmcnt(0)")
+        a(mfma(i, j, sub))
+        for ins in slots[n]:
+            a(ins)
+
+
+# ---------------------------------------------------------------- epilogues
+def acc_index(i: int, j: int) -> int:
+    return 4 * (8 * i + j)
+
+
+def epi_offsets(a: Asm, epi: str):
+    """Per-lane output byte offsets.  Lane l of wave (wm, wn) holds, for
+    fragment pair (i, j): row m = wm*128 + 16 j + (l & 15) and columns
+    n = 16 i + 4 (l >> 4) .. +3 of the wave's W rows."""
+    v = V_T
+    a(f"v_lshrrev_b32 {vr(v)}, 6, {vr(V_TID)}")            # w
+    a(f"v_and_b32 {vr(v + 1)}, 63, {vr(V_TID)}")           # lane
+    a(f"v_and_b32 {vr(v + 2)}, 15, {vr(v + 1)}")
+    a(f"v_and_b32 {vr(v + 3)}, 1, {vr(v)}")
+    a(f"v_lshl_add_u32 {vr(v + 2)}, {vr(v + 3)}, 7, {vr(v + 2)}")  # row in tile
+    a(f"v_lshrrev_b32 {vr(v + 1)}, 4, {vr(v + 1)}")        # lane >> 4
+    a(f"v_lshlrev_b32 {vr(v + 1)}, 3, {vr(v + 1)}")        # 8 B per lane group
+    a(f"v_lshrrev_b32 {vr(v)}, 1, {vr(v)}")                # wn
+    # column bytes of the wave: plain / bwd 128 cols per wave, fwd 64 units
+    a(f"v_lshlrev_b32 {vr(v)}, {8 if epi != 'swiglu_fwd' else 7}, {vr(v)}")
+    a(f"v_add_u32 {vr(v + 1)}, {vr(v + 1)}, {vr(v)}")      # col bytes
+    # V_E+0: C offset, V_E+1: S offset (fwd: s; bwd: gu)
+    a(f"v_mul_lo_u32 {vr(V_E)}, {vr(v + 2)}, {sr(S_LDC)}")
+    a(f"v_add_u32 {vr(V_E)}, {vr(V_E)}, {vr(v + 1)}")
+    if epi != "plain":
+        a(f"v_mul_lo_u32 {vr(V_E + 1)}, {vr(v + 2)}, {sr(S_LDS)}")
+        a(f"v_add_u32 {vr(V_E + 1)}, {vr(V_E + 1)}, {vr(v + 1)}")
+    if epi == "swiglu_fwd":
+        a(f"v_add_u32 {vr(V_E + 2)}, {sr(S_FC)}, {vr(V_E)}")  # up half of gu
+    if epi == "swiglu_bwd":
+        a(f"v_add_u32 {vr(V_E + 2)}, {sr(S_FC)}, {vr(V_E)}")      # up half of dgu
+        a(f"v_add_u32 {vr(V_E + 3)}, {sr(S_FC)}, {vr(V_E + 1)}")  # up half of gu
+
+
+def read_acc4(a: Asm, dst: int, acc: int):
+    for r in range(4):
+        a(f"v_accvgpr_read_b32 {vr(dst + r)}, {ar(acc + r)}")
+
+
+def cvt_pack(a: Asm, dst: int, src: int):
+    a(f"v_cvt_pk_bf16_f32 {vr(dst)}, {vr(src)}, {vr(src + 1)}")
+    a(f"v_cvt_pk_bf16_f32 {vr(dst + 1)}, {vr(src + 2)}, {vr(src + 3)}")
+
+
+def unpack_bf16(a: Asm, dst: int, src: int):
+    """dst[0..3] = f32 of the 4 bf16 in src[0..1] (element order kept)."""
+    a(f"v_lshlrev_b32 {vr(dst)}, 16, {vr(src)}")
+    a(f"v_and_b32 {vr(dst + 1)}, 0xffff0000, {vr(src)}")
+    a(f"v_lshlrev_b32 {vr(dst + 2)}, 16, {vr(src + 1)}")
+    a(f"v_and_b32 {vr(dst + 3)}, 0xffff0000, {vr(src + 1)}")
+
+
+LOG2E = 1.4426950408889634
+
+
+def epilogue_plain(a: Asm):
+    a(f"s_mov_b32 {sr(S_E0)}, 0")                             # row block offset
+    a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")              # 16 rows
+    for j in range(8):
+        base = V_E + 8
+        for i in range(8):
+            read_acc4(a, base + 4 * i, acc_index(i, j))
+        for i in range(8):
+            cvt_pack(a, V_E + 40 + 2 * i, base + 4 * i)
+        for i in range(8):
+            a(f"buffer_store_dwordx2 {vr(V_E + 40 + 2 * i, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+        a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+
+
+def epilogue_swiglu_fwd(a: Asm):
+    """i = 0..3 gate fragments, i + 4 the same hidden units' up fragments."""
+    a(f"s_mov_b32 {sr(S_E0)}, 0")
+    a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")
+    a(f"s_mov_b32 {sr(S_T0)}, 0")
+    a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 4")
+    a(f"v_mov_b32 {vr(V_E + 3)}, {-LOG2E!r}")
+    for j in range(8):
+        g, u = V_E + 8, V_E + 24          # 16 f32 each
+        for i in range(4):
+            read_acc4(a, g + 4 * i, acc_index(i, j))
+            read_acc4(a, u + 4 * i, acc_index(i + 4, j))
+        pg, pu = V_E + 40, V_E + 48       # packed bf16 (8 regs each)
+        for i in range(4):
+            cvt_pack(a, pg + 2 * i, g + 4 * i)
+            cvt_pack(a, pu + 2 * i, u + 4 * i)
+        for i in range(4):
+            a(f"buffer_store_dwordx2 {vr(pg + 2 * i, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+            a(f"buffer_store_dwordx2 {vr(pu + 2 * i, 2)}, {vr(V_E + 2)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+        # s = silu(g) * u on the bf16-rounded values (what backward re-reads)
+        gf, uf, ps = V_E + 56, V_E + 72, V_E + 88
+        for i in range(4):
+            unpack_bf16(a, gf + 4 * i, pg + 2 * i)
+            unpack_bf16(a, uf + 4 * i, pu + 2 * i)
+        t = V_E + 96                      # 16 scratch
+        for e in range(16):
+            a(f"v_mul_f32 {vr(t + e)}, {vr(V_E + 3)}, {vr(gf + e)}")
+        for e in range(16):
+            a(f"v_exp_f32 {vr(t + e)}, {vr(t + e)}")
+        for e in range(16):
+            a(f"v_add_f32 {vr(t + e)}, 1.0, {vr(t + e)}")
+        for e in range(16):
+            a(f"v_rcp_f32 {vr(t + e)}, {vr(t + e)}")
+        for e in range(16):
+            a(f"v_mul_f32 {vr(t + e)}, {vr(gf + e)}, {vr(t + e)}")
+        for e in range(16):
+            a(f"v_mul_f32 {vr(t + e)}, {vr(t + e)}, {vr(uf + e)}")
+        for i in range(4):
+            cvt_pack(a, ps + 2 * i, t + 4 * i)
+        for i in range(4):
+            a(f"buffer_store_dwordx2 {vr(ps + 2 * i, 2)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{32 * i}")
+        a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+        a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T1)}")
+
+
+def epilogue_swiglu_bwd(a: Asm):
+    """acc = ds (never stored).  gu rows: gate at n, up at F + n."""
+    a(f"s_mov_b32 {sr(S_E0)}, 0")                             # dgu row block
+    a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")
+    a(f"s_mov_b32 {sr(S_T0)}, 0")                             # gu row block
+    a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 4")
+    a(f"v_mov_b32 {vr(V_E + 4)}, {-LOG2E!r}")
+    for j in range(8):
+        for half in range(2):             # fragments i = 4 half .. 4 half + 3
+            ig = [4 * half + q for q in range(4)]
+            lg, lu = V_E + 8, V_E + 16    # loaded packed gate / up (8 regs each)
+            for q, i in enumerate(ig):
+                a(f"buffer_load_dwordx2 {vr(lg + 2 * q, 2)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{32 * i}")
+                a(f"buffer_load_dwordx2 {vr(lu + 2 * q, 2)}, {vr(V_E + 3)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{32 * i}")
+            d = V_E + 24                  # 16 f32: ds
+            for q, i in enumerate(ig):
+                read_acc4(a, d + 4 * q, acc_index(i, j))
+            pd = V_E + 40                 # bf16-rounded ds, then unpacked
+            for q in range(4):
+                cvt_pack(a, pd + 2 * q, d + 4 * q)
+            for q in range(4):
+                unpack_bf16(a, d + 4 * q, pd + 2 * q)
+            a("s_waitcnt vmcnt(0)")
+            gf, uf = V_E + 48, V_E + 64
+            for q in range(4):
+                unpack_bf16(a, gf + 4 * q, lg + 2 * q)
+                unpack_bf16(a, uf + 4 * q, lu + 2 * q)
+            sg, tmp = V_E + 80, V_E + 96
+            for e in range(16):            # sg = 1 / (1 + exp(-g))
+                a(f"v_mul_f32 {vr(sg + e)}, {vr(V_E + 4)}, {vr(gf + e)}")
+            for e in range(16):
+                a(f"v_exp_f32 {vr(sg + e)}, {vr(sg + e)}")
+            for e in range(16):
+                a(f"v_add_f32 {vr(sg + e)}, 1.0, {vr(sg + e)}")
+            for e in range(16):
+                a(f"v_rcp_f32 {vr(sg + e)}, {vr(sg + e)}")
+            for e in range(16):            # du = d * g * sg  -> tmp
+                a(f"v_mul_f32 {vr(tmp + e)}, {vr(d + e)}, {vr(gf + e)}")
+                a(f"v_mul_f32 {vr(tmp + e)}, {vr(tmp + e)}, {vr(sg + e)}")
+            for e in range(16):            # dg = d * u * sg * (1 + g (1 - sg)) -> uf
+                a(f"v_sub_f32 {vr(lg)}, 1.0, {vr(sg + e)}")
+                a(f"v_fma_f32 {vr(lg)}, {vr(gf + e)}, {vr(lg)}, 1.0")
+                a(f"v_mul_f32 {vr(uf + e)}, {vr(d + e)}, {vr(uf + e)}")
+                a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(sg + e)}")
+                a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(lg)}")
+            pdg, pdu = V_E + 40, V_E + 112
+            for q in range(4):
+                cvt_pack(a, pdg + 2 * q, uf + 4 * q)
+            for q in range(2):
+                cvt_pack(a, pdu + 2 * q, tmp + 4 * q)
+            for q, i in enumerate(ig):
+                a(f"buffer_store_dwordx2 {vr(pdg + 2 * q, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+            for q, i in enumerate(ig[:2]):
+                a(f"buffer_store_dwordx2 {vr(pdu + 2 * q, 2)}, {vr(V_E + 2)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+            for q in range(2, 4):          # reuse gf for the last two packed du
+                cvt_pack(a, gf + 2 * (q - 2), tmp + 4 * q)
+            for q, i in enumerate(ig[2:]):
+                a(f"buffer_store_dwordx2 {vr(gf + 2 * q, 2)}, {vr(V_E + 2)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+            a("s_waitcnt vmcnt(0)")        # scratch registers are reused next round
+        a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+        a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T1)}")
+
+
+# ---------------------------------------------------------------- kernel
+def kernel(epi: str, trace: bool = False) -> tuple[str, str]:
+    """trace=True: the diagnostic trace variant of the plain kernel (markers
+    into a host-coherent buffer in the S slot; toa_gemm_tn_asm_trace)."""
+    name = "toa_gemm_tn_asm_trace" if trace else f"toa_gemm_tn_asm_{epi}"
+    a = Asm(prefix=("trace_" if trace else epi + "_"))
+    tb = (lambda base: base) if trace else (lambda base: 0)
+    a.raw(f".globl {name}")
+    a.raw(".p2align 8")
+    a.raw(f".type {name},@function")
+    a.raw(f"{name}:")
+    prologue(a, epi)
+    if trace:
+        for ins in trace_setup(a) + trace_mark(1):
+            a(ins)
+    # --- prologue DMA: tile 0 -> stage 0, tile 1 -> stage 1
+    for tile in range(2):
+        for half in ("x", "w"):
+            for j in range(8):
+                for ins in dma(a, half, j):
+                    a(ins)
+            for ins in advance(half):
+                a(ins)
+        a(f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}")
+        a(f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}")
+    # both stages toggled twice: M0 bases are back at stage 0 for tile 2
+    a("s_waitcnt vmcnt(16)")                       # own tile-0 pieces
+    a("s_barrier")                                 # everyone's
+    if trace:
+        for ins in trace_mark(2):
+            a(ins)
+    if epi == "plain" and not trace:
+        stage_exit(a, 1)
+    for j in range(8):
+        a(frag_read("x", j, 0))
+    for i in range(8):
+        a(frag_read("w", i, 0))
+    a("s_waitcnt lgkmcnt(0)")
+    a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_KT)}, 2")
+    l_loop, l_tail = a.fresh("loop"), a.fresh("tail")
+    a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
+    a(f"s_cbranch_scc1 {l_tail}")
+    a.label(l_loop)
+    iteration(a, with_dma=True, next_reads=True, vm_after_dma=16, trace_base=tb(100))
+    a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_LOOP)}, 1")
+    a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
+    a(f"s_cbranch_scc0 {l_loop}")
+    a.label(l_tail)
+    iteration(a, with_dma=False, next_reads=True, vm_after_dma=0, trace_base=tb(200))
+    iteration(a, with_dma=False, next_reads=False, vm_after_dma=0, trace_base=tb(300))
+    if epi == "plain" and not trace:
+        stage_exit(a, 2)
+    # MFMA results -> VALU reads: let the last MFMAs retire
+    a("s_nop 15")
+    a("s_nop 15")
+    if trace:
+        for ins in trace_mark(9000):
+            a(ins)
+    epi_offsets(a, epi)
+    {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
+    a("s_waitcnt vmcnt(0)")
+    if trace:
+        for ins in trace_setup(a)[-3:] + trace_mark(9999):
+            a(ins)
+    a.label(a.abort)
+    a("s_endpgm")
+    if epi == "plain" and not trace:
+        a.label(a.stage_exit)
+        a("s_waitcnt vmcnt(0)")
+        a("s_endpgm")
+    a.raw(f".size {name}, .-{name}")
+    body = "\n".join(a.out)
+    desc, meta = _descriptor(name)
+    return body + "\n" + desc, meta
+
+
+TRACE_REC = 32   # bytes per (workgroup, wave) trace record
+
+
+def trace_setup(a: Asm) -> list[str]:
+    """Diagnostic trace kernel only: SRD over the host-coherent trace buffer
+    (pointer in the S slot), V_T+3 = this wave's record offset."""
+    return [f"s_mov_b32 {sr(SRD_S)}, {sr(S_S)}", f"s_mov_b32 {sr(SRD_S + 1)}, {sr(S_S + 1)}",
+            f"s_mul_i32 {sr(SRD_S + 2)}, {sr(S_TM_N)}, {sr(S_TN_N)}",
+            f"s_mul_i32 {sr(SRD_S + 2)}, {sr(SRD_S + 2)}, {4 * TRACE_REC}",
+            f"s_mov_b32 {sr(SRD_S + 3)}, 0x20000", "s_mov_b32 s71, 0",
+            f"v_lshrrev_b32 {vr(V_T + 3)}, 6, {vr(V_TID)}",
+            f"v_lshl_add_u32 {vr(V_T + 3)}, s2, 2, {vr(V_T + 3)}",
+            f"v_mul_u32_u24 {vr(V_T + 3)}, {TRACE_REC}, {vr(V_T + 3)}"]
+
+
+def trace_mark(code: int) -> list[str]:
+    """Record (code, loop counter, M0, SRD_X lo, SRD_W lo, M0 bases, seq) for
+    this wave, system-coherent, drained: after a fault the host reads how far
+    every wave got (scripts/asm_gemm_bench.py --trace)."""
+    out = ["s_add_u32 s71, s71, 1"]
+    for k, src in enumerate((str(code), sr(S_LOOP), "m0", sr(SRD_X), sr(SRD_W), sr(S_M0X), sr(S_M0W), "s71")):
+        out.append(f"v_mov_b32 {vr(V_T + 2)}, {src}")
+        out.append(f"buffer_store_dword {vr(V_T + 2)}, {vr(V_T + 3)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * k} sc0 sc1")
+    out.append("s_waitcnt vmcnt(0)")
+    return out
+
+
+def stage_exit(a: Asm, stage: int):
+    """Diagnostic (plain kernel only, whose fc argument is otherwise unused):
+    fc == stage ends the workgroup here, after draining its DMA -- bisects a
+    hardware fault by how far the kernel gets (scripts/asm_gemm_bench.py)."""
+    a(f"s_cmp_eq_u32 {sr(S_FC)}, {stage}")
+    a(f"s_cbranch_scc1 {a.stage_exit}")
+
+
+def _descriptor(name: str) -> tuple[str, str]:
+    desc = f"""
+.rodata
+.p2align 6
+.amdhsa_kernel {name}
+  .amdhsa_group_segment_fixed_size {LDS_BYTES}
+  .amdhsa_private_segment_fixed_size 0
+  .amdhsa_kernarg_size {KARG_BYTES}
+  .amdhsa_user_sgpr_count 2
+  .amdhsa_user_sgpr_kernarg_segment_ptr 1
+  .amdhsa_system_sgpr_workgroup_id_x 1
+  .amdhsa_system_vgpr_workitem_id 0
+  .amdhsa_next_free_vgpr 512
+  .amdhsa_next_free_sgpr {N_SGPR}
+  .amdhsa_accum_offset 256
+  .amdhsa_reserve_vcc 1
+  .amdhsa_float_denorm_mode_32 3
+  .amdhsa_float_denorm_mode_16_64 3
+  .amdhsa_dx10_clamp 1
+  .amdhsa_ieee_mode 1
+.end_amdhsa_kernel
+.text
+"""
+    meta = f"""  - .args:
+      - .offset: 0
+        .size: {KARG_BYTES}
+        .value_kind: by_value
+    .group_segment_fixed_size: {LDS_BYTES}
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: {KARG_BYTES}
+    .max_flat_workgroup_size: 256
+    .name: {name}
+    .private_segment_fixed_size: 0
+    .sgpr_count: {N_SGPR + 6}
+    .sgpr_spill_count: 0
+    .symbol: {name}.kd
+    .vgpr_count: 512
+    .agpr_count: 256
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+    .uniform_work_group_size: 1
+    .uses_dynamic_stack: false
+    .language: OpenCL C
+    .language_version:
+      - 2
+      - 0
+"""
+    return desc, meta
+
+
+PROBE_MAGIC = (0x626F7270, 0x31657461)   # "prob" "ate1" in the fw / fc argument slots
+
+
+def probe_kernel() -> tuple[str, str]:
+    """Diagnostic kernel: the plain kernel's prologue, then a dump of every
+    SGPR s0..s71 and, per thread, the DMA / fragment / epilogue offsets to
+    the buffer in the S argument slot -- ONLY when fw / fc hold PROBE_MAGIC
+    (a kernarg block that did not arrive intact stores nothing).  Compared
+    with the emulator's dump of the same prologue (tests/test_asm_gemm.py,
+    scripts/asm_gemm_bench.py --probe)."""
+    name = "toa_gemm_tn_asm_probe"
+    a = Asm(prefix="probe_")
+    a.raw(f".globl {name}")
+    a.raw(".p2align 8")
+    a.raw(f".type {name},@function")
+    a.raw(f"{name}:")
+    prologue(a, "plain")
+    epi_offsets(a, "plain")
+    end = a.fresh("end")
+    a(f"s_cmp_eq_u32 {sr(S_FW)}, {PROBE_MAGIC[0]:#x}")
+    a(f"s_cbranch_scc0 {end}")
+    a(f"s_cmp_eq_u32 {sr(S_FC)}, {PROBE_MAGIC[1]:#x}")
+    a(f"s_cbranch_scc0 {end}")
+    # workgroup b dumps to S + b * PROBE_WORDS * 4
+    a(f"s_mul_i32 {sr(S_E0)}, s2, {PROBE_WORDS * 4}")
+    a(f"s_add_u32 {sr(SRD_S)}, {sr(S_S)}, {sr(S_E0)}")
+    a(f"s_addc_u32 {sr(SRD_S + 1)}, {sr(S_S + 1)}, 0")
+    a(f"s_mov_b32 {sr(SRD_S + 2)}, {PROBE_WORDS * 4}")
+    a(f"s_mov_b32 {sr(SRD_S + 3)}, 0x20000")
+    a(f"v_mov_b32 {vr(V_T + 1)}, 0")
+    for r in range(N_SGPR):
+        if r in (SRD_S, SRD_S + 1, SRD_S + 2, SRD_S + 3, S_E0):
+            continue
+        a(f"v_mov_b32 {vr(V_T)}, {sr(r)}")
+        a(f"buffer_store_dword {vr(V_T)}, {vr(V_T + 1)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * r}")
+    a(f"v_mov_b32 {vr(V_T)}, m0")
+    a(f"buffer_store_dword {vr(V_T)}, {vr(V_T + 1)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * N_SGPR}")
+    # per thread: 8 words at 4 * (PROBE_VBASE + 8 tid)
+    a(f"v_lshlrev_b32 {vr(V_T + 1)}, 5, {vr(V_TID)}")
+    for k, reg in enumerate((V_DX, V_DW, V_RX, V_RW, V_RXT, V_RWT, V_E, V_TID)):
+        a(f"buffer_store_dword {vr(reg)}, {vr(V_T + 1)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * (PROBE_VBASE + k)}")
+    a("s_waitcnt vmcnt(0)")
+    a.label(end)
+    a.label(a.abort)
+    a("s_endpgm")
+    a.raw(f".size {name}, .-{name}")
+    body = "\n".join(a.out)
+    desc, meta = _descriptor(name)
+    return body + "\n" + desc, meta
+
+
+PROBE_VBASE = 128
+PROBE_WORDS = PROBE_VBASE + 8 * 256
+
+
+def generate() -> str:
+    parts = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".amdhsa_code_object_version 5", ".text"]
+    metas = []
+    for epi in EPIS:
+        body, meta = kernel(epi)
+        parts.append(body)
+        metas.append(meta)
+    for body, meta in (probe_kernel(), kernel("plain", trace=True)):
+        parts.append(body)
+        metas.append(meta)
+    # what hipcc emits after the last kernel: s_nop padding, so the
+    # instruction prefetcher never runs off the end of the code object
+    parts.append(".text\n.p2alignl 6, 3212836864\n.fill 256, 4, 3212836864")   # s_nop 0
+    parts.append(".amdgpu_metadata\n---\namdhsa.version:\n  - 1\n  - 2\namdhsa.target: amdgcn-amd-amdhsa--gfx950\namdhsa.kernels:\n" + "".join(metas)
+                 + "...\n.end_amdgpu_metadata")
+    return "\n".join(parts) + "\n"
+
+
+if __name__ == "__main__":
+    out = sys.argv[1] if len(sys.argv) > 1 else "gemm_tn_asm.s"
+    with open(out, "w") as f:
+        f.write(generate())

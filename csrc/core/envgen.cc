@@ -194,7 +194,10 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
       add_env(out, c, "RANK", std::to_string(rank));
       add_env(out, c, "LOCAL_RANK", nl ? std::to_string(rank) : "0");
       add_env(out, c, "LOCAL_WORLD_SIZE", nl ? std::to_string(world) : "1");
-      if (nl) add_env(out, c, "TOA_NODE_LOCAL", "1");
+      if (nl) {
+        add_env(out, c, "TOA_NODE_LOCAL", "1");
+        add_env(out, c, "TOA_DEVICE_SOURCE", "pod-resources");
+      }
     }
     add_env(out, c, "TOA_ROLE", role);
     int64_t n_ps = spec_replicas(job, "PS");
@@ -226,7 +229,10 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
       const bool nl = node_local(job, opt);
       add_env(out, "*", "LOCAL_RANK", nl ? std::to_string(rank) : "0");
       add_env(out, "*", "LOCAL_WORLD_SIZE", nl ? std::to_string(total) : "1");
-      if (nl) add_env(out, "*", "TOA_NODE_LOCAL", "1");
+      if (nl) {
+        add_env(out, "*", "TOA_NODE_LOCAL", "1");
+        add_env(out, "*", "TOA_DEVICE_SOURCE", "pod-resources");
+      }
       rocm_block(job, rtype, index, opt, "*", out);
     }
     return out;

@@ -10,28 +10,48 @@
 // (LOCAL_WORLD_SIZE = 1).
 //
 // Node-local mode keeps one pod per replica (per-replica status, restart and
-// ExitCode semantics unchanged) and makes the ranks a single-node group:
+// ExitCode semantics unchanged) and makes the ranks a single-node group.  It
+// is OPT-IN ONLY and has exactly one mechanism for peer-device access:
+//
+//   annotation amd.com/node-local: "privileged"   ("true" is an alias)
 //
 //   * co-location: a required podAffinity on kubernetes.io/hostname to the
 //     job's other rank pods (the first pod satisfies its own term), so the
 //     scheduler -- or Volcano, which gang-admits the whole PodGroup -- puts
 //     every rank on one node; each pod still requests its `amd.com/gpu: 1`,
 //     so the node's GPU accounting is unchanged;
-//   * peer visibility: hostIPC (dmabuf / IPC handle exchange between the
-//     ranks' processes) and the node's /dev/kfd + /dev/dri mounted into the
-//     training container, so every rank sees all GPUs of the node and RCCL
-//     (and the one-shot IPC all-reduce, parallel/ipc.py) reach peers over
-//     xGMI;
+//   * peer access: the training container runs with
+//     securityContext.privileged = true plus the pod's hostIPC.  A hostPath
+//     mount of /dev/dri alone does NOT work: a mounted device node is not in
+//     the container's device cgroup, so opening a peer GPU fails.  Privileged
+//     puts every device of the node in the cgroup, so RCCL (and the one-shot
+//     IPC all-reduce, parallel/ipc.py) reach peers over xGMI;
+//   * device binding: a privileged container sees every GPU of the node, so
+//     LOCAL_RANK cannot name the pod's device -- on a node shared with other
+//     jobs rank r would drive GPU r whether or not the device plugin gave it
+//     that GPU.  The pod gets the kubelet's pod-resources socket (read-only
+//     hostPath) and its own name / namespace (downward API); the trainer asks
+//     the kubelet which amd.com/gpu device IDs (PCI addresses) were allocated
+//     to THIS pod and binds the HIP device with that PCI address
+//     (train/devices.py).  If the answer is unavailable it refuses to start
+//     rather than guess;
 //   * env: LOCAL_RANK = the rank's index on the node (= RANK: one node),
-//     LOCAL_WORLD_SIZE = the number of ranks on the node, TOA_NODE_LOCAL=1;
-//     the trainer binds device TOA_LOCAL_DEVICE when the node agent names
-//     the pod's allocated GPU, else LOCAL_RANK (train/dist.py);
+//     LOCAL_WORLD_SIZE = the number of ranks on the node, TOA_NODE_LOCAL=1,
+//     TOA_DEVICE_SOURCE=pod-resources;
 //   * the annotation amd.com/gpu-visibility=node, which the local kubelet
-//     (localkubelet/kubelet.py) reads to give the pod node-wide visibility.
+//     (localkubelet/kubelet.py) honours only for a privileged container with
+//     hostIPC -- the same rule a real node enforces.
 //
-// When: annotation amd.com/node-local "true" (opt in) / "false" (opt out);
-// otherwise automatically for a gang-scheduled job whose ranks all request
-// exactly one GPU and fit one node (<= Options.gpus_per_node ranks).
+// Cost, to be accepted explicitly: privileged pods and hostIPC are rejected by
+// the PodSecurity "baseline" and "restricted" levels.  The namespace needs the
+// "privileged" level (or an exemption); otherwise pod creation fails and the
+// operator records a NodeLocalForbidden Warning event on the job
+// (operator/controller.py) instead of leaving it silently Pending.
+//
+// Requirements (else the layout is not applied and the job runs the
+// reference layout): a TFJob / PyTorchJob, 2 <= ranks <= Options.gpus_per_node,
+// every rank pod requesting exactly one GPU.  Without the annotation nothing
+// changes: no automatic selection.
 // Alternative considered and not taken: packing the ranks into ONE
 // `amd.com/gpu: N` pod launched with torchrun -- it collapses Worker=N into a
 // single replica and loses the per-replica semantics the CRD promises.
@@ -42,6 +62,7 @@ namespace toa {
 const char* kAnnNodeLocal = "amd.com/node-local";
 const char* kAnnGpuVisibility = "amd.com/gpu-visibility";
 const char* kLabelNodeLocal = "training.amd.com/node-local";
+const char* kPodResourcesDir = "/var/lib/kubelet/pod-resources";
 
 static bool is_rank_type(const std::string& kind, const std::string& rtype) {
   if (kind == "TFJob") return rtype == "Chief" || rtype == "Master" || rtype == "Worker";
@@ -61,11 +82,9 @@ bool node_local(const Json& job, const Options& opt) {
   const std::string kind = job_kind(job);
   if (kind != "TFJob" && kind != "PyTorchJob") return false;
   const std::string mode = lower(job.path({"metadata", "annotations"}).get(kAnnNodeLocal).str());
-  if (mode == "false") return false;
+  if (mode != "privileged" && mode != "true") return false;
   const int64_t world = rank_world(job);
   if (world < 2 || world > opt.gpus_per_node) return false;
-  if (mode == "true") return true;
-  if (!opt.enable_gang_scheduling) return false;
   for (const auto& kv : replica_specs(job).fields()) {
     if (!is_rank_type(kind, kv.first) || kv.second.is_null()) continue;
     if (pod_resource_request(kv.second, opt.gpu_resource) != 1.0) return false;
@@ -117,10 +136,9 @@ void apply_node_local(const Json& job, const std::string& rtype, Json& tpl, cons
   aff.set("podAffinity", pa);
   ps.set("affinity", aff);
 
-  // the node's GPUs, for peer access over xGMI
+  // the kubelet's pod-resources API: which GPU the device plugin gave THIS pod
   Json vols = ps.get("volumes").is_array() ? ps.get("volumes") : Json::array();
-  vols.push_back(host_path_volume("toa-dev-kfd", "/dev/kfd"));
-  vols.push_back(host_path_volume("toa-dev-dri", "/dev/dri"));
+  vols.push_back(host_path_volume("toa-pod-resources", kPodResourcesDir));
   ps.set("volumes", vols);
   Json& containers = ps["containers"];
   if (!containers.is_array() || containers.size() == 0) return;
@@ -129,14 +147,34 @@ void apply_node_local(const Json& job, const std::string& rtype, Json& tpl, cons
     if (containers.at(i).get("name").str() == ki.container) ci = i;
   Json& c = containers.at(ci);
   Json mounts = c.get("volumeMounts").is_array() ? c.get("volumeMounts") : Json::array();
-  static const char* const kMounts[2][2] = {{"toa-dev-kfd", "/dev/kfd"}, {"toa-dev-dri", "/dev/dri"}};
-  for (const auto& m : kMounts) {
-    Json vm = Json::object();
-    vm.set("name", m[0]);
-    vm.set("mountPath", m[1]);
-    mounts.push_back(vm);
-  }
+  Json vm = Json::object();
+  vm.set("name", "toa-pod-resources");
+  vm.set("mountPath", kPodResourcesDir);
+  vm.set("readOnly", true);
+  mounts.push_back(vm);
   c.set("volumeMounts", mounts);
+  // every GPU of the node in the container's device cgroup (peer access)
+  Json sc = c.get("securityContext").is_object() ? c.get("securityContext") : Json::object();
+  sc.set("privileged", true);
+  c.set("securityContext", sc);
+  // the pod's own identity, for the pod-resources lookup
+  Json env = c.get("env").is_array() ? c.get("env") : Json::array();
+  static const char* const kDownward[2][2] = {{"TOA_POD_NAME", "metadata.name"},
+                                              {"TOA_POD_NAMESPACE", "metadata.namespace"}};
+  for (const auto& d : kDownward) {
+    bool have = false;
+    for (size_t i = 0; i < env.size(); ++i) have = have || env.at(i).get("name").str() == d[0];
+    if (have) continue;
+    Json fr = Json::object();
+    fr.set("fieldPath", d[1]);
+    Json vf = Json::object();
+    vf.set("fieldRef", fr);
+    Json e = Json::object();
+    e.set("name", d[0]);
+    e.set("valueFrom", vf);
+    env.push_back(e);
+  }
+  c.set("env", env);
 }
 
 }  // namespace toa

@@ -1,0 +1,204 @@
+// Host side of the hand-written gfx950 assembly GEMMs (csrc/asm/gemm_gen.py).
+//
+// The build (tf_operator_amd/_build.py) generates the assembly, assembles and
+// links it into a code object and embeds the bytes here (toa_asm_blob.inc),
+// so the kernels live inside libtoa_hip.so like every other kernel: the
+// module is loaded from memory once per device on first use, and launches go
+// through hipModuleLaunchKernel on the caller's stream (graph-capturable).
+//
+//   toa_gemm_asm              C[M][N]  = X[M][K] W[N][K]^T
+//   toa_gemm_asm_swiglu       gu = X Wgu^T (Wgu = [gate; up], F rows each),
+//                             s = silu(gate) * up              (one launch)
+//   toa_gemm_asm_swiglu_bwd   dgu = SwiGLU'(gu) applied to ds = dY WdT^T
+//                             (ds never stored)                  (one launch)
+//
+// Shapes: M, N multiples of 256 (F of 128 forward / 256 backward), K a
+// multiple of 64 and >= 128, row strides multiples of 8 elements, 16-byte
+// aligned bases.  Anything else returns hipErrorInvalidValue before a launch
+// (callers fall back to another GEMM), so the kernel never sees a shape whose
+// tiles it does not cover.  The 80-byte argument block matches KARG in
+// gemm_gen.py (and csrc/asm/host_args.py, which the CPU emulator tests use).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+
+#include "toa_common.h"
+
+namespace {
+
+#include "toa_asm_blob.inc"  // const unsigned char toa_asm_blob[]; size_t toa_asm_blob_len
+
+constexpr int kMaxDev = 64;
+enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_N = 5 };
+const char* kNames[K_N] = {"toa_gemm_tn_asm_plain", "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
+                           "toa_gemm_tn_asm_probe", "toa_gemm_tn_asm_trace"};
+
+struct DevModule {
+  std::once_flag once;
+  hipError_t err = hipSuccess;
+  hipModule_t mod = nullptr;
+  hipFunction_t fn[K_N] = {};
+};
+DevModule g_mod[kMaxDev];
+
+hipFunction_t get_fn(int which, hipError_t* err) {
+  int dev = 0;
+  if ((*err = hipGetDevice(&dev)) != hipSuccess) return nullptr;
+  if (dev < 0 || dev >= kMaxDev) {
+    *err = hipErrorInvalidDevice;
+    return nullptr;
+  }
+  DevModule& m = g_mod[dev];
+  std::call_once(m.once, [&m]() {
+    m.err = hipModuleLoadData(&m.mod, toa_asm_blob);
+    for (int i = 0; m.err == hipSuccess && i < K_N; ++i) m.err = hipModuleGetFunction(&m.fn[i], m.mod, kNames[i]);
+  });
+  *err = m.err;
+  return m.err == hipSuccess ? m.fn[which] : nullptr;
+}
+
+struct __attribute__((packed)) Args {
+  uint64_t X, W, C, S;
+  uint32_t ldx, ldw, ldc, lds;  // bytes
+  uint32_t ktiles, tiles_m, tiles_n, xq, xr, per_group;
+  uint32_t fw, fc;  // swiglu: up-half row offset in W (bytes) / column offset in gu (bytes)
+};
+static_assert(sizeof(Args) == 80, "kernarg block must match csrc/asm/gemm_gen.py KARG_BYTES");
+
+bool ld_ok(int64_t ld, int64_t min_cols) { return ld >= min_cols && ld % 8 == 0 && ld * 2 * 256 < (1ll << 32); }
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int launch(int which, const Args& a, hipStream_t stream) {
+  hipError_t err;
+  hipFunction_t fn = get_fn(which, &err);
+  if (!fn) return (int)err;
+  Args k = a;
+  size_t sz = sizeof(k);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  const unsigned nwg = a.tiles_m * a.tiles_n;
+  return (int)hipModuleLaunchKernel(fn, nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
+}
+
+Args base_args(const void* X, int64_t ldx, const void* W, int64_t ldw, void* C, int64_t ldc, int M, int tiles_n,
+               int K) {
+  Args a;
+  memset(&a, 0, sizeof(a));
+  a.X = (uint64_t)X;
+  a.W = (uint64_t)W;
+  a.C = (uint64_t)C;
+  a.ldx = (uint32_t)(ldx * 2);
+  a.ldw = (uint32_t)(ldw * 2);
+  a.ldc = (uint32_t)(ldc * 2);
+  a.ktiles = (uint32_t)(K / 64);
+  a.tiles_m = (uint32_t)(M / 256);
+  a.tiles_n = (uint32_t)tiles_n;
+  const uint32_t nwg = a.tiles_m * a.tiles_n;
+  a.xq = nwg >> 3;
+  a.xr = nwg & 7;
+  a.per_group = 8 * a.tiles_n;
+  return a;
+}
+
+bool common_ok(int M, int K, int64_t ldx, int64_t ldw, const void* X, const void* W) {
+  return M > 0 && M % 256 == 0 && K >= 128 && K % 64 == 0 && ld_ok(ldx, K) && ld_ok(ldw, K) && al16(X) && al16(W) &&
+         (int64_t)(M / 256) < (1 << 20);
+}
+
+}  // namespace
+
+extern "C" int toa_gemm_asm_available() {
+  hipError_t err;
+  return get_fn(K_PLAIN, &err) != nullptr ? 1 : 0;
+}
+
+extern "C" int toa_gemm_asm(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C, int64_t ldc, int M,
+                            int N, int K, hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  return launch(K_PLAIN, a, stream);
+}
+
+// Diagnostic: the plain kernel ending after `stage` (1 = prologue DMA landed,
+// 2 = main loop done, 0 = everything), for bisecting a hardware fault.
+extern "C" int toa_gemm_asm_stage(int stage, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C,
+                                  int64_t ldc, int M, int N, int K, hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C) || stage < 0 || stage > 2)
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  a.fc = (uint32_t)stage;
+  return launch(K_PLAIN, a, stream);
+}
+
+// Diagnostic: host-coherent memory for the trace kernel (readable by the host
+// even after a device fault has poisoned the context).
+extern "C" void* toa_host_coherent_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+  memset(p, 0, bytes);
+  return p;
+}
+extern "C" int toa_host_free(void* p) { return (int)hipHostFree(p); }
+
+// Diagnostic: the plain kernel with progress markers (csrc/asm/gemm_gen.py
+// trace_mark) written system-coherently into `trace_host` (32 B per
+// workgroup and wave): after a fault, how far every wave got.
+extern "C" int toa_gemm_asm_trace(void* trace_host, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
+                                  bf16_t* C, int64_t ldc, int M, int N, int K, hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C) || !trace_host)
+    return (int)hipErrorInvalidValue;
+  void* dev = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dev, trace_host, 0);
+  if (e != hipSuccess) return (int)e;
+  Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  a.S = (uint64_t)dev;
+  return launch(K_TRACE, a, stream);
+}
+
+// Diagnostic: the plain kernel's prologue on the same arguments, every
+// workgroup b dumping its registers into out + b * 8704 B (csrc/asm/gemm_gen.py
+// probe_kernel).  `out` goes in the S slot and a magic value in fw / fc: an
+// argument block that arrives corrupted stores nothing.
+extern "C" int toa_gemm_asm_probe(void* out, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C,
+                                  int64_t ldc, int M, int N, int K, hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C) || !al16(out))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  a.S = (uint64_t)out;
+  a.fw = 0x626F7270u;
+  a.fc = 0x31657461u;
+  hipError_t err;
+  hipFunction_t fn = get_fn(K_PROBE, &err);
+  if (!fn) return (int)err;
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  return (int)hipModuleLaunchKernel(fn, a.tiles_m * a.tiles_n, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
+}
+
+extern "C" int toa_gemm_asm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* Wgu, int64_t ldw, bf16_t* GU,
+                                   int64_t ldgu, bf16_t* S, int64_t lds_, int M, int F, int K, hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, Wgu) || F <= 0 || F % 128 || !ld_ok(ldgu, 2 * F) || !ld_ok(lds_, F) || !al16(GU) ||
+      !al16(S) || (int64_t)F * ldw * 2 + 128 * ldw * 2 >= (1ll << 32))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, Wgu, ldw, GU, ldgu, M, F / 128, K);
+  a.S = (uint64_t)S;
+  a.lds = (uint32_t)(lds_ * 2);
+  a.fw = (uint32_t)((int64_t)F * ldw * 2);
+  a.fc = (uint32_t)(F * 2);
+  return launch(K_SWIGLU_FWD, a, stream);
+}
+
+extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16_t* WdT, int64_t ldw,
+                                       const bf16_t* GU, int64_t ldgu, bf16_t* dGU, int64_t lddgu, int M, int F, int K,
+                                       hipStream_t stream) {
+  if (!common_ok(M, K, ldy, ldw, dY, WdT) || F <= 0 || F % 256 || !ld_ok(ldgu, 2 * F) || !ld_ok(lddgu, 2 * F) ||
+      !al16(GU) || !al16(dGU))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(dY, ldy, WdT, ldw, dGU, lddgu, M, F / 256, K);
+  a.S = (uint64_t)GU;
+  a.lds = (uint32_t)(ldgu * 2);
+  a.fc = (uint32_t)(F * 2);
+  return launch(K_SWIGLU_BWD, a, stream);
+}

@@ -1,0 +1,271 @@
+"""Hand-written gfx950 assembly GEMM (csrc/asm/gemm_gen.py) vs hipBLASLt and
+the HIP TN kernel at the Llama-3-8B forward / data-gradient forms, in-process
+interleaved rounds on random operands (guide section 5.4 rules 24/25).
+
+    python scripts/asm_gemm_bench.py --check        # numerics only (small shapes)
+    python scripts/asm_gemm_bench.py [--tokens 24576] [--rounds 5] [--reps 5]
+
+Arms: asm (toa_gemm_asm), tn (csrc/hip/gemm_tn.hip default main loop),
+blt_nosk (hipBLASLt non-stream-K table), blt_heur (torch.matmul), and the
+fused MLP ends (asm SwiGLU epilogues vs hipBLASLt + the SwiGLU row kernels).
+"""
+import argparse
+import json
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from tf_operator_amd.ops import _lib, gemm, llm  # noqa: E402
+
+FORMS = {"qkv": (4096, 6144), "o": (4096, 4096), "gate_up": (4096, 28672), "down": (14336, 4096),
+         "lm_head": (4096, 128256)}
+
+
+def asm(x, w, y):
+    M, K = x.shape
+    N = w.shape[0]
+    _lib.call("toa_gemm_asm", _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), y.stride(0), M, N, K,
+              _lib.stream(x))
+
+
+def asm_swiglu(x, wgu):
+    M, F = x.shape[0], wgu.shape[0] // 2
+    gu = torch.empty(M, 2 * F, device=x.device, dtype=x.dtype)
+    s = torch.empty(M, F, device=x.device, dtype=x.dtype)
+    _lib.call("toa_gemm_asm_swiglu", _lib.ptr(x), x.stride(0), _lib.ptr(wgu), wgu.stride(0), _lib.ptr(gu), 2 * F,
+              _lib.ptr(s), F, M, F, x.shape[1], _lib.stream(x))
+    return gu, s
+
+
+def asm_swiglu_bwd(d2, wdt, gu):
+    M, F = d2.shape[0], wdt.shape[0]
+    dgu = torch.empty_like(gu)
+    _lib.call("toa_gemm_asm_swiglu_bwd", _lib.ptr(d2), d2.stride(0), _lib.ptr(wdt), wdt.stride(0), _lib.ptr(gu),
+              2 * F, _lib.ptr(dgu), 2 * F, M, F, d2.shape[1], _lib.stream(d2))
+    return dgu
+
+
+def rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm())
+
+
+def check():
+    torch.manual_seed(0)
+    res = {}
+    for (M, N, K) in ((256, 256, 128), (512, 768, 320), (1024, 512, 4096), (768, 1280, 192)):
+        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+        y = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        asm(x, w, y)
+        torch.cuda.synchronize()
+        res[f"plain_{M}x{N}x{K}"] = rel(y, x.float() @ w.float().t())
+    # strided rows (ld > K) and an output with ld > N
+    x = torch.randn(512, 384, device="cuda").to(torch.bfloat16)[:, :256]
+    w = torch.randn(256, 320, device="cuda").to(torch.bfloat16)[:, :256]
+    yb = torch.zeros(512, 512, device="cuda", dtype=torch.bfloat16)
+    asm(x, w, yb[:, 128:384])
+    torch.cuda.synchronize()
+    res["plain_strided"] = rel(yb[:, 128:384], x.float() @ w.float().t())
+    res["plain_strided_untouched"] = float(yb[:, :128].abs().sum() + yb[:, 384:].abs().sum())
+    M, F, K = 512, 384, 256
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    wgu = (torch.randn(2 * F, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    gu, s = asm_swiglu(x, wgu)
+    torch.cuda.synchronize()
+    ref = (x.float() @ wgu.float().t())
+    res["swiglu_fwd_gu"] = rel(gu, ref)
+    g, u = ref.bfloat16().float().split(F, 1)
+    res["swiglu_fwd_s"] = rel(s, torch.nn.functional.silu(g) * u)
+    M, F, K = 512, 512, 384
+    d2 = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    wdt = (torch.randn(F, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    gu = torch.randn(M, 2 * F, device="cuda").to(torch.bfloat16)
+    dgu = asm_swiglu_bwd(d2, wdt, gu)
+    torch.cuda.synchronize()
+    ds = (d2.float() @ wdt.float().t()).bfloat16().float()
+    g, u = gu.float().split(F, 1)
+    sg = torch.sigmoid(g)
+    res["swiglu_bwd_dg"] = rel(dgu[:, :F], ds * u * sg * (1 + g * (1 - sg)))
+    res["swiglu_bwd_du"] = rel(dgu[:, F:], ds * g * sg)
+    print(json.dumps({"check": res}), flush=True)
+    bad = {k: v for k, v in res.items() if not (v < 1e-2) and k != "plain_strided_untouched"}
+    if bad or res["plain_strided_untouched"] != 0:
+        raise SystemExit(f"asm GEMM numerics FAILED: {bad} untouched={res['plain_strided_untouched']}")
+
+
+def probe():
+    """Run the diagnostic kernel (plain prologue + register dump) and compare
+    its dump with the CPU emulator's run of the same instructions on the same
+    argument block.  Prints every differing SGPR / per-thread word."""
+    import os
+    import numpy as np
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "csrc", "asm"))
+    import emu
+    import gemm_gen
+    import host_args
+
+    res = {}
+    text = gemm_gen.generate()
+    # SGPRs that legitimately differ: kernarg pointer, per-wave values (the
+    # last wave to store wins), never-written scratch
+    skip = {0, 1, 27, 31, 48, 49, 50, 51, 52, 67, 68, 69, 70, 71, 72}
+    for (M, N, K) in ((256, 256, 128), (512, 768, 320), (768, 1280, 192), (1024, 512, 4096), (2048, 2048, 512)):
+        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+        y = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        nwg = (M // 256) * (N // 256)
+        out = torch.zeros(nwg * gemm_gen.PROBE_WORDS, device="cuda", dtype=torch.int32)
+        _lib.call("toa_gemm_asm_probe", _lib.ptr(out), _lib.ptr(x), K, _lib.ptr(w), K, _lib.ptr(y), N, M, N, K,
+                  _lib.stream(x))
+        torch.cuda.synchronize()
+        hw = out.cpu().numpy().view(np.uint32).reshape(nwg, -1)
+        karg = bytearray(host_args.pack(x.data_ptr(), w.data_ptr(), y.data_ptr(), out.data_ptr(), 2 * K, 2 * K,
+                                        2 * N, 0, K, M // 256, N // 256, gemm_gen.PROBE_MAGIC[0],
+                                        gemm_gen.PROBE_MAGIC[1]))
+        mem = emu.Memory()
+        ref = np.zeros(nwg * gemm_gen.PROBE_WORDS, np.uint32)
+        mem.add_at(out.data_ptr(), ref)
+        e = emu.Emu(text, "toa_gemm_tn_asm_probe")
+        for b in range(nwg):
+            e.run(bytes(karg), b, mem)
+        ref = ref.reshape(nwg, -1)
+        diff = [(b, int(i), hex(int(hw[b, i])), hex(int(ref[b, i]))) for b in range(nwg)
+                for i in np.nonzero(hw[b] != ref[b])[0] if int(i) not in skip]
+        res[f"{M}x{N}x{K}"] = {"nwg": nwg, "n_diff": len(diff), "first": diff[:40]}
+    print(json.dumps({"probe": res}), flush=True)
+
+
+def trace(shapes):
+    """Run the trace kernel per shape; print every wave's last marker (also
+    after a device fault: the records live in host-coherent memory)."""
+    import ctypes
+    import numpy as np
+    lib = _lib.lib()
+    for sh in shapes.split(","):
+        M, N, K = (int(v) for v in sh.split("x"))
+        nwg = (M // 256) * (N // 256)
+        nbytes = nwg * 4 * 32
+        host = lib.toa_host_coherent_alloc(nbytes)
+        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+        y = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        err = None
+        try:
+            _lib.call("toa_gemm_asm_trace", ctypes.c_void_p(host), _lib.ptr(x), K, _lib.ptr(w), K, _lib.ptr(y), N,
+                      M, N, K, _lib.stream(x))
+            torch.cuda.synchronize()
+        except Exception as e:  # a device fault: the trace is still readable
+            err = repr(e)[:300]
+        rec = np.frombuffer(ctypes.string_at(host, nbytes), dtype=np.uint32).reshape(nwg * 4, 8)
+        codes = {}
+        for r in rec:
+            codes[int(r[0])] = codes.get(int(r[0]), 0) + 1
+        out = {"shape": sh, "error": err, "last_code_counts": codes,
+               "records_first": rec[:8].tolist(), "records_min_code": rec[rec[:, 0].argmin()].tolist()}
+        if err is None:
+            out["rel"] = rel(y, x.float() @ w.float().t())
+        print(json.dumps(out), flush=True)
+        if err is not None:
+            raise SystemExit(1)
+
+
+def timer(fn, reps):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fn()
+    ev[0].record()
+    for _ in range(reps):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps
+
+
+def bench(a):
+    T = a.tokens
+    torch.manual_seed(0)
+    out = {"tokens": T, "forms": {}}
+    for name, (K, N) in FORMS.items():
+        for kind, (kk, nn) in (("fwd", (K, N)), ("dgrad_wt", (N, K))):
+            if a.forms and f"{name}.{kind}" not in a.forms.split(","):
+                continue
+            x = torch.randn(T, kk, device="cuda").to(torch.bfloat16)
+            w = (torch.randn(nn, kk, device="cuda") / kk ** 0.5).to(torch.bfloat16)
+            y = torch.empty(T, nn, device="cuda", dtype=torch.bfloat16)
+            arms = [("asm", lambda: asm(x, w, y)),
+                    ("blt_nosk", lambda: (gemm.set_mode("nosk"), gemm.linear_fwd(x, w))),
+                    ("blt_heur", lambda: torch.matmul(x, w.t()))]
+            if nn % 256 == 0 and kk % 128 == 0:
+                arms.append(("tn", lambda: _lib.call("toa_gemm_tn", _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn,
+                                                     T, nn, kk, _lib.stream(x))))
+            ts = {k: [] for k, _ in arms}
+            for _ in range(a.rounds):
+                for k, f in arms:
+                    ts[k].append(timer(f, a.reps))
+            asm(x, w, y)
+            err = rel(y, x.float() @ w.float().t()) if T * nn <= 24576 * 28672 else -1.0
+            fl = 2.0 * T * nn * kk
+            rec = {k: {"ms": round(statistics.median(v), 4), "TFps": round(fl / statistics.median(v) / 1e9, 1)}
+                   for k, v in ts.items()}
+            rec["asm_rel_err"] = round(err, 5)
+            out["forms"][f"{name}.{kind}"] = rec
+            print(json.dumps({f"{name}.{kind}": rec}), flush=True)
+            del x, w, y
+            torch.cuda.empty_cache()
+    if a.mlp:
+        F_, Hd = 14336, 4096
+        x = torch.randn(T, Hd, device="cuda").to(torch.bfloat16)
+        wgu = (torch.randn(2 * F_, Hd, device="cuda") / Hd ** 0.5).to(torch.bfloat16)
+        wdt = (torch.randn(F_, Hd, device="cuda") / Hd ** 0.5).to(torch.bfloat16)
+        d2 = torch.randn(T, Hd, device="cuda").to(torch.bfloat16)
+        gu, _ = asm_swiglu(x, wgu)
+        arms = [("asm_fused_fwd", lambda: asm_swiglu(x, wgu)),
+                ("blt_unfused_fwd", lambda: (gemm.set_mode("nosk"), llm.swiglu(gemm.linear_fwd(x, wgu)))),
+                ("asm_fused_bwd", lambda: asm_swiglu_bwd(d2, wdt, gu)),
+                ("blt_unfused_bwd", lambda: (gemm.set_mode("nosk"), llm.swiglu_bwd(gemm.linear_fwd(d2, wdt), gu)))]
+        ts = {k: [] for k, _ in arms}
+        for _ in range(a.rounds):
+            for k, f in arms:
+                ts[k].append(timer(f, a.reps))
+        out["mlp_ms"] = {k: round(statistics.median(v), 4) for k, v in ts.items()}
+        print(json.dumps({"mlp_ms": out["mlp_ms"]}), flush=True)
+    print(json.dumps(out))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--trace", default="", help="diagnostic: MxNxK shapes for the trace kernel, comma-separated")
+    ap.add_argument("--stage", type=int, default=-1, help="diagnostic: run the plain kernel to this stage only")
+    ap.add_argument("--tokens", type=int, default=24576)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--forms", default="")
+    ap.add_argument("--mlp", type=int, default=1)
+    a = ap.parse_args()
+    if a.probe:
+        probe()
+        return
+    if a.trace:
+        trace(a.trace)
+        return
+    if a.stage >= 0:
+        M, N, K = 256, 256, 128
+        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+        y = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        _lib.call("toa_gemm_asm_stage", a.stage, _lib.ptr(x), K, _lib.ptr(w), K, _lib.ptr(y), N, M, N, K,
+                  _lib.stream(x))
+        torch.cuda.synchronize()
+        print(json.dumps({"stage": a.stage, "ok": True,
+                          "rel": rel(y, x.float() @ w.float().t()) if a.stage == 0 else None}), flush=True)
+        return
+    check()
+    if not a.check:
+        bench(a)
+
+
+if __name__ == "__main__":
+    main()

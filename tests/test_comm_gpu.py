@@ -202,11 +202,14 @@ def _operator_env_worker(rank, world, port, env, q):
 
 
 @pytest.mark.timeout(240)
-def test_oneshot_auto_selected_under_operator_env():
-    """Verdict r2: the one-shot path was dead for every operator-launched
-    pod (LOCAL_WORLD_SIZE=1).  With the node-local env of a Worker=2 TFJob
-    it is auto-selected, small buckets go one-shot, the big one stays on the
-    process group, and the replicas stay identical."""
+def test_oneshot_under_operator_env():
+    """The node-local env of a Worker=2 TFJob makes the job one-shot
+    eligible (LOCAL_WORLD_SIZE = world).  On this one-GPU box both replicas
+    share the device over gloo, so automatic selection declines (it needs an
+    RCCL group, one GPU per rank -- ADVICE r3) and the path is forced here:
+    small buckets go one-shot, the big one stays on the process group, and
+    the replicas stay identical.  The automatic RCCL case is the pure
+    decision in tests/test_core_controller.py::test_oneshot_selection_under_operator_env."""
     from tf_operator_amd import core
 
     job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
@@ -216,6 +219,8 @@ def test_oneshot_auto_selected_under_operator_env():
     keep = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "TOA_NODE_LOCAL")
     envs = [{e["name"]: e["value"] for e in core.gen_env(job, "Worker", i) if e["name"] in keep} for i in range(2)]
     assert [e["LOCAL_WORLD_SIZE"] for e in envs] == ["2", "2"]
+    for e in envs:
+        e["TOA_IPC_ALLREDUCE"] = "1"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -228,7 +233,7 @@ def test_oneshot_auto_selected_under_operator_env():
     for rank, got, err in res:
         assert err is None, (rank, err)
         selected, reason, counts, same = got
-        assert selected and reason.startswith("auto"), (rank, reason)
+        assert selected and reason.startswith("forced"), (rank, reason)
         assert counts["oneshot"] > 0 and counts["collective"] > 0, (rank, counts)
         assert same, rank
 

@@ -529,11 +529,14 @@ def _gpu_job(workers, chief=0, ps=0, gpus=1, annotation=None):
 
 
 def test_node_local_pod_spec_and_env():
-    """Worker=8 gang-scheduled, one GPU each: every rank pod is co-located by
-    a required hostname podAffinity, gets hostIPC and the node's /dev/kfd +
-    /dev/dri, and LOCAL_RANK / LOCAL_WORLD_SIZE of the node (the hard-coded
-    0 / 1 of round 2 made the one-shot path unreachable)."""
-    job = _gpu_job(7, chief=1, ps=1)
+    """Worker=8 with amd.com/node-local: privileged, one GPU each: every rank
+    pod is co-located by a required hostname podAffinity, gets hostIPC, a
+    PRIVILEGED training container (a hostPath /dev/dri mount is not in the
+    device cgroup, so peers could not be opened), the kubelet's pod-resources
+    socket read-only and its own name / namespace from the downward API (the
+    trainer binds the GPU the device plugin allocated, not LOCAL_RANK), and
+    LOCAL_RANK / LOCAL_WORLD_SIZE of the node."""
+    job = _gpu_job(7, chief=1, ps=1, annotation="privileged")
     res = run(job, enable_gang_scheduling=True)
     pods = {p["pod"]["metadata"]["name"]: p["pod"] for p in ops(res, "create_pod")}
     w3 = pods["test-tfjob-worker-3"]
@@ -545,27 +548,48 @@ def test_node_local_pod_spec_and_env():
                                                     "training.amd.com/node-local": "true"}
     assert w3["metadata"]["labels"]["training.amd.com/node-local"] == "true"
     assert w3["metadata"]["annotations"]["amd.com/gpu-visibility"] == "node"
-    assert {v["hostPath"]["path"] for v in spec["volumes"]} == {"/dev/kfd", "/dev/dri"}
+    # no host device mounts: the privileged container's device cgroup is what grants peer access
+    assert [v["hostPath"]["path"] for v in spec["volumes"]] == ["/var/lib/kubelet/pod-resources"]
     c = spec["containers"][0]
-    assert {m["mountPath"] for m in c["volumeMounts"]} == {"/dev/kfd", "/dev/dri"}
-    env = {e["name"]: e["value"] for e in c["env"]}
+    assert c["securityContext"]["privileged"] is True
+    assert c["volumeMounts"] == [{"name": "toa-pod-resources", "mountPath": "/var/lib/kubelet/pod-resources",
+                                  "readOnly": True}]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    downward = {e["name"]: e["valueFrom"]["fieldRef"]["fieldPath"] for e in c["env"] if "valueFrom" in e}
+    assert downward == {"TOA_POD_NAME": "metadata.name", "TOA_POD_NAMESPACE": "metadata.namespace"}
     assert env["RANK"] == "4" and env["LOCAL_RANK"] == "4"  # chief is rank 0
     assert env["LOCAL_WORLD_SIZE"] == "8" and env["WORLD_SIZE"] == "8" and env["TOA_NODE_LOCAL"] == "1"
-    chief = {e["name"]: e["value"] for e in pods["test-tfjob-chief-0"]["spec"]["containers"][0]["env"]}
+    assert env["TOA_DEVICE_SOURCE"] == "pod-resources"
+    chief = {e["name"]: e.get("value") for e in pods["test-tfjob-chief-0"]["spec"]["containers"][0]["env"]}
     assert chief["LOCAL_RANK"] == "0" and chief["LOCAL_WORLD_SIZE"] == "8"
     ps = pods["test-tfjob-ps-0"]  # outside the RCCL world: unchanged
     assert "hostIPC" not in ps["spec"] and "affinity" not in ps["spec"]
+    assert "securityContext" not in ps["spec"]["containers"][0]
     assert "LOCAL_RANK" not in {e["name"] for e in ps["spec"]["containers"][0]["env"]}
 
 
+def test_node_local_keeps_user_security_context_and_env():
+    job = _gpu_job(2, annotation="privileged")
+    c0 = job["spec"]["tfReplicaSpecs"]["Worker"]["template"]["spec"]["containers"][0]
+    c0["securityContext"] = {"runAsUser": 1000}
+    c0["env"] = [{"name": "TOA_POD_NAME", "value": "explicit"}]
+    pod = ops(run(job), "create_pod")[0]["pod"]
+    c = pod["spec"]["containers"][0]
+    assert c["securityContext"] == {"runAsUser": 1000, "privileged": True}
+    names = [e["name"] for e in c["env"]]
+    assert names.count("TOA_POD_NAME") == 1 and names.count("TOA_POD_NAMESPACE") == 1
+
+
 @pytest.mark.parametrize("workers,gpus,annotation,gang,expected", [
-    (2, 1, None, False, False),    # no gang scheduling, no annotation: the classic layout
-    (2, 1, None, True, True),      # gang-scheduled, one GPU per rank, fits a node: automatic
-    (2, 1, "true", False, True),   # opt in
-    (8, 1, "false", True, False),  # opt out
-    (9, 1, "true", True, False),   # does not fit one 8-GPU node
-    (1, 1, "true", True, False),   # a single rank has no peers
-    (4, 2, None, True, False),     # automatic only with exactly one GPU per rank
+    (2, 1, None, False, False),          # no annotation: the reference layout
+    (2, 1, None, True, False),           # gang scheduling alone never selects it (opt-in only)
+    (2, 1, "privileged", False, True),   # opt in
+    (2, 1, "true", True, True),          # "true" is an alias of "privileged"
+    (8, 1, "false", True, False),        # explicit off
+    (8, 1, "host-mounts", True, False),  # unknown mode: off
+    (9, 1, "privileged", True, False),   # does not fit one 8-GPU node
+    (1, 1, "privileged", True, False),   # a single rank has no peers
+    (4, 2, "privileged", True, False),   # exactly one GPU per rank pod
 ])
 def test_node_local_selection(workers, gpus, annotation, gang, expected):
     job = _gpu_job(workers, gpus=gpus, annotation=annotation)
@@ -574,14 +598,16 @@ def test_node_local_selection(workers, gpus, annotation, gang, expected):
     env = {e["name"]: e["value"] for e in core.gen_env(job, "Worker", workers - 1, opts)}
     assert env["LOCAL_WORLD_SIZE"] == (str(workers) if expected else "1")
     assert env["LOCAL_RANK"] == (str(workers - 1) if expected else "0")
-    assert not core.node_local(_gpu_job(4), {"enable_gang_scheduling": True, "gpus_per_node": 2})
+    assert ("TOA_DEVICE_SOURCE" in env) is expected
+    assert not core.node_local(_gpu_job(4, annotation="privileged"), {"gpus_per_node": 2})
 
 
 def test_node_local_pytorchjob_env():
     tpl = fx.replica_template()
     tpl["spec"]["containers"][0]["name"] = "pytorch"
+    tpl["spec"]["containers"][0]["resources"] = {"limits": {"amd.com/gpu": 1}}
     job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
-           "metadata": {"name": "pt", "namespace": "default", "annotations": {"amd.com/node-local": "true"}},
+           "metadata": {"name": "pt", "namespace": "default", "annotations": {"amd.com/node-local": "privileged"}},
            "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "template": tpl},
                                             "Worker": {"replicas": 3, "template": tpl}}}}
     env = {e["name"]: e["value"] for e in core.gen_env(job, "Worker", 1)}
@@ -603,3 +629,7 @@ def test_oneshot_selection_under_operator_env():
     assert not ok and "span nodes" in why
     assert not ipc_decision("auto", 2, True, True, True, 0, "2")[0]  # nothing small enough
     assert not ipc_decision("0", 2, True, True, True, 1, "2")[0]
+    # a gloo group with GPU gradients (replicas possibly sharing one device): never automatic
+    ok, why = ipc_decision("auto", 2, True, True, True, 1, "2", backend="gloo")
+    assert not ok and "gloo" in why
+    assert ipc_decision("1", 2, True, True, True, 1, "2", backend="gloo")[0]  # forced still works

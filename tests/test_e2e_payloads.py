@@ -66,19 +66,28 @@ def test_dist_mnist_allreduce(cluster):
     assert "rank 0/3" in chief and "accuracy" in chief
 
 
-def test_dist_mnist_node_local_auto_oneshot(cluster):
-    """The node-local layout reaches the payload: both ranks get
-    LOCAL_WORLD_SIZE=2 from the operator (no TOA_IPC_ALLREDUCE in their
-    env), and GradBucketer's automatic selection finds the job eligible for
-    the one-shot IPC all-reduce -- here only the CPU gradients keep it on
-    gloo; on GPUs the same decision turns it on (tests/test_comm_gpu.py)."""
+def test_dist_mnist_node_local_auto_oneshot():
+    """The node-local layout (annotation amd.com/node-local: privileged, one
+    GPU per rank) reaches the payload: both ranks get LOCAL_WORLD_SIZE=2 from
+    the operator (no TOA_IPC_ALLREDUCE in their env), the local kubelet grants
+    node-wide visibility to the privileged containers and names each pod's
+    allocated device, and GradBucketer's automatic selection finds the job
+    eligible for the one-shot IPC all-reduce -- here only the CPU gradients
+    keep it on gloo; on GPUs with RCCL the same decision turns it on."""
     args = ("--train_steps", 40, "--log_every", 20, "--min_accuracy", 0.0)
-    job = tfjob("mnist-nl", {"Worker": rs(2, payload("dist_mnist", *args))},
-                annotations={"amd.com/node-local": "true"})
-    done, logs = _run(cluster, job)
+    job = tfjob("mnist-nl", {"Worker": rs(2, payload("dist_mnist", *args, gpus=1,
+                                                      env={"TOA_NO_GPU": "1"}))},
+                annotations={"amd.com/node-local": "privileged"})
+    with LocalCluster(gpus=2) as c2:
+        done, logs = _run(c2, job)
+        envs = {}
+        for name in ("mnist-nl-worker-0", "mnist-nl-worker-1"):
+            pod = c2.api.get("pods", "default", name)
+            envs[name] = c2.kubelet._build_env(pod, pod["spec"]["containers"][0], [int(name[-1])])
     assert "Succeeded" in conds(done), (conds(done), logs)
     for name in ("mnist-nl-worker-0", "mnist-nl-worker-1"):
         assert "one-shot IPC off (eligible (2 ranks on this node" in logs[name], logs[name]
+        assert envs[name]["TOA_LOCAL_DEVICE"] == name[-1] and "HIP_VISIBLE_DEVICES" not in envs[name]
 
 
 @pytest.mark.parametrize("sync", [False, True])

@@ -114,7 +114,8 @@ def _tfjob(name: str, n: int, command: list[str], env: dict | None = None, cold:
     # node-local xGMI layout (csrc/core/nodelocal.cc): the ranks share one
     # node, see each other's GPUs and get LOCAL_RANK / LOCAL_WORLD_SIZE of it
     return {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
-            "metadata": {"name": name, "namespace": "default", "annotations": {"amd.com/node-local": "true"}},
+            "metadata": {"name": name, "namespace": "default",
+                         "annotations": {"amd.com/node-local": "privileged"}},
             "spec": {"runPolicy": {"cleanPodPolicy": "All"},
                      "tfReplicaSpecs": {"Worker": {"replicas": n, "restartPolicy": "Never", "template": tpl}}}}
 
@@ -389,6 +390,18 @@ def summarize_rccl_log(path: str | None) -> dict | None:
     return {"version": ver, "channel_connections_by_transport": trans, "coll_channels": nch, "log": path}
 
 
+def transport_ok(summary: dict | None, n_ranks: int):
+    """True when every RCCL channel connection of this one-node job is P2P
+    (P2P/IPC, P2P/direct pointer, ...), False when any went SHM / NET, None
+    when unknown (no log, a single rank, or no channels parsed)."""
+    if not summary or n_ranks <= 1:
+        return None
+    trans = summary.get("channel_connections_by_transport") or {}
+    if not trans:
+        return None
+    return all(t.upper().startswith("P2P") for t in trans)
+
+
 def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_by: str = "replica",
                 t_probes_done: float | None = None) -> int:
     """t_probes_done: under torchrun rank 0 ran the latency probes before
@@ -527,6 +540,15 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
         rl = summarize_rccl_log(rccl_log)
         if rl:
             out["rccl"] = rl
+        ok = transport_ok(rl, n_gpus)
+        if ok is not None:
+            # one node: every channel must ride P2P (xGMI); SHM / NET means the
+            # ranks could not see each other's GPUs and this run measured the
+            # degraded path -- flagged in the record, not hidden
+            out["rccl_transport_ok"] = ok
+            if not ok:
+                print(f"[bench] WARNING: RCCL channels not all P2P on one node: "
+                      f"{rl['channel_connections_by_transport']}", file=sys.stderr, flush=True)
         if probe is not None:
             _attach_probe(out, probe)
         if args.result_file:

@@ -94,6 +94,10 @@ def main(argv=None):
         loss, _ = tr.step(*data.next())
         if (i + 1) % 10 == 0 or i + 1 == a.steps:
             rt.log(f"step {a.warmup + i + 1} loss {float(loss):.4f}")
+    if hasattr(tr, "sync_params"):
+        # sync PS: the last step's parameter pulls are part of the step (gloo
+        # work is not covered by cuda.synchronize), so they end inside the clock
+        tr.sync_params()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0

@@ -244,6 +244,34 @@ class FakeAPIServer:
                 return "metadata.name: Required value"
         return None
 
+    def _pod_security(self, obj):
+        """PodSecurity admission (the API server's built-in plugin) for
+        namespaces labelled pod-security.kubernetes.io/enforce = baseline or
+        restricted: host namespaces, privileged containers and hostPath
+        volumes are rejected with 403, message in the real server's format."""
+        ns = obj.get("metadata", {}).get("namespace", "default")
+        nso = self.objects["namespaces"].get((None, ns))
+        level = ((nso or {}).get("metadata", {}).get("labels") or {}).get("pod-security.kubernetes.io/enforce")
+        if level not in ("baseline", "restricted"):
+            return None
+        spec = obj.get("spec") or {}
+        why = []
+        hn = [f"{k}=true" for k in ("hostNetwork", "hostPID", "hostIPC") if spec.get(k)]
+        if hn:
+            why.append("host namespaces (" + ", ".join(hn) + ")")
+        priv = [c.get("name", "") for c in (spec.get("containers") or [])
+                if (c.get("securityContext") or {}).get("privileged")]
+        if priv:
+            why.append("privileged (" + ", ".join(f'container "{n}" must not set securityContext.privileged=true'
+                                                   for n in priv) + ")")
+        hp = [v.get("name", "") for v in (spec.get("volumes") or []) if "hostPath" in v]
+        if hp:
+            why.append("hostPath volumes (" + ", ".join(f'volume "{n}"' for n in hp) + ")")
+        if not why:
+            return None
+        return (f'pods "{obj.get("metadata", {}).get("name", "")}" is forbidden: violates PodSecurity '
+                f'"{level}:latest": ' + ", ".join(why))
+
     async def h_collection(self, req, key, ns):
         self.requests += 1
         if req.method == "GET":
@@ -269,6 +297,10 @@ class FakeAPIServer:
             err = self._admit(key, obj)
             if err:
                 return _status(422, "Invalid", err)
+            if key == "pods":
+                forbidden = self._pod_security(obj)
+                if forbidden:
+                    return _status(403, "Forbidden", forbidden)
             k = (md.get("namespace") if RESOURCES[key][1] else None, md["name"])
             if k in self.objects[key]:
                 return _status(409, "AlreadyExists", f'{key} "{md["name"]}" already exists')

@@ -174,7 +174,8 @@ class LocalKubelet:
         if warm_python is None:
             warm_python = os.environ.get("TOA_KUBELET_WARM", "0") == "1"
         self.warm_python = warm_python
-        self._fs = None  # fork server process
+        self._fs = None
+        self._pagecache = None  # fork server process
         self._fs_ready = None
         self._fs_pending: dict[int, asyncio.Future] = {}
         self._fs_procs: dict[int, _ForkedProc] = {}
@@ -368,18 +369,21 @@ class LocalKubelet:
         self.running[key] = rec
         rec["task"] = asyncio.create_task(self._run_pod(key, rec))
 
-    def _node_visible(self, pod) -> bool:
+    def _node_visible(self, pod, container) -> bool:
         """Node-wide GPU visibility for this pod: the node is configured that
-        way (TOA_KUBELET_DEVICES=node), or the pod asks for it -- the
-        operator's node-local layout (csrc/core/nodelocal.cc) marks its rank
-        pods with amd.com/gpu-visibility=node next to hostIPC and the
-        /dev/kfd + /dev/dri host mounts that give a real container the same
-        view."""
+        way (TOA_KUBELET_DEVICES=node), or the pod qualifies the way a real
+        node decides it.  A container sees the node's other GPUs only when
+        they are in its device cgroup, i.e. when it is privileged; a hostPath
+        mount of /dev/dri does not do it.  So: the operator's node-local mark
+        (amd.com/gpu-visibility=node, csrc/core/nodelocal.cc) AND hostIPC AND
+        this container privileged.  The annotation alone grants nothing."""
         if self.device_visibility == "node":
             return True
         md = pod.get("metadata") or {}
+        spec = pod.get("spec") or {}
         return ((md.get("annotations") or {}).get("amd.com/gpu-visibility") == "node"
-                and bool((pod.get("spec") or {}).get("hostIPC")))
+                and bool(spec.get("hostIPC"))
+                and (container.get("securityContext") or {}).get("privileged") is True)
 
     def _build_env(self, pod, container, gpus):
         env = {}
@@ -400,7 +404,7 @@ class LocalKubelet:
         base["TOA_POD_NAMESPACE"] = ns
         base["TOA_NODE_NAME"] = self.node
         base["PYTHONPATH"] = REPO_ROOT + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
-        if gpus and self._node_visible(pod):
+        if gpus and self._node_visible(pod, container):
             base.pop("HIP_VISIBLE_DEVICES", None)
             base.pop("TOA_NO_GPU", None)
             base["TOA_LOCAL_DEVICE"] = str(gpus[0])
@@ -725,6 +729,20 @@ class LocalKubelet:
         self._stop.set()
         for key in list(self.running):
             await self._kill(key)
+        pc, self._pagecache = self._pagecache, None
+        if pc is not None and pc.returncode is None:  # the page-cache warmer: end it, reap it
+            try:
+                os.killpg(pc.pid, signal.SIGTERM)
+            except (ProcessLookupError, PermissionError):
+                pass
+            try:
+                await asyncio.wait_for(pc.wait(), 5)
+            except asyncio.TimeoutError:
+                try:
+                    os.killpg(pc.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                await pc.wait()
         if self._fs is not None and self._fs.returncode is None:
             self._fs.stdin.close()  # the server's loop ends on EOF
             try:

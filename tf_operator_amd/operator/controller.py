@@ -349,6 +349,24 @@ class JobController:
                     self.expectations.creation_observed(a["expectation_key"])
                 if e.status in (404, 409):
                     return
+                if op == "create_pod":
+                    pod = a["pod"]
+                    pname = pod.get("metadata", {}).get("name", "")
+                    nl = (pod.get("metadata", {}).get("labels") or {}).get("training.amd.com/node-local") == "true"
+                    if e.status == 403 and nl and "PodSecurity" in str(e):
+                        # the node-local layout needs a privileged pod + hostIPC
+                        # (csrc/core/nodelocal.cc): say so instead of a silent Pending
+                        await self._emit_events(job, [{
+                            "type": "Warning", "reason": "NodeLocalForbidden",
+                            "message": f"Error creating pod {pname}: the node-local xGMI layout "
+                                       f"(annotation amd.com/node-local) needs a privileged container and hostIPC, "
+                                       f"which this namespace's PodSecurity level rejects; label the namespace "
+                                       f"pod-security.kubernetes.io/enforce=privileged or remove the annotation: "
+                                       f"{e}"}], job.get("kind"))
+                    else:
+                        # the Go controllers' FailedCreatePod event (kubeflow/common pod control)
+                        await self._emit_events(job, [{"type": "Warning", "reason": "FailedCreatePod",
+                                                       "message": f"Error creating: {e}"}], job.get("kind"))
                 if op == "delete_job":
                     await self._record_event(job, "Warning", "FailedDeleteJob", str(e))
                 log.warning("action %s failed: %s", op, e)

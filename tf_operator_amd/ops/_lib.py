@@ -83,6 +83,14 @@ _SIGS = {
     "toa_gemm_tn_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_tn_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_tn_set_variant": [c_int],
+    "toa_gemm_asm": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_asm_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_asm_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_asm_available": [],
+    "toa_gemm_asm_trace": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_host_free": [c_p],
+    "toa_gemm_asm_stage": [c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_asm_probe": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_attn_set_dkdv_variant": [c_int],
     "toa_attn_set_bwd_variant": [c_int],
     "toa_attn_set_kb_order": [c_int],
@@ -123,6 +131,9 @@ def _load():
         aw = getattr(lib, "toa_attn_bwd_ws_bytes", None)
         if aw is not None:
             aw.argtypes, aw.restype = [c_int, c_int, c_int, c_int], c_i64
+        ha = getattr(lib, "toa_host_coherent_alloc", None)
+        if ha is not None:
+            ha.argtypes, ha.restype = [ctypes.c_size_t], ctypes.c_void_p
         ww = getattr(lib, "toa_wgrad_workspace", None)
         if ww is not None:
             ww.argtypes, ww.restype = [c_int, c_int, c_int, c_int], c_i64

@@ -113,6 +113,7 @@ def _install():
 
 
 _prewarm_thread = None
+_prewarm_dev = None
 
 
 def prewarm(device=None, background: bool = True):
@@ -123,14 +124,19 @@ def prewarm(device=None, background: bool = True):
     caller initialises the process group and the model meanwhile -- and the
     thread is returned (the GEMM layer's lock orders the first real GEMM
     after it).  Idempotent; None when the policy uses no table."""
-    global _prewarm_thread
+    global _prewarm_thread, _prewarm_dev
     if _MODE not in ("tuned", "nosk", "hip") or not _lib.has("toa_gemm_prewarm"):
         return None
-    if _prewarm_thread is not None:
-        return _prewarm_thread
-    _install()
     dev = None if device is None else torch.device(device).index
     dev = torch.cuda.current_device() if dev is None else dev
+    if _prewarm_thread is not None:
+        if _prewarm_dev != dev:
+            # started for another device (a caller guessed LOCAL_RANK): the
+            # handle it built is not this replica's -- fail loudly
+            raise RuntimeError(f"GEMM prewarm ran on cuda:{_prewarm_dev}, trainer binds cuda:{dev}")
+        return _prewarm_thread
+    _install()
+    _prewarm_dev = dev
 
     def work():
         torch.cuda.set_device(dev)
@@ -145,16 +151,20 @@ def prewarm(device=None, background: bool = True):
 
 
 def prewarm_early():
-    """Start :func:`prewarm` at process start, on this replica's GPU
-    (LOCAL_RANK), before the process group and the model exist.  No-op off
-    the GPU, for the ``torch`` policy, or without the HIP library."""
+    """Start :func:`prewarm` at process start, on this replica's GPU (the
+    device train/dist.py binds: TOA_LOCAL_DEVICE, the pod-resources
+    allocation, else LOCAL_RANK), before the process group and the model
+    exist.  No-op off the GPU, for the ``torch`` policy, or without the HIP
+    library."""
     if not torch.cuda.is_available():
         return None
     resolve_auto()
+    from ..train import dist as tdist
+
     try:
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-    except ValueError:
-        local = 0
+        local = tdist.local_device_index()
+    except (ValueError, RuntimeError, LookupError):
+        return None  # the trainer's own init reports the binding error
     if local >= torch.cuda.device_count():
         return None
     return prewarm(torch.device("cuda", local))

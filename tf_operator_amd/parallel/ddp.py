@@ -28,9 +28,13 @@ from .flat import FlatParams, _round_up
 
 
 def ipc_decision(mode: str, world: int, reducing: bool, on_gpu: bool, dist_ready: bool, n_small: int,
-                 local_world_size: str | None):
+                 local_world_size: str | None, backend: str = "nccl"):
     """(use the one-shot IPC all-reduce?, why) -- a pure function of the
-    job's layout, so every rank decides alike."""
+    job's layout, so every rank decides alike.  Automatic selection needs an
+    RCCL group (backend "nccl"): RCCL puts every rank on its own GPU, which
+    is the layout the one-shot kernel's cross-process peer spinning is built
+    for; a gloo group with GPU gradients may be replicas SHARING one device
+    (TOA_DIST_BACKEND=gloo), where it is only ever forced (TOA_IPC_ALLREDUCE=1)."""
     if mode == "0":
         return False, "disabled (TOA_IPC_ALLREDUCE=0)"
     if not reducing:
@@ -51,6 +55,9 @@ def ipc_decision(mode: str, world: int, reducing: bool, on_gpu: bool, dist_ready
         return False, "every bucket is above the one-shot size"
     if not on_gpu:
         return False, f"eligible ({world} ranks on this node, {n_small} small buckets) but gradients are on the CPU"
+    if backend != "nccl":
+        return False, (f"eligible ({world} ranks on this node, {n_small} small buckets) but the process group is "
+                       f"{backend}: auto needs RCCL (one GPU per rank); TOA_IPC_ALLREDUCE=1 forces it")
     return True, f"auto: {world} ranks on this node, {n_small} bucket(s) <= {GradBucketer.IPC_MAX_BUCKET >> 20} MB"
 
 
@@ -125,9 +132,10 @@ class GradBucketer:
             return None
         mode = os.environ.get("TOA_IPC_ALLREDUCE", "auto")
         small = [(e - s) * esz for s, e, _ in self.buckets if (e - s) * esz <= self.IPC_MAX_BUCKET]
+        backend = dist.get_backend(group) if dist.is_initialized() else None
         ok, self.ipc_reason = ipc_decision(mode, self.world, self.enabled and not self.shard,
                                            flat.grad.is_cuda, dist.is_initialized(), len(small),
-                                           os.environ.get("LOCAL_WORLD_SIZE"))
+                                           os.environ.get("LOCAL_WORLD_SIZE"), str(backend))
         if not ok:
             return None
         from .ipc import IpcAllReduce

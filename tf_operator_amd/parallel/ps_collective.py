@@ -179,6 +179,10 @@ class CollectivePS:
         new parameters come back into ``flat.param``."""
         f = self.flat
         if self.mode == "sync":
+            # pulls of the previous step that no forward hook waited for
+            # (buckets whose modules did not run): the broadcasts below write
+            # the same parameters
+            self.wait_params()
             while self.next_bucket < len(self.buckets):  # buckets whose params got no gradient
                 self._launch(self.next_bucket)
                 self.next_bucket += 1
@@ -210,8 +214,9 @@ class CollectivePS:
             return
         for w in works:
             w.wait()
-        if not self.pulls:
-            self.flat.params_changed()
+        # per bucket: a cache keyed on the parameters (e.g. a bf16 copy) must
+        # not wait for buckets no forward touches
+        self.flat.params_changed()
 
     def wait_params(self):
         for b in list(self.pulls):

@@ -46,13 +46,29 @@ def env_rank_world():
     return 0, 1
 
 
+_DEVICE_CACHE: dict = {}
+
+
 def local_device_index() -> int:
-    """GPU this replica drives: ``TOA_LOCAL_DEVICE`` (the local kubelet's
-    node-visible mode names the pod's device there) else ``LOCAL_RANK``
-    (torchrun; 0 under per-pod HIP_VISIBLE_DEVICES pinning)."""
+    """GPU this replica drives:
+
+    * ``TOA_LOCAL_DEVICE`` when set (the local kubelet names the pod's device
+      in its node-visible mode);
+    * ``TOA_DEVICE_SOURCE=pod-resources`` (the operator's node-local layout,
+      csrc/core/nodelocal.cc): the GPU the kubelet allocated to this pod, by
+      PCI address (train/devices.py) -- never LOCAL_RANK, which on a node
+      shared with other jobs would pick another job's GPU; raises if the
+      kubelet cannot answer;
+    * else ``LOCAL_RANK`` (torchrun; 0 under per-pod device pinning)."""
     v = os.environ.get("TOA_LOCAL_DEVICE")
     if v not in (None, ""):
         return int(v)
+    if os.environ.get("TOA_DEVICE_SOURCE") == "pod-resources":
+        if "idx" not in _DEVICE_CACHE:
+            from . import devices
+
+            _DEVICE_CACHE["idx"] = devices.allocated_device_index()
+        return _DEVICE_CACHE["idx"]
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
