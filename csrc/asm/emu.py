@@ -448,7 +448,13 @@ class Emu:
             buf[rel + i] = data[:, i]
 
     def op_buffer_load_dwordx4(self, w, a, mods):
-        assert "lds" in mods and "offen" in mods, "only the LDS-DMA form is emulated"
+        if "lds" not in mods:
+            addr = self._buffer_addr(w, a[1:], mods, 16)
+            data = self._gread(addr, 16).view(np.uint32).reshape(64, 4)
+            lo, hi = self.vrange(w, a[0])
+            w.v[lo:hi] = data.T
+            return
+        assert "offen" in mods
         addr = self._buffer_addr(w, a, mods, 16)
         data = self._gread(addr, 16)
         dst = w.m0 + 16 * np.arange(64)
@@ -467,6 +473,11 @@ class Emu:
         addr = self._buffer_addr(w, a[1:], mods, 4)
         lo, hi = self.vrange(w, a[0])
         self._gwrite(addr, np.ascontiguousarray(w.v[lo]).view(np.uint8).reshape(64, 4))
+
+    def op_buffer_store_dwordx4(self, w, a, mods):
+        addr = self._buffer_addr(w, a[1:], mods, 16)
+        lo, hi = self.vrange(w, a[0])
+        self._gwrite(addr, np.ascontiguousarray(w.v[lo:hi].T).view(np.uint8).reshape(64, 16))
 
     def op_buffer_store_dwordx2(self, w, a, mods):
         addr = self._buffer_addr(w, a[1:], mods, 8)

@@ -288,22 +288,27 @@ def prologue(a: Asm, epi: str):
     a(f"v_lshl_add_u32 {vr(V_DX)}, {vr(v + 2)}, 4, {vr(v)}")
     a(f"v_mul_lo_u32 {vr(V_DX)}, {vr(V_DX)}, {sr(S_LDX)}")
     a(f"v_add_u32 {vr(V_DX)}, {vr(V_DX)}, {vr(v + 3)}")
+    # W: LDS row t = w + 4 jj + 16 q (q = lane >> 3) holds W row n(t) with
+    # n = 32 (q >> 1) + 8 jj + 4 (q & 1) + w, so MFMA fragments 2p and 2p+1
+    # give each lane 8 CONSECUTIVE output columns (16-byte epilogue stores).
+    # SwiGLU: the same within each 64-row half, q & 3 in place of q, the up
+    # half (q >> 2) F rows further.
+    qq = v + 2
+    a(f"v_and_b32 {vr(V_DW)}, {3 if epi == 'swiglu_fwd' else 7}, {vr(qq)}")
+    a(f"v_lshrrev_b32 {vr(V_DW)}, 1, {vr(V_DW)}")                 # (q[&3]) >> 1
+    a(f"v_lshlrev_b32 {vr(V_DW)}, 5, {vr(V_DW)}")                 # 32 (q >> 1)
+    a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v)}")               # + w
+    a(f"v_and_b32 {vr(V_E)}, 1, {vr(qq)}")                        # q & 1
+    a(f"v_lshl_add_u32 {vr(V_DW)}, {vr(V_E)}, 2, {vr(V_DW)}")     # + 4 (q & 1)
+    a(f"v_mul_lo_u32 {vr(V_DW)}, {vr(V_DW)}, {sr(S_LDW)}")
+    a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v + 3)}")           # + chunk bytes
     if epi == "swiglu_fwd":
-        # row = w + 16 ((lane>>3) & 3) [+ F rows when lane >> 5]
-        a(f"v_and_b32 {vr(V_DW)}, 3, {vr(v + 2)}")
-        a(f"v_lshl_add_u32 {vr(V_DW)}, {vr(V_DW)}, 4, {vr(v)}")
-        a(f"v_mul_lo_u32 {vr(V_DW)}, {vr(V_DW)}, {sr(S_LDW)}")
-        a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v + 3)}")
-        a(f"v_lshrrev_b32 {vr(v + 2)}, 2, {vr(v + 2)}")    # 0 / 1: gate / up
-        a(f"v_mul_lo_u32 {vr(v + 2)}, {vr(v + 2)}, {sr(S_FW)}")
-        a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v + 2)}")
-    else:
-        a(f"v_lshl_add_u32 {vr(V_DW)}, {vr(v + 2)}, 4, {vr(v)}")
-        a(f"v_mul_lo_u32 {vr(V_DW)}, {vr(V_DW)}, {sr(S_LDW)}")
-        a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(v + 3)}")
+        a(f"v_lshrrev_b32 {vr(V_E)}, 2, {vr(qq)}")                # 0 / 1: gate / up
+        a(f"v_mul_lo_u32 {vr(V_E)}, {vr(V_E)}, {sr(S_FW)}")
+        a(f"v_add_u32 {vr(V_DW)}, {vr(V_DW)}, {vr(V_E)}")
     for j in range(1, 8):
         rows_x = 4 * (j % 4) + 128 * (j // 4)
-        rows_w = 4 * (j % 4) + (UNIT_GATE_ROWS if epi == "swiglu_fwd" else 128) * (j // 4)
+        rows_w = 8 * (j % 4) + (UNIT_GATE_ROWS if epi == "swiglu_fwd" else 128) * (j // 4)
         a(f"s_mul_i32 {sr(S_SOX + j - 1)}, {sr(S_LDX)}, {rows_x}")
         a(f"s_mul_i32 {sr(S_SOW + j - 1)}, {sr(S_LDW)}, {rows_w}")
     # --- LDS-DMA bases (M0): wave w at line w of the stage's half
@@ -431,8 +436,9 @@ def acc_index(i: int, j: int) -> int:
 
 def epi_offsets(a: Asm, epi: str):
     """Per-lane output byte offsets.  Lane l of wave (wm, wn) holds, for
-    fragment pair (i, j): row m = wm*128 + 16 j + (l & 15) and columns
-    n = 16 i + 4 (l >> 4) .. +3 of the wave's W rows."""
+    fragments (2p, j) and (2p+1, j): row m = wm*128 + 16 j + (l & 15) and the
+    8 columns n = 32 p + 8 (l >> 4) .. +7 of the wave's W rows (the W-row
+    permutation of the DMA): one 16-byte store per pair p."""
     v = V_T
     a(f"v_lshrrev_b32 {vr(v)}, 6, {vr(V_TID)}")            # w
     a(f"v_and_b32 {vr(v + 1)}, 63, {vr(V_TID)}")           # lane
@@ -440,7 +446,7 @@ def epi_offsets(a: Asm, epi: str):
     a(f"v_and_b32 {vr(v + 3)}, 1, {vr(v)}")
     a(f"v_lshl_add_u32 {vr(v + 2)}, {vr(v + 3)}, 7, {vr(v + 2)}")  # row in tile
     a(f"v_lshrrev_b32 {vr(v + 1)}, 4, {vr(v + 1)}")        # lane >> 4
-    a(f"v_lshlrev_b32 {vr(v + 1)}, 3, {vr(v + 1)}")        # 8 B per lane group
+    a(f"v_lshlrev_b32 {vr(v + 1)}, 4, {vr(v + 1)}")        # 16 B per lane group
     a(f"v_lshrrev_b32 {vr(v)}, 1, {vr(v)}")                # wn
     # column bytes of the wave: plain / bwd 128 cols per wave, fwd 64 units
     a(f"v_lshlrev_b32 {vr(v)}, {8 if epi != 'swiglu_fwd' else 7}, {vr(v)}")
@@ -479,94 +485,125 @@ def unpack_bf16(a: Asm, dst: int, src: int):
 LOG2E = 1.4426950408889634
 
 
+def read_pair(a: Asm, dst: int, p: int, j: int, ioff: int = 0):
+    """dst[0..7] = the lane's 8 consecutive columns of fragments (2p, j) and
+    (2p+1, j) (ioff: fragment offset, 4 for SwiGLU's up half)."""
+    read_acc4(a, dst, acc_index(2 * p + ioff, j))
+    read_acc4(a, dst + 4, acc_index(2 * p + 1 + ioff, j))
+
+
+def cvt_pack8(a: Asm, dst: int, src: int):
+    cvt_pack(a, dst, src)
+    cvt_pack(a, dst + 2, src + 4)
+
+
+def unpack8(a: Asm, dst: int, src: int):
+    unpack_bf16(a, dst, src)
+    unpack_bf16(a, dst + 4, src + 2)
+
+
+def store16(a: Asm, data: int, voff: int, srd_: int, soff: int, p: int):
+    a(f"buffer_store_dwordx4 {vr(data, 4)}, {vr(voff)}, {sr(srd_, 4)}, {sr(soff)} offen offset:{64 * p} nt")
+
+
 def epilogue_plain(a: Asm):
     a(f"s_mov_b32 {sr(S_E0)}, 0")                             # row block offset
     a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")              # 16 rows
     for j in range(8):
-        base = V_E + 8
-        for i in range(8):
-            read_acc4(a, base + 4 * i, acc_index(i, j))
-        for i in range(8):
-            cvt_pack(a, V_E + 40 + 2 * i, base + 4 * i)
-        for i in range(8):
-            a(f"buffer_store_dwordx2 {vr(V_E + 40 + 2 * i, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+        f, pk = V_E + 8, V_E + 40                             # 32 f32, 16 packed
+        for p in range(4):
+            read_pair(a, f + 8 * p, p, j)
+        for p in range(4):
+            cvt_pack8(a, pk + 4 * p, f + 8 * p)
+        for p in range(4):
+            store16(a, pk + 4 * p, V_E, SRD_C, S_E0, p)
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
 
 
+def silu_times(a: Asm, out: int, g: int, u: int, t: int, n: int):
+    """out[e] = silu(g[e]) * u[e] = g / (1 + 2^(-g log2 e)) * u, e < n
+    (batched per op: a transcendental's result is consumed n instructions
+    later, past the forwarding hazard)."""
+    for e in range(n):
+        a(f"v_mul_f32 {vr(t + e)}, {vr(V_E + 3)}, {vr(g + e)}")
+    for e in range(n):
+        a(f"v_exp_f32 {vr(t + e)}, {vr(t + e)}")
+    for e in range(n):
+        a(f"v_add_f32 {vr(t + e)}, 1.0, {vr(t + e)}")
+    for e in range(n):
+        a(f"v_rcp_f32 {vr(t + e)}, {vr(t + e)}")
+    for e in range(n):
+        a(f"v_mul_f32 {vr(t + e)}, {vr(g + e)}, {vr(t + e)}")
+    for e in range(n):
+        a(f"v_mul_f32 {vr(out + e)}, {vr(t + e)}, {vr(u + e)}")
+
+
 def epilogue_swiglu_fwd(a: Asm):
-    """i = 0..3 gate fragments, i + 4 the same hidden units' up fragments."""
+    """Fragments 0..3 gate, 4..7 the same hidden units' up values: pairs
+    p = 0, 1 of each give a lane 8 consecutive units."""
     a(f"s_mov_b32 {sr(S_E0)}, 0")
     a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")
     a(f"s_mov_b32 {sr(S_T0)}, 0")
     a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 4")
     a(f"v_mov_b32 {vr(V_E + 3)}, {-LOG2E!r}")
     for j in range(8):
-        g, u = V_E + 8, V_E + 24          # 16 f32 each
-        for i in range(4):
-            read_acc4(a, g + 4 * i, acc_index(i, j))
-            read_acc4(a, u + 4 * i, acc_index(i + 4, j))
-        pg, pu = V_E + 40, V_E + 48       # packed bf16 (8 regs each)
-        for i in range(4):
-            cvt_pack(a, pg + 2 * i, g + 4 * i)
-            cvt_pack(a, pu + 2 * i, u + 4 * i)
-        for i in range(4):
-            a(f"buffer_store_dwordx2 {vr(pg + 2 * i, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
-            a(f"buffer_store_dwordx2 {vr(pu + 2 * i, 2)}, {vr(V_E + 2)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
+        g, u = V_E + 8, V_E + 24            # 16 f32 each (2 pairs)
+        for p in range(2):
+            read_pair(a, g + 8 * p, p, j)
+            read_pair(a, u + 8 * p, p, j, ioff=4)
+        pg, pu = V_E + 40, V_E + 48         # packed bf16 (8 regs each)
+        for p in range(2):
+            cvt_pack8(a, pg + 4 * p, g + 8 * p)
+            cvt_pack8(a, pu + 4 * p, u + 8 * p)
+        for p in range(2):
+            store16(a, pg + 4 * p, V_E, SRD_C, S_E0, p)
+            store16(a, pu + 4 * p, V_E + 2, SRD_C, S_E0, p)
         # s = silu(g) * u on the bf16-rounded values (what backward re-reads)
-        gf, uf, ps = V_E + 56, V_E + 72, V_E + 88
-        for i in range(4):
-            unpack_bf16(a, gf + 4 * i, pg + 2 * i)
-            unpack_bf16(a, uf + 4 * i, pu + 2 * i)
-        t = V_E + 96                      # 16 scratch
-        for e in range(16):
-            a(f"v_mul_f32 {vr(t + e)}, {vr(V_E + 3)}, {vr(gf + e)}")
-        for e in range(16):
-            a(f"v_exp_f32 {vr(t + e)}, {vr(t + e)}")
-        for e in range(16):
-            a(f"v_add_f32 {vr(t + e)}, 1.0, {vr(t + e)}")
-        for e in range(16):
-            a(f"v_rcp_f32 {vr(t + e)}, {vr(t + e)}")
-        for e in range(16):
-            a(f"v_mul_f32 {vr(t + e)}, {vr(gf + e)}, {vr(t + e)}")
-        for e in range(16):
-            a(f"v_mul_f32 {vr(t + e)}, {vr(t + e)}, {vr(uf + e)}")
-        for i in range(4):
-            cvt_pack(a, ps + 2 * i, t + 4 * i)
-        for i in range(4):
-            a(f"buffer_store_dwordx2 {vr(ps + 2 * i, 2)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{32 * i}")
+        gf, uf, sv, ps, t = V_E + 56, V_E + 72, V_E + 88, V_E + 104, V_E + 8   # t: g/u regs, consumed
+        for p in range(2):
+            unpack8(a, gf + 8 * p, pg + 4 * p)
+            unpack8(a, uf + 8 * p, pu + 4 * p)
+        for h in range(2):                  # 8 elements at a time (scratch t: 8 regs)
+            silu_times(a, sv + 8 * h, gf + 8 * h, uf + 8 * h, t, 8)
+        for p in range(2):
+            cvt_pack8(a, ps + 4 * p, sv + 8 * p)
+        for p in range(2):
+            store16(a, ps + 4 * p, V_E + 1, SRD_S, S_T0, p)
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
         a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T1)}")
+        a("s_waitcnt vmcnt(0)")             # scratch reused by the next row block
 
 
 def epilogue_swiglu_bwd(a: Asm):
-    """acc = ds (never stored).  gu rows: gate at n, up at F + n."""
+    """acc = ds (never stored).  gu rows: gate at n, up at F + n; pairs p of
+    fragments give 8 consecutive n per lane: 16-byte loads and stores."""
     a(f"s_mov_b32 {sr(S_E0)}, 0")                             # dgu row block
     a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")
     a(f"s_mov_b32 {sr(S_T0)}, 0")                             # gu row block
     a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 4")
     a(f"v_mov_b32 {vr(V_E + 4)}, {-LOG2E!r}")
     for j in range(8):
-        for half in range(2):             # fragments i = 4 half .. 4 half + 3
-            ig = [4 * half + q for q in range(4)]
-            lg, lu = V_E + 8, V_E + 16    # loaded packed gate / up (8 regs each)
-            for q, i in enumerate(ig):
-                a(f"buffer_load_dwordx2 {vr(lg + 2 * q, 2)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{32 * i}")
-                a(f"buffer_load_dwordx2 {vr(lu + 2 * q, 2)}, {vr(V_E + 3)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{32 * i}")
-            d = V_E + 24                  # 16 f32: ds
-            for q, i in enumerate(ig):
-                read_acc4(a, d + 4 * q, acc_index(i, j))
-            pd = V_E + 40                 # bf16-rounded ds, then unpacked
-            for q in range(4):
-                cvt_pack(a, pd + 2 * q, d + 4 * q)
-            for q in range(4):
-                unpack_bf16(a, d + 4 * q, pd + 2 * q)
+        for half in range(2):               # pairs p = 2 half, 2 half + 1
+            ps_ = (2 * half, 2 * half + 1)
+            lg, lu = V_E + 8, V_E + 16      # loaded packed gate / up (4 regs per pair)
+            for q, p in enumerate(ps_):
+                a(f"buffer_load_dwordx4 {vr(lg + 4 * q, 4)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{64 * p}")
+                a(f"buffer_load_dwordx4 {vr(lu + 4 * q, 4)}, {vr(V_E + 3)}, {sr(SRD_S, 4)}, {sr(S_T0)} offen offset:{64 * p}")
+            d = V_E + 24                    # 16 f32: ds
+            for q, p in enumerate(ps_):
+                read_pair(a, d + 8 * q, p, j)
+            pd = V_E + 40                   # bf16-rounded ds, then unpacked
+            for q in range(2):
+                cvt_pack8(a, pd + 4 * q, d + 8 * q)
+            for q in range(2):
+                unpack8(a, d + 8 * q, pd + 4 * q)
             a("s_waitcnt vmcnt(0)")
             gf, uf = V_E + 48, V_E + 64
-            for q in range(4):
-                unpack_bf16(a, gf + 4 * q, lg + 2 * q)
-                unpack_bf16(a, uf + 4 * q, lu + 2 * q)
+            for q in range(2):
+                unpack8(a, gf + 8 * q, lg + 4 * q)
+                unpack8(a, uf + 8 * q, lu + 4 * q)
             sg, tmp = V_E + 80, V_E + 96
-            for e in range(16):            # sg = 1 / (1 + exp(-g))
+            for e in range(16):             # sg = 1 / (1 + exp(-g))
                 a(f"v_mul_f32 {vr(sg + e)}, {vr(V_E + 4)}, {vr(gf + e)}")
             for e in range(16):
                 a(f"v_exp_f32 {vr(sg + e)}, {vr(sg + e)}")
@@ -574,29 +611,25 @@ def epilogue_swiglu_bwd(a: Asm):
                 a(f"v_add_f32 {vr(sg + e)}, 1.0, {vr(sg + e)}")
             for e in range(16):
                 a(f"v_rcp_f32 {vr(sg + e)}, {vr(sg + e)}")
-            for e in range(16):            # du = d * g * sg  -> tmp
+            for e in range(16):             # du = d * g * sg  -> tmp
                 a(f"v_mul_f32 {vr(tmp + e)}, {vr(d + e)}, {vr(gf + e)}")
                 a(f"v_mul_f32 {vr(tmp + e)}, {vr(tmp + e)}, {vr(sg + e)}")
-            for e in range(16):            # dg = d * u * sg * (1 + g (1 - sg)) -> uf
+            for e in range(16):             # dg = d * u * sg * (1 + g (1 - sg)) -> uf
                 a(f"v_sub_f32 {vr(lg)}, 1.0, {vr(sg + e)}")
                 a(f"v_fma_f32 {vr(lg)}, {vr(gf + e)}, {vr(lg)}, 1.0")
                 a(f"v_mul_f32 {vr(uf + e)}, {vr(d + e)}, {vr(uf + e)}")
                 a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(sg + e)}")
                 a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(lg)}")
-            pdg, pdu = V_E + 40, V_E + 112
-            for q in range(4):
-                cvt_pack(a, pdg + 2 * q, uf + 4 * q)
+            pdg, pdu = V_E + 40, V_E + 112  # 8 + 4 regs: reuse gf for the last du pair
             for q in range(2):
-                cvt_pack(a, pdu + 2 * q, tmp + 4 * q)
-            for q, i in enumerate(ig):
-                a(f"buffer_store_dwordx2 {vr(pdg + 2 * q, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
-            for q, i in enumerate(ig[:2]):
-                a(f"buffer_store_dwordx2 {vr(pdu + 2 * q, 2)}, {vr(V_E + 2)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
-            for q in range(2, 4):          # reuse gf for the last two packed du
-                cvt_pack(a, gf + 2 * (q - 2), tmp + 4 * q)
-            for q, i in enumerate(ig[2:]):
-                a(f"buffer_store_dwordx2 {vr(gf + 2 * q, 2)}, {vr(V_E + 2)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * i}")
-            a("s_waitcnt vmcnt(0)")        # scratch registers are reused next round
+                cvt_pack8(a, pdg + 4 * q, uf + 8 * q)
+            cvt_pack8(a, pdu, tmp)
+            cvt_pack8(a, gf, tmp + 8)
+            for q, p in enumerate(ps_):
+                store16(a, pdg + 4 * q, V_E, SRD_C, S_E0, p)
+            store16(a, pdu, V_E + 2, SRD_C, S_E0, ps_[0])
+            store16(a, gf, V_E + 2, SRD_C, S_E0, ps_[1])
+            a("s_waitcnt vmcnt(0)")         # scratch registers are reused next round
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
         a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T1)}")
 

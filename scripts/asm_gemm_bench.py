@@ -5,8 +5,8 @@ interleaved rounds on random operands (guide section 5.4 rules 24/25).
     python scripts/asm_gemm_bench.py --check        # numerics only (small shapes)
     python scripts/asm_gemm_bench.py [--tokens 24576] [--rounds 5] [--reps 5]
 
-Arms: asm (toa_gemm_asm), tn (csrc/hip/gemm_tn.hip default main loop),
-blt_nosk (hipBLASLt non-stream-K table), blt_heur (torch.matmul), and the
+Arms: asm (toa_gemm_asm), blt_nosk (hipBLASLt non-stream-K table),
+blt_heur (torch.matmul), and the
 fused MLP ends (asm SwiGLU epilogues vs hipBLASLt + the SwiGLU row kernels).
 """
 import argparse
@@ -196,9 +196,6 @@ def bench(a):
             arms = [("asm", lambda: asm(x, w, y)),
                     ("blt_nosk", lambda: (gemm.set_mode("nosk"), gemm.linear_fwd(x, w))),
                     ("blt_heur", lambda: torch.matmul(x, w.t()))]
-            if nn % 256 == 0 and kk % 128 == 0:
-                arms.append(("tn", lambda: _lib.call("toa_gemm_tn", _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn,
-                                                     T, nn, kk, _lib.stream(x))))
             ts = {k: [] for k, _ in arms}
             for _ in range(a.rounds):
                 for k, f in arms:

@@ -129,5 +129,5 @@ def test_bench_under_torchrun_four_ranks():
     r = _json_line(p.stdout)
     assert r["n_gpus"] == 4 and r["rccl_world"] == 4 and r["config"]["global_batch"] == 8
     assert r["replicas_identical"] is True and "ZeRO-1" in r["config"]["optimizer"]
-    assert r["config"]["gemm_policy"] == "nosk"
+    assert r["config"]["gemm_policy"] in ("asm", "nosk")  # asm when libtoa_hip carries the kernels
     assert r["submit_to_first_step_p50_s"] > 0

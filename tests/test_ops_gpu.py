@@ -1062,53 +1062,99 @@ def test_fused_batchnorm_momentum_none_matches_torch():
     assert rel(bn.running_var, ref.running_var) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [1, 0, 2, 3, 4, 5, 6])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 1536, 4096), (768, 512, 256)])
-def test_gemm_tn_matches_fp32(M, N, K, variant):
-    """csrc/hip/gemm_tn.hip plain epilogue: y = x w^T vs fp32 torch, with an
-    asymmetric non-square operand (guide §3: catch a transposed C write) and
-    padded row strides; every main loop (1 = full-line 64-k stages, 8 waves,
-    the default; 0 = 32-k stages; 2 = one wave per SIMD, 128 x 128 per wave;
-    3 = 1 with a per-tile k rotation; 4 = 1 with the DMA between the MFMAs;
-    5 = 0 with the DMA three stages ahead; 6 = full lines, five-slot ring)."""
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 384), (1024, 1536, 4096), (768, 512, 256),
+                                   (512, 256, 192), (2048, 1024, 1152)])
+def test_gemm_asm_matches_fp32(M, N, K):
+    """The hand-written assembly GEMM (csrc/asm/gemm_gen.py), plain epilogue:
+    y = x w^T vs fp32 torch, with an asymmetric non-square operand (guide
+    section 3: catch a transposed C write), padded row strides on every
+    operand, and K values that run 0, 1 and many main-loop iterations."""
     L = _lib()
     torch.manual_seed(M + N + K)
     xb = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K]
     w = (torch.randn(N, K, device=DEV) * 0.5 + torch.arange(N, device=DEV)[:, None] / N).to(torch.bfloat16)
-    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    L.call("toa_gemm_tn_set_variant", variant)
-    try:
-        L.call("toa_gemm_tn", L.ptr(xb), xb.stride(0), L.ptr(w), w.stride(0), L.ptr(y), N, M, N, K, L.stream(y))
-    finally:
-        L.call("toa_gemm_tn_set_variant", -1)
+    yb = torch.full((M, N + 256), 7.0, device=DEV, dtype=torch.bfloat16)
+    y = yb[:, 128:128 + N]
+    L.call("toa_gemm_asm", L.ptr(xb), xb.stride(0), L.ptr(w), w.stride(0), L.ptr(y), yb.stride(0), M, N, K, L.stream(y))
     ref = xb.float() @ w.float().t()
     torch.cuda.synchronize()
     assert rel(y, ref) < 1e-2, rel(y, ref)
+    assert bool((yb[:, :128] == 7.0).all()) and bool((yb[:, 128 + N:] == 7.0).all())  # nothing outside C
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 512, 128), (2048, 1024, 4096), (512, 768, 640), (256, 512, 1152)])
-def test_gemm_tn_main_loops_bit_identical(M, N, K):
-    """Every main loop sums the same 32-k MFMA chunks in the same order, so
-    they agree bit for bit (a staging race or a wrong swizzle shows up as a
-    difference)."""
+@pytest.mark.parametrize("M,N,K", [(512, 512, 128), (2048, 1024, 4096), (768, 1280, 640)])
+def test_gemm_asm_repeatable_bit_for_bit(M, N, K):
+    """Eleven launches agree bit for bit: the k order is fixed, so a staging
+    race (an LDS stage read before its DMA landed, or overwritten while
+    read) shows up as a difference."""
     L = _lib()
     torch.manual_seed(K)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
     ys = []
-    for v in (0, 1, 2, 4, 5, 6, 1, 2, 4, 5, 6):
+    for _ in range(11):
         y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        L.call("toa_gemm_tn_set_variant", v)
-        L.call("toa_gemm_tn", L.ptr(x), K, L.ptr(w), K, L.ptr(y), N, M, N, K, L.stream(y))
+        L.call("toa_gemm_asm", L.ptr(x), K, L.ptr(w), K, L.ptr(y), N, M, N, K, L.stream(y))
         ys.append(y)
-    L.call("toa_gemm_tn_set_variant", -1)
     torch.cuda.synchronize()
     for y in ys[1:]:
         assert torch.equal(ys[0], y)
 
 
+def test_gemm_asm_rejects_shapes_it_does_not_tile():
+    """The launcher refuses (hipErrorInvalidValue) rather than run a shape
+    whose tiles the kernel does not cover."""
+    L = _lib()
+    x = torch.randn(256, 128, device=DEV).to(torch.bfloat16)
+    w = torch.randn(256, 128, device=DEV).to(torch.bfloat16)
+    y = torch.empty(256, 256, device=DEV, dtype=torch.bfloat16)
+    for M, N, K in ((255, 256, 128), (256, 200, 128), (256, 256, 96), (256, 256, 64)):
+        rc = L.call_ret("toa_gemm_asm", L.ptr(x), 128, L.ptr(w), 128, L.ptr(y), 256, M, N, K, L.stream(y))
+        assert rc != 0, (M, N, K)
+
+
+def test_gemm_asm_prologue_matches_emulator():
+    """The diagnostic probe kernel runs the plain kernel's prologue (tile
+    mapping, buffer resources, DMA and fragment offsets) and dumps every
+    register; the CPU emulator of the same instructions must agree for every
+    workgroup (this caught a v_readfirstlane read-after-write hazard)."""
+    import os
+    import sys
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "asm"))
+    import emu
+    import gemm_gen
+    import host_args
+
+    L = _lib()
+    skip = {0, 1, 27, 31, 48, 49, 50, 51, 52, 67, 68, 69, 70, 71, 72}
+    text = gemm_gen.generate()
+    for M, N, K in ((512, 768, 320), (2048, 1280, 256)):
+        x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+        w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+        y = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        nwg = (M // 256) * (N // 256)
+        out = torch.zeros(nwg * gemm_gen.PROBE_WORDS, device=DEV, dtype=torch.int32)
+        L.call("toa_gemm_asm_probe", L.ptr(out), L.ptr(x), K, L.ptr(w), K, L.ptr(y), N, M, N, K, L.stream(x))
+        torch.cuda.synchronize()
+        hw = out.cpu().numpy().view(np.uint32).reshape(nwg, -1)
+        karg = host_args.pack(x.data_ptr(), w.data_ptr(), y.data_ptr(), out.data_ptr(), 2 * K, 2 * K, 2 * N, 0, K,
+                              M // 256, N // 256, *gemm_gen.PROBE_MAGIC)
+        ref = np.zeros(nwg * gemm_gen.PROBE_WORDS, np.uint32)
+        mem = emu.Memory()
+        mem.add_at(out.data_ptr(), ref)
+        e = emu.Emu(text, "toa_gemm_tn_asm_probe")
+        for b in range(nwg):
+            e.run(karg, b, mem)
+        ref = ref.reshape(nwg, -1)
+        bad = [(b, i) for b in range(nwg) for i in np.nonzero(hw[b] != ref[b])[0] if int(i) not in skip]
+        assert not bad, bad[:10]
+
+
 @pytest.mark.parametrize("M,F,K", [(256, 128, 128), (512, 384, 256), (1024, 1024, 1024)])
-def test_gemm_tn_swiglu_epilogues(M, F, K):
+def test_gemm_asm_swiglu_epilogues(M, F, K):
     """Fused SwiGLU forward (gu and s from one GEMM, W kept [gate; up]) and
     backward (dgu from the down projection's data gradient, ds never
     stored) vs fp32 references."""
@@ -1119,7 +1165,7 @@ def test_gemm_tn_swiglu_epilogues(M, F, K):
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     wgu = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
     old = gemm.mode()
-    gemm.set_mode("hip")
+    gemm.set_mode("asm")
     try:
         gu, s = gemm.swiglu_gate_up(x, wgu)
         ref_gu = x.float() @ wgu.float().t()
@@ -1141,14 +1187,14 @@ def test_gemm_tn_swiglu_epilogues(M, F, K):
 
 
 def test_llama_layer_fused_mlp_matches_library_path():
-    """A llama-tiny128 training step with the hand-written TN GEMMs and the
-    fused SwiGLU (TOA_GEMM=hip) follows the hipBLASLt path's loss."""
+    """A llama-tiny128 training step with the assembly GEMMs and the fused
+    SwiGLU (TOA_GEMM=asm, the default) follows the hipBLASLt path's loss."""
     from tf_operator_amd.ops import gemm
     from tf_operator_amd.train.llm import LlamaTrainer
 
     _lib()
     losses = {}
-    for mode in ("nosk", "hip"):
+    for mode in ("nosk", "asm"):
         gemm.set_mode(mode)
         try:
             tr = LlamaTrainer("llama-tiny128", torch.device(DEV), micro_batch=2, seq_len=256, seed=0)
@@ -1157,5 +1203,5 @@ def test_llama_layer_fused_mlp_matches_library_path():
             del tr
         finally:
             gemm.set_mode("auto")
-    for a, b in zip(losses["nosk"], losses["hip"]):
+    for a, b in zip(losses["nosk"], losses["asm"]):
         assert abs(a - b) < 2e-2 * abs(a), losses

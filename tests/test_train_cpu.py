@@ -143,7 +143,7 @@ def test_fused_batchnorm_momentum_none_is_cumulative_average():
 
 
 def test_fused_swiglu_mlp_autograd_matches_unfused():
-    """ops.llm.swiglu_mlp under TOA_GEMM=hip (the fused-GEMM autograd
+    """ops.llm.swiglu_mlp under TOA_GEMM=asm (the fused-GEMM autograd
     function; on the CPU its GEMMs take the library fallbacks) gives the
     unfused path's output and gradients, weight gradients into main_grad."""
     from tf_operator_amd.ops import gemm, llm
@@ -153,7 +153,7 @@ def test_fused_swiglu_mlp_autograd_matches_unfused():
     T, Hd, F_ = 64, 32, 48
     x0 = torch.randn(T, Hd)
     outs = []
-    for mode in ("torch", "hip"):
+    for mode in ("torch", "asm"):
         wgu = torch.nn.Parameter(torch.randn(2 * F_, Hd) * 0.2)
         wd = torch.nn.Parameter(torch.randn(Hd, F_) * 0.2)
         with torch.no_grad():
@@ -206,4 +206,4 @@ def test_gemm_prewarm_is_a_noop_off_the_gpu(monkeypatch):
         gemm.set_mode(old)
     tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device("cpu"), micro_batch=1, seq_len=16)
     assert tr._gemm_prewarm is None
-    assert tr.gemm_mode in ("nosk", "torch", "tuned", "hip")
+    assert tr.gemm_mode in ("nosk", "torch", "tuned", "asm")

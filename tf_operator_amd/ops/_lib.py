@@ -79,10 +79,6 @@ _SIGS = {
                    c_p],
     "toa_gemm_set_no_streamk": [c_int],
     "toa_gemm_prewarm": [],
-    "toa_gemm_tn": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
-    "toa_gemm_tn_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
-    "toa_gemm_tn_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
-    "toa_gemm_tn_set_variant": [c_int],
     "toa_gemm_asm": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_swiglu": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_swiglu_bwd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],

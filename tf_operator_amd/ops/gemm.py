@@ -14,33 +14,26 @@ heuristic.
 
 Modes (``TOA_GEMM``):
 
-* ``torch`` (default at world 1): torch.matmul, i.e. hipBLASLt's own
-  heuristic.  Measured on the MI355X (profiles/r1_gemm_tuning*.log,
-  r1_gemm_ab_*.log): per-form winners picked in isolation are 2-22 % faster
-  alone, yet the full Llama-3-8B step was ~1.3 % SLOWER with them -- a
-  solution picked alone is not the best one in the sustained, power-limited
-  sequence of the real step.
+* ``asm``: the hand-written gfx950 assembly GEMM (csrc/asm/gemm_gen.py,
+  launched from csrc/hip/gemm_asm.hip) for every forward / data-gradient
+  GEMM whose shape it takes (M, N multiples of 256, K a multiple of 64 and
+  >= 128 -- all Llama forms), with the Llama MLP's SwiGLU fused into the
+  gate|up projection's epilogue and its backward into the down projection's
+  data gradient (``ops.llm.swiglu_mlp``); anything else as ``nosk``.  No
+  hipBLASLt table to load, so nothing to prewarm for these forms.
+  ``hip`` is an alias (it named the round-3 HIP TN kernel this replaced).
+* ``torch``: torch.matmul, i.e. hipBLASLt's own heuristic.  Per-form
+  winners picked in isolation were 2-22 % faster alone, yet the full
+  Llama-3-8B step was ~1.3 % SLOWER with them (profiles/r1_gemm_*).
 * ``tuned``: the measured per-form table (``gemm_tuning_gfx950.json``).
 * ``nosk``: the fastest solution per form among those that are NOT
   stream-K (``gemm_tuning_gfx950_nosk.json``, ``scripts/tune_gemm.py
-  --exclude-streamk``; forms not in the table take the heuristic's best
-  non-stream-K solution).  hipBLASLt's stream-K kernels run one persistent
-  workgroup per CU holding the whole register file: a collective on another
-  stream either gets no CU until the GEMM ends or, once resident, holds
-  back one of the GEMM's workgroups for its whole duration
-  (profiles/r2_sk_contention).  With world-8 ZeRO-1 traffic emulated on
-  one MI355X (profiles/r3_overlap) the collectives cost the stream-K step
-  +6.7 % and the nosk step +3.4 %, at equal step time without traffic.
-* ``hip``: the hand-written TN kernel (csrc/hip/gemm_tn.hip) for the
-  forward and data-gradient GEMMs whose shapes it takes (M, N multiples of
-  256, K of 128), with the Llama MLP's SwiGLU fused into the gate|up
-  projection's epilogue and its backward into the down projection's data
-  gradient (``ops.llm.swiglu_mlp``); everything else as ``nosk``.
-* ``auto`` (the default): ``nosk``, resolved by :func:`resolve_auto` when
-  the trainer starts.  At world 1 the two are equal in-model (996.5 vs
-  999.2 ms/step, two alternating runs each on one box,
-  profiles/r3_gemm_policy); from world 2 on the collectives overlap the
-  GEMMs and nosk is the one that tolerates it.
+  --exclude-streamk``).  Stream-K kernels hold one workgroup per CU for the
+  whole GEMM, so a collective on another stream gets no CU until it ends
+  (profiles/r2_sk_contention; +6.7 % vs +3.4 % under emulated world-8
+  ZeRO-1 traffic, profiles/r3_overlap).
+* ``auto`` (the default): resolved by :func:`resolve_auto` when the trainer
+  starts -- ``asm`` when the kernel library carries it, else ``nosk``.
 """
 from __future__ import annotations
 
@@ -57,6 +50,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 TABLE = os.path.join(_HERE, "gemm_tuning_gfx950.json")
 TABLE_NOSK = os.path.join(_HERE, "gemm_tuning_gfx950_nosk.json")
 _MODE = os.environ.get("TOA_GEMM", "auto")
+if _MODE == "hip":
+    _MODE = "asm"
 _installed = False
 
 
@@ -67,19 +62,20 @@ def mode() -> str:
 def set_mode(m: str):
     """Select the GEMM policy for this process (before the first GEMM)."""
     global _MODE, _installed
-    if m not in ("auto", "torch", "tuned", "nosk", "hip"):
+    if m not in ("auto", "torch", "tuned", "nosk", "hip", "asm"):
         raise ValueError(f"unknown GEMM mode {m!r}")
-    _MODE = m
+    _MODE = "asm" if m == "hip" else m
     _installed = False
 
 
 def resolve_auto(world: int = 1) -> str:
-    """``auto`` -> ``nosk`` (an explicit TOA_GEMM is kept).  Returns the mode
-    in force.  `world` is kept for the policy record: the choice does not
-    depend on it since world-1 steps measured equal."""
+    """``auto`` -> ``asm`` when the library has the assembly kernels, else
+    ``nosk`` (an explicit TOA_GEMM is kept).  Returns the mode in force.
+    The assembly kernel is not persistent (one workgroup per tile), so under
+    world-N collectives it yields CUs as tiles retire, like ``nosk``."""
     del world
     if _MODE == "auto":
-        set_mode("nosk")
+        set_mode("asm" if _lib.has("toa_gemm_asm") else "nosk")
     return _MODE
 
 
@@ -98,8 +94,8 @@ def _install():
         return
     _installed = True
     if _lib.has("toa_gemm_set_no_streamk"):
-        _lib.call("toa_gemm_set_no_streamk", int(_MODE in ("nosk", "hip")))
-    table = TABLE_NOSK if _MODE in ("nosk", "hip") else TABLE
+        _lib.call("toa_gemm_set_no_streamk", int(_MODE in ("nosk", "asm")))
+    table = TABLE_NOSK if _MODE in ("nosk", "asm") else TABLE
     if not os.path.exists(table):
         return
     with open(table) as f:
@@ -125,7 +121,7 @@ def prewarm(device=None, background: bool = True):
     thread is returned (the GEMM layer's lock orders the first real GEMM
     after it).  Idempotent; None when the policy uses no table."""
     global _prewarm_thread, _prewarm_dev
-    if _MODE not in ("tuned", "nosk", "hip") or not _lib.has("toa_gemm_prewarm"):
+    if _MODE not in ("tuned", "nosk") or not _lib.has("toa_gemm_prewarm"):
         return None
     dev = None if device is None else torch.device(device).index
     dev = torch.cuda.current_device() if dev is None else dev
@@ -171,7 +167,7 @@ def prewarm_early():
 
 
 def _ok(*ts):
-    if _MODE not in ("tuned", "nosk", "hip") or not _lib.has("toa_gemm"):
+    if _MODE not in ("tuned", "nosk", "asm") or not _lib.has("toa_gemm"):
         return False
     for t in ts:
         if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
@@ -185,10 +181,12 @@ def _gemm(ta, tb, m, n, k, a, lda, b, ldb, c, ldc, beta):
               int(c.dtype == torch.float32), _lib.stream(c))
 
 
-def _tn_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
-    """Operands csrc/hip/gemm_tn.hip takes: bf16 GPU rows with unit column
-    stride, 16-byte aligned, M and N multiples of 256 (n_mult), K of 128."""
-    if not _lib.has("toa_gemm_tn"):
+def _asm_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
+    """Operands the assembly GEMM takes (csrc/hip/gemm_asm.hip checks the
+    same and refuses anything else): bf16 GPU rows with unit column stride,
+    16-byte aligned rows, M and N multiples of 256 (n_mult), K a multiple of
+    64 and >= 128."""
+    if _MODE != "asm" or not _lib.has("toa_gemm_asm"):
         return False
     if not (x2.is_cuda and x2.dtype == w.dtype == torch.bfloat16 and x2.dim() == 2 and w.dim() == 2):
         return False
@@ -196,32 +194,15 @@ def _tn_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
         return False
     M, K = x2.shape
     N = w.shape[0]
-    return (M % 256 == 0 and N % n_mult == 0 and K % 128 == 0 and w.shape[1] == K
+    return (M % 256 == 0 and N % n_mult == 0 and K % 64 == 0 and K >= 128 and w.shape[1] == K
             and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _lib.use_hip(x2))
 
 
-def _tn_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
-    return _MODE == "hip" and _tn_shape_ok(x2, w, n_mult)
-
-
-# TOA_GEMM_TN_FIRST=0: the first step waits for the hipBLASLt table instead
-_TN_FIRST = os.environ.get("TOA_GEMM_TN_FIRST", "1") != "0"
-
-
-def _prewarm_pending() -> bool:
-    """True while the helper thread is still resolving the hipBLASLt table
-    (~0.47 s of code-object loading from process start): the first step's
-    forward / data-gradient GEMMs then run on the hand-written TN kernel
-    instead of waiting for the library (profiles/r3_first)."""
-    th = _prewarm_thread
-    return _TN_FIRST and th is not None and th.is_alive()
-
-
 def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    if _tn_ok(x2, w) or (_prewarm_pending() and _tn_shape_ok(x2, w)):
+    if _asm_shape_ok(x2, w):
         M, N = x2.shape[0], w.shape[0]
         y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
-        _lib.call("toa_gemm_tn", _lib.ptr(x2), x2.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), N, M, N,
+        _lib.call("toa_gemm_asm", _lib.ptr(x2), x2.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), N, M, N,
                   x2.shape[1], _lib.stream(x2))
         return y
     if not _ok(x2, w):
@@ -247,28 +228,29 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 def swiglu_gate_up(x2: torch.Tensor, wgu: torch.Tensor):
-    """(gu, s) = (x Wgu^T, silu(gate) * up) from ONE hand-written GEMM with
-    the SwiGLU in its epilogue; None when the TN kernel cannot take it."""
-    if not (_tn_ok(x2, wgu) and (wgu.shape[0] // 2) % 128 == 0):
+    """(gu, s) = (x Wgu^T, silu(gate) * up) from ONE assembly GEMM with the
+    SwiGLU in its epilogue; None when the kernel cannot take the shapes."""
+    if not (_asm_shape_ok(x2, wgu, n_mult=2) and (wgu.shape[0] // 2) % 128 == 0):
         return None
     M, F = x2.shape[0], wgu.shape[0] // 2
     gu = torch.empty(M, 2 * F, device=x2.device, dtype=x2.dtype)
     s = torch.empty(M, F, device=x2.device, dtype=x2.dtype)
-    _lib.call("toa_gemm_tn_swiglu", _lib.ptr(x2), x2.stride(0), _lib.ptr(wgu), wgu.stride(0), _lib.ptr(gu), 2 * F,
+    _lib.call("toa_gemm_asm_swiglu", _lib.ptr(x2), x2.stride(0), _lib.ptr(wgu), wgu.stride(0), _lib.ptr(gu), 2 * F,
               _lib.ptr(s), F, M, F, x2.shape[1], _lib.stream(x2))
     return gu, s
 
 
 def swiglu_down_dgrad(d2: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor):
-    """dgu = SwiGLU-backward(gu, ds = d2 Wd) from ONE hand-written GEMM on
-    the transposed weight copy (ops/wt.py) with the SwiGLU backward in its
-    epilogue (ds is never stored); None when the TN kernel cannot take it."""
+    """dgu = SwiGLU-backward(gu, ds = d2 Wd) from ONE assembly GEMM on the
+    transposed weight copy (ops/wt.py) with the SwiGLU backward in its
+    epilogue (ds is never stored); None when the kernel cannot take it."""
     wdt = getattr(wd, "_toa_wt", None)
-    if wdt is None or not (_tn_ok(d2, wdt) and gu.is_contiguous() and gu.shape[1] == 2 * wdt.shape[0]):
+    if wdt is None or not (_asm_shape_ok(d2, wdt) and gu.is_contiguous() and gu.shape[1] == 2 * wdt.shape[0]
+                           and gu.data_ptr() % 16 == 0):
         return None
     M, F = d2.shape[0], wdt.shape[0]
     dgu = torch.empty_like(gu)
-    _lib.call("toa_gemm_tn_swiglu_bwd", _lib.ptr(d2), d2.stride(0), _lib.ptr(wdt), wdt.stride(0), _lib.ptr(gu),
+    _lib.call("toa_gemm_asm_swiglu_bwd", _lib.ptr(d2), d2.stride(0), _lib.ptr(wdt), wdt.stride(0), _lib.ptr(gu),
               2 * F, _lib.ptr(dgu), 2 * F, M, F, d2.shape[1], _lib.stream(d2))
     return dgu
 

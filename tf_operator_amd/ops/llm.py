@@ -162,7 +162,7 @@ def swiglu_down(gu, wd):
 class _SwiGLUMLP(torch.autograd.Function):
     """out = swiglu(x Wgu^T) Wd^T with the SwiGLU fused into the GEMMs
     (ops/gemm.py ``swiglu_gate_up`` / ``swiglu_down_dgrad``,
-    csrc/hip/gemm_tn.hip): the gate|up GEMM writes gu and s = silu(gate) *
+    csrc/asm/gemm_gen.py): the gate|up GEMM writes gu and s = silu(gate) *
     up, and the down projection's data gradient emits dgu directly -- no
     separate SwiGLU pass over the [T, 2F] activations in either direction.
     Weight gradients land in the flat buffer as in ``ops.linear``."""
@@ -195,9 +195,10 @@ class _SwiGLUMLP(torch.autograd.Function):
 
 
 def swiglu_mlp(x, wgu, wd):
-    """The Llama MLP, x -> swiglu(x Wgu^T) Wd^T, fused where the hand-written
-    GEMM takes the shapes (TOA_GEMM=hip), else the two-GEMM + SwiGLU path."""
-    if gemm.mode() == "hip":
+    """The Llama MLP, x -> swiglu(x Wgu^T) Wd^T, fused where the assembly
+    GEMM takes the shapes (TOA_GEMM=asm, the default), else the two-GEMM +
+    SwiGLU path."""
+    if gemm.mode() == "asm":
         return _SwiGLUMLP.apply(x, wgu, wd)
     from .linear import linear
 

@@ -166,13 +166,23 @@ class FlatAdamW:
             self.done = None
 
     @torch.no_grad()
-    def step(self, grad_scale=1.0, lr=None):
+    def step(self, grad_scale=1.0, lr=None, bucket_order=None, after_bucket=None):
+        """One update.  With a sharded update (``owned``: one range per
+        gradient bucket) and ``bucket_order`` / ``after_bucket``, the owned
+        shards are updated bucket by bucket in that order and
+        ``after_bucket(b)`` runs right after bucket b's update is enqueued --
+        the ZeRO-1 all-gather of b then starts as soon as ITS shard is done
+        instead of after the whole update (parallel/zero.ParamGather.launch_one).
+        Every element is updated exactly once either way: bit-identical."""
         f = self.flat
         self.step_count += 1
         lr = self.lr if lr is None else lr
         clip = self.max_grad_norm and self.max_grad_norm > 0
         if clip:
             self._norm_sq()
+        if bucket_order is not None and self.owned is not None and not self.overlap:
+            self._step_pipelined(lr, grad_scale, clip, bucket_order, after_bucket)
+            return
         if self.overlap and f.param.dtype == torch.bfloat16:
             main = torch.cuda.current_stream(f.device)
             self.side.wait_stream(main)
@@ -222,6 +232,32 @@ class FlatAdamW:
                 f.param[lo:hi].copy_(f.state_view(f.master, lo, hi).to(f.param.dtype))
             if self.post_update is not None:
                 self.post_update(0, f.numel)
+
+    def _step_pipelined(self, lr, grad_scale, clip, order, after):
+        f = self.flat
+        self.grads_zeroed = False
+        hip = _lib.use_hip(f.grad)
+        if hip and self.device_step:
+            _lib.call("toa_step_inc", _lib.ptr(self._dstep), _lib.stream(f.grad))
+        for b in order:
+            lo, hi = self.owned[b]
+            for a, e, decay in self.runs:
+                a2, b2 = max(a, lo), min(e, hi)
+                if a2 >= b2:
+                    continue
+                if hip:
+                    self._launch(a2, b2, decay, lr, grad_scale, clip, self.fuse_zero_grad, _lib.stream(f.grad))
+                else:
+                    adamw_reference(f.state_view(f.master, a2, b2), f.grad[a2:b2], f.state_view(f.exp_avg, a2, b2),
+                                    f.state_view(f.exp_avg_sq, a2, b2), lr=lr, beta1=self.beta1,
+                                    beta2=self.beta2, eps=self.eps,
+                                    weight_decay=self.weight_decay if decay else 0.0, step=self.step_count,
+                                    grad_scale=grad_scale, norm_sq=self._norm if clip else None,
+                                    max_norm=self.max_grad_norm or 0.0)
+            if not hip or f.param.dtype != torch.bfloat16:
+                f.param[lo:hi].copy_(f.state_view(f.master, lo, hi).to(f.param.dtype))
+            if after is not None:
+                after(b)
 
     def sync_step_count(self):
         """Host copy of the device step count (after graph replays)."""

@@ -88,14 +88,23 @@ class ParamGather:
         self.on_gathered = on_gathered  # fn(lo, hi) on the waiting stream (W^T refresh)
         self.works = [None] * len(self.ranges)
 
-    def launch(self):
-        # flat order is backward order: the forward needs the last bucket first
-        for b in reversed(range(len(self.ranges))):
-            lo, hi = self.ranges[b]
-            if self.emu is not None:
-                self.works[b] = self.emu.collective(self.flat.param[lo:hi])
-                continue
+    def order(self):
+        """Forward-need order: flat order is backward order, so the forward
+        needs the last bucket first."""
+        return list(reversed(range(len(self.ranges))))
+
+    def launch_one(self, b):
+        """All-gather bucket b (its owned shard must be updated on the
+        current stream already: the collective waits for that stream)."""
+        lo, hi = self.ranges[b]
+        if self.emu is not None:
+            self.works[b] = self.emu.collective(self.flat.param[lo:hi])
+        else:
             self.works[b] = all_gather_(self.flat.param[lo:hi], self.rank, self.world, self.group)
+
+    def launch(self):
+        for b in self.order():
+            self.launch_one(b)
 
     def wait(self, b):
         w = self.works[b]

@@ -10,6 +10,7 @@ Reference parity: SURVEY D7 (pytorch.go:13-68 env contract), P4.
 """
 from __future__ import annotations
 
+import atexit
 import dataclasses
 import datetime
 import json
@@ -92,6 +93,10 @@ def init(backend=None, timeout_s=1800) -> DistInfo:
             kw["device_id"] = device
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        # a group still alive when the interpreter exits can abort in its
+        # destructor ("terminate called without an active exception") and turn
+        # a finished replica into a failed one: tear it down at exit
+        atexit.register(_shutdown_quietly)
     return DistInfo(rank, world, local_rank, device, backend if world > 1 else None)
 
 
@@ -114,6 +119,13 @@ def all_max(x: float, device) -> float:
 def shutdown():
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _shutdown_quietly():
+    try:
+        shutdown()
+    except Exception:  # pragma: no cover - a peer already gone
+        pass
 
 
 def resolve_endpoint(addr: str) -> tuple[str, int]:

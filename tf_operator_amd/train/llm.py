@@ -8,7 +8,10 @@ over the flat fp32 master/m/v (device-side grad clipping, no host sync).
 shard_optimizer=True (``TOA_ZERO=1``; bench.py's default for N > 1):
 reduce-scatter instead of all-reduce, AdamW over this rank's shards only,
 then an in-place all-gather of the bf16 weights that the next forward waits
-for per bucket (parallel/zero.py).
+for per bucket (parallel/zero.py).  The tail is pipelined (``TOA_ZERO_PIPE``,
+default on): buckets are updated in forward-need order and each bucket's
+all-gather is launched right after its shard's update, so the first gather
+no longer waits for the whole update.
 """
 from __future__ import annotations
 
@@ -69,6 +72,7 @@ class LlamaTrainer:
         self.bucketer = GradBucketer(self.flat, bucket_bytes=None if bucket_mb is None else int(bucket_mb * 2**20),
                                      shard=shard_optimizer, enabled=True if force_collectives else None)
         self.gather = None
+        self.pipeline_tail = os.environ.get("TOA_ZERO_PIPE", "1") != "0"
         if self.bucketer.shard:  # ZeRO-1: reduce-scatter, owned-shard AdamW, in-place all-gather
             # fp32 master / m / v only for the owned shards: 12 B/param x (1 - 1/world) of HBM freed
             self.flat.shard_state(self.bucketer.owned)
@@ -142,9 +146,15 @@ class LlamaTrainer:
             self.flat.zero_stale()  # parameters no producer wrote this step
         self.bucketer.armed = True
         self.bucketer.finish()
-        self.opt.step(grad_scale=self.bucketer.grad_scale)
-        if self.gather is not None:
-            self.gather.launch()
+        if self.gather is not None and self.pipeline_tail:
+            # ZeRO-1 tail, bucket by bucket in forward-need order: each
+            # bucket's all-gather starts as soon as its shard is updated
+            self.opt.step(grad_scale=self.bucketer.grad_scale, bucket_order=self.gather.order(),
+                          after_bucket=self.gather.launch_one)
+        else:
+            self.opt.step(grad_scale=self.bucketer.grad_scale)
+            if self.gather is not None:
+                self.gather.launch()
         self.step_idx += 1
         return loss_sum / len(batches)
 
