@@ -611,7 +611,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int H, int Hk, int S, float scale,
-    float scale_log2, int o_bshd, int light_first) {
+    float scale_log2, int o_bshd) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
   constexpr int QBUF = DKV<D>::QBUF, KVB = DKV<D>::KVB;
@@ -624,12 +624,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
   const int r = lane & 31, hh = lane >> 5;
   const int kg = wave & 3, m = wave >> 2;
   // (b, hk) fastest
-  const int nkb = (S + 127) / 128;
   // heaviest first: key block kb sees S / 64 - 2 kb query tiles, so kb = 0
   // leads (largest-first keeps the last wave of workgroups short: a
   // simulated 800 vs 912 tile-units makespan at the bench shape)
-  const int kbi = (int)(blockIdx.x / (B * Hk));
-  const int kb = light_first ? nkb - 1 - kbi : kbi;
+  const int kb = (int)(blockIdx.x / (B * Hk));
   const int bh = blockIdx.x % (B * Hk);
   const int b = bh / Hk, hk = bh % Hk;
   const int rep = H / Hk;
@@ -812,227 +810,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
         dv[dt][j + i] += c[i];
       }
     }
-  // store: lane owns key `mykey`, d rows 32dt + 8g + 4hh + (0..3)
-  bf16_t* dkr = dK + koff + (int64_t)mykey * D;
-  bf16_t* dvr = dV + koff + (int64_t)mykey * D;
-#pragma unroll
-  for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      uint2 a[2], c[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int g = 2 * k + u;
-        a[u].x = pack2(dk[dt][4 * g + 0] * scale, dk[dt][4 * g + 1] * scale);
-        a[u].y = pack2(dk[dt][4 * g + 2] * scale, dk[dt][4 * g + 3] * scale);
-        c[u].x = pack2(dv[dt][4 * g + 0], dv[dt][4 * g + 1]);
-        c[u].y = pack2(dv[dt][4 * g + 2], dv[dt][4 * g + 3]);
-      }
-      store_pair16(dkr, 32 * dt + 16 * k, hh, a[0], a[1]);
-      store_pair16(dvr, 32 * dt + 16 * k, hh, c[0], c[1]);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// dK / dV, 4-wave form (opt-in, TOA_ATTN_DKDV=4; measured SLOWER than the
-// 8-wave form at the bench shape: dQ + dK/dV 3.61 vs 3.45 ms,
-// profiles/r3_kernels/attn_bwd_ab.log -- one wave per SIMD leaves the
-// LDS-read and exp latencies of each half to the compiler's scheduling, which
-// the 8-wave form hides with the partner wave).
-// Workgroup = 4 waves, one per SIMD with up to 512 registers each, = 128 keys
-// of one (batch, kv head).  Wave w owns keys 32w..32w+31 and BOTH 32-row
-// halves of every 64-row query tile, so its dK^T / dV^T need no cross-wave
-// sum, and the K / V fragments of its keys -- the B operands of S = Q K^T
-// and dP = dO V^T -- stay in registers for the whole kernel (one 16-B load
-// per fragment from HBM).  Only the Q / dO tiles (and their lse / delta)
-// pass through LDS, double buffered: per 64 MFMAs a wave reads 32 row
-// fragments and 64 transposed halves, 1 KB of LDS per MFMA against 1.5 KB
-// in the 8-wave form, which re-reads K and V from LDS for every query tile
-// (profiles/r2_attn_pmc: 37 % MFMA busy).  The two query halves of a tile
-// are independent up to the dK^T / dV^T accumulation chains, which gives the
-// compiler two softmax bodies to interleave with the other half's MFMAs.
-// ---------------------------------------------------------------------------
-template <int D>
-struct DKV4 {
-  static constexpr int QBUF = 2 * TK * AG<D>::ROWB + 512;  // Q tile, dO tile, lse, -delta
-  static constexpr int LDS = 2 * QBUF;
-};
-
-template <int D, bool TAIL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv4_kernel(
-    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
-    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int H, int Hk, int S, float scale,
-    float scale_log2, int o_bshd, int light_first) {
-  using G = AG<D>;
-  constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
-  constexpr int QBUF = DKV4<D>::QBUF;
-  constexpr int NLQ = TK * NCH / 256;
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // [Q/dO/lse/-delta buffer 0][buffer 1]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, hh = lane >> 5;
-  // (b, hk) fastest
-  const int nkb = (S + 127) / 128;
-  // heaviest first: key block kb sees S / 64 - 2 kb query tiles, so kb = 0
-  // leads (largest-first keeps the last wave of workgroups short: a
-  // simulated 800 vs 912 tile-units makespan at the bench shape)
-  const int kbi = (int)(blockIdx.x / (B * Hk));
-  const int kb = light_first ? nkb - 1 - kbi : kbi;
-  const int bh = blockIdx.x % (B * Hk);
-  const int b = bh / Hk, hk = bh % Hk;
-  const int rep = H / Hk;
-  const int kw = kb * 128 + wave * 32;  // first key of this wave
-  const int mykey = kw + r;
-  const int64_t koff = ((int64_t)(b * Hk + hk) * S) * D;
-
-  // B operands of S and dP: lane holds K / V[mykey][16s + 8hh .. +7]
-  bf16x8 kf[NS], vf[NS];
-  {
-    const int64_t kr = koff + (int64_t)(TAIL ? min(mykey, S - 1) : mykey) * D + 8 * hh;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      kf[s] = as_bf16x8(ld16(K + kr + 16 * s));
-      vf[s] = as_bf16x8(ld16(V + kr + 16 * s));
-    }
-  }
-  f32x16 dk[ND], dv[ND];
-#pragma unroll
-  for (int i = 0; i < ND; ++i)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) { dk[i][j] = 0.f; dv[i][j] = 0.f; }
-
-  int rro[NS], tro[ND], tro8[ND];
-  {
-#pragma unroll
-    for (int s = 0; s < NS; ++s) rro[s] = rt_off<D>(r, 2 * s + hh);
-    const int g = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-#pragma unroll
-    for (int dt = 0; dt < ND; ++dt) {
-      const int c = 4 * dt + 2 * (g & 1) + (pp >> 1);
-      tro[dt] = rt_off<D>(4 * hh + qq, c) + (pp & 1) * 8;
-      tro8[dt] = rt_off<D>(4 * hh + qq + 8, c) + (pp & 1) * 8;
-    }
-  }
-
-  const int qt0 = (kb * 128) / 64;  // first causal 64-row query tile of the block
-  const int nqt = (S + TK - 1) / TK - qt0;
-  const int total = nqt * rep;
-  u32x4 sq[NLQ], sdo[NLQ];
-  float slse = 0.f, sdel = 0.f;
-  auto gload = [&](int it) {
-    const int hq = hk * rep + it / nqt;
-    const int qt = qt0 + it % nqt;
-    const int64_t qoff = ((int64_t)(b * H + hq) * S) * D;
-#pragma unroll
-    for (int i = 0; i < NLQ; ++i) {
-      const int e = tid + 256 * i;
-      const int row = e / NCH, c = e % NCH;
-      const int qr = TAIL ? min(qt * 64 + row, S - 1) : qt * 64 + row;
-      sq[i] = ld16(Q + qoff + (int64_t)qr * D + c * 8);
-      sdo[i] = ld16(dO + o_off<D>(b, hq, qr, H, S, o_bshd) + c * 8);
-    }
-    if (tid < 64) {
-      const int q = qt * 64 + tid;
-      const int64_t li = (int64_t)(b * H + hq) * S + (TAIL ? min(q, S - 1) : q);
-      const float x = LSE[li];
-      slse = (!TAIL || q < S) ? x : INFINITY;  // padded query row: p = exp2(. - inf) = 0
-      sdel = DELTA[li];
-    }
-  };
-  auto swrite = [&](int buf) {
-    char* qb_ = smem + buf * QBUF;
-    char* ob = qb_ + TILEB;
-    float* lb = (float*)(qb_ + 2 * TILEB);
-#pragma unroll
-    for (int i = 0; i < NLQ; ++i) {
-      const int e = tid + 256 * i;
-      const int row = e / NCH, c = e % NCH;
-      *(u32x4*)(qb_ + rt_off<D>(row, c)) = sq[i];
-      *(u32x4*)(ob + rt_off<D>(row, c)) = sdo[i];
-    }
-    if (tid < 64) {
-      lb[tid] = -(slse * LOG2E);
-      lb[64 + tid] = -sdel;
-    }
-  };
-
-  // one 32-query half m of the tile in `buf` against this wave's 32 keys
-  auto half = [&](int buf, int m, int qs, bool mask) {
-    const char* qi = smem + buf * QBUF;
-    const char* oi = qi + TILEB;
-    const float* lb = (const float*)(qi + 2 * TILEB);
-    f32x16 dp;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 d4 = *(const f32x4*)(lb + 64 + 32 * m + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) dp[4 * g4 + j] = d4[j];
-    }
-    f32x16 sc = {};
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      sc = mfma32(as_bf16x8(*(const u32x4*)(qi + rro[s] + 32 * ROWB * m)), kf[s], sc);
-      dp = mfma32(as_bf16x8(*(const u32x4*)(oi + rro[s] + 32 * ROWB * m)), vf[s], dp);
-    }
-    uint32_t pw[8], sw[8];
-#pragma unroll
-    for (int j = 0; j < 16; j += 2) {
-      const f32x4 l4 = *(const f32x4*)(lb + 32 * m + 8 * (j >> 2) + 4 * hh);  // -lse * log2(e)
-      float p0 = EXP2(fmaf(sc[j], scale_log2, l4[j & 3]));
-      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, l4[(j + 1) & 3]));
-      if (mask) {
-        const int q = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        if (q < mykey) p0 = 0.f;
-        if (q + 1 < mykey) p1 = 0.f;
-      }
-      pw[j >> 1] = pack2(p0, p1);
-      sw[j >> 1] = pack2(p0 * dp[j], p1 * dp[j + 1]);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      u32x4 a, c;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = pw[4 * s2 + i];
-        c[i] = sw[4 * s2 + i];
-      }
-      const bf16x8 pb = as_bf16x8(a), sb = as_bf16x8(c);
-      const int rb = (32 * m + 16 * s2) * ROWB;
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt) {
-        const bf16x4 o0 = tr_read(oi, tro[dt] + rb), o1 = tr_read(oi, tro8[dt] + rb);
-        dv[dt] = mfma32((bf16x8)__builtin_shufflevector(o0, o1, 0, 1, 2, 3, 4, 5, 6, 7), pb, dv[dt]);
-        const bf16x4 q0 = tr_read(qi, tro[dt] + rb), q1 = tr_read(qi, tro8[dt] + rb);
-        dk[dt] = mfma32((bf16x8)__builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7), sb, dk[dt]);
-      }
-    }
-  };
-  auto step = [&](int it, int buf) {
-    if (it + 1 < total) gload(it + 1);
-    const int q0 = (qt0 + it % nqt) * 64;
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int qs = q0 + 32 * m;
-      if (qs > kw) half(buf, m, qs, false);        // strictly below this wave's diagonal
-      else if (qs == kw) half(buf, m, qs, true);  // the diagonal half-tile
-    }
-    if (it + 1 < total) swrite(buf ^ 1);
-    __syncthreads();
-  };
-
-  gload(0);
-  swrite(0);
-#pragma unroll
-  for (int s = 0; s < NS; ++s) asm volatile("" ::"v"(kf[s]), "v"(vf[s]));  // retire the resident loads (see fwd)
-  __syncthreads();
-  int it = 0;
-  for (; it + 1 < total; it += 2) {  // unrolled by 2: buffer offsets become immediates
-    step(it, 0);
-    step(it + 1, 1);
-  }
-  if (it < total) step(it, 0);
-
-  if (TAIL && mykey >= S) return;
   // store: lane owns key `mykey`, d rows 32dt + 8g + 4hh + (0..3)
   bf16_t* dkr = dK + koff + (int64_t)mykey * D;
   bf16_t* dvr = dV + koff + (int64_t)mykey * D;
@@ -1344,7 +1121,7 @@ struct DQG {
 //    block's (key, 4-query) pieces gives the B operand (query on the lane, 4
 //    keys per read; the key order matches the K^T read's, as in the split
 //    kernel).
-template <int D, bool ROPE = false, bool PRE = false>
+template <int D, bool ROPE = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __restrict__ K,
                                                               const bf16_t* __restrict__ dS, bf16_t* __restrict__ dQ,
                                                               int B, int H, int Hk, int S, float scale,
@@ -1437,10 +1214,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
   for (int i = 0; i < ND; ++i)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
-  // PRE: the epilogue's cos / sin rows loaded ahead of the main loop, so
-  // their latency hides under it instead of following it
+  // the epilogue's cos / sin rows loaded ahead of the main loop, so their
+  // latency hides under it instead of following it
   f32x4 rcs[D / 64][4], rsn[D / 64][4];
-  if constexpr (ROPE && PRE)
+  if constexpr (ROPE)
     rope_cs_load<D>(rcs, rsn, cosv + (int64_t)(qi * 32 + r) * (D / 2), sinv + (int64_t)(qi * 32 + r) * (D / 2), hh);
 
   auto compute = [&](int t, const char* st) {
@@ -1500,10 +1277,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
   bf16_t* qrow = dQ + ((int64_t)(b * H + h) * S + myq) * D;
   float osc = scale;
   if constexpr (ROPE) {  // rotate back and write the q part of d(qkv) row (b, myq)
-    if constexpr (PRE)
-      rope_bwd_acc<D>(acc, rcs, rsn, scale);
-    else
-      rope_bwd_acc<D>(acc, cosv + (int64_t)myq * (D / 2), sinv + (int64_t)myq * (D / 2), hh, scale);
+    rope_bwd_acc<D>(acc, rcs, rsn, scale);
     qrow = dQ + ((int64_t)b * S + myq) * H3 * D + h * D;
     osc = 1.f;
   }
@@ -1534,12 +1308,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
 // Each step ends with its own DMA and stores retired (vmcnt(0)) and a
 // barrier.  LSE / DELTA here are the delta pass's -lse log2(e) / -delta rows.
 // S % 256 == 0 only (no ragged tiles).
-template <int D, bool STORE = true, bool ROPE = false>
+template <int D, bool ROPE = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, bf16_t* __restrict__ dS, int B, int H, int Hk, int S,
-    float scale, float scale_log2, int o_bshd, int light_first,
+    float scale, float scale_log2, int o_bshd,
     const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr, int H3 = 0) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
@@ -1558,12 +1332,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
   const int r = lane & 31, hh = lane >> 5;
   const int kg = wave & 3, m = wave >> 2;
   // (b, hk) fastest
-  const int nkb = (S + 127) / 128;
   // heaviest first: key block kb sees S / 64 - 2 kb query tiles, so kb = 0
   // leads (largest-first keeps the last wave of workgroups short: a
   // simulated 800 vs 912 tile-units makespan at the bench shape)
-  const int kbi = (int)(blockIdx.x / (B * Hk));
-  const int kb = light_first ? nkb - 1 - kbi : kbi;
+  const int kb = (int)(blockIdx.x / (B * Hk));
   const int bh = blockIdx.x % (B * Hk);
   const int b = bh / Hk, hk = bh % Hk;
   const int rep = H / Hk;
@@ -1701,7 +1473,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
         const bf16x4 q0 = tr_read(qi, tro[dt] + rb), q1 = tr_read(qi, tro8[dt] + rb);
         dk[dt] = mfma32((bf16x8)__builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7), sb, dk[dt]);
       }
-      if (STORE && s2 == 0) {  // chunk (key r, queries 8g' .. + 7), g' = 2k + hh, at g' * 512 + r * 16 bytes
+      if (s2 == 0) {  // chunk (key r, queries 8g' .. + 7), g' = 2k + hh, at g' * 512 + r * 16 bytes
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
           const auto x = __builtin_amdgcn_permlane32_swap(sw[4 * k], sw[4 * k + 2], false, false);
@@ -1788,37 +1560,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     }
 }
 
-// dK/dV key-block launch order: heaviest first (default) or, for A/B,
-// lightest first (TOA_ATTN_KB_ORDER=light / toa_attn_set_kb_order(1)).
-static int g_kb_light = -1;
-static int attn_kb_light_first() {
-  if (g_kb_light < 0) {
-    const char* e = getenv("TOA_ATTN_KB_ORDER");
-    g_kb_light = (e && e[0] == 'l') ? 1 : 0;
-  }
-  return g_kb_light;
-}
-// dQ GEMM of the RoPE-fused backward: cos / sin loaded before the main loop
-// (default; TOA_ATTN_ROPE_PREFETCH=0 / toa_attn_set_rope_prefetch(0) loads them in
-// the epilogue: 2.792 vs 2.782 ms per backward, bit-identical,
-// profiles/r3_attn_pmc/ab_rope_prefetch.log)
-static int g_rope_pre = -1;
-static int attn_rope_prefetch() {
-  if (g_rope_pre < 0) {
-    const char* e = getenv("TOA_ATTN_ROPE_PREFETCH");
-    g_rope_pre = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_rope_pre;
-}
-extern "C" int toa_attn_set_rope_prefetch(int v) {
-  g_rope_pre = v < 0 ? -1 : (v ? 1 : 0);
-  return 0;
-}
-extern "C" int toa_attn_set_kb_order(int light_first) {
-  g_kb_light = light_first < 0 ? -1 : (light_first ? 1 : 0);
-  return 0;
-}
-
 // Backward form: 1 = dS through HBM (default where S % 256 == 0: the
 // Llama-3-8B step 987.9 -> 978.1 ms, profiles/r3_attn_ds), 0 = split (dQ
 // recomputes S / dP; ragged S always).  TOA_ATTN_BWD=split|ds, or
@@ -1831,14 +1572,8 @@ static int attn_bwd_variant() {
   }
   return g_bwd_variant;
 }
-// 2 (A/B only): the split form's dQ kernel, then the delta pass and the dS
-// form's dK/dV kernel without its dS stores -- prices the LDS-DMA staging
 extern "C" int toa_attn_set_bwd_variant(int v) {
-  if (v == -1) {
-    g_bwd_variant = -1;
-    return 0;
-  }
-  if (v < 0 || v > 2) return (int)hipErrorInvalidValue;
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
   g_bwd_variant = v;
   return 0;
 }
@@ -1857,22 +1592,6 @@ extern "C" int64_t toa_attn_bwd_ws_bytes(int B, int H, int S, int D) {
   return attn_bwd_uses_ds(S) ? attn_ds_bytes(B, H, S) : 0;
 }
 
-// dK/dV kernel form: 8 (8-wave, K/V in LDS; default) or 4 (4-wave, K/V in
-// registers); TOA_ATTN_DKDV=4 or toa_attn_set_dkdv_variant for A/B runs.
-static int g_dkdv_variant = -1;
-static int attn_dkdv_variant() {
-  if (g_dkdv_variant < 0) {
-    const char* e = getenv("TOA_ATTN_DKDV");
-    g_dkdv_variant = (e && e[0] == '4') ? 4 : 8;
-  }
-  return g_dkdv_variant;
-}
-extern "C" int toa_attn_set_dkdv_variant(int waves) {
-  if (waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
-  g_dkdv_variant = waves;
-  return 0;
-}
-
 template <int D, bool TAIL>
 static void attn_set_lds_limits() {
   static bool done = false;
@@ -1883,26 +1602,18 @@ static void attn_set_lds_limits() {
                             DKV<D>::LDS);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, TAIL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             4 * AG<D>::TILEB);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv4_kernel<D, TAIL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            DKV4<D>::LDS);
   done = true;
 }
 
-// Forward form: 1 = LDS-DMA staged K/V (default where S % 256 == 0: 0.868 ->
-// 0.811 ms at the bench shape, bit-identical, profiles/r3_attn_ds), 0 =
-// register staged (ragged S always).  TOA_ATTN_FWD=reg|gl or
-// toa_attn_set_fwd_variant (-1: back to the environment's choice).
-static int g_fwd_variant = -1;
-static int attn_fwd_variant() {
-  if (g_fwd_variant < 0) {
-    const char* e = getenv("TOA_ATTN_FWD");
-    g_fwd_variant = (e && e[0] == 'r' && e[1] == 'e') ? 0 : 1;
-  }
-  return g_fwd_variant;
-}
+// Forward form: 1 = LDS-DMA staged K/V (where S % 256 == 0: 0.868 -> 0.811
+// ms at the bench shape, bit-identical, profiles/r3_attn_ds), 0 = register
+// staged (ragged S always).  toa_attn_set_fwd_variant pins the full-tile
+// form for in-process tests (-1: back to the default).
+static int g_fwd_variant = 1;
+static int attn_fwd_variant() { return g_fwd_variant; }
 extern "C" int toa_attn_set_fwd_variant(int v) {
   if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
-  g_fwd_variant = v;
+  g_fwd_variant = v < 0 ? 1 : v;
   return 0;
 }
 
@@ -1934,20 +1645,10 @@ static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
       bf16_t* ds = (bf16_t*)ws;
       float* nlse2 = (float*)((char*)ws + attn_ds_blocks_bytes(B, H, S));
       const int rows = B * H * S;
-      if (attn_bwd_variant() == 2) {
-        hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), dim3((S / FWD_QB) * H * B), dim3(64 * FWD_WAVES),
-                           4 * AG<D>::TILEB, stream, q, k, v, dout, o, lse, delta, dq, B, H, Hk, S, scale,
-                           scale * LOG2E, o_bshd);
-        hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
-                           stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
-        hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, false>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k,
-                           v, dout, nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
-        return (int)hipGetLastError();
-      }
       hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
                          stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
       hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k, v, dout,
-                         nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
+                         nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
       hipLaunchKernelGGL((attn_bwd_dqg_kernel<D>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, dq, B, H,
                          Hk, S, scale);
       return (int)hipGetLastError();
@@ -1957,12 +1658,8 @@ static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, TAIL>), dim3(((S + FWD_QB - 1) / FWD_QB) * H * B), dim3(64 * FWD_WAVES),
                      4 * AG<D>::TILEB, stream, q, k, v, dout, o, lse, delta, dq, B, H, Hk, S, scale, scale * LOG2E,
                      o_bshd);
-  if (attn_dkdv_variant() == 8)
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, TAIL>), dim3(((S + 127) / 128) * B * Hk), dim3(512), DKV<D>::LDS,
-                       stream, q, k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
-  else
-    hipLaunchKernelGGL((attn_bwd_dkdv4_kernel<D, TAIL>), dim3(((S + 127) / 128) * B * Hk), dim3(256), DKV4<D>::LDS,
-                       stream, q, k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd, attn_kb_light_first());
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, TAIL>), dim3(((S + 127) / 128) * B * Hk), dim3(512), DKV<D>::LDS, stream,
+                     q, k, v, dout, lse, delta, dk, dv, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
   return (int)hipGetLastError();
 }
 
@@ -2030,15 +1727,11 @@ extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t*
   do {                                                                                                           \
     hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 256 / (DD / 8) - 1) / (256 / (DD / 8))), dim3(256), \
                        0, stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);                               \
-    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<DD, true, true>), dim3((S / 128) * B * Hk), dim3(512), 0,       \
+    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<DD, true>), dim3((S / 128) * B * Hk), dim3(512), 0,       \
                        stream, q, k, v, dout, nlse2, delta, dqkv, dqkv, ds, B, H, Hk, S, scale, scale * LOG2E,  \
-                       o_bshd, attn_kb_light_first(), cosv, sinv, H3);                                          \
-    if (attn_rope_prefetch())                                                                                   \
-      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, \
-                         k, ds, dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                       \
-    else                                                                                                         \
-      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,   \
-                         ds, dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                          \
+                       o_bshd, cosv, sinv, H3);                                          \
+    hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \
+                       dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                               \
   } while (0)
 #ifdef TOA_ATTN_D128_ONLY
   if (D != 128) return (int)hipErrorInvalidValue;

@@ -309,18 +309,12 @@ static inline int pick_ch(int cols) {
 
 // RMSNorm form for bf16 rows of 2048-multiple width up to 8192: 1 = one row
 // per workgroup (rms_fwd_row_kernel / rms_bwd_row_kernel, the default), 0 =
-// one row per wave (norm_fwd_kernel / norm_bwd_kernel).  TOA_NORM_ROW=0|1,
-// toa_norm_set_row for A/B (-1 = the environment's choice).
-static int g_norm_row = -1;
-static int norm_row_form() {
-  if (g_norm_row < 0) {
-    const char* e = getenv("TOA_NORM_ROW");
-    g_norm_row = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_norm_row;
-}
+// one row per wave (norm_fwd_kernel / norm_bwd_kernel, every other shape).
+// toa_norm_set_row pins a form for in-process tests (-1 = the default).
+static int g_norm_row = 1;
+static int norm_row_form() { return g_norm_row; }
 extern "C" int toa_norm_set_row(int v) {
-  g_norm_row = v < 0 ? -1 : (v ? 1 : 0);
+  g_norm_row = v < 0 ? 1 : (v ? 1 : 0);
   return 0;
 }
 

@@ -30,7 +30,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <cstdlib>
 
 #include "toa_common.h"
 
@@ -106,7 +105,6 @@ __device__ __forceinline__ void wg_tile_coords(int tile, int tiles_m, int tiles_
   *tn = (tile - group * per_group) / gsz;
 }
 
-template <int DIST>
 __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                           const bf16_t* __restrict__ B, int64_t ldb,
                                                           bf16_t* __restrict__ C, int64_t ldc, float* __restrict__ W,
@@ -158,9 +156,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
   // first read of phase p+1 (both rows wait before their first barrier of
   // a phase: exact for the lagging row, one barrier early for the leading
   // one), and restages a buffer only two phases after its last read (4
-  // buffers: the lagging row finished it by then).  DIST = 3: the DMA runs
-  // three phases ahead (vmcnt(8)) into the buffer read in phase p - 1, so
-  // each phase retires its own reads (lgkmcnt(0)) before its first barrier.
+  // buffers: the lagging row finished it by then).
   const bool lag = wm == 1;
   int ga[2], gb[2];
 #pragma unroll
@@ -181,13 +177,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
     for (int i = 0; i < 8; ++i) af[i] = wg_frag(cur, 0, wm * 128 + 16 * i, lane);
     // past the end the last stage is re-fetched into a buffer nobody reads
     // again: keeps the DMA count per phase constant (no branches, vmcnt(4))
-    const int q = min(p + DIST, np - 1);
+    const int q = min(p + 2, np - 1);
     wg_stage(Ab + (int64_t)q * WG_BK * lda, ga, pre, wave);
     wg_stage(Bb + (int64_t)q * WG_BK * ldb, gb, pre + WG_TILE, wave);
-    if (DIST == 2)
-      __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // my DMA of phase p+1 retired
-    else
-      __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) lgkmcnt(0)
+    __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // my DMA of phase p+1 retired
     sync();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -203,27 +196,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
   wg_stage(Bb, gb, sb0 + WG_TILE, wave);
   wg_stage(Ab + (int64_t)WG_BK * lda, ga, sb1, wave);
   wg_stage(Bb + (int64_t)WG_BK * ldb, gb, sb1 + WG_TILE, wave);
-  if (DIST == 3) {
-    wg_stage(Ab + (int64_t)2 * WG_BK * lda, ga, sb2, wave);
-    wg_stage(Bb + (int64_t)2 * WG_BK * ldb, gb, sb2 + WG_TILE, wave);
-    __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): phase 0's DMA retired
-  } else {
-    __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // phase 0's DMA retired
-  }
+  __builtin_amdgcn_s_waitcnt(WG_VMCNT4);  // phase 0's DMA retired
   sync();
   if (lag) sync();
   for (int p = 0; p < np; p += 4) {
-    if (DIST == 2) {
-      phase(sb0, sb2, p);
-      phase(sb1, sb3, p + 1);
-      phase(sb2, sb0, p + 2);
-      phase(sb3, sb1, p + 3);
-    } else {
-      phase(sb0, sb3, p);
-      phase(sb1, sb0, p + 1);
-      phase(sb2, sb1, p + 2);
-      phase(sb3, sb2, p + 3);
-    }
+    phase(sb0, sb2, p);
+    phase(sb1, sb3, p + 1);
+    phase(sb2, sb0, p + 2);
+    phase(sb3, sb1, p + 3);
   }
   if (!lag) sync();
   __builtin_amdgcn_s_waitcnt(WG_VMCNT0);  // no LDS-DMA left in flight at exit
@@ -258,203 +238,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) *(f32x4*)(ws + (lrow + 16 * i) * WG_BN + lcol + 16 * jj) = acc[i][jj];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 4-wave variant (TOA_WGRAD_4W=1): one wave per SIMD, 128 x 128 of C per
-// wave (2 x 2 waves) as 4 x 4 v_mfma_f32_32x32x16_bf16 tiles (16 f32x16
-// accumulators in AGPRs; with 64 16x16 f32x4 tiles hipcc shuttles the
-// accumulators between VGPRs and AGPRs inside the loop).  Per k-phase a
-// wave reads 16 fragments (32 transposed reads) for 32 MFMAs of 32 cycles,
-// against 12 fragments for 32 MFMAs of 16 cycles in the 8-wave kernel: a
-// third of the LDS read instructions per FLOP (profiles/r2_gemm_pmc).  With
-// no partner wave on the SIMD, the fragments of phase p + 1 are read into a
-// second register set between the MFMAs of phase p, and LDS-DMA runs three
-// stages ahead in the same 4 x 32 KiB ring.
-//
-// LDS image: chunk c of row r at c ^ ((r & 3) << 2).  A 32x32x16 operand
-// read takes, per 32-lane half, chunk pairs P, P + 1 (P even) of 4
-// consecutive rows; the XOR moves pair P of row q to P ^ 2q, so the 8
-// 32-byte segments land in 8 distinct bank slots.
-// ---------------------------------------------------------------------------
-#define W4_VMCNT16 0x4F70  // vmcnt(16): vmcnt[5:4] in simm16[15:14]
-#define W4_LGKM0 0xC07F    // lgkmcnt(0)
-
-typedef __attribute__((ext_vector_type(16))) float w4_f32x16;
-
-__device__ __forceinline__ int w4_off(int r, int c) { return r * WG_ROWB + ((c ^ ((r & 3) << 2)) << 4); }
-
-// one 2-row (1 KiB) global_load_lds per u: rows 8 wave + 2u + (lane >> 5)
-__device__ __forceinline__ int w4_goff(int64_t ld, int wave, int lane, int u) {
-  const int r = 8 * wave + 2 * u + (lane >> 5);
-  return (int)(r * ld) + (((lane & 31) ^ ((r & 3) << 2)) * 8);
-}
-
-__device__ __forceinline__ void w4_stage(const bf16_t* __restrict__ g, const int* goff, char* lds_tile, int wave) {
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    char* dst = lds_tile + (8 * wave + 2 * u) * WG_ROWB;  // wave-uniform
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + (uint32_t)goff[u]),
-                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-  }
-}
-
-// 32x32x16 operand of rows k0..k0+15 and 32 columns from col0: lane l gets
-// image[k0 + 8(l>>5) + j][col0 + (l & 31)], j = 0..7 (two transposed reads:
-// 16-lane group g takes rows k0 + 8(g>>1) + 0..3 / 4..7, columns
-// col0 + 16(g&1) .. +15).
-__device__ __forceinline__ wg_s16x8 w4_frag(const char* img, int k0, int col0, int lane) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int r = k0 + 8 * (g >> 1) + q;
-  const int c = (col0 >> 3) + 2 * (g & 1) + (p >> 1);
-  const int b = 8 * (p & 1);
-  const wg_s16x4 lo = wg_tr(img, w4_off(r, c) + b);
-  const wg_s16x4 hi = wg_tr(img, w4_off(r + 4, c) + b);
-  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
-// fragments of one stage: [x][kk] = 32 columns x, k half kk
-__device__ __forceinline__ void w4_read(const char* img, int wm, int wn, int lane, wg_s16x8 (*af)[2],
-                                        wg_s16x8 (*bf)[2]) {
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      bf[x][kk] = w4_frag(img + WG_TILE, 16 * kk, wn * 128 + 32 * x, lane);
-      af[x][kk] = w4_frag(img, 16 * kk, wm * 128 + 32 * x, lane);
-    }
-}
-
-__global__ __launch_bounds__(256, 1) void wgrad_nt4_kernel(const bf16_t* __restrict__ A, int64_t lda,
-                                                           const bf16_t* __restrict__ B, int64_t ldb,
-                                                           bf16_t* __restrict__ C, int64_t ldc, float* __restrict__ W,
-                                                           int M, int N, int K, int full, int split, int beta) {
-  __shared__ __attribute__((aligned(1024))) char sb0[WG_STAGE];
-  __shared__ __attribute__((aligned(1024))) char sb1[WG_STAGE];
-  __shared__ __attribute__((aligned(1024))) char sb2[WG_STAGE];
-  __shared__ __attribute__((aligned(1024))) char sb3[WG_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int tiles_m = M / WG_BM, tiles_n = N / WG_BN, tiles = tiles_m * tiles_n;
-  const int rem = tiles - full;
-  const bool piece = (int)blockIdx.x >= full;
-  int tile, s = 0, j = 0;
-  if (!piece) {
-    tile = wg_xcd_remap(blockIdx.x, full);
-  } else {
-    const int w2 = wg_xcd_remap(blockIdx.x - full, rem * split);
-    s = w2 / rem;
-    j = w2 - s * rem;
-    tile = full + j;
-  }
-  int tm, tn;
-  wg_tile_coords(tile, tiles_m, tiles_n, &tm, &tn);
-  const int kc = piece ? K / split : K, k_begin = s * kc, np = kc / WG_BK;
-  const bf16_t* Ab = A + (int64_t)k_begin * lda + (int64_t)tm * WG_BM;
-  const bf16_t* Bb = B + (int64_t)k_begin * ldb + (int64_t)tn * WG_BN;
-
-  w4_f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = w4_f32x16{};
-  int ga[4], gb[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    ga[u] = w4_goff(lda, wave, lane, u);
-    gb[u] = w4_goff(ldb, wave, lane, u);
-  }
-  auto sync = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // Phase p: DMA of stage p + 3 into the buffer stage p - 1 used (its reads,
-  // issued in phase p - 2, retired before barrier p - 1); wait for this
-  // wave's DMA of stage p + 1; barrier (everyone's has landed); then the 32
-  // MFMAs of stage p (fragments in registers) with the 32 transposed reads
-  // of stage p + 1 between them.
-  auto phase = [&](wg_s16x8 (*fa)[2], wg_s16x8 (*fb)[2], wg_s16x8 (*na)[2], wg_s16x8 (*nb)[2], const char* rd,
-                   char* dma, int p) {
-    const int q = min(p + 3, np - 1);  // past the end: re-fetch into a buffer nobody reads again
-    w4_stage(Ab + (int64_t)q * WG_BK * lda, ga, dma, wave);
-    w4_stage(Bb + (int64_t)q * WG_BK * ldb, gb, dma + WG_TILE, wave);
-    __builtin_amdgcn_s_waitcnt(W4_VMCNT16);
-    sync();
-    w4_read(rd, wm, wn, lane, na, nb);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[jj][kk], fa[i][kk], acc[i][jj], 0, 0, 0);
-    // 4 reads per 3 MFMAs over the first 24 MFMAs; the last 8 (256 cycles)
-    // cover the latency of the final reads
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS read
-      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);  // MFMA
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-    __builtin_amdgcn_s_waitcnt(W4_LGKM0);  // this phase's reads retired before the next barrier
-  };
-  wg_s16x8 fa0[4][2], fb0[4][2], fa1[4][2], fb1[4][2];
-  w4_stage(Ab, ga, sb0, wave);
-  w4_stage(Bb, gb, sb0 + WG_TILE, wave);
-  w4_stage(Ab + (int64_t)WG_BK * lda, ga, sb1, wave);
-  w4_stage(Bb + (int64_t)WG_BK * ldb, gb, sb1 + WG_TILE, wave);
-  w4_stage(Ab + (int64_t)2 * WG_BK * lda, ga, sb2, wave);
-  w4_stage(Bb + (int64_t)2 * WG_BK * ldb, gb, sb2 + WG_TILE, wave);
-  __builtin_amdgcn_s_waitcnt(W4_VMCNT16);  // stage 0 landed (this wave)
-  sync();
-  w4_read(sb0, wm, wn, lane, fa0, fb0);
-  __builtin_amdgcn_s_waitcnt(W4_LGKM0);
-  for (int p = 0; p < np; p += 4) {
-    phase(fa0, fb0, fa1, fb1, sb1, sb3, p);
-    phase(fa1, fb1, fa0, fb0, sb2, sb0, p + 1);
-    phase(fa0, fb0, fa1, fb1, sb3, sb1, p + 2);
-    phase(fa1, fb1, fa0, fb0, sb0, sb2, p + 3);
-  }
-  __builtin_amdgcn_s_waitcnt(WG_VMCNT0);  // no LDS-DMA left in flight at exit
-
-  // epilogue: acc[i][jj] register r of lane l is C[m][n .. n+3] with
-  // m = 32 i + (l & 31), n = 32 jj + 8 (r >> 2) + 4 (l >> 5)  (r % 4 = 0)
-  const int lrow = wm * 128 + (lane & 31), lcol = wn * 128 + 4 * (lane >> 5);
-  if (!piece) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16_t* p = C + (int64_t)(tm * WG_BM + lrow + 32 * i) * ldc + tn * WG_BN + lcol + 32 * jj + 8 * g;
-          float v0 = acc[i][jj][4 * g], v1 = acc[i][jj][4 * g + 1], v2 = acc[i][jj][4 * g + 2],
-                v3 = acc[i][jj][4 * g + 3];
-          if (beta) {
-            const uint2 o = *(const uint2*)p;
-            v0 += __uint_as_float(o.x << 16);
-            v1 += __uint_as_float(o.x & 0xffff0000u);
-            v2 += __uint_as_float(o.y << 16);
-            v3 += __uint_as_float(o.y & 0xffff0000u);
-          }
-          uint2 w;
-          w.x = pack2(v0, v1);
-          w.y = pack2(v2, v3);
-          *(uint2*)p = w;
-        }
-  } else {
-    float* ws = W + ((int64_t)s * rem + j) * (WG_BM * WG_BN);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *(f32x4*)(ws + (lrow + 32 * i) * WG_BN + lcol + 32 * jj + 8 * g) =
-              f32x4{acc[i][jj][4 * g], acc[i][jj][4 * g + 1], acc[i][jj][4 * g + 2], acc[i][jj][4 * g + 3]};
   }
 }
 
@@ -509,24 +292,6 @@ static void wg_plan(int M, int N, int K, int* full, int* split) {
   *split = best;
 }
 
-// Kernel variant: 8 (waves, default), 4 (TOA_WGRAD_4W=1) or 3 (8 waves with
-// the DMA three phases ahead, TOA_WGRAD_VARIANT=3); settable for in-process
-// A/B runs.
-static int g_wg_variant = -1;
-static int wg_variant() {
-  if (g_wg_variant < 0) {
-    const char* e = getenv("TOA_WGRAD_4W");
-    const char* v = getenv("TOA_WGRAD_VARIANT");
-    g_wg_variant = (e && e[0] == '1') ? 4 : (v && v[0] == '3') ? 3 : 8;
-  }
-  return g_wg_variant;
-}
-extern "C" int toa_wgrad_set_variant(int waves) {
-  if (waves != 3 && waves != 4 && waves != 8) return (int)hipErrorInvalidValue;
-  g_wg_variant = waves;
-  return 0;
-}
-
 // Auto plan's split factor (1 = no split-K at all).
 extern "C" int toa_wgrad_split(int M, int N, int K) {
   int full, split;
@@ -563,15 +328,8 @@ extern "C" int toa_wgrad(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t 
     return (int)hipErrorInvalidValue;
   const int rem = tiles - full;
   const int nwg = full + (split > 1 ? rem * split : 0);
-  if (wg_variant() == 4)
-    hipLaunchKernelGGL(wgrad_nt4_kernel, dim3(nwg), dim3(256), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
-                       split, beta);
-  else if (wg_variant() == 3)
-    hipLaunchKernelGGL(wgrad_nt_kernel<3>, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
-                       split, beta);
-  else
-    hipLaunchKernelGGL(wgrad_nt_kernel<2>, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full,
-                       split, beta);
+  hipLaunchKernelGGL(wgrad_nt_kernel, dim3(nwg), dim3(512), 0, stream, A, lda, B, ldb, C, ldc, W, M, N, K, full, split,
+                     beta);
   if (split > 1 && rem > 0)
     hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split,
                        beta);

@@ -2,16 +2,12 @@
 shape (B=6, H=32, Hkv=8, S=4096, D=128, O/dO in [B,S,H,D]), interleaved
 rounds on random data (guide §5.4 rules 24/25):
 
-    split8  dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
-    split4  the same with the 4-wave dK/dV (K/V fragments in registers)
+    split   dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
-    gl      split dQ + delta pass + the ds form's LDS-DMA dK/dV without stores
-            (prices the staging alone)
-    *_light the same with the dK/dV key blocks launched lightest first
 
-Also checks every form agrees with split8.
+Also checks every form agrees with the first.
 
-    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5] [--variants split8,ds]
+    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5] [--variants split,ds]
 """
 import argparse
 import json
@@ -30,7 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=6)
-    ap.add_argument("--variants", default="split8,split4,ds")
+    ap.add_argument("--variants", default="split,ds")
     a = ap.parse_args()
     B, H, Hk, S, D = a.batch, 32, 8, 4096, 128
     dev = "cuda"
@@ -48,16 +44,12 @@ def main():
     _lib.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, flags, scale, _lib.stream(q))
     outs = {}
 
-    # (dK/dV waves, backward form, key blocks lightest-first)
-    forms = {"split8": (8, 0, 0), "split4": (4, 0, 0), "ds": (8, 1, 0), "gl": (8, 2, 0),
-             "split8_light": (8, 0, 1), "ds_light": (8, 1, 1)}
+    # backward form: 0 = split (dQ recomputes S / dP), 1 = dS through HBM + dQ GEMM
+    forms = {"split": 0, "ds": 1}
     variants = a.variants.split(",")
 
     def run(variant):
-        dkdv, bwd, light = forms[variant]
-        _lib.call("toa_attn_set_kb_order", light)
-        _lib.call("toa_attn_set_dkdv_variant", dkdv)
-        _lib.call("toa_attn_set_bwd_variant", bwd)
+        _lib.call("toa_attn_set_bwd_variant", forms[variant])
         nws = _lib.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D)
         ws = torch.empty(nws, device=dev, dtype=torch.uint8) if nws > 0 else None
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
@@ -90,7 +82,6 @@ def main():
         res[var] = {"median_ms": round(med, 3), "min_ms": round(min(t), 3),
                              "useful_PFps": round(2.5 * flops_fwd / med / 1e12, 3)}
     _lib.call("toa_attn_set_bwd_variant", -1)
-    _lib.call("toa_attn_set_kb_order", -1)
     print(json.dumps(res))
 
 

@@ -10,8 +10,10 @@ replaced by paced traffic on a high-priority side stream.  Variants:
     <policy>.traffic   the collectives move (N-1)/N of each bucket at --gbps
     <policy>.quiet     same step, collectives moving nothing (TOA_EMULATE_BYTES=0)
 
-for policy in --policies (torch = hipBLASLt heuristic, i.e. its stream-K
-kernels; nosk = the non-stream-K table, ops/gemm.py).  The overlap cost of a
+for each entry of --policies: a GEMM policy (asm = the assembly kernel, the
+default; torch = hipBLASLt heuristic, i.e. its stream-K kernels; nosk = the
+non-stream-K table, ops/gemm.py), optionally followed by "+VAR=VALUE" extra
+environment, e.g. ``asm+TOA_ZERO_PIPE=0`` for the unpipelined ZeRO-1 tail.  The overlap cost of a
 policy is traffic - quiet; policies are compared on traffic.
 
     python scripts/overlap_emulation.py --out gpurun_out/r3_overlap [--steps 4] [--gbps 350]
@@ -52,14 +54,16 @@ def main():
     ap.add_argument("--channels", type=int, default=32)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--policies", default="torch,nosk")
+    ap.add_argument("--policies", default="asm,asm+TOA_ZERO_PIPE=0")
     ap.add_argument("--timeout", type=float, default=240)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     rows = []
     for pol in a.policies.split(","):
+        gemm, *assigns = pol.split("+")
+        env = {"TOA_GEMM": gemm, **dict(x.split("=", 1) for x in assigns)}
         for kind, extra in (("traffic", {}), ("quiet", {"TOA_EMULATE_BYTES": "0"})):
-            rows.append(run(f"{pol}.{kind}", {"TOA_GEMM": pol, **extra}, a, a.out))
+            rows.append(run(f"{pol}.{kind}", {**env, **extra}, a, a.out))
     by = {r["_variant"]: r for r in rows}
     summary = {"world": a.world, "gbps": a.gbps, "channels": a.channels, "steps": a.steps, "variants": {}}
     for pol in a.policies.split(","):

@@ -64,7 +64,9 @@ def test_simple_tfjob_and_pod_names(cluster):
     # (workers still Running when the chief finished are cleaned up too)
     names = c.get_pod_names("simple")
     assert "simple-chief-0" in names and names <= expected - {"simple-ps-0", "simple-ps-1"}
-    assert {s["metadata"]["name"] for s in cluster.services(labels={"job-name": "simple"})} == names
+    # services are deleted after their pods (a separate API call): wait for them too
+    cluster.wait(lambda: {s["metadata"]["name"] for s in cluster.services(labels={"job-name": "simple"})} == names,
+                 15, what="ps service cleanup")
     assert c.get_pod_names("simple", master=True) == {"simple-chief-0"}
     assert c.get_pod_names("simple", replica_type="ps") is None
     logs = c.get_logs("simple", master=True)

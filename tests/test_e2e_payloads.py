@@ -78,12 +78,16 @@ def test_dist_mnist_node_local_auto_oneshot():
     job = tfjob("mnist-nl", {"Worker": rs(2, payload("dist_mnist", *args, gpus=1,
                                                       env={"TOA_NO_GPU": "1"}))},
                 annotations={"amd.com/node-local": "privileged"})
+    names = ("mnist-nl-worker-0", "mnist-nl-worker-1")
     with LocalCluster(gpus=2) as c2:
-        done, logs = _run(c2, job)
-        envs = {}
-        for name in ("mnist-nl-worker-0", "mnist-nl-worker-1"):
-            pod = c2.api.get("pods", "default", name)
-            envs[name] = c2.kubelet._build_env(pod, pod["spec"]["containers"][0], [int(name[-1])])
+        c2.client.create(job)
+        # the pods as the operator created them (they may be cleaned up once the job ends)
+        pods = c2.wait(lambda: [c2.api.get("pods", "default", n) for n in names]
+                       if all(c2.api.get("pods", "default", n) for n in names) else None, 60, what="pods")
+        envs = {n: c2.kubelet._build_env(p, p["spec"]["containers"][0], [int(n[-1])]) for n, p in zip(names, pods)}
+        done = c2.client.wait_for_job("mnist-nl", polling_interval=0.2, timeout_seconds=180)
+        logs = {p[1]: open(c2.kubelet.log_path(p[0], p[1])).read() for p in c2.kubelet.start_times
+                if p[1].startswith("mnist-nl-") and c2.kubelet.log_path(p[0], p[1])}
     assert "Succeeded" in conds(done), (conds(done), logs)
     for name in ("mnist-nl-worker-0", "mnist-nl-worker-1"):
         assert "one-shot IPC off (eligible (2 ranks on this node" in logs[name], logs[name]

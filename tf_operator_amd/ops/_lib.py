@@ -67,7 +67,6 @@ _SIGS = {
                      c_f, c_p],
     "toa_wgrad": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
     "toa_wgrad_split": [c_int, c_int, c_int],
-    "toa_wgrad_set_variant": [c_int],
     "toa_transpose_bf16": [c_p, c_i64, c_p, c_i64, c_int, c_int, c_p],
     "toa_gemm": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p],
     "toa_gemm_set_algo": [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int],
@@ -87,10 +86,7 @@ _SIGS = {
     "toa_host_free": [c_p],
     "toa_gemm_asm_stage": [c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_probe": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
-    "toa_attn_set_dkdv_variant": [c_int],
     "toa_attn_set_bwd_variant": [c_int],
-    "toa_attn_set_kb_order": [c_int],
-    "toa_attn_set_rope_prefetch": [c_int],
     "toa_norm_set_row": [c_int],
     "toa_attn_set_fwd_variant": [c_int],
     "toa_attn_bwd_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,

@@ -1,16 +1,16 @@
-"""Row-major bf16 GEMM entry points of the training step, on the tuned
-hipBLASLt layer (csrc/hip/gemm.hip).
+"""Row-major bf16 GEMM entry points of the training step.
 
     linear_fwd(x, w)           y  = x w^T            [M,K] x [N,K] -> [M,N]
     linear_dgrad(dy, w)        dx = dy w             [M,N] x [N,K] -> [M,K]
     wgrad_acc_(g, dy, x)       g += dy^T x           (beta = 1, in place)
 
-Each maps to one column-major hipBLASLt call (see gemm.hip for the
-transposition algebra).  The per-form solution table measured by
-``scripts/tune_gemm.py`` on an MI355X is stored next to this file
-(``gemm_tuning_gfx950.json``, keyed by the hipBLASLt build it was measured
-with) and installed once per process; untuned forms use the library
-heuristic.
+The forward / data-gradient forms run on the hand-written assembly kernel
+under the default policy; the weight gradient on the NT kernel
+(csrc/hip/wgrad.hip).  The hipBLASLt layer (csrc/hip/gemm.hip, one
+column-major call per form, see there for the transposition algebra) serves
+the shapes the assembly kernel does not tile and the ``tuned`` / ``nosk``
+policies: its per-form solution tables measured by ``scripts/tune_gemm.py``
+on an MI355X are stored next to this file, keyed by the hipBLASLt build.
 
 Modes (``TOA_GEMM``):
 
@@ -255,7 +255,6 @@ def swiglu_down_dgrad(d2: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor):
     return dgu
 
 
-_WGRAD = os.environ.get("TOA_WGRAD", "hip")
 _ws = {}
 
 
@@ -270,7 +269,7 @@ def _workspace(dev, nbytes):
 def wgrad_hip_ok(g, dy2, x2) -> bool:
     """Shapes/layouts csrc/hip/wgrad.hip takes: bf16, 256-multiple output
     dims, token count a multiple of 64, unit column stride."""
-    if _WGRAD != "hip" or not _lib.has("toa_wgrad"):
+    if not _lib.has("toa_wgrad"):
         return False
     if not (dy2.is_cuda and g.dtype == dy2.dtype == x2.dtype == torch.bfloat16 and g.is_contiguous()):
         return False
