@@ -22,11 +22,14 @@ Structure (every number below is what the generator emits):
   workgroup   256 threads = 4 waves (one per SIMD), tile 256 x 256, BK = 64
   wave        (wm, wn) = (wave & 1, wave >> 1): 128 rows of X x 128 rows of W
               = 8 x 8 tiles of v_mfma_f32_16x16x32_bf16, 256 AGPR accumulators
-  LDS         two stages of 65 KiB (X half, W half).  A half is 32 "lines" of
-              1040 B (1024 B of data + 16 B pad): line i of the wave-row block
-              holds tile rows i, i+16, ..., i+112 (128 B = 64 k each), so the
-              16 lanes of a fragment read (rows 16f + lane&15) fall on 16
-              distinct 16-B bank slots (1040 B = 260 dwords = 4 banks apart)
+  LDS         two stages of 66 KiB (X half, W half).  A half is 32 "lines" of
+              1056 B (1024 B of data + 32 B pad): line i of the wave-row block
+              holds tile rows i, i+16, ..., i+112 (128 B = 64 k each).  A
+              fragment read (ds_read_b128: lane l reads line l & 15, 16-B
+              chunk l >> 4) is serviced in 4 lane groups of 16; with lines 264
+              dwords = 8 banks apart every group covers the 64 banks once, 4
+              LDS cycles per read (a 16-B pad, 4 banks apart, collides chunk 1
+              of line i with chunk 0 of line i + 1 inside a group: 8 cycles)
   staging     LDS-DMA (`buffer_load_dwordx4 ... lds`): one instruction per
               wave fills one line = 8 rows x 128 B (8 whole cache lines), the
               swizzle-free image needs no source permutation.  16 DMA
@@ -69,10 +72,10 @@ from __future__ import annotations
 
 import sys
 
-LINE = 1040              # one LDS line: 8 tile rows x 128 B + 16 B pad
-HALF = 32 * LINE         # 256 rows of one operand = 33280 B
-STAGE = 2 * HALF         # X half + W half = 66560 B
-LDS_BYTES = 2 * STAGE    # 133120 B
+LINE = 1056              # one LDS line: 8 tile rows x 128 B + 32 B pad
+HALF = 32 * LINE         # 256 rows of one operand = 33792 B
+STAGE = 2 * HALF         # X half + W half = 67584 B
+LDS_BYTES = 2 * STAGE    # 135168 B
 KARG_BYTES = 80
 
 # kernarg layout (byte offsets; mirrored by csrc/hip/gemm_asm.hip)
@@ -235,10 +238,15 @@ def prologue(a: Asm, epi: str):
     a(f"s_cselect_b32 {sr(S_TILE)}, {sr(S_T3)}, {sr(S_TILE)}")
     a(f"s_add_u32 {sr(S_TILE)}, {sr(S_TILE)}, {sr(S_T1)}")
     # --- tile -> (tm, tn): groups of 8 row tiles walk the column tiles
+    grp = SCHED["group"]
+    lg = grp.bit_length() - 1
+    assert grp == 1 << lg
+    if grp != 8:  # an A/B arm's group size: per_group from tiles_n here
+        a(f"s_lshl_b32 {sr(S_PG)}, {sr(S_TN_N)}, {lg}")
     udiv(a, S_Q, S_R, S_TILE, S_PG)                   # group, within
-    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, 3")         # first_m
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, {lg}")      # first_m
     a(f"s_sub_u32 {sr(S_T1)}, {sr(S_TM_N)}, {sr(S_T0)}")
-    a(f"s_min_u32 {sr(S_T1)}, {sr(S_T1)}, 8")         # gsz
+    a(f"s_min_u32 {sr(S_T1)}, {sr(S_T1)}, {grp}")     # gsz
     a(f"s_mov_b32 {sr(S_T2)}, {sr(S_R)}")
     udiv(a, S_Q, S_R, S_T2, S_T1)                     # within / gsz, within % gsz
     a(f"s_add_u32 {sr(S_TM)}, {sr(S_T0)}, {sr(S_R)}")
@@ -379,24 +387,36 @@ def mfma(i: int, j: int, sub: int) -> str:
     return f"v_mfma_f32_16x16x32_bf16 {ar(acc, 4)}, {vr(fw, 4)}, {vr(fx, 4)}, {ar(acc, 4)}"
 
 
+# schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
+SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 79, "read_gap": 2, "group": 8, "sub1_gap": 2, "xbar": 15,
+         "xdma_gap": 4}
+
+
 def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0):
     """One 64-k tile: 128 MFMAs with the reads / DMA / waits placed in the
     gaps after MFMA n (n = 0..127; 0..63 phase 1, 64..127 phase 2)."""
+    gap = SCHED["dma_gap"]
     slots: dict[int, list[str]] = {n: [] for n in range(128)}
     # phase 1: sub-step 1 fragment reads of this stage (X then W)
+    g1 = SCHED["sub1_gap"]
+    w0 = 17 if g1 == 2 else 8 * g1
     for j in range(8):
-        slots[2 * j].append(frag_read("x", j, 1))
+        slots[g1 * j].append(frag_read("x", j, 1))
+    xb = SCHED["xbar"]
+    assert xb > g1 * 7
     if with_dma:
-        slots[15] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]      # X half of this stage free
+        slots[xb] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]      # X half of this stage free
     for i in range(8):
-        slots[17 + 2 * i].append(frag_read("w", i, 1))
+        slots[w0 + g1 * i].append(frag_read("w", i, 1))
     if with_dma:
+        xg = SCHED["xdma_gap"]
+        assert xb + 1 + xg * 7 < 47 and w0 + g1 * 7 < 47
         for j in range(8):
-            slots[16 + 4 * j] += dma(a, "x", j)
+            slots[xb + 1 + xg * j] += dma(a, "x", j)
         slots[47] += advance("x")
         slots[47] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]      # W half free
         for j in range(8):
-            slots[48 + 4 * j] += dma(a, "w", j)                 # 48..76
+            slots[48 + gap * j] += dma(a, "w", j)               # 48..76
         slots[78] += advance("w")
         slots[78] += [f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}",
                       f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}"]
@@ -406,21 +426,27 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
     if next_reads:
         # the next tile (staged one iteration ago) has landed: own DMA by the
         # counted wait, everyone's by the barrier
-        slots[79] += [f"s_waitcnt vmcnt({vm_after_dma})", "s_barrier",
+        ws, rg = SCHED["wait_slot"], SCHED["read_gap"]
+        slots[ws] += [f"s_waitcnt vmcnt({vm_after_dma})", "s_barrier",
                       f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
                       f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
         for j in range(8):
-            slots[80 + 2 * j].append(frag_read("x", j, 0))
+            slots[ws + 1 + rg * j].append(frag_read("x", j, 0))
         for i in range(8):
-            slots[96 + 2 * i].append(frag_read("w", i, 0))
+            slots[ws + 1 + rg * (8 + i)].append(frag_read("w", i, 0))
+        assert ws + 1 + rg * 15 < 126
         slots[126].append("s_waitcnt lgkmcnt(0)")
         if trace_base:
-            slots[79] += trace_mark(trace_base + 3)
+            slots[ws] += trace_mark(trace_base + 3)
     if trace_base:
         slots[127] += trace_mark(trace_base + 4)
+    if SCHED["prio"]:
+        slots[127].append("s_setprio 0")
     for n in range(128):
         sub, m = divmod(n, 64)
         i, j = divmod(m, 8)
+        if n == 0 and SCHED["prio"]:
+            a("s_setprio 1")
         if n == 64:
             # phase 2 consumes the sub-step 1 fragments read in phase 1
             a("s_waitcnt lgkmcnt(0)")
@@ -635,11 +661,12 @@ def epilogue_swiglu_bwd(a: Asm):
 
 
 # ---------------------------------------------------------------- kernel
-def kernel(epi: str, trace: bool = False) -> tuple[str, str]:
+def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     """trace=True: the diagnostic trace variant of the plain kernel (markers
-    into a host-coherent buffer in the S slot; toa_gemm_tn_asm_trace)."""
-    name = "toa_gemm_tn_asm_trace" if trace else f"toa_gemm_tn_asm_{epi}"
-    a = Asm(prefix=("trace_" if trace else epi + "_"))
+    into a host-coherent buffer in the S slot; toa_gemm_tn_asm_trace).
+    variant: an A/B arm of the plain kernel (PLAIN_VARIANTS)."""
+    name = "toa_gemm_tn_asm_trace" if trace else f"toa_gemm_tn_asm_{epi}" + (f"_{variant}" if variant else "")
+    a = Asm(prefix=("trace_" if trace else epi + "_" + (variant + "_" if variant else "")))
     tb = (lambda base: base) if trace else (lambda base: 0)
     a.raw(f".globl {name}")
     a.raw(".p2align 8")
@@ -665,7 +692,7 @@ def kernel(epi: str, trace: bool = False) -> tuple[str, str]:
     if trace:
         for ins in trace_mark(2):
             a(ins)
-    if epi == "plain" and not trace:
+    if epi == "plain" and not trace and not variant:
         stage_exit(a, 1)
     for j in range(8):
         a(frag_read("x", j, 0))
@@ -684,7 +711,7 @@ def kernel(epi: str, trace: bool = False) -> tuple[str, str]:
     a.label(l_tail)
     iteration(a, with_dma=False, next_reads=True, vm_after_dma=0, trace_base=tb(200))
     iteration(a, with_dma=False, next_reads=False, vm_after_dma=0, trace_base=tb(300))
-    if epi == "plain" and not trace:
+    if epi == "plain" and not trace and not variant:
         stage_exit(a, 2)
     # MFMA results -> VALU reads: let the last MFMAs retire
     a("s_nop 15")
@@ -700,7 +727,7 @@ def kernel(epi: str, trace: bool = False) -> tuple[str, str]:
             a(ins)
     a.label(a.abort)
     a("s_endpgm")
-    if epi == "plain" and not trace:
+    if epi == "plain" and not trace and not variant:
         a.label(a.stage_exit)
         a("s_waitcnt vmcnt(0)")
         a("s_endpgm")
@@ -850,11 +877,49 @@ PROBE_VBASE = 128
 PROBE_WORDS = PROBE_VBASE + 8 * 256
 
 
+# A/B arms of the plain kernel, launched by index through toa_gemm_asm_variant
+# (scripts/asm_gemm_bench.py --variants): layout / schedule knobs against the
+# product kernel, measured in one process.  Index 0 is the product kernel.
+PLAIN_VARIANTS = (
+    ("v1", {"group": 4}),                   # groups of 4 row tiles
+    ("v2", {"group": 4, "wait_slot": 95, "read_gap": 1}),   # + next-tile wait 16 MFMAs later
+    ("v3", {"sub1_gap": 1, "xbar": 23, "xdma_gap": 3}),     # X-free barrier 16 MFMAs after the last X read
+    ("v4", {"group": 4, "wait_slot": 95, "read_gap": 1, "sub1_gap": 1, "xbar": 23, "xdma_gap": 3}),
+    ("v5", {"group": 2}),                   # groups of 2 row tiles
+)
+# measured and rejected (profiles/r4_asm_gemm/ab1): LDS lines of 1040 B (same
+# speed despite 2-way read conflicts), DMA pieces bunched after each barrier
+# (-2..-4 %), groups of 16 row tiles (-1..-7 %)
+
+
+def _with_knobs(knobs: dict, fn):
+    """Run fn() with the layout globals / SCHED entries in `knobs` overridden."""
+    g = globals()
+    saved = {k: g[k] for k in ("LINE", "HALF", "STAGE", "LDS_BYTES")}
+    saved_sched = dict(SCHED)
+    try:
+        if "LINE" in knobs:
+            g["LINE"] = knobs["LINE"]
+            g["HALF"] = 32 * g["LINE"]
+            g["STAGE"] = 2 * g["HALF"]
+            g["LDS_BYTES"] = 2 * g["STAGE"]
+        SCHED.update({k: v for k, v in knobs.items() if k in SCHED})
+        return fn()
+    finally:
+        g.update(saved)
+        SCHED.clear()
+        SCHED.update(saved_sched)
+
+
 def generate() -> str:
     parts = ['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".amdhsa_code_object_version 5", ".text"]
     metas = []
     for epi in EPIS:
         body, meta = kernel(epi)
+        parts.append(body)
+        metas.append(meta)
+    for vname, knobs in PLAIN_VARIANTS:
+        body, meta = _with_knobs(knobs, lambda: kernel("plain", variant=vname))
         parts.append(body)
         metas.append(meta)
     for body, meta in (probe_kernel(), kernel("plain", trace=True)):

@@ -1,13 +1,14 @@
-"""Hand-written gfx950 assembly GEMM (csrc/asm/gemm_gen.py) vs hipBLASLt and
-the HIP TN kernel at the Llama-3-8B forward / data-gradient forms, in-process
-interleaved rounds on random operands (guide section 5.4 rules 24/25).
+"""Hand-written gfx950 assembly GEMM (csrc/asm/gemm_gen.py) vs hipBLASLt at
+the Llama-3-8B forward / data-gradient forms, in-process interleaved rounds on
+random operands (guide section 5.4 rules 24/25).
 
     python scripts/asm_gemm_bench.py --check        # numerics only (small shapes)
-    python scripts/asm_gemm_bench.py [--tokens 24576] [--rounds 5] [--reps 5]
+    python scripts/asm_gemm_bench.py [--tokens 24576] [--rounds 5] [--reps 5] [--variants 1,2,3]
 
 Arms: asm (toa_gemm_asm), blt_nosk (hipBLASLt non-stream-K table),
-blt_heur (torch.matmul), and the
-fused MLP ends (asm SwiGLU epilogues vs hipBLASLt + the SwiGLU row kernels).
+blt_heur (torch.matmul), asm_v<n> (the plain kernel's A/B arms,
+gemm_gen.py PLAIN_VARIANTS; checked bit-identical to asm), and the fused MLP
+ends (asm SwiGLU epilogues vs hipBLASLt + the SwiGLU row kernels).
 """
 import argparse
 import json
@@ -45,6 +46,13 @@ def asm_swiglu_bwd(d2, wdt, gu):
     _lib.call("toa_gemm_asm_swiglu_bwd", _lib.ptr(d2), d2.stride(0), _lib.ptr(wdt), wdt.stride(0), _lib.ptr(gu),
               2 * F, _lib.ptr(dgu), 2 * F, M, F, d2.shape[1], _lib.stream(d2))
     return dgu
+
+
+def asm_variant(v, x, w, y):
+    M, K = x.shape
+    N = w.shape[0]
+    _lib.call("toa_gemm_asm_variant", v, _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), y.stride(0),
+              M, N, K, _lib.stream(x))
 
 
 def rel(a, b):
@@ -186,6 +194,7 @@ def bench(a):
     T = a.tokens
     torch.manual_seed(0)
     out = {"tokens": T, "forms": {}}
+    variants = [int(v) for v in a.variants.split(",") if v]
     for name, (K, N) in FORMS.items():
         for kind, (kk, nn) in (("fwd", (K, N)), ("dgrad_wt", (N, K))):
             if a.forms and f"{name}.{kind}" not in a.forms.split(","):
@@ -196,16 +205,25 @@ def bench(a):
             arms = [("asm", lambda: asm(x, w, y)),
                     ("blt_nosk", lambda: (gemm.set_mode("nosk"), gemm.linear_fwd(x, w))),
                     ("blt_heur", lambda: torch.matmul(x, w.t()))]
+            yv = torch.empty_like(y)
+            for v in variants:
+                arms.append((f"asm_v{v}", lambda v=v: asm_variant(v, x, w, yv)))
             ts = {k: [] for k, _ in arms}
             for _ in range(a.rounds):
                 for k, f in arms:
                     ts[k].append(timer(f, a.reps))
             asm(x, w, y)
+            same = {}
+            for v in variants:
+                asm_variant(v, x, w, yv)
+                same[f"asm_v{v}"] = bool(torch.equal(y, yv))
             err = rel(y, x.float() @ w.float().t()) if T * nn <= 24576 * 28672 else -1.0
             fl = 2.0 * T * nn * kk
             rec = {k: {"ms": round(statistics.median(v), 4), "TFps": round(fl / statistics.median(v) / 1e9, 1)}
                    for k, v in ts.items()}
             rec["asm_rel_err"] = round(err, 5)
+            if same:
+                rec["variants_bit_identical"] = same
             out["forms"][f"{name}.{kind}"] = rec
             print(json.dumps({f"{name}.{kind}": rec}), flush=True)
             del x, w, y
@@ -241,6 +259,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--forms", default="")
     ap.add_argument("--mlp", type=int, default=1)
+    ap.add_argument("--variants", default="", help="plain-kernel A/B arms to add, e.g. 1,2,3")
     a = ap.parse_args()
     if a.probe:
         probe()

@@ -60,6 +60,25 @@ def test_asm_gemm_plain_emulated(M, N, K):
     assert np.mean(np.abs(C - tof(bf16(ref))) <= np.abs(ref) * 2 ** -7) > 0.999
 
 
+@pytest.mark.parametrize("variant", [v for v, _ in gemm_gen.PLAIN_VARIANTS])
+def test_asm_gemm_variants_match_product_kernel(variant):
+    """Each A/B arm of the plain kernel (other LDS pad, DMA spacing, wait slot,
+    row-group size) writes exactly the product kernel's C on a 5 x 2 grid."""
+    rng = np.random.default_rng(11)
+    M, N, K = 1280, 512, 128
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)))
+    out = []
+    for name in ("toa_gemm_tn_asm_plain", f"toa_gemm_tn_asm_plain_{variant}"):
+        mem = emu.Memory()
+        ax, aw, ac = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16))
+        karg = host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256)
+        run_all(name, karg, (M // 256) * (N // 256), mem)
+        out.append(mem.bufs[2][1].view(np.uint16).reshape(M, N).copy())
+    assert np.array_equal(out[0], out[1])
+    close(tof(out[0]), tof(X) @ tof(W).T)
+
+
 def test_asm_gemm_strided_rows_emulated():
     """ld > K on both operands and an output view with ld > N, offset columns."""
     rng = np.random.default_rng(7)

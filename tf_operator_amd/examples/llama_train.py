@@ -65,6 +65,7 @@ def _train(a, rt, info):
     zero = rt.world > 1 if a.zero == "auto" else a.zero == "1"
     tr = LlamaTrainer(a.model, dev, micro_batch=a.micro_batch, seq_len=a.seq_len, lr=a.lr, shard_optimizer=zero)
     rt.mark("model_init")
+    tr.on_phase = rt.mark  # the first step's host-side issue points, in the start-up phases
     ck = sharded_ckpt.Checkpointer(rt.ckpt_dir, rt.rank, rt.world) if rt.ckpt_dir else None
     if ck is not None:
         ck.sync_attempt()  # markers of a crashed earlier attempt never commit this run's saves

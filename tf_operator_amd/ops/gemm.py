@@ -4,13 +4,12 @@
     linear_dgrad(dy, w)        dx = dy w             [M,N] x [N,K] -> [M,K]
     wgrad_acc_(g, dy, x)       g += dy^T x           (beta = 1, in place)
 
-The forward / data-gradient forms run on the hand-written assembly kernel
-under the default policy; the weight gradient on the NT kernel
-(csrc/hip/wgrad.hip).  The hipBLASLt layer (csrc/hip/gemm.hip, one
-column-major call per form, see there for the transposition algebra) serves
-the shapes the assembly kernel does not tile and the ``tuned`` / ``nosk``
-policies: its per-form solution tables measured by ``scripts/tune_gemm.py``
-on an MI355X are stored next to this file, keyed by the hipBLASLt build.
+The forward / data-gradient forms run on the hipBLASLt layer
+(csrc/hip/gemm.hip, one column-major call per form, see there for the
+transposition algebra) or, under ``TOA_GEMM=asm``, on the hand-written
+assembly kernel; the weight gradient on the NT kernel (csrc/hip/wgrad.hip).
+The per-form solution tables measured by ``scripts/tune_gemm.py`` on an
+MI355X are stored next to this file, keyed by the hipBLASLt build.
 
 Modes (``TOA_GEMM``):
 
@@ -33,7 +32,7 @@ Modes (``TOA_GEMM``):
   (profiles/r2_sk_contention; +6.7 % vs +3.4 % under emulated world-8
   ZeRO-1 traffic, profiles/r3_overlap).
 * ``auto`` (the default): resolved by :func:`resolve_auto` when the trainer
-  starts -- ``asm`` when the kernel library carries it, else ``nosk``.
+  starts, to ``nosk``.
 """
 from __future__ import annotations
 
@@ -69,13 +68,13 @@ def set_mode(m: str):
 
 
 def resolve_auto(world: int = 1) -> str:
-    """``auto`` -> ``asm`` when the library has the assembly kernels, else
-    ``nosk`` (an explicit TOA_GEMM is kept).  Returns the mode in force.
-    The assembly kernel is not persistent (one workgroup per tile), so under
-    world-N collectives it yields CUs as tiles retire, like ``nosk``."""
+    """``auto`` -> ``nosk`` (an explicit TOA_GEMM is kept).  Returns the mode
+    in force.  ``asm`` stays opt-in until it wins in-model: the Llama-3-8B
+    step measured 1010.7 / 1014.8 ms on it against 977.2 / 978.4 ms on
+    ``nosk``, alternating on one box (profiles/r4_asm_gemm/ab1)."""
     del world
     if _MODE == "auto":
-        set_mode("asm" if _lib.has("toa_gemm_asm") else "nosk")
+        set_mode("nosk")
     return _MODE
 
 

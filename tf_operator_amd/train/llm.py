@@ -88,6 +88,14 @@ class LlamaTrainer:
         if self.opt.overlap or self.gather is not None:
             self._hooks = self._install_param_waits()
         self.step_idx = 0
+        # start-up diagnostics: called with a phase name after the first
+        # step's forward / backward / update are issued (host side; the
+        # replica runtime's mark, examples/llama_train.py)
+        self.on_phase = None
+
+    def _phase(self, name):
+        if self.on_phase is not None and self.step_idx == 0:
+            self.on_phase(name)
 
     def _wait_bucket(self, b):
         self.opt.wait_bucket(b)
@@ -136,11 +144,13 @@ class LlamaTrainer:
         loss_sum = None
         for i, (tok, tgt) in enumerate(batches):
             loss = self.model(tok, tgt)
+            self._phase("first_fwd_issued")
             self.opt.wait_all()  # backward writes gradients the update is still zeroing
             if self.gather is not None:
                 self.gather.wait_all()  # backward reads every weight (and W^T)
             self.bucketer.armed = i == len(batches) - 1  # reduce once, after the last micro-batch
             (loss / len(batches)).backward()
+            self._phase("first_bwd_issued")
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
         if self.fresh_grads and not self.opt.overlap:
             self.flat.zero_stale()  # parameters no producer wrote this step
@@ -155,6 +165,7 @@ class LlamaTrainer:
             self.opt.step(grad_scale=self.bucketer.grad_scale)
             if self.gather is not None:
                 self.gather.launch()
+        self._phase("first_update_issued")
         self.step_idx += 1
         return loss_sum / len(batches)
 
