@@ -203,6 +203,14 @@ class Emu:
     def op_s_load_dwordx4(self, w, a, m):
         self._sload(w, a, 4)
 
+    def op_s_memtime(self, w, a, m):
+        """A monotonically increasing stand-in for the shader clock: this
+        wave's instruction count (the timing kernel's records stay ordered)."""
+        kind, lo, hi = self._reg(w, a[0])
+        w.ticks = getattr(w, "ticks", 0) + 1000
+        t = w.ticks + w.pc
+        w.s[lo], w.s[lo + 1] = t & M32, t >> 32
+
     def _sload(self, w, a, n):
         kind, lo, hi = self._reg(w, a[0])
         off = self._lit(a[2])
@@ -462,6 +470,31 @@ class Emu:
             raise IndexError("LDS-DMA past the LDS")
         for l in range(64):
             self.lds[dst[l]:dst[l] + 16] = data[l]
+
+    def op_buffer_load_dword(self, w, a, mods):
+        """4-B load into a VGPR.  Lanes past num_records read 0, as on the
+        hardware: the kernels use this form only for L2-prefetch loads whose
+        result is discarded (gemm_gen.py l2pf), which run past the tensor on
+        the last tiles.  Every other buffer access past num_records raises."""
+        assert "lds" not in mods
+        voff = self.vget(w, a[1]).astype(np.uint64)
+        kind, lo_, hi_ = self._reg(w, a[2])
+        srd = [int(w.s[lo_ + i]) & M32 for i in range(4)]
+        base, nrec = srd[0] | ((srd[1] & 0xFFFF) << 32), srd[2]
+        ioff = 0
+        for md in mods:
+            if md.startswith("offset:"):
+                ioff = int(md.split(":")[1])
+        off = voff + self.sget(w, a[3]) + ioff
+        out = np.zeros(64, np.uint32)
+        ok = off + 4 <= nrec
+        if ok.any():
+            addr = base + off[ok]
+            b0, buf = self.mem.locate(addr, 4)
+            rel = (addr - b0).astype(np.int64)
+            out[ok] = np.stack([buf[rel + i] for i in range(4)], axis=1).view(np.uint32).reshape(-1)
+        lo, hi = self.vrange(w, a[0])
+        w.v[lo] = out
 
     def op_buffer_load_dwordx2(self, w, a, mods):
         addr = self._buffer_addr(w, a[1:], mods, 8)

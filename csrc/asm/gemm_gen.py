@@ -104,7 +104,12 @@ S_SOX = 53          # s53..s59: X DMA row offsets, instructions 1..7
 S_SOW = 60          # s60..s66: W DMA row offsets
 S_E0, S_E1 = 67, 68  # epilogue scratch
 S_Q, S_R = 69, 70   # division results
-N_SGPR = 72
+SRD_PX, SRD_PW, S_PK = 72, 76, 80   # L2-prefetch resources / k offset (l2pf arms)
+# timing kernel (never with l2pf, whose SGPRs it reuses): s72..s83 six
+# s_memtime stamps (aligned pairs), s84..s86 accumulated waits (vm, X-free
+# barrier, W-free barrier), s88..s89 the kernel's start stamp
+S_TMT, S_ACC, S_T_START = 72, 84, 88
+N_SGPR = 90
 
 # VGPRs
 V_TID = 132
@@ -114,6 +119,7 @@ V_RXT, V_RWT = 134, 135    # stage toggles (xor masks)
 V_FX0, V_FX1 = 4, 36       # X fragments, sub-steps 0 / 1 (8 x 4 VGPRs each)
 V_FW0, V_FW1 = 68, 100     # W fragments
 V_T = 136                  # 136..139 scratch
+V_PX, V_PW = 250, 251      # L2-prefetch row offsets (l2pf arms; in the epilogue scratch, free in the loop)
 V_E = 140                  # 140..255 epilogue scratch
 
 UNIT_GATE_ROWS = 64        # swiglu_fwd: W rows per wave column per half
@@ -237,12 +243,11 @@ def prologue(a: Asm, epi: str):
     a(f"s_cmp_lt_u32 {sr(S_T0)}, {sr(S_XR)}")
     a(f"s_cselect_b32 {sr(S_TILE)}, {sr(S_T3)}, {sr(S_TILE)}")
     a(f"s_add_u32 {sr(S_TILE)}, {sr(S_TILE)}, {sr(S_T1)}")
-    # --- tile -> (tm, tn): groups of 8 row tiles walk the column tiles
+    # --- tile -> (tm, tn): groups of `group` row tiles walk the column tiles
     grp = SCHED["group"]
     lg = grp.bit_length() - 1
     assert grp == 1 << lg
-    if grp != 8:  # an A/B arm's group size: per_group from tiles_n here
-        a(f"s_lshl_b32 {sr(S_PG)}, {sr(S_TN_N)}, {lg}")
+    a(f"s_lshl_b32 {sr(S_PG)}, {sr(S_TN_N)}, {lg}")   # tiles per group (the kernarg's is not used)
     udiv(a, S_Q, S_R, S_TILE, S_PG)                   # group, within
     a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, {lg}")      # first_m
     a(f"s_sub_u32 {sr(S_T1)}, {sr(S_TM_N)}, {sr(S_T0)}")
@@ -319,6 +324,20 @@ def prologue(a: Asm, epi: str):
         rows_w = 8 * (j % 4) + (UNIT_GATE_ROWS if epi == "swiglu_fwd" else 128) * (j // 4)
         a(f"s_mul_i32 {sr(S_SOX + j - 1)}, {sr(S_LDX)}, {rows_x}")
         a(f"s_mul_i32 {sr(S_SOW + j - 1)}, {sr(S_LDW)}, {rows_w}")
+    if SCHED["l2pf"]:
+        assert epi == "plain"
+        # L2 prefetch rows: 64 w + lane of each operand (one 128-B line each);
+        # resources over exactly the tile's rows x K, k offset of tile 2 + l2pf
+        a(f"v_mul_lo_u32 {vr(V_PX)}, {vr(V_TID)}, {sr(S_LDX)}")
+        a(f"v_mul_lo_u32 {vr(V_PW)}, {vr(V_TID)}, {sr(S_LDW)}")
+        a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_KT)}, 7")                 # K bytes
+        for dst, src, ld in ((SRD_PX, SRD_X, S_LDX), (SRD_PW, SRD_W, S_LDW)):
+            a(f"s_mov_b32 {sr(dst)}, {sr(src)}")
+            a(f"s_mov_b32 {sr(dst + 1)}, {sr(src + 1)}")
+            a(f"s_mul_i32 {sr(dst + 2)}, {sr(ld)}, 255")
+            a(f"s_add_u32 {sr(dst + 2)}, {sr(dst + 2)}, {sr(S_T0)}")
+            a(f"s_mov_b32 {sr(dst + 3)}, 0x20000")
+        a(f"s_mov_b32 {sr(S_PK)}, {128 * (2 + SCHED['l2pf'])}")
     # --- LDS-DMA bases (M0): wave w at line w of the stage's half
     a("s_nop 4")
     a(f"v_readfirstlane_b32 {sr(S_T0)}, {vr(v)}")          # w
@@ -388,8 +407,19 @@ def mfma(i: int, j: int, sub: int) -> str:
 
 
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
-SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 79, "read_gap": 2, "group": 8, "sub1_gap": 2, "xbar": 15,
-         "xdma_gap": 4}
+SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
+         "xdma_gap": 3, "merge_bar": False, "l2pf": 0, "timing": False}
+
+
+def _stamp(k: int) -> str:
+    return f"s_memtime {sr(S_TMT + 2 * k, 2)}"
+
+
+def _accum(acc: int, k_end: int, k_begin: int) -> list[str]:
+    """acc += low dword of stamp k_end - stamp k_begin (timing kernel; the
+    stamps have returned: called after an lgkmcnt(0))."""
+    return [f"s_sub_u32 {sr(S_E0)}, {sr(S_TMT + 2 * k_end)}, {sr(S_TMT + 2 * k_begin)}",
+            f"s_add_u32 {sr(S_ACC + acc)}, {sr(S_ACC + acc)}, {sr(S_E0)}"]
 
 
 def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0):
@@ -404,19 +434,40 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
         slots[g1 * j].append(frag_read("x", j, 1))
     xb = SCHED["xbar"]
     assert xb > g1 * 7
+    if with_dma and SCHED["l2pf"]:
+        # warm the L2 with the tile `l2pf` beyond the one the DMA fetches
+        # next: one 4-B load per 128-B line (lane = row), result discarded;
+        # issued before this iteration's DMA, so the counted waits below
+        # (vm_after_dma + 2) retire them a whole iteration later
+        # (own resources bounded to the tile's rows x K: past K they read 0
+        # and touch no memory, the running k offset in S_PK)
+        slots[1].append(f"buffer_load_dword {vr(V_E)}, {vr(V_PX)}, {sr(SRD_PX, 4)}, {sr(S_PK)} offen")
+        slots[3].append(f"buffer_load_dword {vr(V_E + 1)}, {vr(V_PW)}, {sr(SRD_PW, 4)}, {sr(S_PK)} offen")
+        slots[5].append(f"s_add_u32 {sr(S_PK)}, {sr(S_PK)}, 128")
+    tm = SCHED["timing"]
     if with_dma:
-        slots[xb] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]      # X half of this stage free
+        slots[xb] += ([_stamp(2)] if tm else []) + ["s_waitcnt lgkmcnt(0)", "s_barrier"] + ([_stamp(3)] if tm else [])
     for i in range(8):
         slots[w0 + g1 * i].append(frag_read("w", i, 1))
-    if with_dma:
+    if with_dma and SCHED["merge_bar"]:
+        # one barrier frees both halves (every sub-step 1 read is issued
+        # before it), then the 16 DMA pieces, X first
+        assert w0 + g1 * 7 < xb
+        xg = SCHED["xdma_gap"]
+        for j in range(16):
+            slots[xb + 1 + xg * j] += dma(a, "x" if j < 8 else "w", j % 8)
+        assert xb + 1 + xg * 15 < 78
+        slots[xb + 1 + xg * 8 - 1] += advance("x")
+    elif with_dma:
         xg = SCHED["xdma_gap"]
         assert xb + 1 + xg * 7 < 47 and w0 + g1 * 7 < 47
         for j in range(8):
             slots[xb + 1 + xg * j] += dma(a, "x", j)
         slots[47] += advance("x")
-        slots[47] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]      # W half free
+        slots[47] += ([_stamp(4)] if tm else []) + ["s_waitcnt lgkmcnt(0)", "s_barrier"] + ([_stamp(5)] if tm else [])
         for j in range(8):
             slots[48 + gap * j] += dma(a, "w", j)               # 48..76
+    if with_dma:
         slots[78] += advance("w")
         slots[78] += [f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}",
                       f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}"]
@@ -427,7 +478,8 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
         # the next tile (staged one iteration ago) has landed: own DMA by the
         # counted wait, everyone's by the barrier
         ws, rg = SCHED["wait_slot"], SCHED["read_gap"]
-        slots[ws] += [f"s_waitcnt vmcnt({vm_after_dma})", "s_barrier",
+        vm = vm_after_dma + (2 if (with_dma and SCHED["l2pf"]) else 0)
+        slots[ws] += ([_stamp(0)] if tm else []) + [f"s_waitcnt vmcnt({vm})", "s_barrier"] + ([_stamp(1)] if tm else []) + [
                       f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
                       f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
         for j in range(8):
@@ -436,6 +488,8 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
             slots[ws + 1 + rg * (8 + i)].append(frag_read("w", i, 0))
         assert ws + 1 + rg * 15 < 126
         slots[126].append("s_waitcnt lgkmcnt(0)")
+        if tm:
+            slots[126] += _accum(0, 1, 0)
         if trace_base:
             slots[ws] += trace_mark(trace_base + 3)
     if trace_base:
@@ -450,6 +504,9 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
         if n == 64:
             # phase 2 consumes the sub-step 1 fragments read in phase 1
             a("s_waitcnt lgkmcnt(0)")
+            if tm and with_dma:
+                for ins in _accum(1, 3, 2) + ([] if SCHED["merge_bar"] else _accum(2, 5, 4)):
+                    a(ins)
         a(mfma(i, j, sub))
         for ins in slots[n]:
             a(ins)
@@ -666,6 +723,8 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     into a host-coherent buffer in the S slot; toa_gemm_tn_asm_trace).
     variant: an A/B arm of the plain kernel (PLAIN_VARIANTS)."""
     name = "toa_gemm_tn_asm_trace" if trace else f"toa_gemm_tn_asm_{epi}" + (f"_{variant}" if variant else "")
+    if SCHED["timing"]:
+        name = "toa_gemm_tn_asm_timing"
     a = Asm(prefix=("trace_" if trace else epi + "_" + (variant + "_" if variant else "")))
     tb = (lambda base: base) if trace else (lambda base: 0)
     a.raw(f".globl {name}")
@@ -673,6 +732,12 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     a.raw(f".type {name},@function")
     a.raw(f"{name}:")
     prologue(a, epi)
+    timing = SCHED["timing"]
+    assert not (timing and SCHED["l2pf"])
+    if timing:
+        a(f"s_memtime {sr(S_T_START, 2)}")
+        for k in range(3):
+            a(f"s_mov_b32 {sr(S_ACC + k)}, 0")
     if trace:
         for ins in trace_setup(a) + trace_mark(1):
             a(ins)
@@ -713,6 +778,8 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     iteration(a, with_dma=False, next_reads=False, vm_after_dma=0, trace_base=tb(300))
     if epi == "plain" and not trace and not variant:
         stage_exit(a, 2)
+    if timing:
+        a(_stamp(0))                                # main loop done
     # MFMA results -> VALU reads: let the last MFMAs retire
     a("s_nop 15")
     a("s_nop 15")
@@ -722,6 +789,20 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     epi_offsets(a, epi)
     {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
     a("s_waitcnt vmcnt(0)")
+    if timing:
+        # record per (workgroup, wave): vm wait, X-free barrier, W-free barrier,
+        # start -> loop end, epilogue, k-tiles, workgroup id, 0 (cycles)
+        a(_stamp(1))
+        a("s_waitcnt lgkmcnt(0)")
+        a(f"s_sub_u32 {sr(S_TMT + 4)}, {sr(S_TMT)}, {sr(S_T_START)}")
+        a(f"s_sub_u32 {sr(S_TMT + 5)}, {sr(S_TMT + 2)}, {sr(S_TMT)}")
+        for ins in trace_setup(a):
+            a(ins)
+        for k, src in enumerate((sr(S_ACC), sr(S_ACC + 1), sr(S_ACC + 2), sr(S_TMT + 4), sr(S_TMT + 5), sr(S_KT),
+                                 "s2", "0")):
+            a(f"v_mov_b32 {vr(V_T + 2)}, {src}")
+            a(f"buffer_store_dword {vr(V_T + 2)}, {vr(V_T + 3)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * k}")
+        a("s_waitcnt vmcnt(0)")
     if trace:
         for ins in trace_setup(a)[-3:] + trace_mark(9999):
             a(ins)
@@ -822,6 +903,7 @@ def _descriptor(name: str) -> tuple[str, str]:
     return desc, meta
 
 
+PROBE_SGPRS = 72   # s0..s71: what the plain prologue writes (the l2pf arms' s72.. are not dumped)
 PROBE_MAGIC = (0x626F7270, 0x31657461)   # "prob" "ate1" in the fw / fc argument slots
 
 
@@ -852,13 +934,13 @@ def probe_kernel() -> tuple[str, str]:
     a(f"s_mov_b32 {sr(SRD_S + 2)}, {PROBE_WORDS * 4}")
     a(f"s_mov_b32 {sr(SRD_S + 3)}, 0x20000")
     a(f"v_mov_b32 {vr(V_T + 1)}, 0")
-    for r in range(N_SGPR):
+    for r in range(PROBE_SGPRS):
         if r in (SRD_S, SRD_S + 1, SRD_S + 2, SRD_S + 3, S_E0):
             continue
         a(f"v_mov_b32 {vr(V_T)}, {sr(r)}")
         a(f"buffer_store_dword {vr(V_T)}, {vr(V_T + 1)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * r}")
     a(f"v_mov_b32 {vr(V_T)}, m0")
-    a(f"buffer_store_dword {vr(V_T)}, {vr(V_T + 1)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * N_SGPR}")
+    a(f"buffer_store_dword {vr(V_T)}, {vr(V_T + 1)}, {sr(SRD_S, 4)}, 0 offen offset:{4 * PROBE_SGPRS}")
     # per thread: 8 words at 4 * (PROBE_VBASE + 8 tid)
     a(f"v_lshlrev_b32 {vr(V_T + 1)}, 5, {vr(V_TID)}")
     for k, reg in enumerate((V_DX, V_DW, V_RX, V_RW, V_RXT, V_RWT, V_E, V_TID)):
@@ -881,15 +963,17 @@ PROBE_WORDS = PROBE_VBASE + 8 * 256
 # (scripts/asm_gemm_bench.py --variants): layout / schedule knobs against the
 # product kernel, measured in one process.  Index 0 is the product kernel.
 PLAIN_VARIANTS = (
-    ("v1", {"group": 4}),                   # groups of 4 row tiles
-    ("v2", {"group": 4, "wait_slot": 95, "read_gap": 1}),   # + next-tile wait 16 MFMAs later
-    ("v3", {"sub1_gap": 1, "xbar": 23, "xdma_gap": 3}),     # X-free barrier 16 MFMAs after the last X read
-    ("v4", {"group": 4, "wait_slot": 95, "read_gap": 1, "sub1_gap": 1, "xbar": 23, "xdma_gap": 3}),
-    ("v5", {"group": 2}),                   # groups of 2 row tiles
+    ("v1", {"l2pf": 2}),                    # + L2 prefetch of the tile two beyond the DMA
+    ("v2", {"l2pf": 2, "group": 2}),        # + groups of 2 row tiles
+    ("v3", {"merge_bar": True}),            # two barriers per tile: one frees both halves
+    ("v4", {"wait_slot": 79, "read_gap": 2}),   # next-tile wait 16 MFMAs earlier
+    ("v5", {"group": 8, "wait_slot": 79, "read_gap": 2, "sub1_gap": 2, "xbar": 15, "xdma_gap": 4}),  # round-4 v2
 )
-# measured and rejected (profiles/r4_asm_gemm/ab1): LDS lines of 1040 B (same
-# speed despite 2-way read conflicts), DMA pieces bunched after each barrier
-# (-2..-4 %), groups of 16 row tiles (-1..-7 %)
+# measured (profiles/r4_asm_gemm/ab1, ab2): LDS lines of 1040 B (same speed
+# despite 2-way read conflicts), DMA pieces bunched after each barrier
+# (-2..-4 %) and groups of 16 row tiles (-1..-7 %) rejected; groups of 4, the
+# next-tile wait at MFMA 95 and the X-free barrier 16 MFMAs after the last X
+# read taken into the product kernel (+1..+4 %)
 
 
 def _with_knobs(knobs: dict, fn):
@@ -922,7 +1006,8 @@ def generate() -> str:
         body, meta = _with_knobs(knobs, lambda: kernel("plain", variant=vname))
         parts.append(body)
         metas.append(meta)
-    for body, meta in (probe_kernel(), kernel("plain", trace=True)):
+    for body, meta in (probe_kernel(), kernel("plain", trace=True),
+                       _with_knobs({"timing": True}, lambda: kernel("plain", variant="timing"))):
         parts.append(body)
         metas.append(meta)
     # what hipcc emits after the last kernel: s_nop padding, so the

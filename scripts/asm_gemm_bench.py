@@ -179,6 +179,44 @@ def trace(shapes):
             raise SystemExit(1)
 
 
+def timing(a):
+    """Where the product kernel's cycles go (the timing kernel, gemm_gen.py
+    SCHED["timing"]): per form, the mean over (workgroup, wave) of the cycles
+    parked in the next-tile vmcnt wait + barrier, the X-free and W-free
+    barriers, the epilogue, as shares of start -> end."""
+    import numpy as np
+
+    T = a.tokens
+    res = {}
+    for name, (K, N) in FORMS.items():
+        for kind, (kk, nn) in (("fwd", (K, N)), ("dgrad_wt", (N, K))):
+            if a.forms and f"{name}.{kind}" not in a.forms.split(","):
+                continue
+            x = torch.randn(T, kk, device="cuda").to(torch.bfloat16)
+            w = (torch.randn(nn, kk, device="cuda") / kk ** 0.5).to(torch.bfloat16)
+            y = torch.empty(T, nn, device="cuda", dtype=torch.bfloat16)
+            nwg = (T // 256) * (nn // 256)
+            rec = torch.zeros(nwg * 32, device="cuda", dtype=torch.int32)
+            for _ in range(3):  # warm (clocks, caches); the last run's records are read
+                _lib.call("toa_gemm_asm_timing", _lib.ptr(rec), _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn,
+                          T, nn, kk, _lib.stream(x))
+            torch.cuda.synchronize()
+            r = rec.cpu().numpy().view(np.uint32).reshape(nwg, 4, 8).astype(np.float64)
+            tot = r[:, :, 3] + r[:, :, 4]
+            res[f"{name}.{kind}"] = {
+                "cycles_per_tile": round(float(tot.mean()), 0),
+                "loop_cycles_per_ktile": round(float((r[:, :, 3] / r[:, :, 5]).mean()), 1),
+                "vm_wait_pct": round(float(100 * (r[:, :, 0] / tot).mean()), 2),
+                "xbar_pct": round(float(100 * (r[:, :, 1] / tot).mean()), 2),
+                "wbar_pct": round(float(100 * (r[:, :, 2] / tot).mean()), 2),
+                "epilogue_pct": round(float(100 * (r[:, :, 4] / tot).mean()), 2),
+                "tile_cycles_p10_p90": [float(np.percentile(tot, 10)), float(np.percentile(tot, 90))]}
+            print(json.dumps({f"{name}.{kind}": res[f"{name}.{kind}"]}), flush=True)
+            del x, w, y
+            torch.cuda.empty_cache()
+    print(json.dumps({"timing": res}))
+
+
 def timer(fn, reps):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     fn()
@@ -260,12 +298,16 @@ def main():
     ap.add_argument("--forms", default="")
     ap.add_argument("--mlp", type=int, default=1)
     ap.add_argument("--variants", default="", help="plain-kernel A/B arms to add, e.g. 1,2,3")
+    ap.add_argument("--timing", action="store_true", help="wait-cycle breakdown of the product kernel (--forms)")
     a = ap.parse_args()
     if a.probe:
         probe()
         return
     if a.trace:
         trace(a.trace)
+        return
+    if a.timing:
+        timing(a)
         return
     if a.stage >= 0:
         M, N, K = 256, 256, 128

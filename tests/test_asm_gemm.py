@@ -65,7 +65,7 @@ def test_asm_gemm_variants_match_product_kernel(variant):
     """Each A/B arm of the plain kernel (other LDS pad, DMA spacing, wait slot,
     row-group size) writes exactly the product kernel's C on a 5 x 2 grid."""
     rng = np.random.default_rng(11)
-    M, N, K = 1280, 512, 128
+    M, N, K = 1280, 512, 384   # 6 k-tiles: the loop runs (DMA, L2 prefetch past K)
     X = bf16(rng.standard_normal((M, K)))
     W = bf16(rng.standard_normal((N, K)))
     out = []
@@ -77,6 +77,25 @@ def test_asm_gemm_variants_match_product_kernel(variant):
         out.append(mem.bufs[2][1].view(np.uint16).reshape(M, N).copy())
     assert np.array_equal(out[0], out[1])
     close(tof(out[0]), tof(X) @ tof(W).T)
+
+
+def test_asm_gemm_timing_kernel_emulated():
+    """The timing diagnostic computes the product kernel's C and writes one
+    8-dword record per (workgroup, wave) with ordered stamps."""
+    rng = np.random.default_rng(5)
+    M, N, K = 512, 256, 384
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)))
+    mem = emu.Memory()
+    ax, aw, ac = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16))
+    nwg = (M // 256) * (N // 256)
+    at = mem.add(np.zeros(nwg * 4 * 8, np.uint32))
+    karg = host_args.pack(ax, aw, ac, at, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256)
+    run_all("toa_gemm_tn_asm_timing", karg, nwg, mem)
+    close(tof(mem.bufs[2][1].view(np.uint16).reshape(M, N)), tof(X) @ tof(W).T)
+    rec = mem.bufs[3][1].view(np.uint32).reshape(nwg, 4, 8)
+    assert (rec[:, :, 5] == K // 64).all() and (rec[:, :, 6] == np.arange(nwg)[:, None]).all()
+    assert (rec[:, :, 3] > 0).all() and (rec[:, :, 4] > 0).all()
 
 
 def test_asm_gemm_strided_rows_emulated():
@@ -132,21 +151,36 @@ def test_asm_gemm_swiglu_bwd_emulated():
     close(dgu[:, F:], ds * g * sg)
 
 
-def test_asm_gemm_tile_order_is_a_bijection():
+@pytest.mark.parametrize("grp", [2, 4, 8, 16])
+def test_asm_gemm_tile_order_is_a_bijection(grp):
     """The XCD remap + row-group walk visits every (tm, tn) exactly once, for
-    grids that are and are not multiples of 8 (checked on the formulas the
-    prologue implements, via the emulator's scalar unit on a no-op grid)."""
+    grids that are and are not multiples of 8 and of the group size (the
+    formulas the prologue implements)."""
     for tm_n, tn_n in ((1, 1), (3, 5), (96, 16), (7, 9), (96, 501)):
-        nwg, xq, xr, pg = host_args.grid_params(tm_n, tn_n)
+        nwg, xq, xr, _ = host_args.grid_params(tm_n, tn_n)
+        pg = grp * tn_n
         seen = set()
         for b in range(nwg):
             xcd, bq = b & 7, b >> 3
             tile = (xcd * (xq + 1) if xcd < xr else xr * (xq + 1) + (xcd - xr) * xq) + bq
             group, within = divmod(tile, pg)
-            first = group * 8
-            gsz = min(tm_n - first, 8)
+            first = group * grp
+            gsz = min(tm_n - first, grp)
             seen.add((first + within % gsz, within // gsz))
         assert seen == {(i, j) for i in range(tm_n) for j in range(tn_n)}
+
+
+def test_host_kernel_table_matches_generator():
+    """Every kernel name csrc/hip/gemm_asm.hip resolves exists in the code
+    object (a missing one fails the module load, i.e. every asm GEMM)."""
+    import re
+
+    src = open(os.path.join(os.path.dirname(HERE), "csrc", "hip", "gemm_asm.hip")).read()
+    generated = set(re.findall(r"^(toa_gemm_\w+):", TEXT, re.M))
+    wanted = re.findall(r'"(toa_gemm_tn_asm_\w+)"', src)
+    assert wanted and set(wanted) <= generated, set(wanted) - generated
+    n = int(re.search(r"K_N = (\d+)", src).group(1))
+    assert n == len(wanted) == 6 + len(gemm_gen.PLAIN_VARIANTS)
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/clang"), reason="no ROCm LLVM")

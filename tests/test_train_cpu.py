@@ -207,3 +207,33 @@ def test_gemm_prewarm_is_a_noop_off_the_gpu(monkeypatch):
     tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device("cpu"), micro_batch=1, seq_len=16)
     assert tr._gemm_prewarm is None
     assert tr.gemm_mode in ("nosk", "torch", "tuned", "asm")
+
+
+def test_first_step_asm_scope(monkeypatch):
+    """gemm.first_step: on for the hipBLASLt policies when the library has
+    the assembly kernel, nested scopes restore the outer state, off for the
+    other policies; the trainer enters it for step 0 only."""
+    monkeypatch.setattr(gemm._lib, "has", lambda name: True)
+    old = gemm.mode()
+    try:
+        gemm.set_mode("nosk")
+        assert not gemm._asm_first
+        with gemm.first_step(True):
+            assert gemm._asm_first
+            with gemm.first_step(False):
+                assert gemm._asm_first  # an inner "off" keeps the outer scope
+            assert gemm._asm_first
+        assert not gemm._asm_first
+        gemm.set_mode("torch")
+        with gemm.first_step(True):
+            assert not gemm._asm_first
+    finally:
+        gemm.set_mode(old)
+    seen = []
+    tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device("cpu"), micro_batch=1, seq_len=16)
+    monkeypatch.setattr(tr, "_step", lambda batches: seen.append(gemm._asm_first and tr.gemm_mode == "nosk"))
+    monkeypatch.setattr(gemm, "_MODE", "nosk")
+    tr.step([])
+    tr.step_idx = 1
+    tr.step([])
+    assert seen == [True, False]

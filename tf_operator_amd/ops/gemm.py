@@ -180,12 +180,39 @@ def _gemm(ta, tb, m, n, k, a, lda, b, ldb, c, ldc, beta):
               int(c.dtype == torch.float32), _lib.stream(c))
 
 
+_asm_first = False
+
+
+class first_step:
+    """Context of a trainer's FIRST step under the hipBLASLt policies: every
+    forward / data-gradient GEMM the assembly kernel takes runs on it, so the
+    step does not wait for the hipBLASLt plans that :func:`prewarm` is still
+    loading on its helper thread (profiles/r4_fresh: model_init ->
+    first forward issued 0.48-0.63 s without it).  Deterministic: the first
+    step always takes this path, whatever the helper thread's progress, and
+    later steps never do.  The MLP stays unfused (ops.llm.swiglu_mlp keys on
+    the policy)."""
+
+    def __init__(self, on: bool = True):
+        self.on = bool(on) and _MODE in ("nosk", "tuned") and _lib.has("toa_gemm_asm")
+
+    def __enter__(self):
+        global _asm_first
+        self.prev, _asm_first = _asm_first, self.on or _asm_first
+        return self
+
+    def __exit__(self, *exc):
+        global _asm_first
+        _asm_first = self.prev
+        return False
+
+
 def _asm_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
     """Operands the assembly GEMM takes (csrc/hip/gemm_asm.hip checks the
     same and refuses anything else): bf16 GPU rows with unit column stride,
     16-byte aligned rows, M and N multiples of 256 (n_mult), K a multiple of
     64 and >= 128."""
-    if _MODE != "asm" or not _lib.has("toa_gemm_asm"):
+    if not (_MODE == "asm" or _asm_first) or not _lib.has("toa_gemm_asm"):
         return False
     if not (x2.is_cuda and x2.dtype == w.dtype == torch.bfloat16 and x2.dim() == 2 and w.dim() == 2):
         return False

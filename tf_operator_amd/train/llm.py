@@ -137,6 +137,12 @@ class LlamaTrainer:
 
     def step(self, batches):
         """batches: list (len grad_accum) of (tokens, targets)."""
+        from ..ops import gemm as _gemm
+
+        with _gemm.first_step(self.step_idx == 0):
+            return self._step(batches)
+
+    def _step(self, batches):
         if self.fresh_grads and not self.opt.overlap:
             self.flat.mark_fresh()
         elif not self.opt.grads_zeroed:
