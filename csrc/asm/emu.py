@@ -473,9 +473,9 @@ class Emu:
 
     def op_buffer_load_dword(self, w, a, mods):
         """4-B load into a VGPR.  Lanes past num_records read 0, as on the
-        hardware: the kernels use this form only for L2-prefetch loads whose
-        result is discarded (gemm_gen.py l2pf), which run past the tensor on
-        the last tiles.  Every other buffer access past num_records raises."""
+        hardware (kept for prefetch-style loads whose result is discarded;
+        the product kernels do not issue this form).  Every other buffer
+        access past num_records raises."""
         assert "lds" not in mods
         voff = self.vget(w, a[1]).astype(np.uint64)
         kind, lo_, hi_ = self._reg(w, a[2])

@@ -104,8 +104,7 @@ S_SOX = 53          # s53..s59: X DMA row offsets, instructions 1..7
 S_SOW = 60          # s60..s66: W DMA row offsets
 S_E0, S_E1 = 67, 68  # epilogue scratch
 S_Q, S_R = 69, 70   # division results
-SRD_PX, SRD_PW, S_PK = 72, 76, 80   # L2-prefetch resources / k offset (l2pf arms)
-# timing kernel (never with l2pf, whose SGPRs it reuses): s72..s83 six
+# timing kernel: s72..s83 six
 # s_memtime stamps (aligned pairs), s84..s86 accumulated waits (vm, X-free
 # barrier, W-free barrier), s88..s89 the kernel's start stamp
 S_TMT, S_ACC, S_T_START = 72, 84, 88
@@ -119,7 +118,6 @@ V_RXT, V_RWT = 134, 135    # stage toggles (xor masks)
 V_FX0, V_FX1 = 4, 36       # X fragments, sub-steps 0 / 1 (8 x 4 VGPRs each)
 V_FW0, V_FW1 = 68, 100     # W fragments
 V_T = 136                  # 136..139 scratch
-V_PX, V_PW = 250, 251      # L2-prefetch row offsets (l2pf arms; in the epilogue scratch, free in the loop)
 V_E = 140                  # 140..255 epilogue scratch
 
 UNIT_GATE_ROWS = 64        # swiglu_fwd: W rows per wave column per half
@@ -324,20 +322,6 @@ def prologue(a: Asm, epi: str):
         rows_w = 8 * (j % 4) + (UNIT_GATE_ROWS if epi == "swiglu_fwd" else 128) * (j // 4)
         a(f"s_mul_i32 {sr(S_SOX + j - 1)}, {sr(S_LDX)}, {rows_x}")
         a(f"s_mul_i32 {sr(S_SOW + j - 1)}, {sr(S_LDW)}, {rows_w}")
-    if SCHED["l2pf"]:
-        assert epi == "plain"
-        # L2 prefetch rows: 64 w + lane of each operand (one 128-B line each);
-        # resources over exactly the tile's rows x K, k offset of tile 2 + l2pf
-        a(f"v_mul_lo_u32 {vr(V_PX)}, {vr(V_TID)}, {sr(S_LDX)}")
-        a(f"v_mul_lo_u32 {vr(V_PW)}, {vr(V_TID)}, {sr(S_LDW)}")
-        a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_KT)}, 7")                 # K bytes
-        for dst, src, ld in ((SRD_PX, SRD_X, S_LDX), (SRD_PW, SRD_W, S_LDW)):
-            a(f"s_mov_b32 {sr(dst)}, {sr(src)}")
-            a(f"s_mov_b32 {sr(dst + 1)}, {sr(src + 1)}")
-            a(f"s_mul_i32 {sr(dst + 2)}, {sr(ld)}, 255")
-            a(f"s_add_u32 {sr(dst + 2)}, {sr(dst + 2)}, {sr(S_T0)}")
-            a(f"s_mov_b32 {sr(dst + 3)}, 0x20000")
-        a(f"s_mov_b32 {sr(S_PK)}, {128 * (2 + SCHED['l2pf'])}")
     # --- LDS-DMA bases (M0): wave w at line w of the stage's half
     a("s_nop 4")
     a(f"v_readfirstlane_b32 {sr(S_T0)}, {vr(v)}")          # w
@@ -408,7 +392,8 @@ def mfma(i: int, j: int, sub: int) -> str:
 
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
-         "xdma_gap": 3, "merge_bar": False, "l2pf": 0, "timing": False}
+         "xdma_gap": 3, "merge_bar": False, "timing": False,
+         "align": True}
 
 
 def _stamp(k: int) -> str:
@@ -434,16 +419,6 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
         slots[g1 * j].append(frag_read("x", j, 1))
     xb = SCHED["xbar"]
     assert xb > g1 * 7
-    if with_dma and SCHED["l2pf"]:
-        # warm the L2 with the tile `l2pf` beyond the one the DMA fetches
-        # next: one 4-B load per 128-B line (lane = row), result discarded;
-        # issued before this iteration's DMA, so the counted waits below
-        # (vm_after_dma + 2) retire them a whole iteration later
-        # (own resources bounded to the tile's rows x K: past K they read 0
-        # and touch no memory, the running k offset in S_PK)
-        slots[1].append(f"buffer_load_dword {vr(V_E)}, {vr(V_PX)}, {sr(SRD_PX, 4)}, {sr(S_PK)} offen")
-        slots[3].append(f"buffer_load_dword {vr(V_E + 1)}, {vr(V_PW)}, {sr(SRD_PW, 4)}, {sr(S_PK)} offen")
-        slots[5].append(f"s_add_u32 {sr(S_PK)}, {sr(S_PK)}, 128")
     tm = SCHED["timing"]
     if with_dma:
         slots[xb] += ([_stamp(2)] if tm else []) + ["s_waitcnt lgkmcnt(0)", "s_barrier"] + ([_stamp(3)] if tm else [])
@@ -478,8 +453,7 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
         # the next tile (staged one iteration ago) has landed: own DMA by the
         # counted wait, everyone's by the barrier
         ws, rg = SCHED["wait_slot"], SCHED["read_gap"]
-        vm = vm_after_dma + (2 if (with_dma and SCHED["l2pf"]) else 0)
-        slots[ws] += ([_stamp(0)] if tm else []) + [f"s_waitcnt vmcnt({vm})", "s_barrier"] + ([_stamp(1)] if tm else []) + [
+        slots[ws] += ([_stamp(0)] if tm else []) + [f"s_waitcnt vmcnt({vm_after_dma})", "s_barrier"] + ([_stamp(1)] if tm else []) + [
                       f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
                       f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
         for j in range(8):
@@ -507,6 +481,12 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
             if tm and with_dma:
                 for ins in _accum(1, 3, 2) + ([] if SCHED["merge_bar"] else _accum(2, 5, 4)):
                     a(ins)
+        if SCHED["align"]:
+            # every MFMA (8 B) on an 8-byte boundary: a hand-written stream
+            # shifted by 4 mod 8 bytes runs ~13 % slower on gfx950
+            # (MI355X_MICROARCH.md, code-placement sensitivity); the
+            # assembler pads with a 4-byte s_nop 0 only where needed
+            a(".p2alignl 3, 0xbf800000")
         a(mfma(i, j, sub))
         for ins in slots[n]:
             a(ins)
@@ -733,7 +713,6 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     a.raw(f"{name}:")
     prologue(a, epi)
     timing = SCHED["timing"]
-    assert not (timing and SCHED["l2pf"])
     if timing:
         a(f"s_memtime {sr(S_T_START, 2)}")
         for k in range(3):
@@ -768,6 +747,8 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     l_loop, l_tail = a.fresh("loop"), a.fresh("tail")
     a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
     a(f"s_cbranch_scc1 {l_tail}")
+    if SCHED["align"]:
+        a(".p2alignl 6, 0xbf800000")   # loop head on a 64-byte boundary (s_nop padding)
     a.label(l_loop)
     iteration(a, with_dma=True, next_reads=True, vm_after_dma=16, trace_base=tb(100))
     a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_LOOP)}, 1")
@@ -903,7 +884,7 @@ def _descriptor(name: str) -> tuple[str, str]:
     return desc, meta
 
 
-PROBE_SGPRS = 72   # s0..s71: what the plain prologue writes (the l2pf arms' s72.. are not dumped)
+PROBE_SGPRS = 72   # s0..s71: what the plain prologue writes (the timing kernel's s72.. are not dumped)
 PROBE_MAGIC = (0x626F7270, 0x31657461)   # "prob" "ate1" in the fw / fc argument slots
 
 
@@ -963,17 +944,19 @@ PROBE_WORDS = PROBE_VBASE + 8 * 256
 # (scripts/asm_gemm_bench.py --variants): layout / schedule knobs against the
 # product kernel, measured in one process.  Index 0 is the product kernel.
 PLAIN_VARIANTS = (
-    ("v1", {"l2pf": 2}),                    # + L2 prefetch of the tile two beyond the DMA
-    ("v2", {"l2pf": 2, "group": 2}),        # + groups of 2 row tiles
-    ("v3", {"merge_bar": True}),            # two barriers per tile: one frees both halves
+    ("v1", {"align": False}),               # MFMAs wherever the stream puts them (4 mod 8 possible)
+    ("v2", {"merge_bar": True}),            # two barriers per tile: one frees both halves
+    ("v3", {"group": 8}),                   # groups of 8 row tiles
     ("v4", {"wait_slot": 79, "read_gap": 2}),   # next-tile wait 16 MFMAs earlier
-    ("v5", {"group": 8, "wait_slot": 79, "read_gap": 2, "sub1_gap": 2, "xbar": 15, "xdma_gap": 4}),  # round-4 v2
+    ("v5", {"xbar": 31, "xdma_gap": 2}),    # X-free barrier 8 MFMAs later, DMA denser
 )
 # measured (profiles/r4_asm_gemm/ab1, ab2): LDS lines of 1040 B (same speed
 # despite 2-way read conflicts), DMA pieces bunched after each barrier
 # (-2..-4 %) and groups of 16 row tiles (-1..-7 %) rejected; groups of 4, the
 # next-tile wait at MFMA 95 and the X-free barrier 16 MFMAs after the last X
-# read taken into the product kernel (+1..+4 %)
+# read taken into the product kernel (+1..+4 %); an L2 prefetch of the tile two
+# beyond the DMA (one 4-B load per line, its own bounded resources) -16..-24 %
+# (profiles/r4_asm_gemm/ab3): the extra loads share the counted vmcnt waits
 
 
 def _with_knobs(knobs: dict, fn):

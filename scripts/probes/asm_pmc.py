@@ -16,7 +16,8 @@ from tf_operator_amd.ops import _lib, gemm  # noqa: E402
 
 
 def main():
-    T, N, K = 24576, 28672, 4096
+    # ASM_PMC_SHAPE="T,N,K" (default: the gate|up forward)
+    T, N, K = (int(v) for v in os.environ.get("ASM_PMC_SHAPE", "24576,28672,4096").split(","))
     torch.manual_seed(0)
     x = (torch.rand(T, K, device="cuda") - 0.5).to(torch.bfloat16)
     w = (torch.rand(N, K, device="cuda") - 0.5).to(torch.bfloat16)

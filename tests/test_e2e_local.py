@@ -254,6 +254,12 @@ def test_sdk_typed_models_e2e(cluster):
 
 
 def test_metrics_and_events(cluster):
+    # self-contained: under xdist this test may run in a worker whose cluster
+    # has seen no other job
+    c = cluster.client
+    c.create(tfjob("metrics", {"Worker": replica(1, sh("print('ok')"))}))
+    done = c.wait_for_job("metrics", polling_interval=POLL, timeout_seconds=60)
+    assert conditions(done)[-1] == "Succeeded"
     text = cluster.metrics_text()
     assert 'tf_operator_jobs_created_total{job_namespace="default"}' in text
     assert 'tf_operator_jobs_successful_total{job_namespace="default"}' in text

@@ -240,6 +240,20 @@ def _run_job(c, name: str, n: int, command: list[str], timeout: float, env=None,
             "replica_phases_s": rep.get("phases") or {}, "_logs": logs}
 
 
+def _cleanup_after_failure(c, name: str, vram_baseline: int | None):
+    """A failed probe job: delete it and wait until its processes are gone and
+    the node's HBM is scrubbed, so the next job (the benchmark itself) does
+    not start on a node still draining (profiles/r4_fresh2: 5.6 s of
+    dist_init -> model_init behind a failed probe)."""
+    try:
+        c.client.delete(name)
+        c.wait(lambda: not c.pods(labels={"job-name": name}) and not any(
+            k[1].startswith(name + "-") for k in c.kubelet.running), 120, 0.05, f"{name}: cleanup")
+        wait_vram_drained(vram_baseline)
+    except Exception as e:  # noqa: BLE001
+        print(f"[bench] cleanup after {name}: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+
+
 def _summary(samples: list[dict]) -> dict:
     if not samples:
         return {}
@@ -285,6 +299,14 @@ def probe_latency(args, n: int, c=None) -> dict:
     if own:
         c = _cluster(n, args.warm_start == "1")
     samples, cold, err = [], [], None
+    # the node's trainer image is "pulled" (page cache warm, the local
+    # kubelet's pagecache.py) before jobs are timed, as on a real node
+    t_w = time.monotonic()
+    try:
+        c.wait(c.kubelet.node_warm, 180, 0.05, "node page cache warm")
+    except TimeoutError:
+        print("[bench] page-cache warmer still running: probes start anyway", file=sys.stderr, flush=True)
+    warm_s = round(time.monotonic() - t_w, 3)
     settle_s = wait_vram_settled()  # a clean drain baseline
     base = vram_used_bytes()
     start_mode = _start_mode(c)
@@ -296,6 +318,7 @@ def probe_latency(args, n: int, c=None) -> dict:
                 s = _run_job(c, name, n, _payload(args), args.probe_timeout, vram_baseline=base, cold=is_cold)
             except Exception as e:  # keep the throughput run alive; report why latency is missing
                 err = f"{type(e).__name__}: {str(e)[:2000]}"
+                _cleanup_after_failure(c, name, base)
                 break
             s.pop("_logs", None)
             s["replica_start"] = "cold process" if is_cold else start_mode
@@ -310,6 +333,7 @@ def probe_latency(args, n: int, c=None) -> dict:
     out["_cold"] = cold
     out["replica_start"] = start_mode
     out["node_settle_before_probes_s"] = settle_s
+    out["node_warm_wait_s"] = warm_s
     if err:
         out["error"] = err
     return out
@@ -625,6 +649,8 @@ def run_launcher(args) -> int:
     p["replica_start"] = start_mode
     if "node_settle_before_probes_s" in probe:
         p["node_settle_before_probes_s"] = probe["node_settle_before_probes_s"]
+    if "node_warm_wait_s" in probe:
+        p["node_warm_wait_s"] = probe["node_warm_wait_s"]
     _attach_probe(out, p)
     print(json.dumps(out), flush=True)
     return 0

@@ -725,6 +725,12 @@ class LocalKubelet:
         if self.warm_python:
             await self._start_forkserver()  # not awaited ready: cold starts until it is
 
+    def node_warm(self) -> bool:
+        """The page-cache warmer (the node's image pre-pull analogue) has
+        finished, or none runs."""
+        pc = self._pagecache
+        return pc is None or pc.returncode is not None
+
     async def stop(self):
         self._stop.set()
         for key in list(self.running):

@@ -36,6 +36,7 @@ Modes (``TOA_GEMM``):
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import json
 import os
@@ -142,7 +143,19 @@ def prewarm(device=None, background: bool = True):
         return None
     _prewarm_thread = threading.Thread(target=work, name="toa-gemm-prewarm", daemon=True)
     _prewarm_thread.start()
+    # the first step no longer waits for it (first_step), so a one-step job
+    # can reach interpreter exit while it is inside the HIP / hipBLASLt
+    # loaders; a daemon thread killed there takes the process down with a
+    # non-zero exit (profiles/r4_fresh2: a one-step probe job Failed after
+    # "done: 1 steps").  Join it at exit instead.
+    atexit.register(_join_prewarm)
     return _prewarm_thread
+
+
+def _join_prewarm(timeout: float = 120.0):
+    t = _prewarm_thread
+    if t is not None and t.is_alive():
+        t.join(timeout)
 
 
 def prewarm_early():
