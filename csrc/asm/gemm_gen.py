@@ -392,8 +392,8 @@ def mfma(i: int, j: int, sub: int) -> str:
 
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
-         "xdma_gap": 3, "merge_bar": False, "timing": False,
-         "align": True}
+         "xdma_gap": 3, "merge_bar": False, "timing": 0,
+         "align": True, "drain_end": False, "map": ""}
 
 
 def _stamp(k: int) -> str:
@@ -419,7 +419,8 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
         slots[g1 * j].append(frag_read("x", j, 1))
     xb = SCHED["xbar"]
     assert xb > g1 * 7
-    tm = SCHED["timing"]
+    tm = SCHED["timing"] == 1      # waits: vmcnt / X-free / W-free barriers
+    sp = SCHED["timing"] == 2      # spans: X-DMA, W-DMA and bare MFMA stretches
     if with_dma:
         slots[xb] += ([_stamp(2)] if tm else []) + ["s_waitcnt lgkmcnt(0)", "s_barrier"] + ([_stamp(3)] if tm else [])
     for i in range(8):
@@ -464,8 +465,20 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
         slots[126].append("s_waitcnt lgkmcnt(0)")
         if tm:
             slots[126] += _accum(0, 1, 0)
+        if sp and with_dma:
+            slots[126] += _accum(0, 1, 0) + _accum(1, 3, 2) + _accum(2, 5, 4)
         if trace_base:
             slots[ws] += trace_mark(trace_base + 3)
+    if sp and with_dma:
+        # stamps AFTER MFMA n (slot lists run after it): [24, 45] X DMA,
+        # [47 after the W barrier, 76] W DMA, [77, 94] bare MFMAs
+        assert not SCHED["merge_bar"] and xb == 23 and SCHED["xdma_gap"] == 3 and gap == 4 and ws == 95
+        slots[23].append(_stamp(0))
+        slots[45].append(_stamp(1))
+        slots[47].append(_stamp(2))
+        slots[76].append(_stamp(3))
+        slots[77].append(_stamp(4))
+        slots[94].append(_stamp(5))
     if trace_base:
         slots[127] += trace_mark(trace_base + 4)
     if SCHED["prio"]:
@@ -486,6 +499,76 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace
             # shifted by 4 mod 8 bytes runs ~13 % slower on gfx950
             # (MI355X_MICROARCH.md, code-placement sensitivity); the
             # assembler pads with a 4-byte s_nop 0 only where needed
+            a(".p2alignl 3, 0xbf800000")
+        a(mfma(i, j, sub))
+        for ins in slots[n]:
+            a(ins)
+
+
+# Explicit slot maps (SCHED["map"]): every fragment read, barrier, DMA piece
+# and the next-tile wait placed after a given MFMA (0..127).  M0 is set once
+# before the first piece of each half and advanced right AFTER each piece, so
+# the next piece (at least one MFMA later) needs no s_nop.  The next-tile wait
+# counts the pieces issued before it in this iteration; pieces after it (for
+# tile t + 2) land by the NEXT iteration's wait.
+SLOT_MAPS = {
+    # the placement a well-tuned 4-wave, 256 x 256 x 64 library kernel uses
+    # on gfx950 (observed from its instruction stream: pieces spread over the
+    # whole iteration, three of the W pieces after the next-tile wait)
+    "spread": {"x1": [0, 2, 4, 6, 8, 10, 12, 14], "xbar": 20, "w1": [24, 27, 30, 33, 36, 38, 40, 42], "wbar": 50,
+               "xdma": [22, 25, 28, 31, 34, 52, 55, 58], "wdma": [61, 64, 85, 87, 89, 96, 100, 124], "wait": 91,
+               "x0": [93, 94, 95, 97, 98, 102, 103, 104], "w0": [105, 106, 109, 112, 114, 117, 120, 123]},
+    # the product schedule's positions with M0 advanced after each piece
+    "prod": {"x1": list(range(8)), "xbar": 23, "w1": list(range(8, 16)), "wbar": 47,
+             "xdma": [24 + 3 * j for j in range(8)], "wdma": [48 + 4 * j for j in range(8)], "wait": 95,
+             "x0": list(range(96, 104)), "w0": list(range(104, 112))},
+}
+
+
+def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0):
+    m = SLOT_MAPS[SCHED["map"]]
+    slots: dict[int, list[str]] = {n: [] for n in range(128)}
+    for j, n in enumerate(m["x1"]):
+        slots[n].append(frag_read("x", j, 1))
+    for i, n in enumerate(m["w1"]):
+        slots[n].append(frag_read("w", i, 1))
+    assert max(m["x1"]) < m["xbar"] and max(m["w1"]) < m["wbar"] and max(m["x1"] + m["w1"]) < 63
+    if with_dma:
+        slots[m["xbar"]] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+        slots[m["wbar"]] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+        for half, key, bar in (("x", "xdma", m["xbar"]), ("w", "wdma", m["wbar"])):
+            srd_, vo, so, m0 = (SRD_X, V_DX, S_SOX, S_M0X) if half == "x" else (SRD_W, V_DW, S_SOW, S_M0W)
+            pos = m[key]
+            assert sorted(pos) == pos and pos[0] > bar and len(set(pos)) == 8
+            slots[pos[0] - 1].append(f"s_mov_b32 m0, {sr(m0)}")
+            for j, n in enumerate(pos):
+                soff = "0" if j == 0 else sr(so + j - 1)
+                slots[n].append(f"buffer_load_dwordx4 {vr(vo)}, {sr(srd_, 4)}, {soff} offen lds")
+                if j < 7:
+                    slots[n].append(f"s_add_u32 m0, m0, {4 * LINE}")
+            slots[pos[-1]] += advance(half) + [f"s_xor_b32 {sr(m0)}, {sr(m0)}, {sr(m0 + 1)}"]
+        # the two halves' pieces must not interleave (one running M0)
+        assert max(m["xdma"]) < min(m["wdma"]) - 1
+        vm = sum(1 for n in m["xdma"] + m["wdma"] if n < m["wait"])
+    else:
+        vm = 0
+    if next_reads:
+        w = m["wait"]
+        slots[w] += [f"s_waitcnt vmcnt({vm if with_dma else vm_after_dma})", "s_barrier",
+                     f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
+                     f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
+        assert min(m["x0"] + m["w0"]) > w and max(m["x0"] + m["w0"]) < 126
+        for j, n in enumerate(m["x0"]):
+            slots[n].append(frag_read("x", j, 0))
+        for i, n in enumerate(m["w0"]):
+            slots[n].append(frag_read("w", i, 0))
+        slots[126].append("s_waitcnt lgkmcnt(0)")
+    for n in range(128):
+        sub, mm = divmod(n, 64)
+        i, j = divmod(mm, 8)
+        if n == 64:
+            a("s_waitcnt lgkmcnt(0)")
+        if SCHED["align"]:
             a(".p2alignl 3, 0xbf800000")
         a(mfma(i, j, sub))
         for ins in slots[n]:
@@ -704,7 +787,7 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     variant: an A/B arm of the plain kernel (PLAIN_VARIANTS)."""
     name = "toa_gemm_tn_asm_trace" if trace else f"toa_gemm_tn_asm_{epi}" + (f"_{variant}" if variant else "")
     if SCHED["timing"]:
-        name = "toa_gemm_tn_asm_timing"
+        name = "toa_gemm_tn_asm_timing" + ("" if SCHED["timing"] == 1 else str(SCHED["timing"]))
     a = Asm(prefix=("trace_" if trace else epi + "_" + (variant + "_" if variant else "")))
     tb = (lambda base: base) if trace else (lambda base: 0)
     a.raw(f".globl {name}")
@@ -750,13 +833,14 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     if SCHED["align"]:
         a(".p2alignl 6, 0xbf800000")   # loop head on a 64-byte boundary (s_nop padding)
     a.label(l_loop)
-    iteration(a, with_dma=True, next_reads=True, vm_after_dma=16, trace_base=tb(100))
+    it = iteration_map if SCHED["map"] else iteration
+    it(a, with_dma=True, next_reads=True, vm_after_dma=16, trace_base=tb(100))
     a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_LOOP)}, 1")
     a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
     a(f"s_cbranch_scc0 {l_loop}")
     a.label(l_tail)
-    iteration(a, with_dma=False, next_reads=True, vm_after_dma=0, trace_base=tb(200))
-    iteration(a, with_dma=False, next_reads=False, vm_after_dma=0, trace_base=tb(300))
+    it(a, with_dma=False, next_reads=True, vm_after_dma=0, trace_base=tb(200))
+    it(a, with_dma=False, next_reads=False, vm_after_dma=0, trace_base=tb(300))
     if epi == "plain" and not trace and not variant:
         stage_exit(a, 2)
     if timing:
@@ -769,7 +853,11 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
             a(ins)
     epi_offsets(a, epi)
     {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
-    a("s_waitcnt vmcnt(0)")
+    if trace or timing or SCHED["drain_end"]:
+        a("s_waitcnt vmcnt(0)")
+    # else: end with the epilogue's stores still in flight -- the wave's end
+    # does not wait for them, so the next workgroup on this CU starts its
+    # prologue while they drain (the hardware completes them)
     if timing:
         # record per (workgroup, wave): vm wait, X-free barrier, W-free barrier,
         # start -> loop end, epilogue, k-tiles, workgroup id, 0 (cycles)
@@ -944,13 +1032,15 @@ PROBE_WORDS = PROBE_VBASE + 8 * 256
 # (scripts/asm_gemm_bench.py --variants): layout / schedule knobs against the
 # product kernel, measured in one process.  Index 0 is the product kernel.
 PLAIN_VARIANTS = (
-    ("v1", {"align": False}),               # MFMAs wherever the stream puts them (4 mod 8 possible)
-    ("v2", {"merge_bar": True}),            # two barriers per tile: one frees both halves
-    ("v3", {"group": 8}),                   # groups of 8 row tiles
-    ("v4", {"wait_slot": 79, "read_gap": 2}),   # next-tile wait 16 MFMAs earlier
-    ("v5", {"xbar": 31, "xdma_gap": 2}),    # X-free barrier 8 MFMAs later, DMA denser
+    ("v1", {"map": "spread"}),              # DMA pieces spread over the whole iteration
+    ("v2", {"map": "prod"}),                # product positions, M0 advanced after each piece (no s_nop)
+    ("v3", {"map": "spread", "group": 8}),
+    ("v4", {"map": "spread", "align": False}),
+    ("v5", {"drain_end": True}),            # wait for the epilogue's stores before s_endpgm
 )
-# measured (profiles/r4_asm_gemm/ab1, ab2): LDS lines of 1040 B (same speed
+# measured (profiles/r4_asm_gemm/ab1..diag2): MFMAs on 8-byte boundaries, ending
+# with the epilogue's stores in flight, two barriers per tile and the wait 16
+# MFMAs earlier all within noise (+-1.5 %); LDS lines of 1040 B (same speed
 # despite 2-way read conflicts), DMA pieces bunched after each barrier
 # (-2..-4 %) and groups of 16 row tiles (-1..-7 %) rejected; groups of 4, the
 # next-tile wait at MFMA 95 and the X-free barrier 16 MFMAs after the last X
@@ -990,7 +1080,8 @@ def generate() -> str:
         parts.append(body)
         metas.append(meta)
     for body, meta in (probe_kernel(), kernel("plain", trace=True),
-                       _with_knobs({"timing": True}, lambda: kernel("plain", variant="timing"))):
+                       _with_knobs({"timing": 1}, lambda: kernel("plain", variant="timing")),
+                       _with_knobs({"timing": 2}, lambda: kernel("plain", variant="timing2"))):
         parts.append(body)
         metas.append(meta)
     # what hipcc emits after the last kernel: s_nop padding, so the

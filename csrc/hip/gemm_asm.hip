@@ -31,11 +31,12 @@ namespace {
 #include "toa_asm_blob.inc"  // const unsigned char toa_asm_blob[]; size_t toa_asm_blob_len
 
 constexpr int kMaxDev = 64;
-enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_V1 = 6, K_N = 11 };
+enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6, K_V1 = 7,
+       K_N = 12 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
-                           "toa_gemm_tn_asm_plain_v1",
+                           "toa_gemm_tn_asm_timing2",  "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
                            "toa_gemm_tn_asm_plain_v5"};
 
@@ -135,17 +136,20 @@ extern "C" int toa_gemm_asm_variant(int v, const bf16_t* X, int64_t ldx, const b
   return launch(v == 0 ? K_PLAIN : K_V1 + v - 1, a, stream);
 }
 
-// Diagnostic: the product kernel with s_memtime stamps around its waits
-// (csrc/asm/gemm_gen.py SCHED["timing"]); per workgroup and wave, 8 dwords at
-// out + 32 (4 wg + wave): vmcnt wait, X-free barrier, W-free barrier, start ->
-// loop end, epilogue (shader clocks), k-tiles, workgroup id, 0.
-extern "C" int toa_gemm_asm_timing(void* out, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C,
-                                   int64_t ldc, int M, int N, int K, hipStream_t stream) {
-  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C) || !out || !al16(out))
+// Diagnostic: the product kernel with s_memtime stamps (csrc/asm/gemm_gen.py
+// SCHED["timing"]); per workgroup and wave, 8 dwords at out + 32 (4 wg + wave):
+// three accumulated stretches, start -> loop end, epilogue (shader clocks),
+// k-tiles, workgroup id, 0.  which = 1: the stretches are the vmcnt wait, the
+// X-free and the W-free barrier; which = 2: the X-DMA, W-DMA and bare-MFMA
+// stretches of the main loop.
+extern "C" int toa_gemm_asm_timing(int which, void* out, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw,
+                                   bf16_t* C, int64_t ldc, int M, int N, int K, hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C) || !out || !al16(out) ||
+      (which != 1 && which != 2))
     return (int)hipErrorInvalidValue;
   Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
   a.S = (uint64_t)out;
-  return launch(K_TIMING, a, stream);
+  return launch(which == 1 ? K_TIMING : K_TIMING2, a, stream);
 }
 
 // Diagnostic: the plain kernel ending after `stage` (1 = prologue DMA landed,

@@ -198,12 +198,20 @@ def timing(a):
             nwg = (T // 256) * (nn // 256)
             rec = torch.zeros(nwg * 32, device="cuda", dtype=torch.int32)
             for _ in range(3):  # warm (clocks, caches); the last run's records are read
-                _lib.call("toa_gemm_asm_timing", _lib.ptr(rec), _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn,
+                _lib.call("toa_gemm_asm_timing", 2, _lib.ptr(rec), _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn,
+                          T, nn, kk, _lib.stream(x))
+            torch.cuda.synchronize()
+            r2 = rec.cpu().numpy().view(np.uint32).reshape(nwg, 4, 8).astype(np.float64)
+            loops = np.maximum(r2[:, :, 5] - 2, 1)  # main-loop iterations (the two tail tiles carry no DMA)
+            spans = {"xdma_cyc_per_mfma": 22, "wdma_cyc_per_mfma": 29, "bare_cyc_per_mfma": 17}
+            sp = {k: round(float((r2[:, :, i] / loops).mean() / n), 2) for i, (k, n) in enumerate(spans.items())}
+            for _ in range(3):
+                _lib.call("toa_gemm_asm_timing", 1, _lib.ptr(rec), _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn,
                           T, nn, kk, _lib.stream(x))
             torch.cuda.synchronize()
             r = rec.cpu().numpy().view(np.uint32).reshape(nwg, 4, 8).astype(np.float64)
             tot = r[:, :, 3] + r[:, :, 4]
-            res[f"{name}.{kind}"] = {
+            res[f"{name}.{kind}"] = {**sp,
                 "cycles_per_tile": round(float(tot.mean()), 0),
                 "loop_cycles_per_ktile": round(float((r[:, :, 3] / r[:, :, 5]).mean()), 1),
                 "vm_wait_pct": round(float(100 * (r[:, :, 0] / tot).mean()), 2),

@@ -180,7 +180,7 @@ def test_host_kernel_table_matches_generator():
     wanted = re.findall(r'"(toa_gemm_tn_asm_\w+)"', src)
     assert wanted and set(wanted) <= generated, set(wanted) - generated
     n = int(re.search(r"K_N = (\d+)", src).group(1))
-    assert n == len(wanted) == 6 + len(gemm_gen.PLAIN_VARIANTS)
+    assert n == len(wanted) == 7 + len(gemm_gen.PLAIN_VARIANTS)
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/clang"), reason="no ROCm LLVM")
