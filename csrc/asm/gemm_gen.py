@@ -393,7 +393,7 @@ def mfma(i: int, j: int, sub: int) -> str:
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
-         "align": True, "drain_end": False, "map": ""}
+         "align": True, "drain_end": False, "map": "spread"}
 
 
 def _stamp(k: int) -> str:
@@ -518,11 +518,29 @@ SLOT_MAPS = {
     "spread": {"x1": [0, 2, 4, 6, 8, 10, 12, 14], "xbar": 20, "w1": [24, 27, 30, 33, 36, 38, 40, 42], "wbar": 50,
                "xdma": [22, 25, 28, 31, 34, 52, 55, 58], "wdma": [61, 64, 85, 87, 89, 96, 100, 124], "wait": 91,
                "x0": [93, 94, 95, 97, 98, 102, 103, 104], "w0": [105, 106, 109, 112, 114, 117, 120, 123]},
-    # the product schedule's positions with M0 advanced after each piece
-    "prod": {"x1": list(range(8)), "xbar": 23, "w1": list(range(8, 16)), "wbar": 47,
-             "xdma": [24 + 3 * j for j in range(8)], "wdma": [48 + 4 * j for j in range(8)], "wait": 95,
-             "x0": list(range(96, 104)), "w0": list(range(104, 112))},
+    # the same, pieces evenly every 5-6 MFMAs
+    "spread2": {"x1": [0, 2, 4, 6, 8, 10, 12, 14], "xbar": 20, "w1": [24, 27, 30, 33, 36, 38, 40, 42],
+                "wbar": 50, "xdma": [22, 27, 32, 37, 42, 47, 52, 57], "wdma": [62, 68, 74, 80, 86, 98, 110, 122],
+                "wait": 91, "x0": [93, 94, 95, 97, 99, 101, 103, 104], "w0": [105, 106, 109, 112, 114, 117, 120, 123]},
+    # fewer pieces before the wait (10): a longer flight for the rest
+    "spread3": {"x1": [0, 2, 4, 6, 8, 10, 12, 14], "xbar": 20, "w1": [24, 27, 30, 33, 36, 38, 40, 42],
+                "wbar": 50, "xdma": [22, 26, 30, 34, 38, 44, 52, 58], "wdma": [64, 76, 93, 99, 105, 111, 117, 123],
+                "wait": 91, "x0": [94, 95, 96, 97, 98, 100, 101, 102], "w0": [103, 104, 106, 108, 110, 113, 116, 119]},
 }
+
+
+def span_slots(m: dict):
+    """Stamp slots of the timing kernel's three stretches (after MFMA lo ..
+    after MFMA hi): X pieces, W pieces before the next-tile wait, W pieces
+    after it."""
+    pre = [n for n in m["wdma"] if n < m["wait"]]
+    post = [n for n in m["wdma"] if n > m["wait"]]
+    return ((m["xdma"][0] - 1, m["xdma"][-1]), (pre[0] - 1, pre[-1]),
+            ((post[0] - 1, post[-1]) if post else (m["wait"] + 1, m["wait"] + 2)))
+
+
+def span_mfmas(m: dict) -> list[int]:
+    return [hi - lo for lo, hi in span_slots(m)]
 
 
 def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0):
@@ -552,9 +570,21 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
         vm = sum(1 for n in m["xdma"] + m["wdma"] if n < m["wait"])
     else:
         vm = 0
+    tm, sp = SCHED["timing"] == 1, SCHED["timing"] == 2
+    if with_dma and tm:  # waits: X-free and W-free barriers (the vm wait below)
+        for k, bar in ((2, m["xbar"]), (4, m["wbar"])):
+            slots[bar].insert(0, _stamp(k))
+            slots[bar].insert(3, _stamp(k + 1))
+    if with_dma and sp:  # stretches: X pieces, W pieces before the wait, W pieces after it
+        (x0, x1), (w0, w1), (v0, v1) = span_slots(m)
+        for k, (lo, hi) in enumerate(((x0, x1), (w0, w1), (v0, v1))):
+            slots[lo].append(_stamp(2 * k))
+            slots[hi].append(_stamp(2 * k + 1))
     if next_reads:
         w = m["wait"]
-        slots[w] += [f"s_waitcnt vmcnt({vm if with_dma else vm_after_dma})", "s_barrier",
+        slots[w] += ([_stamp(0)] if (tm and with_dma) else []) + [
+                     f"s_waitcnt vmcnt({vm if with_dma else vm_after_dma})", "s_barrier"] + (
+                     [_stamp(1)] if (tm and with_dma) else []) + [
                      f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
                      f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
         assert min(m["x0"] + m["w0"]) > w and max(m["x0"] + m["w0"]) < 126
@@ -563,6 +593,10 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
         for i, n in enumerate(m["w0"]):
             slots[n].append(frag_read("w", i, 0))
         slots[126].append("s_waitcnt lgkmcnt(0)")
+        if with_dma and tm:
+            slots[126] += _accum(0, 1, 0) + _accum(1, 3, 2) + _accum(2, 5, 4)
+        if with_dma and sp:
+            slots[126] += _accum(0, 1, 0) + _accum(1, 3, 2) + _accum(2, 5, 4)
     for n in range(128):
         sub, mm = divmod(n, 64)
         i, j = divmod(mm, 8)
@@ -1032,11 +1066,11 @@ PROBE_WORDS = PROBE_VBASE + 8 * 256
 # (scripts/asm_gemm_bench.py --variants): layout / schedule knobs against the
 # product kernel, measured in one process.  Index 0 is the product kernel.
 PLAIN_VARIANTS = (
-    ("v1", {"map": "spread"}),              # DMA pieces spread over the whole iteration
-    ("v2", {"map": "prod"}),                # product positions, M0 advanced after each piece (no s_nop)
-    ("v3", {"map": "spread", "group": 8}),
-    ("v4", {"map": "spread", "align": False}),
-    ("v5", {"drain_end": True}),            # wait for the epilogue's stores before s_endpgm
+    ("v1", {"map": ""}),                    # round-4 slot schedule (pieces bunched after each barrier)
+    ("v2", {"map": "spread2"}),
+    ("v3", {"map": "spread3"}),
+    ("v4", {"group": 2}),
+    ("v5", {"group": 8}),
 )
 # measured (profiles/r4_asm_gemm/ab1..diag2): MFMAs on 8-byte boundaries, ending
 # with the epilogue's stores in flight, two barriers per tile and the wait 16

@@ -18,6 +18,7 @@ import sys
 import torch
 
 sys.path.insert(0, ".")
+sys.path.insert(0, "csrc/asm")
 from tf_operator_amd.ops import _lib, gemm, llm  # noqa: E402
 
 FORMS = {"qkv": (4096, 6144), "o": (4096, 4096), "gate_up": (4096, 28672), "down": (14336, 4096),
@@ -203,7 +204,9 @@ def timing(a):
             torch.cuda.synchronize()
             r2 = rec.cpu().numpy().view(np.uint32).reshape(nwg, 4, 8).astype(np.float64)
             loops = np.maximum(r2[:, :, 5] - 2, 1)  # main-loop iterations (the two tail tiles carry no DMA)
-            spans = {"xdma_cyc_per_mfma": 22, "wdma_cyc_per_mfma": 29, "bare_cyc_per_mfma": 17}
+            import gemm_gen  # csrc/asm: the product slot map's stretch lengths
+            nm = gemm_gen.span_mfmas(gemm_gen.SLOT_MAPS[gemm_gen.SCHED["map"]])
+            spans = dict(zip(("xdma_cyc_per_mfma", "wdma_pre_wait_cyc_per_mfma", "wdma_post_wait_cyc_per_mfma"), nm))
             sp = {k: round(float((r2[:, :, i] / loops).mean() / n), 2) for i, (k, n) in enumerate(spans.items())}
             for _ in range(3):
                 _lib.call("toa_gemm_asm_timing", 1, _lib.ptr(rec), _lib.ptr(x), kk, _lib.ptr(w), kk, _lib.ptr(y), nn,
