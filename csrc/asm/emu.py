@@ -378,6 +378,10 @@ class Emu:
     def op_v_mul_lo_u32(self, w, a, m):
         self._vbin(w, a, lambda x, y: (x.astype(np.uint64) * y) & M32)
 
+    def op_v_bfe_u32(self, w, a, m):
+        x, off, width = (self.vget(w, t) for t in a[1:4])
+        self.vset(w, a[0], (x >> (off & 31)) & ((1 << (width & 31)) - 1))
+
     def op_v_mul_u32_u24(self, w, a, m):
         self._vbin(w, a, lambda x, y: ((x & 0xFFFFFF).astype(np.uint64) * (y & 0xFFFFFF)) & M32)
 
@@ -517,6 +521,25 @@ class Emu:
         lo, hi = self.vrange(w, a[0])
         data = np.ascontiguousarray(w.v[lo:hi].T).view(np.uint8).reshape(64, 8)
         self._gwrite(addr, data)
+
+    def op_ds_read_b64_tr_b16(self, w, a, mods):
+        """Transposed 64-bit read: lane 16 G + 4 q + p reads four bf16 at its
+        address; lane 16 G + i receives element i & 3 of lane 16 G + 4 q +
+        (i >> 2) for q = 0..3 (its column, four rows)."""
+        addr = self.vget(w, a[1]).astype(np.int64)
+        for md in mods:
+            if md.startswith("offset:"):
+                addr = addr + int(md.split(":")[1])
+        if addr.max() + 8 > self.lds.size:
+            raise IndexError("ds_read past the LDS")
+        src = np.stack([self.lds[x:x + 8] for x in addr]).view(np.uint16).reshape(64, 4)
+        out = np.empty((64, 4), np.uint16)
+        for lane in range(64):
+            g, i = lane >> 4, lane & 15
+            for q in range(4):
+                out[lane, q] = src[16 * g + 4 * q + (i >> 2), i & 3]
+        lo, hi = self.vrange(w, a[0])
+        w.v[lo:hi] = out.view(np.uint32).reshape(64, 2).T
 
     def op_ds_read_b128(self, w, a, mods):
         addr = self.vget(w, a[1]).astype(np.int64)

@@ -956,7 +956,9 @@ def stage_exit(a: Asm, stage: int):
     a(f"s_cbranch_scc1 {a.stage_exit}")
 
 
-def _descriptor(name: str) -> tuple[str, str]:
+def _descriptor(name: str, lds_bytes: int | None = None, n_sgpr: int | None = None) -> tuple[str, str]:
+    LDS_BYTES = globals()["LDS_BYTES"] if lds_bytes is None else lds_bytes  # noqa: N806
+    N_SGPR = globals()["N_SGPR"] if n_sgpr is None else n_sgpr  # noqa: N806
     desc = f"""
 .rodata
 .p2align 6
@@ -1113,7 +1115,9 @@ def generate() -> str:
         body, meta = _with_knobs(knobs, lambda: kernel("plain", variant=vname))
         parts.append(body)
         metas.append(meta)
-    for body, meta in (probe_kernel(), kernel("plain", trace=True),
+    import wgrad_gen  # the weight-gradient kernel shares this code object (lazy: it imports this module)
+
+    for body, meta in (wgrad_gen.kernel(), probe_kernel(), kernel("plain", trace=True),
                        _with_knobs({"timing": 1}, lambda: kernel("plain", variant="timing")),
                        _with_knobs({"timing": 2}, lambda: kernel("plain", variant="timing2"))):
         parts.append(body)

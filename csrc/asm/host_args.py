@@ -21,3 +21,29 @@ def pack(X, W, C, S, ldx_b, ldw_b, ldc_b, lds_b, K, tiles_m, tiles_n, fw_b=0, fc
     struct.pack_into("<IIIIII", buf, KARG["ktiles"], K // 64, tiles_m, tiles_n, xq, xr, pg)
     struct.pack_into("<II", buf, KARG["fw"], fw_b, fc_b)
     return bytes(buf)
+
+
+def wgrad_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(full, split) of csrc/hip/wgrad.hip's wg_plan: whole-K tiles for
+    whole waves of 256 CUs, the tail cut into 2..4 K-pieces that fill it."""
+    tiles = (M // 256) * (N // 256)
+    rem = tiles % 256
+    if rem == 0:
+        return tiles, 1
+    best = 1
+    for s in range(2, 5):
+        if rem * s <= 256 and K % (128 * s) == 0 and K // s >= 512:
+            best = s
+    return (tiles, 1) if best == 1 else (tiles - rem, best)
+
+
+def pack_nt(A, B, C, WS, lda_b, ldb_b, ldc_b, beta, K, tiles_m, tiles_n, full, split) -> bytes:
+    """The weight-gradient kernel's block (csrc/asm/wgrad_gen.py KARG): the
+    same 80 bytes, with beta / full / rem / split in the forward kernels'
+    lds / xq / xr / per_group slots."""
+    rem = tiles_m * tiles_n - full
+    buf = bytearray(KARG_BYTES)
+    struct.pack_into("<QQQQ", buf, 0, A, B, C, WS)
+    struct.pack_into("<IIII", buf, 32, lda_b, ldb_b, ldc_b, beta)
+    struct.pack_into("<IIIIII", buf, 48, K // 64, tiles_m, tiles_n, full, rem, split)
+    return bytes(buf)

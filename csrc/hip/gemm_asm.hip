@@ -31,12 +31,12 @@ namespace {
 #include "toa_asm_blob.inc"  // const unsigned char toa_asm_blob[]; size_t toa_asm_blob_len
 
 constexpr int kMaxDev = 64;
-enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6, K_V1 = 7,
-       K_N = 12 };
+enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
+       K_WGRAD = 7, K_V1 = 8, K_N = 13 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
-                           "toa_gemm_tn_asm_timing2",  "toa_gemm_tn_asm_plain_v1",
+                           "toa_gemm_tn_asm_timing2",  "toa_wgrad_nt_asm",           "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
                            "toa_gemm_tn_asm_plain_v5"};
 
@@ -206,6 +206,62 @@ extern "C" int toa_gemm_asm_probe(void* out, const bf16_t* X, int64_t ldx, const
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   return (int)hipModuleLaunchKernel(fn, a.tiles_m * a.tiles_n, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
+}
+
+// Weight gradient on the assembly NT kernel (csrc/asm/wgrad_gen.py), the
+// contract of toa_wgrad (csrc/hip/wgrad.hip): C[M][N] (+)= A[K][M]^T B[K][N],
+// split == 0 the auto plan (whole-K tiles for whole waves of 256 CUs, the tail
+// cut into k-pieces), split >= 1 every tile cut into `split` pieces; the
+// pieces' fp32 partials (workspace W, toa_wgrad_workspace bytes) are summed in
+// a fixed order by wgrad.hip's reduce kernel.
+extern "C" int toa_wgrad_split(int M, int N, int K);
+extern "C" int toa_wgrad_reduce(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem, int split,
+                                int beta, hipStream_t stream);
+
+extern "C" int toa_wgrad_asm(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc,
+                             float* W, int M, int N, int K, int split, int beta, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || split < 0 || split > 4 || !ld_ok(lda, M) ||
+      !ld_ok(ldb, N) || !ld_ok(ldc, N) || !al16(A) || !al16(B) || !al16(C) || (lda * 2) * 64 >= (1ll << 31) ||
+      (ldb * 2) * 64 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  const int tiles = (M / 256) * (N / 256);
+  int full;
+  if (split == 0) {
+    split = toa_wgrad_split(M, N, K);
+    full = split > 1 ? tiles - tiles % 256 : tiles;
+  } else {
+    full = split == 1 ? tiles : 0;
+  }
+  const int rem = tiles - full;
+  if (K % (64 * split) || K / split < 128 || (split > 1 && (W == nullptr || !al16(W))) ||
+      (int64_t)split * rem >= (1 << 14))
+    return (int)hipErrorInvalidValue;
+  Args a;
+  memset(&a, 0, sizeof(a));
+  a.X = (uint64_t)A;
+  a.W = (uint64_t)B;
+  a.C = (uint64_t)C;
+  a.S = (uint64_t)W;
+  a.ldx = (uint32_t)(lda * 2);
+  a.ldw = (uint32_t)(ldb * 2);
+  a.ldc = (uint32_t)(ldc * 2);
+  a.lds = (uint32_t)(beta ? 1 : 0);
+  a.ktiles = (uint32_t)(K / 64);
+  a.tiles_m = (uint32_t)(M / 256);
+  a.tiles_n = (uint32_t)(N / 256);
+  a.xq = (uint32_t)full;
+  a.xr = (uint32_t)rem;
+  a.per_group = (uint32_t)split;
+  hipError_t err;
+  hipFunction_t fn = get_fn(K_WGRAD, &err);
+  if (!fn) return (int)err;
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  const unsigned nwg = (unsigned)(full + (split > 1 ? rem * split : 0));
+  err = hipModuleLaunchKernel(fn, nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
+  if (err != hipSuccess) return (int)err;
+  if (split > 1 && rem > 0) return toa_wgrad_reduce(W, C, ldc, M, N, full, rem, split, beta, stream);
+  return 0;
 }
 
 extern "C" int toa_gemm_asm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* Wgu, int64_t ldw, bf16_t* GU,

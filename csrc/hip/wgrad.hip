@@ -292,6 +292,16 @@ static void wg_plan(int M, int N, int K, int* full, int* split) {
   *split = best;
 }
 
+// The reduce kernel of a split plan, for the assembly NT kernel
+// (csrc/hip/gemm_asm.hip toa_wgrad_asm), which writes the same tile-major
+// fp32 partials.
+extern "C" int toa_wgrad_reduce(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem, int split,
+                                int beta, hipStream_t stream) {
+  if (rem <= 0 || split < 2 || W == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split, beta);
+  return (int)hipGetLastError();
+}
+
 // Auto plan's split factor (1 = no split-K at all).
 extern "C" int toa_wgrad_split(int M, int N, int K) {
   int full, split;

@@ -228,6 +228,54 @@ def timing(a):
     print(json.dumps({"timing": res}))
 
 
+WGRAD_FORMS = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+               "lm_head": (128256, 4096)}
+
+
+def wgrad(a):
+    """Weight gradient g[N][K] = dy^T x at T tokens: the assembly NT kernel
+    (toa_wgrad_asm), the HIP kernel (toa_wgrad), hipBLASLt (torch.mm);
+    auto plans, interleaved rounds; asm checked against the HIP kernel."""
+    T = a.tokens
+    torch.manual_seed(0)
+    res = {}
+    for name, (N, K) in WGRAD_FORMS.items():
+        if a.forms and f"{name}.wgrad" not in a.forms.split(","):
+            continue
+        dy = torch.randn(T, N, device="cuda").to(torch.bfloat16)
+        x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
+        g = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+        g2 = torch.empty_like(g)
+        nbytes = int(_lib.call_ret("toa_wgrad_workspace", N, K, T, 0))
+        ws = torch.empty(max(nbytes, 16) // 4, device="cuda", dtype=torch.float32)
+
+        def hip():
+            _lib.call("toa_wgrad", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g2), K, _lib.ptr(ws), N, K, T, 0, 0,
+                      _lib.stream(dy))
+
+        def asm_():
+            _lib.call("toa_wgrad_asm", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g), K, _lib.ptr(ws), N, K, T, 0, 0,
+                      _lib.stream(dy))
+
+        arms = [("asm", asm_), ("hip", hip), ("blt", lambda: torch.mm(dy.t(), x))]
+        ts = {k: [] for k, _ in arms}
+        for _ in range(a.rounds):
+            for k, f in arms:
+                ts[k].append(timer(f, a.reps))
+        asm_()
+        hip()
+        torch.cuda.synchronize()
+        fl = 2.0 * T * N * K
+        rec = {k: {"ms": round(statistics.median(v), 4), "TFps": round(fl / statistics.median(v) / 1e9, 1)}
+               for k, v in ts.items()}
+        rec["asm_vs_hip_rel"] = round(rel(g, g2), 6)
+        res[f"{name}.wgrad"] = rec
+        print(json.dumps({f"{name}.wgrad": rec}), flush=True)
+        del dy, x, g, g2, ws
+        torch.cuda.empty_cache()
+    print(json.dumps({"wgrad": res}))
+
+
 def timer(fn, reps):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     fn()
@@ -310,6 +358,7 @@ def main():
     ap.add_argument("--mlp", type=int, default=1)
     ap.add_argument("--variants", default="", help="plain-kernel A/B arms to add, e.g. 1,2,3")
     ap.add_argument("--timing", action="store_true", help="wait-cycle breakdown of the product kernel (--forms)")
+    ap.add_argument("--wgrad", action="store_true", help="weight-gradient forms: asm NT vs HIP vs hipBLASLt")
     a = ap.parse_args()
     if a.probe:
         probe()
@@ -319,6 +368,9 @@ def main():
         return
     if a.timing:
         timing(a)
+        return
+    if a.wgrad:
+        wgrad(a)
         return
     if a.stage >= 0:
         M, N, K = 256, 256, 128

@@ -176,11 +176,11 @@ def test_host_kernel_table_matches_generator():
     import re
 
     src = open(os.path.join(os.path.dirname(HERE), "csrc", "hip", "gemm_asm.hip")).read()
-    generated = set(re.findall(r"^(toa_gemm_\w+):", TEXT, re.M))
-    wanted = re.findall(r'"(toa_gemm_tn_asm_\w+)"', src)
+    generated = set(re.findall(r"^(toa_\w+):", TEXT, re.M))
+    wanted = re.findall(r'"(toa_(?:gemm_tn|wgrad_nt)_asm\w*)"', src)
     assert wanted and set(wanted) <= generated, set(wanted) - generated
     n = int(re.search(r"K_N = (\d+)", src).group(1))
-    assert n == len(wanted) == 7 + len(gemm_gen.PLAIN_VARIANTS)
+    assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS)
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/clang"), reason="no ROCm LLVM")
