@@ -1,0 +1,72 @@
+"""In-model A/B of a kernel choice on the Llama-3-8B bench step, in ONE
+process (one model, one set of buffers): alternating timed windows of
+`--steps` steps under each arm after a shared warm-up, median ms/step per arm.
+
+    python scripts/wgrad_inmodel_ab.py [--rounds 3] [--steps 4] [--arms wgrad=asm+gemm=nosk,wgrad=hip+gemm=nosk]
+
+An arm is settings joined by '+': wgrad=asm|hip (ops.gemm.set_wgrad_kernel),
+gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy).  Same-process windows
+remove the box-to-box spread (about +-2.5 %) from the comparison.
+"""
+import argparse
+import json
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from tf_operator_amd.ops import gemm  # noqa: E402
+from tf_operator_amd.train.llm import LlamaTrainer  # noqa: E402
+
+
+def apply(arm: str):
+    """arm: settings joined by '+', e.g. wgrad=hip+gemm=nosk."""
+    for part in arm.split("+"):
+        key, val = part.split("=")
+        if key == "wgrad":
+            gemm.set_wgrad_kernel(val)
+        elif key == "gemm":
+            gemm.set_mode(val)
+        else:
+            raise SystemExit(f"unknown arm {arm}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--arms", default="wgrad=asm+gemm=nosk,wgrad=hip+gemm=nosk,wgrad=asm+gemm=asm")
+    ap.add_argument("--micro-batch", type=int, default=6)
+    a = ap.parse_args()
+    arms = a.arms.split(",")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    tr = LlamaTrainer("llama3-8b", dev, micro_batch=a.micro_batch, seq_len=4096)
+    batch = [tr.synthetic_batch()]
+    for arm in arms:  # every arm warm (code objects, plans)
+        apply(arm)
+        for _ in range(a.warmup):
+            tr.step(batch)
+    torch.cuda.synchronize()
+    times = {arm: [] for arm in arms}
+    for r in range(a.rounds):
+        for arm in arms:
+            apply(arm)
+            tr.step(batch)  # one untimed step after the switch
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                loss = tr.step(batch)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / a.steps
+            times[arm].append(ms)
+            print(json.dumps({"round": r, "arm": arm, "ms_per_step": round(ms, 2), "loss": float(loss)}), flush=True)
+    print(json.dumps({"median_ms_per_step": {k: round(statistics.median(v), 2) for k, v in times.items()},
+                      "all": times}))
+
+
+if __name__ == "__main__":
+    main()

@@ -793,33 +793,35 @@ def test_gemm_prewarm_resolves_table():
         gemm.set_mode("auto")
 
 
-def test_gemm_runs_on_tn_kernel_while_prewarm_pending(monkeypatch):
-    """While the hipBLASLt table is still being resolved (a live prewarm
-    thread), forward GEMMs of TN-compatible shapes run on the hand-written
-    kernel instead of blocking on the library; results match fp32."""
-    _lib()
-    import threading
-
+def test_first_step_gemms_run_on_the_assembly_kernel():
+    """gemm.first_step (a trainer's step 0 under the hipBLASLt policies):
+    forward GEMMs the assembly kernel takes run on it -- bit-identical to a
+    direct toa_gemm_asm launch -- so the step never waits for the hipBLASLt
+    plans still loading; other shapes take the library path."""
+    L = _lib()
     from tf_operator_amd.ops import gemm
 
-    release = threading.Event()
-    th = threading.Thread(target=release.wait, daemon=True)
-    th.start()
-    monkeypatch.setattr(gemm, "_prewarm_thread", th)
+    old = gemm.mode()
+    gemm.set_mode("nosk")
     try:
-        assert gemm._prewarm_pending()
         torch.manual_seed(1)
         x = torch.randn(512, 384, device=DEV, dtype=torch.bfloat16)
         w = torch.randn(768, 384, device=DEV, dtype=torch.bfloat16) / 384 ** 0.5
-        assert gemm._tn_shape_ok(x, w)
-        y = gemm.linear_fwd(x, w)
+        direct = torch.empty(512, 768, device=DEV, dtype=torch.bfloat16)
+        L.call("toa_gemm_asm", L.ptr(x), 384, L.ptr(w), 384, L.ptr(direct), 768, 512, 768, 384, L.stream(x))
+        with gemm.first_step(True):
+            assert gemm._asm_shape_ok(x, w)
+            y = gemm.linear_fwd(x, w)
+            xo = torch.randn(100, 384, device=DEV, dtype=torch.bfloat16)  # not a 256-row multiple: the library
+            assert not gemm._asm_shape_ok(xo, w)
+            yo = gemm.linear_fwd(xo, w)
+        assert not gemm._asm_shape_ok(x, w)  # outside the scope: the policy's library path
+        torch.cuda.synchronize()
+        assert torch.equal(y, direct)
         assert rel(y, x.float() @ w.float().t()) < 1e-2
-        xo = torch.randn(100, 384, device=DEV, dtype=torch.bfloat16)  # not TN-compatible: the library path
-        assert not gemm._tn_shape_ok(xo, w)
-        assert rel(gemm.linear_fwd(xo, w), xo.float() @ w.float().t()) < 1e-2
+        assert rel(yo, xo.float() @ w.float().t()) < 1e-2
     finally:
-        release.set()
-        th.join()
+        gemm.set_mode(old)
 
 
 @pytest.mark.parametrize("B,H,Hk,S", [(2, 4, 2, 384), (1, 8, 2, 1024)])

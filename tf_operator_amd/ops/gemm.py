@@ -295,6 +295,26 @@ def swiglu_down_dgrad(d2: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor):
 
 
 _ws = {}
+# weight-gradient kernel: the assembly NT kernel (csrc/asm/wgrad_gen.py;
+# 1.30-1.50 PF/s at the Llama forms, 1-12 % faster than the HIP kernel and
+# bit-identical to it, profiles/r4_wgrad/) where the library carries it, else
+# the HIP kernel (csrc/hip/wgrad.hip).  set_wgrad_kernel switches it for
+# in-process A/B runs (scripts/wgrad_inmodel_ab.py).
+_WGRAD_KERNEL = None
+
+
+def wgrad_kernel() -> str:
+    global _WGRAD_KERNEL
+    if _WGRAD_KERNEL is None:
+        _WGRAD_KERNEL = "asm" if _lib.has("toa_wgrad_asm") else "hip"
+    return _WGRAD_KERNEL
+
+
+def set_wgrad_kernel(name: str):
+    global _WGRAD_KERNEL
+    if name not in ("asm", "hip"):
+        raise ValueError(f"unknown weight-gradient kernel {name!r}")
+    _WGRAD_KERNEL = name
 
 
 def _workspace(dev, nbytes):
@@ -331,7 +351,8 @@ def wgrad_hip_(g, dy2, x2, beta=1.0, split=None):
     split = 0 if split is None else int(split)
     nbytes = int(_lib.call_ret("toa_wgrad_workspace", N, K, T, split))
     ws = _workspace(dy2.device, nbytes) if nbytes > 0 else None
-    _lib.call("toa_wgrad", _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(g), K, _lib.ptr(ws),
+    fn = "toa_wgrad_asm" if wgrad_kernel() == "asm" else "toa_wgrad"
+    _lib.call(fn, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(g), K, _lib.ptr(ws),
               N, K, T, int(split), int(beta != 0.0), _lib.stream(dy2))
     return g
 
