@@ -265,6 +265,9 @@ class Emu:
         w.scc = int(r != 0)
         self.sset(w, a[0], r)
 
+    def op_s_bitcmp1_b32(self, w, a, m):
+        w.scc = int((self.sget(w, a[0]) >> (self.sget(w, a[1]) & 31)) & 1)
+
     def op_s_min_u32(self, w, a, m):
         x, y = self.sget(w, a[1]), self.sget(w, a[2])
         w.scc = int(x < y)

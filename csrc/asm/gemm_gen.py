@@ -108,7 +108,8 @@ S_Q, S_R = 69, 70   # division results
 # s_memtime stamps (aligned pairs), s84..s86 accumulated waits (vm, X-free
 # barrier, W-free barrier), s88..s89 the kernel's start stamp
 S_TMT, S_ACC, S_T_START = 72, 84, 88
-N_SGPR = 90
+S_ITER, S_GRID = 90, 91   # persistent arms: this workgroup's tile-order index, the grid size
+N_SGPR = 92
 
 # VGPRs
 V_TID = 132
@@ -209,7 +210,7 @@ def mul64(a: Asm, lo: int, hi: int, x: int, y: int):
 
 
 # ---------------------------------------------------------------- prologue
-def prologue(a: Asm, epi: str):
+def prologue_args(a: Asm):
     a(f"s_load_dwordx16 {sr(S_ARGS, 16)}, s[0:1], 0x0")
     a(f"s_load_dwordx4 {sr(S_ARGS + 16, 4)}, s[0:1], 0x40")
     a("s_mov_b32 m0, 0")
@@ -228,10 +229,17 @@ def prologue(a: Asm, epi: str):
     a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_XR)}")
     a(f"s_cmp_lg_u32 {sr(S_T1)}, {sr(S_T0)}")
     a(f"s_cbranch_scc1 {a.abort}")
+    if SCHED["persist"]:
+        a(f"s_mov_b32 {sr(S_GRID)}, {sr(S_PG)}")        # persistent: the grid size (per_group slot)
+        a(f"s_mov_b32 {sr(S_ITER)}, s2")
+
+
+def tile_setup(a: Asm, epi: str, bid: str = "s2"):
+    """Tile of block `bid` -> S_TILE, (S_TM, S_TN), SRD_X / SRD_W."""
     # --- XCD remap: blocks b, b+8, ... share an XCD; give each XCD a
     # contiguous range of the tile order (bijective for any nwg)
-    a(f"s_and_b32 {sr(S_T0)}, s2, 7")                 # xcd
-    a(f"s_lshr_b32 {sr(S_T1)}, s2, 3")                # b / 8
+    a(f"s_and_b32 {sr(S_T0)}, {bid}, 7")              # xcd
+    a(f"s_lshr_b32 {sr(S_T1)}, {bid}, 3")             # b / 8
     a(f"s_add_u32 {sr(S_T2)}, {sr(S_XQ)}, 1")         # q + 1
     a(f"s_mul_i32 {sr(S_T3)}, {sr(S_T0)}, {sr(S_T2)}")  # xcd * (q+1)
     a(f"s_mul_i32 {sr(S_TILE)}, {sr(S_XR)}, {sr(S_T2)}")  # r * (q+1)
@@ -269,6 +277,10 @@ def prologue(a: Asm, epi: str):
         a(f"s_lshr_b32 {sr(S_T1)}, {sr(S_T1)}, 1")    # 128 rows of each half
         a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_FW)}")  # + the up half's offset
     srd(a, SRD_W, S_W, S_T2, S_T3, S_T1)
+
+
+def tile_c(a: Asm, epi: str):
+    """SRD_C (and SRD_S) of the tile at (S_TM, S_TN)."""
     # C (and S): rows tm*256, columns tn*256 (tn*128 for the gate|up epilogue)
     a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
     mul64(a, S_T2, S_T3, S_T0, S_LDC)
@@ -286,6 +298,16 @@ def prologue(a: Asm, epi: str):
         a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 8")
         srd(a, SRD_S, S_S, S_T2, S_T3, S_T1)
 
+
+
+def prologue(a: Asm, epi: str):
+    prologue_args(a)
+    tile_setup(a, epi, sr(S_ITER) if SCHED["persist"] else "s2")
+    tile_c(a, epi)
+    prologue_lanes(a, epi)
+
+
+def prologue_lanes(a: Asm, epi: str):
     # --- DMA lane offsets.  Wave w's instruction j fills LDS line w + 4j of
     # the half: rows (w + 4(j%4)) + 16*(lane>>3) [+ 128 for j >= 4], k chunk
     # lane & 7.  Per-lane part -> V_DX / V_DW, per-instruction part -> s[SO*].
@@ -348,7 +370,10 @@ def prologue(a: Asm, epi: str):
     a(f"v_xor_b32 {vr(V_RXT)}, {vr(V_RXT)}, {vr(V_RX)}")
     a(f"v_add_u32 {vr(V_RWT)}, {STAGE}, {vr(V_RW)}")
     a(f"v_xor_b32 {vr(V_RWT)}, {vr(V_RWT)}, {vr(V_RW)}")
-    # --- zero the accumulators
+    zero_acc(a)
+
+
+def zero_acc(a: Asm):
     for i in range(256):
         a(f"v_accvgpr_write_b32 {ar(i)}, 0")
 
@@ -393,7 +418,7 @@ def mfma(i: int, j: int, sub: int) -> str:
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
-         "align": True, "drain_end": False, "map": "spread"}
+         "align": True, "drain_end": False, "map": "spread", "persist": False}
 
 
 def _stamp(k: int) -> str:
@@ -838,15 +863,7 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
         for ins in trace_setup(a) + trace_mark(1):
             a(ins)
     # --- prologue DMA: tile 0 -> stage 0, tile 1 -> stage 1
-    for tile in range(2):
-        for half in ("x", "w"):
-            for j in range(8):
-                for ins in dma(a, half, j):
-                    a(ins)
-            for ins in advance(half):
-                a(ins)
-        a(f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}")
-        a(f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}")
+    prologue_dma(a)
     # both stages toggled twice: M0 bases are back at stage 0 for tile 2
     a("s_waitcnt vmcnt(16)")                       # own tile-0 pieces
     a("s_barrier")                                 # everyone's
@@ -855,6 +872,11 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
             a(ins)
     if epi == "plain" and not trace and not variant:
         stage_exit(a, 1)
+    persist = SCHED["persist"]
+    assert not persist or (epi == "plain" and not trace and not SCHED["timing"])
+    l_tile = a.fresh("tile")
+    if persist:
+        a.label(l_tile)
     for j in range(8):
         a(frag_read("x", j, 0))
     for i in range(8):
@@ -885,6 +907,8 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     if trace:
         for ins in trace_mark(9000):
             a(ins)
+    if persist:
+        persistent_next(a, epi, l_tile)
     epi_offsets(a, epi)
     {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
     if trace or timing or SCHED["drain_end"]:
@@ -919,6 +943,55 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     body = "\n".join(a.out)
     desc, meta = _descriptor(name)
     return body + "\n" + desc, meta
+
+
+def prologue_dma(a: Asm):
+    """k-tiles 0 and 1 of the tile -> stages 0 and 1 (M0 bases end at stage 0)."""
+    for _ in range(2):
+        for half in ("x", "w"):
+            for j in range(8):
+                for ins in dma(a, half, j):
+                    a(ins)
+            for ins in advance(half):
+                a(ins)
+        a(f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}")
+        a(f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}")
+
+
+def persistent_next(a: Asm, epi: str, l_tile: str):
+    """Persistent arms: this workgroup's next tile is S_ITER + grid.  If there
+    is one, its first two k-tiles are staged (every wave's reads of the
+    current tile are done: barrier) BEFORE the current tile's epilogue, so
+    their flight hides under the epilogue; then the epilogue, the next tile's
+    C resource, zeroed accumulators, and back to the tile loop."""
+    l_last, l_even, l_par = a.fresh("last"), a.fresh("even"), a.fresh("par")
+    # stage parity back to 0: the M0 bases toggled KT times this tile, the read bases KT - 1
+    a(f"s_bitcmp1_b32 {sr(S_KT)}, 0")
+    a(f"s_cbranch_scc0 {l_even}")
+    a(f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}")
+    a(f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}")
+    a(f"s_branch {l_par}")
+    a.label(l_even)
+    a(f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}")
+    a(f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}")
+    a.label(l_par)
+    a(f"s_add_u32 {sr(S_ITER)}, {sr(S_ITER)}, {sr(S_GRID)}")
+    a(f"s_mul_i32 {sr(S_T0)}, {sr(S_TM_N)}, {sr(S_TN_N)}")
+    a(f"s_cmp_ge_u32 {sr(S_ITER)}, {sr(S_T0)}")
+    a(f"s_cbranch_scc1 {l_last}")
+    a("s_barrier")                                 # every wave done reading this tile's LDS
+    tile_setup(a, epi, sr(S_ITER))                 # SRD_X / SRD_W / (S_TM, S_TN) of the next tile
+    prologue_dma(a)
+    epi_offsets(a, epi)
+    epilogue_plain(a)
+    tile_c(a, epi)
+    zero_acc(a)
+    # the next tile's k-tile 0 landed: the epilogue's 32 stores and k-tile 1's
+    # 16 pieces are younger
+    a("s_waitcnt vmcnt(48)")
+    a("s_barrier")
+    a(f"s_branch {l_tile}")
+    a.label(l_last)
 
 
 TRACE_REC = 32   # bytes per (workgroup, wave) trace record
@@ -1072,7 +1145,7 @@ PLAIN_VARIANTS = (
     ("v2", {"map": "spread2"}),
     ("v3", {"map": "spread3"}),
     ("v4", {"group": 2}),
-    ("v5", {"group": 8}),
+    ("v5", {"persist": True}),              # persistent: a workgroup per CU walks its tiles, next tile staged under the epilogue
 )
 # measured (profiles/r4_asm_gemm/ab1..diag2): MFMAs on 8-byte boundaries, ending
 # with the epilogue's stores in flight, two barriers per tile and the wait 16

@@ -13,8 +13,12 @@ def grid_params(tiles_m: int, tiles_n: int):
     return nwg, nwg >> 3, nwg & 7, 8 * tiles_n
 
 
-def pack(X, W, C, S, ldx_b, ldw_b, ldc_b, lds_b, K, tiles_m, tiles_n, fw_b=0, fc_b=0) -> bytes:
+def pack(X, W, C, S, ldx_b, ldw_b, ldc_b, lds_b, K, tiles_m, tiles_n, fw_b=0, fc_b=0, grid=None) -> bytes:
+    """grid: a persistent kernel's workgroup count (in the per_group slot,
+    which the non-persistent kernels do not read)."""
     nwg, xq, xr, pg = grid_params(tiles_m, tiles_n)
+    if grid is not None:
+        pg = grid
     buf = bytearray(KARG_BYTES)
     struct.pack_into("<QQQQ", buf, KARG["X"], X, W, C, S)
     struct.pack_into("<IIII", buf, KARG["ldx"], ldx_b, ldw_b, ldc_b, lds_b)

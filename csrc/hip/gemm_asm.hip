@@ -75,14 +75,20 @@ static_assert(sizeof(Args) == 80, "kernarg block must match csrc/asm/gemm_gen.py
 bool ld_ok(int64_t ld, int64_t min_cols) { return ld >= min_cols && ld % 8 == 0 && ld * 2 * 256 < (1ll << 32); }
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-int launch(int which, const Args& a, hipStream_t stream) {
+// A/B arms that walk several tiles per workgroup (gemm_gen.py SCHED
+// "persist"), by variant number 1..: their grid is one workgroup per CU.
+constexpr bool kVariantPersist[K_N - K_V1] = {false, false, false, false, true};
+constexpr unsigned kPersistGrid = 256;
+
+int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
   hipError_t err;
   hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
   Args k = a;
   size_t sz = sizeof(k);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  const unsigned nwg = a.tiles_m * a.tiles_n;
+  const unsigned nwg = grid ? grid : a.tiles_m * a.tiles_n;
+  if (grid) k.per_group = grid;  // the persistent kernels read their grid size here
   return (int)hipModuleLaunchKernel(fn, nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
 }
 
@@ -133,6 +139,10 @@ extern "C" int toa_gemm_asm_variant(int v, const bf16_t* X, int64_t ldx, const b
   if (v < 0 || v > K_N - K_V1 || !common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C))
     return (int)hipErrorInvalidValue;
   Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  if (v > 0 && kVariantPersist[v - 1]) {
+    const unsigned tiles = a.tiles_m * a.tiles_n;
+    return launch(K_V1 + v - 1, a, stream, tiles < kPersistGrid ? tiles : kPersistGrid);
+  }
   return launch(v == 0 ? K_PLAIN : K_V1 + v - 1, a, stream);
 }
 

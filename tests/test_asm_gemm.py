@@ -79,6 +79,26 @@ def test_asm_gemm_variants_match_product_kernel(variant):
     close(tof(out[0]), tof(X) @ tof(W).T)
 
 
+@pytest.mark.parametrize("grid", [1, 3, 10])
+def test_asm_gemm_persistent_arm_emulated(grid):
+    """The persistent arm: `grid` workgroups walk the 10 tiles of a 5 x 2
+    grid (S_ITER += grid), staging the next tile under the epilogue; C equals
+    the product kernel's bit for bit."""
+    name = next(f"toa_gemm_tn_asm_plain_{v}" for v, k in gemm_gen.PLAIN_VARIANTS if k.get("persist"))
+    rng = np.random.default_rng(13)
+    M, N, K = 1280, 512, 320   # odd k-tile count: the stage parity fix-up runs
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)))
+    outs = []
+    for kname, g in (("toa_gemm_tn_asm_plain", None), (name, grid)):
+        mem = emu.Memory()
+        ax, aw, ac = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16))
+        karg = host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256, grid=g)
+        run_all(kname, karg, (M // 256) * (N // 256) if g is None else g, mem)
+        outs.append(mem.bufs[2][1].view(np.uint16).reshape(M, N).copy())
+    assert np.array_equal(outs[0], outs[1])
+
+
 def test_asm_gemm_timing_kernel_emulated():
     """The timing diagnostic computes the product kernel's C and writes one
     8-dword record per (workgroup, wave) with ordered stamps."""
@@ -181,6 +201,8 @@ def test_host_kernel_table_matches_generator():
     assert wanted and set(wanted) <= generated, set(wanted) - generated
     n = int(re.search(r"K_N = (\d+)", src).group(1))
     assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS)
+    flags = re.search(r"kVariantPersist\[K_N - K_V1\] = \{([^}]*)\}", src).group(1)
+    assert [f.strip() == "true" for f in flags.split(",")] == [bool(k.get("persist")) for _, k in gemm_gen.PLAIN_VARIANTS]
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/llvm/bin/clang"), reason="no ROCm LLVM")
