@@ -1,0 +1,14 @@
+#!/bin/bash
+# Attention-backward A/B at the bench shape: forms ds / ds2 (store-aware
+# step-end wait) / ds3 (static priority, younger half) / ds4 (both), with the
+# dK/dV kernel's issue-vs-wait timing, then a kernel trace of the same run.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/${1:-r4_attn}; mkdir -p "$O"
+export TMPDIR=/tmp
+V=${VARIANTS:-ds,ds2,ds3,ds4}
+timeout -k 10 300 python scripts/attn_bwd_ab.py --variants "$V" --timing --rounds 6 > "$O/ab.log" 2>&1 || exit $?
+tail -1 "$O/ab.log"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 scripts/attn_bwd_ab.py --variants "$V" --rounds 2 --reps 3 > "$O/prof.log" 2>&1 || exit $?
+find "$O/prof" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats.csv" \;
+head -12 "$O/kernel_stats.csv"
