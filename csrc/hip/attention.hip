@@ -36,6 +36,7 @@
 // query (the diagonal mask removes it), a padded query's outputs are never
 // stored, and in dK/dV a padded query row gets lse = +inf, i.e. p = 0.
 #include <cstdlib>
+#include <type_traits>
 
 #include "toa_common.h"
 
@@ -75,6 +76,40 @@ template <int D>
 __device__ __forceinline__ int v_off(int key, int chunk) {
   return key * AG<D>::ROWB + ((chunk ^ ((key & 3) << (D == 128 ? 2 : 1))) << 4);
 }
+
+// LDS-DMA through the buffer path (MUBUF `buffer_load ... lds`) instead of
+// global_load_lds: hipcc's wait-count pass counts a pending FLAT-encoded
+// LDS-DMA against both the VM and the LGKM counters and then waits
+// lgkmcnt(0) before every LDS read that follows it; with the MUBUF form the
+// reads keep counted lgkmcnt(N) waits, so fragments can be read ahead of the
+// MFMAs that use them.  base: the tensor slice the offsets are relative to.
+// (__device__ helpers, not macros in the kernel bodies: the host pass of a
+// kernel template that names these builtins drops the kernel's launch stub)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void buf_dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds, int aux = 0) {
+  if (aux)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 2);
+  else
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+__device__ __forceinline__ void buf_dma4(__amdgpu_buffer_rsrc_t r, uint32_t voff, void* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, 0, 0, 0);
+}
+#define BUF_DMA(BYTES, rsrc, voff, lds) buf_dma##BYTES((rsrc), (voff), (lds))
+
+// the shader clock after the wave's outstanding LDS / scalar reads retire
+__device__ __forceinline__ unsigned long long memtime_sync() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+// an empty asm on a value: hipcc must assume it changed here, so work
+// derived from it is not hoisted above this point (a __device__ helper: the
+// host pass never sees the VGPR constraint)
+__device__ __forceinline__ void opaque_v(int& x) { asm volatile("" : "+v"(x)); }
 
 typedef short __attribute__((ext_vector_type(4))) s16x4;
 __device__ __forceinline__ bf16x4 tr_read(const char* lds_base, int byte_off) {
@@ -377,7 +412,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
 // body as attn_fwd_kernel, the K / V tiles brought in by global_load_lds
 // into two distinct LDS objects instead of register staging + ds_write
 // (the change that took the dK/dV kernel from 2.19 to 1.97 ms).
-template <int D>
+// VAR 1: tiles by buffer_load ... lds (counted lgkmcnt waits, see BUF_DMA) and
+// the compute with every LDS fragment read one MFMA pair ahead of its use
+// (the two S chains interleaved; same per-chain order, same results).
+template <int D, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int H, int Hk, int S,
@@ -441,6 +479,16 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __res
   auto stage = [&](int t, int buf) {
     char* st = buf ? kv1 : kv0;
     const bf16_t* base = (wave < 4 ? K : V) + koff + (int64_t)t * TK * D;
+    if constexpr (VAR != 0) {
+      const auto rs = buf_rsrc(base);
+#pragma unroll
+      for (int u = 0; u < PW; ++u) {
+        const int pt = PW * (wave & 3) + u;
+        const int col = wave < 4 ? (D == 128 ? kcol ^ ((4 * (pt & 3)) << 3) : kcol) : vcol;
+        BUF_DMA(16, rs, (uint32_t)((RPP * pt + lkey) * D + col) * 2, st + (wave < 4 ? 0 : TILEB) + pt * 1024);
+      }
+      return;
+    }
     if (wave < 4) {
 #pragma unroll
       for (int u = 0; u < PW; ++u) {
@@ -533,10 +581,102 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __res
         }
       }
   };
+  auto compute_pipe = [&](int t, int buf, bool mask) {
+    const char* kb = buf ? kv1 : kv0;
+    const char* vb = kb + TILEB;
+    // ---- S^T = K Q^T: the two 32-key chains interleaved, K fragments of
+    // k-step s + 1 read while the MFMAs of s issue
+    f32x16 sc[2] = {{}, {}};
+    bf16x8 kf[2][2];
+    auto ldk = [&](int s, bf16x8(&f)[2]) {
+      f[0] = as_bf16x8(*(const u32x4*)(kb + kro[s]));
+      f[1] = as_bf16x8(*(const u32x4*)(kb + kro[s] + 32 * ROWB));
+    };
+    ldk(0, kf[0]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) ldk(s + 1, kf[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      sc[0] = mfma32(kf[s & 1][0], qf[s], sc[0]);
+      sc[1] = mfma32(kf[s & 1][1], qf[s], sc[1]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (mask) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int key = t * TK + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          if (key > myq) sc[n][j] = -INFINITY;
+        }
+    }
+    float mx = rowmax32(sc[0], sc[1]);
+    mx = xhalf_max(mx) * scale_log2;
+    if (__any(mx > m_run + RESCALE_THR)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = (m_run == -INFINITY) ? 0.f : EXP2(m_run - m_new);
+      l_run *= alpha;
+      m_run = m_new;
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
+    }
+    f32x2 ls;
+    const f32x2 c2 = {scale_log2, scale_log2}, nm2 = {-m_run, -m_run};
+    uint32_t pw[2][8];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) {
+        f32x2 x = pk_fma(f32x2{sc[n][j], sc[n][j + 1]}, c2, nm2);
+        x[0] = EXP2(x[0]);
+        x[1] = EXP2(x[1]);
+        ls = (n == 0 && j == 0) ? x : ls + x;
+        pw[n][j >> 1] = cvt_pk(x[0], x[1]);
+      }
+    l_run += ls[0] + ls[1];
+    // ---- O^T += V^T P^T: 4 (n, s) x ND MFMAs in pairs, V^T fragments of the
+    // next pair read while a pair issues
+    constexpr int NP = 4 * ND / 2;
+    bf16x4 vf[2][4];
+    auto ldv = [&](int p, bf16x4(&f)[4]) {
+      const int ns = (2 * p) / ND, dt0 = (2 * p) % ND;
+      const int kb0 = (32 * (ns >> 1) + 16 * (ns & 1)) * ROWB;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        f[2 * e] = tr_read(vb, vro[dt0 + e] + kb0);
+        f[2 * e + 1] = tr_read(vb, vro[dt0 + e] + kb0 + 8 * ROWB);
+      }
+    };
+    ldv(0, vf[0]);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int ns = (2 * p) / ND, dt0 = (2 * p) % ND, n = ns >> 1, s2 = ns & 1;
+      u32x4 w;
+      w[0] = pw[n][4 * s2 + 0];
+      w[1] = pw[n][4 * s2 + 1];
+      w[2] = pw[n][4 * s2 + 2];
+      w[3] = pw[n][4 * s2 + 3];
+      const bf16x8 pf = as_bf16x8(w);
+      if (p + 1 < NP) ldv(p + 1, vf[(p + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        acc[dt0 + e] = mfma32(__builtin_shufflevector(vf[p & 1][2 * e], vf[p & 1][2 * e + 1], 0, 1, 2, 3, 4, 5, 6, 7),
+                              pf, acc[dt0 + e]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   auto step = [&](int t, int buf) {
     if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
-    if (t < t_diag) compute(t, buf, false);
-    else if (t == t_diag) compute(t, buf, true);
+    if constexpr (VAR & 1) {
+      if (t < t_diag) compute_pipe(t, buf, false);
+      else if (t == t_diag) compute_pipe(t, buf, true);
+    } else {
+      if (t < t_diag) compute(t, buf, false);
+      else if (t == t_diag) compute(t, buf, true);
+    }
     // my DMA retired, then everyone's (the next step reads buf ^ 1 and restages buf)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
@@ -780,7 +920,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_kernel(
     step(it + 1, 1);
   }
   if (it < total) step(it, 0);
-
   // sum the two query halves' partials: waves m = 1 park theirs in LDS
   // (4 waves x 2 x 64 lanes x 16 ND floats; Q/dO/K/V are dead)
   constexpr int RW = ND * 16 * 64;  // floats per (wave, dk|dv)
@@ -1121,7 +1260,10 @@ struct DQG {
 //    block's (key, 4-query) pieces gives the B operand (query on the lane, 4
 //    keys per read; the key order matches the K^T read's, as in the split
 //    kernel).
-template <int D, bool ROPE = false>
+// VAR 1: tiles by buffer_load ... lds (counted lgkmcnt waits, see BUF_DMA)
+// and the compute with each MFMA pair's transposed reads issued one pair
+// ahead (same per-accumulator order, same results).
+template <int D, bool ROPE = false, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __restrict__ K,
                                                               const bf16_t* __restrict__ dS, bf16_t* __restrict__ dQ,
                                                               int B, int H, int Hk, int S, float scale,
@@ -1170,6 +1312,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     dsg[half] = (32 * gq + (((lane & 31) - 4 * gq) & 31)) * 8;
   }
   auto stage_k = [&](int t, char* st) {  // this wave's pieces of K tile t (shared by the workgroup)
+    if constexpr (VAR != 0) {
+      const auto rs = buf_rsrc(kbase + (int64_t)t * TK * D);
+#pragma unroll
+      for (int u = 0; u < NKP; ++u) BUF_DMA(16, rs, (uint32_t)kgo[u] * 2, st + (wave * NKP + u) * 1024);
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < NKP; ++u)
       __builtin_amdgcn_global_load_lds(
@@ -1177,6 +1325,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
           (__attribute__((address_space(3))) void*)(st + (wave * NKP + u) * 1024), 16, 0, 0);
   };
   auto stage_s = [&](int t, char* st) {  // this wave's own dS blocks 2t, 2t + 1 (clamped to the diagonal)
+    if constexpr (VAR != 0) {
+      const auto rs = buf_rsrc(dsrow);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ki = min(2 * t + (v >> 1), qi);
+        // slc (aux bit 1): read once; leave L2 to the K tiles
+        buf_dma16(rs, (uint32_t)((ki << 10) + dsg[v & 1]) * 2, st + KT + wave * DQG<D>::DSW + v * 1024, 1);
+      }
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int ki = min(2 * t + (v >> 1), qi);
@@ -1216,8 +1374,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
   // the epilogue's cos / sin rows loaded ahead of the main loop, so their
   // latency hides under it instead of following it
+  // (the pipelined form loads them after the loop: its fragments in flight
+  // leave no room for them)
   f32x4 rcs[D / 64][4], rsn[D / 64][4];
-  if constexpr (ROPE)
+  if constexpr (ROPE && (VAR & 1) == 0)
     rope_cs_load<D>(rcs, rsn, cosv + (int64_t)(qi * 32 + r) * (D / 2), sinv + (int64_t)(qi * 32 + r) * (D / 2), hh);
 
   auto compute = [&](int t, const char* st) {
@@ -1239,6 +1399,56 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
       }
     }
   };
+  // the same MFMAs, (n, s2, dt) flattened, the next pair's reads (dS^T
+  // operand when it changes, K^T fragments) issued before a pair's MFMAs
+  auto compute_pipe = [&](auto nn_tag, int t, const char* st) {
+    constexpr int NN = decltype(nn_tag)::value;  // 32-key halves of the tile below the diagonal
+    constexpr int NI = NN * 2 * ND, NP = NI / 2;
+    const char* dimg = st + KT + wave * DQG<D>::DSW;
+    bf16x4 sf[2][2], kf[2][4];
+    auto ld = [&](int p, int slot) {
+      const int i0 = 2 * p, ns = i0 / ND, dt0 = i0 % ND, n = ns >> 1, s2 = ns & 1;
+      if (dt0 == 0) {
+        sf[slot][0] = tr_read(dimg + n * 2048, dso[s2][0]);
+        sf[slot][1] = tr_read(dimg + n * 2048, dso[s2][1]);
+      }
+      const int rb = (32 * n + 16 * s2) * ROWB;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        kf[slot][2 * e] = tr_read(st, tro[dt0 + e] + rb);
+        kf[slot][2 * e + 1] = tr_read(st, tro8[dt0 + e] + rb);
+      }
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int i0 = 2 * p, dt0 = i0 % ND;
+      // the dS^T operand slot: pairs of one (n, s2) share it
+      const int sslot = ((i0 / ND) & 1);
+      if (p + 1 < NP) {
+        const int i1 = i0 + 2;
+        if (i1 % ND == 0) {  // next (n, s2): its dS^T operand into the other slot
+          const int ns = i1 / ND, n = ns >> 1, s2 = ns & 1;
+          sf[sslot ^ 1][0] = tr_read(dimg + n * 2048, dso[s2][0]);
+          sf[sslot ^ 1][1] = tr_read(dimg + n * 2048, dso[s2][1]);
+        }
+        const int ns = i1 / ND, n = ns >> 1, s2 = ns & 1, rb = (32 * n + 16 * s2) * ROWB;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          kf[(p + 1) & 1][2 * e] = tr_read(st, tro[i1 % ND + e] + rb);
+          kf[(p + 1) & 1][2 * e + 1] = tr_read(st, tro8[i1 % ND + e] + rb);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 sb = (bf16x8)__builtin_shufflevector(sf[sslot][0], sf[sslot][1], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        acc[dt0 + e] = mfma32(
+            (bf16x8)__builtin_shufflevector(kf[p & 1][2 * e], kf[p & 1][2 * e + 1], 0, 1, 2, 3, 4, 5, 6, 7), sb,
+            acc[dt0 + e]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   auto sync = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -1255,7 +1465,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     __builtin_amdgcn_s_waitcnt(0x0F70 | (8 + NKP));
     sync();  // every wave's K pieces of t landed; every wave done with K t - 1
     stage_k(min(t + 2, ntiles - 1), kpre);
-    if (t <= tdiag) compute(t, cur);
+    if constexpr (VAR & 1) {
+      if (t < tdiag || (t == tdiag && 2 * t + 1 <= qi)) compute_pipe(std::integral_constant<int, 2>{}, t, cur);
+      else if (t == tdiag) compute_pipe(std::integral_constant<int, 1>{}, t, cur);
+    } else {
+      if (t <= tdiag) compute(t, cur);
+    }
     stage_s(min(t + 3, ntiles - 1), (char*)cur);
   };
   stage_s(0, s0);
@@ -1277,6 +1492,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
   bf16_t* qrow = dQ + ((int64_t)(b * H + h) * S + myq) * D;
   float osc = scale;
   if constexpr (ROPE) {  // rotate back and write the q part of d(qkv) row (b, myq)
+    if constexpr ((VAR & 1) != 0)
+      rope_cs_load<D>(rcs, rsn, cosv + (int64_t)(qi * 32 + r) * (D / 2), sinv + (int64_t)(qi * 32 + r) * (D / 2), hh);
     rope_bwd_acc<D>(acc, rcs, rsn, scale);
     qrow = dQ + ((int64_t)b * S + myq) * H3 * D + h * D;
     osc = 1.f;
@@ -1308,13 +1525,18 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
 // Each step ends with its own DMA and stores retired (vmcnt(0)) and a
 // barrier.  LSE / DELTA here are the delta pass's -lse log2(e) / -delta rows.
 // S % 256 == 0 only (no ragged tiles).
-template <int D, bool ROPE = false>
+// VAR bit 0: the step-end wait retires the step's LDS-DMA only (vmcnt(2): the
+// wave's two dS stores, issued after it, drain under the next step).
+// VAR bit 1: s_setprio 1 for the younger half (waves 4-7) before the loop.
+// TIMED: per wave, s_memtime sums of issue time and step-end wait time.
+template <int D, bool ROPE = false, int VAR = 0, bool TIMED = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, bf16_t* __restrict__ dS, int B, int H, int Hk, int S,
     float scale, float scale_log2, int o_bshd,
-    const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr, int H3 = 0) {
+    const float* __restrict__ cosv = nullptr, const float* __restrict__ sinv = nullptr, int H3 = 0,
+    unsigned long long* __restrict__ tstat = nullptr) {
   using G = AG<D>;
   constexpr int ROWB = G::ROWB, NCH = G::NCH, NS = G::NS, ND = G::ND, TILEB = G::TILEB;
   constexpr int QBUF = DKV<D>::QBUF, KVB = DKV<D>::KVB;
@@ -1388,33 +1610,149 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const int qt = qt0 + it % nqt;
     char* st = buf ? qd1 : qd0;
     if (wave < 4) {
-      const bf16_t* src = Q + ((int64_t)(b * H + hq) * S + qt * 64) * D;
+      const auto rs = buf_rsrc(Q + ((int64_t)(b * H + hq) * S + qt * 64) * D);
 #pragma unroll
       for (int u = 0; u < PW; ++u) {
         const int pt = PW * wave + u;
         const int col = D == 128 ? lcol ^ ((pt & 3) << 3) : lcol;
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + (uint32_t)((RPP * pt + lrow) * D + col)),
-            (__attribute__((address_space(3))) void*)(st + pt * 1024), 16, 0, 0);
+        BUF_DMA(16, rs, (uint32_t)((RPP * pt + lrow) * D + col) * 2, st + pt * 1024);
       }
     } else {
-      const int64_t rs = o_bshd ? (int64_t)H * D : D;  // dO row stride
-      const bf16_t* src = dO + o_off<D>(b, hq, qt * 64, H, S, o_bshd);
+      const int rstr = o_bshd ? H * D : D;  // dO row stride (elements)
+      const auto rs = buf_rsrc(dO + o_off<D>(b, hq, qt * 64, H, S, o_bshd));
 #pragma unroll
       for (int u = 0; u < PW; ++u) {
         const int pt = PW * (wave - 4) + u;
         const int col = D == 128 ? lcol ^ ((pt & 3) << 3) : lcol;
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(src + (uint32_t)((RPP * pt + lrow) * rs + col)),
-            (__attribute__((address_space(3))) void*)(st + TILEB + pt * 1024), 16, 0, 0);
+        BUF_DMA(16, rs, (uint32_t)((RPP * pt + lrow) * rstr + col) * 2, st + TILEB + pt * 1024);
       }
     }
     if (wave == 0) {  // -lse log2e and -delta rows (the delta pass wrote them): 256 B each
-      const int64_t li = (int64_t)(b * H + hq) * S + qt * 64 + lane;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(LSE + li),
-                                       (__attribute__((address_space(3))) void*)(st + 2 * TILEB), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(DELTA + li),
-                                       (__attribute__((address_space(3))) void*)(st + 2 * TILEB + 256), 4, 0, 0);
+      const int64_t li = (int64_t)(b * H + hq) * S + qt * 64;
+      BUF_DMA(4, buf_rsrc(LSE + li), lane * 4, st + 2 * TILEB);
+      BUF_DMA(4, buf_rsrc(DELTA + li), lane * 4, st + 2 * TILEB + 256);
+    }
+  };
+
+  // VAR bit 2: the sub-tile with its LDS operands read one MFMA pair ahead
+  // (two fragment sets; the waits become counted lgkmcnt instead of a
+  // lgkmcnt(0) before every MFMA) and the -lse rows read under the last
+  // S / dP pair.  Same arithmetic in the same order as `subtile`.
+  auto subtile_pipe = [&](int buf, int qs, bool mask, bf16_t* dsb) {
+    const char* qi = buf ? qd1 : qd0;
+    const char* oi = qi + TILEB;
+    const float* lb = (const float*)(qi + 2 * TILEB);
+    // D = 128: the operand offsets from 4 per-lane values instead of 16
+    // registers (rro[s] = rb + 32 (s ^ rc), tro[dt] = tb + 64 (dt ^ qq),
+    // tro8 = tro + d8); the empty asm keeps hipcc from hoisting the 16 back
+    // out of the loop
+    int rb = 0, rc = 0, tb = 0, d8 = 0, tq = 0;
+    if constexpr (D == 128) {
+      const int swz = ((r & 3) << 2) | ((r >> 2) & 3);
+      rb = r * ROWB + ((hh ^ (swz & 1)) << 4);
+      rc = swz >> 1;
+      tq = (lane & 15) >> 2;
+      tb = tro[0] - (tq << 6);
+      d8 = tro8[0] - tro[0];
+      opaque_v(rb);
+      opaque_v(rc);
+      opaque_v(tb);
+      opaque_v(d8);
+      opaque_v(tq);
+    }
+    auto rro_at = [&](int s) { return D == 128 ? rb + ((s ^ rc) << 5) : rro[s]; };
+    auto tro_at = [&](int dt) { return D == 128 ? tb + ((dt ^ tq) << 6) : tro[dt]; };
+    auto tro8_at = [&](int dt) { return D == 128 ? tb + ((dt ^ tq) << 6) + d8 : tro8[dt]; };
+    f32x16 dp;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 d4 = *(const f32x4*)(lb + 64 + 32 * m + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dp[4 * g4 + j] = d4[j];
+    }
+    f32x16 sc = {};
+    // S / dP: the (Q, K) and (dO, V) fragment pairs of step s + 1 are read
+    // while the MFMAs of step s issue, staggered by half a step (the Q/K pair
+    // of s + 1 before S(s), the dO/V pair before dP(s)): 24 fragment
+    // registers, two MFMAs of cover for every read
+    bf16x8 qk[2][2], ov[2][2];
+    auto ldqk = [&](int s, bf16x8(&f)[2]) {
+      const int o = rro_at(s);
+      f[0] = as_bf16x8(*(const u32x4*)(qi + o + 32 * ROWB * m));
+      f[1] = as_bf16x8(*(const u32x4*)(kimg + o + 32 * ROWB * kg));
+    };
+    auto ldov = [&](int s, bf16x8(&f)[2]) {
+      const int o = rro_at(s);
+      f[0] = as_bf16x8(*(const u32x4*)(oi + o + 32 * ROWB * m));
+      f[1] = as_bf16x8(*(const u32x4*)(vimg + o + 32 * ROWB * kg));
+    };
+    f32x4 l4[4];
+    ldqk(0, qk[0]);
+    ldov(0, ov[0]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) ldqk(s + 1, qk[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      sc = mfma32(qk[s & 1][0], qk[s & 1][1], sc);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < NS) {
+        ldov(s + 1, ov[(s + 1) & 1]);
+      } else {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) l4[g4] = *(const f32x4*)(lb + 32 * m + 8 * g4 + 4 * hh);  // -lse * log2(e)
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      dp = mfma32(ov[s & 1][0], ov[s & 1][1], dp);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t pw[8], sw[8];
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      float p0 = EXP2(fmaf(sc[j], scale_log2, l4[j >> 2][j & 3]));
+      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, l4[j >> 2][(j + 1) & 3]));
+      if (mask) {
+        const int q = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        if (q < mykey) p0 = 0.f;
+        if (q + 1 < mykey) p1 = 0.f;
+      }
+      pw[j >> 1] = pack2(p0, p1);
+      sw[j >> 1] = pack2(p0 * dp[j], p1 * dp[j + 1]);
+    }
+    // dV^T / dK^T: 8 (s2, dt) pairs of MFMAs, the transposed reads one pair ahead
+    bf16x4 ft[2][4];
+    auto ldt = [&](int i, bf16x4(&f)[4]) {
+      const int s2 = i / ND, dt = i % ND;
+      const int rbo = (32 * m + 16 * s2) * ROWB;
+      const int o = tro_at(dt) + rbo, o8 = tro8_at(dt) + rbo;
+      f[0] = tr_read(oi, o);
+      f[1] = tr_read(oi, o8);
+      f[2] = tr_read(qi, o);
+      f[3] = tr_read(qi, o8);
+    };
+    ldt(0, ft[0]);
+#pragma unroll
+    for (int i = 0; i < 2 * ND; ++i) {
+      const int s2 = i / ND, dt = i % ND;
+      u32x4 a, c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] = pw[4 * s2 + e];
+        c[e] = sw[4 * s2 + e];
+      }
+      if (i + 1 < 2 * ND) ldt(i + 1, ft[(i + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x4* f = ft[i & 1];
+      dv[dt] = mfma32((bf16x8)__builtin_shufflevector(f[0], f[1], 0, 1, 2, 3, 4, 5, 6, 7), as_bf16x8(a), dv[dt]);
+      dk[dt] = mfma32((bf16x8)__builtin_shufflevector(f[2], f[3], 0, 1, 2, 3, 4, 5, 6, 7), as_bf16x8(c), dk[dt]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (i == ND - 1) {  // dS chunks (as in `subtile`), draining under the second half
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const auto x = __builtin_amdgcn_permlane32_swap(sw[4 * k], sw[4 * k + 2], false, false);
+          const auto y = __builtin_amdgcn_permlane32_swap(sw[4 * k + 1], sw[4 * k + 3], false, false);
+          __builtin_nontemporal_store(u32x4{x[0], y[0], x[1], y[1]}, (u32x4*)(dsb + (2 * k + hh) * 256 + r * 8));
+        }
+      }
     }
   };
 
@@ -1484,24 +1822,57 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       }
     }
   };
+  unsigned long long t_issue = 0, t_wait = 0;
+  auto stamp = [&]() { return memtime_sync(); };
   auto step = [&](int it, int buf) {
+    unsigned long long t0 = 0, t1 = 0;
+    if constexpr (TIMED) t0 = stamp();
     if (it + 1 < total) stage(it + 1, buf ^ 1);
     const int qs = (qt0 + it % nqt) * 64 + 32 * m;
     const int hq = hk * rep + it / nqt, qb32 = qs >> 5, nb = S >> 5;
     bf16_t* dsb = dS + (int64_t)(b * H + hq) * (nb * (nb + 1) / 2) * 1024 + ((uint32_t)(qb32 * (qb32 + 1) / 2 + (kw >> 5)) << 10);
-    if (qs > kw) subtile(buf, qs, false, dsb);        // strictly below this wave's diagonal
-    else if (qs == kw) subtile(buf, qs, true, dsb);  // the diagonal sub-tile
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr ((VAR & 4) != 0) {
+      if (qs > kw) subtile_pipe(buf, qs, false, dsb);
+      else if (qs == kw) subtile_pipe(buf, qs, true, dsb);
+    } else {
+      if (qs > kw) subtile(buf, qs, false, dsb);        // strictly below this wave's diagonal
+      else if (qs == kw) subtile(buf, qs, true, dsb);  // the diagonal sub-tile
+    }
+    if constexpr (TIMED) t1 = stamp();
+    if constexpr (VAR & 1) {
+      if (qs < kw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no stores this step
+      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if constexpr (TIMED) {
+      const unsigned long long t2 = stamp();
+      t_issue += t1 - t0;
+      t_wait += t2 - t1;
+    }
   };
 
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if constexpr ((VAR & 2) != 0) {
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   int it = 0;
   for (; it + 1 < total; it += 2) {  // unrolled by 2: buffer offsets become immediates
     step(it, 0);
     step(it + 1, 1);
   }
   if (it < total) step(it, 0);
+  if constexpr (VAR & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (TIMED) {
+    if (lane == 0) {
+      unsigned long long* o = tstat + ((int64_t)blockIdx.x * 8 + wave) * 4;
+      o[0] = t_issue;
+      o[1] = t_wait;
+      o[2] = (unsigned long long)total;
+      o[3] = 0;
+    }
+  }
 
   // sum the two query halves' partials: waves m = 1 park theirs in LDS
   // (dK^T partials in kv, dV^T in qd0 / qd1: ND 16 64 floats per wave)
@@ -1573,9 +1944,45 @@ static int attn_bwd_variant() {
   return g_bwd_variant;
 }
 extern "C" int toa_attn_set_bwd_variant(int v) {
-  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
+  if (v < -1 || v > 24) return (int)hipErrorInvalidValue;
   g_bwd_variant = v;
   return 0;
+}
+// A/B instrumentation (scripts/attn_bwd_ab.py --timing): when set, the dS
+// form's dK/dV kernel writes per-wave {issue cycles, step-end wait cycles,
+// steps, 0} (u64) at tstat[(block * 8 + wave) * 4]
+static unsigned long long* g_attn_tstat = nullptr;
+extern "C" int toa_attn_set_bwd_timing(void* tstat) {
+  g_attn_tstat = (unsigned long long*)tstat;
+  return 0;
+}
+template <int D, bool ROPE>
+static void dkdv_ds_launch(hipStream_t stream, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
+                           const float* nlse2, const float* delta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B, int H,
+                           int Hk, int S, float scale, int o_bshd, const float* cosv, const float* sinv, int H3) {
+  const dim3 grid((S / 128) * B * Hk), block(512);
+  const int var = g_bwd_variant >= 2 ? (g_bwd_variant - 1) & 7 : 0;  // forms 2..8 (10..16, 18..24) -> VAR 1..7
+#define TOA_DKDV(VV, TT)                                                                                            \
+  hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE, VV, TT>), grid, block, 0, stream, q, k, v, dout, nlse2,      \
+                     delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, cosv, sinv, H3, g_attn_tstat)
+#define TOA_DKDV_T(TT)                  \
+  switch (var) {                        \
+    case 1: TOA_DKDV(1, TT); break;     \
+    case 2: TOA_DKDV(2, TT); break;     \
+    case 3: TOA_DKDV(3, TT); break;     \
+    case 4: TOA_DKDV(4, TT); break;     \
+    case 5: TOA_DKDV(5, TT); break;     \
+    case 6: TOA_DKDV(6, TT); break;     \
+    case 7: TOA_DKDV(7, TT); break;     \
+    default: TOA_DKDV(0, TT); break;    \
+  }
+  if (g_attn_tstat) {
+    TOA_DKDV_T(true);
+  } else {
+    TOA_DKDV_T(false);
+  }
+#undef TOA_DKDV_T
+#undef TOA_DKDV
 }
 static bool attn_bwd_uses_ds(int S) { return attn_bwd_variant() >= 1 && S % FWD_QB == 0; }
 // [dS blocks][-lse log2e rows]; the -delta rows go to the caller's delta buffer
@@ -1612,7 +2019,7 @@ static void attn_set_lds_limits() {
 static int g_fwd_variant = 1;
 static int attn_fwd_variant() { return g_fwd_variant; }
 extern "C" int toa_attn_set_fwd_variant(int v) {
-  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
+  if (v < -1 || v > 3) return (int)hipErrorInvalidValue;
   g_fwd_variant = v < 0 ? 1 : v;
   return 0;
 }
@@ -1626,6 +2033,16 @@ static int attn_fwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf
     if (attn_fwd_variant() == 1) {
       hipLaunchKernelGGL((attn_fwd_gl_kernel<D>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o, lse,
                          B, H, Hk, S, scale * LOG2E, o_bshd);
+      return (int)hipGetLastError();
+    }
+    if (attn_fwd_variant() == 2) {
+      hipLaunchKernelGGL((attn_fwd_gl_kernel<D, 1>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o,
+                         lse, B, H, Hk, S, scale * LOG2E, o_bshd);
+      return (int)hipGetLastError();
+    }
+    if (attn_fwd_variant() == 3) {
+      hipLaunchKernelGGL((attn_fwd_gl_kernel<D, 2>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o,
+                         lse, B, H, Hk, S, scale * LOG2E, o_bshd);
       return (int)hipGetLastError();
     }
   }
@@ -1647,10 +2064,17 @@ static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
       const int rows = B * H * S;
       hipLaunchKernelGGL((attn_delta_kernel<D>), dim3((rows + 256 / (D / 8) - 1) / (256 / (D / 8))), dim3(256), 0,
                          stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
-      hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D>), dim3((S / 128) * B * Hk), dim3(512), 0, stream, q, k, v, dout,
-                         nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd);
-      hipLaunchKernelGGL((attn_bwd_dqg_kernel<D>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, dq, B, H,
-                         Hk, S, scale);
+      dkdv_ds_launch<D, false>(stream, q, k, v, dout, nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, o_bshd, nullptr,
+                               nullptr, 0);
+      if (g_bwd_variant >= 17)
+        hipLaunchKernelGGL((attn_bwd_dqg_kernel<D, false, 2>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,
+                           ds, dq, B, H, Hk, S, scale, nullptr, nullptr, 0);
+      else if (g_bwd_variant >= 9)
+        hipLaunchKernelGGL((attn_bwd_dqg_kernel<D, false, 1>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,
+                           ds, dq, B, H, Hk, S, scale, nullptr, nullptr, 0);
+      else
+        hipLaunchKernelGGL((attn_bwd_dqg_kernel<D>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, dq, B,
+                           H, Hk, S, scale, nullptr, nullptr, 0);
       return (int)hipGetLastError();
     }
   }
@@ -1716,7 +2140,7 @@ extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t*
                                  const float* sinv, bf16_t* dqkv, int B, int H, int Hk, int S, int D, int flags,
                                  float scale, hipStream_t stream) {
   if (!attn_shape_ok(B, H, Hk, S, D, flags)) return (int)hipErrorInvalidValue;
-  if (!attn_bwd_uses_ds(S) || attn_bwd_variant() != 1) return (int)hipErrorNotSupported;
+  if (!attn_bwd_uses_ds(S)) return (int)hipErrorNotSupported;
   if (ws == nullptr || dqkv == nullptr || cosv == nullptr || sinv == nullptr) return (int)hipErrorInvalidValue;
   const int o_bshd = (flags >> 1) & 1;
   const int H3 = H + 2 * Hk;
@@ -1727,11 +2151,14 @@ extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t*
   do {                                                                                                           \
     hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 256 / (DD / 8) - 1) / (256 / (DD / 8))), dim3(256), \
                        0, stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);                               \
-    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<DD, true>), dim3((S / 128) * B * Hk), dim3(512), 0,       \
-                       stream, q, k, v, dout, nlse2, delta, dqkv, dqkv, ds, B, H, Hk, S, scale, scale * LOG2E,  \
-                       o_bshd, cosv, sinv, H3);                                          \
-    hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \
-                       dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                               \
+    dkdv_ds_launch<DD, true>(stream, q, k, v, dout, nlse2, delta, dqkv, dqkv, ds, B, H, Hk, S, scale, o_bshd,  \
+                             cosv, sinv, H3);                                                                   \
+    if (g_bwd_variant >= 9)                                                                                     \
+      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true, 1>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,  \
+                         ds, dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                         \
+    else                                                                                                         \
+      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \
+                         dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                             \
   } while (0)
 #ifdef TOA_ATTN_D128_ONLY
   if (D != 128) return (int)hipErrorInvalidValue;

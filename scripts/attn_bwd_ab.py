@@ -4,10 +4,21 @@ rounds on random data (guide §5.4 rules 24/25):
 
     split   dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
+    ds2     ds with the dK/dV step-end wait retiring only the step's LDS-DMA
+            (the dS stores drain under the next step)
+    ds3     ds with s_setprio 1 for the younger half of the dK/dV workgroup
+    ds4     ds2 + ds3
+    ds5..8  ds1..4 with the pipelined sub-tile (LDS fragments read one MFMA
+            pair ahead under counted lgkmcnt waits)
+    ds9..16 ds1..8 with the pipelined dQ GEMM
+    ds17..24 ds1..8 with the dQ GEMM staged by buffer-path DMA (hipcc's schedule)
+
+--timing: one extra run per ds form with the dK/dV kernel's s_memtime
+instrumentation (issue vs step-end wait cycles per step, per wave).
 
 Also checks every form agrees with the first.
 
-    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5] [--variants split,ds]
+    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5] [--variants split,ds,ds2] [--timing]
 """
 import argparse
 import json
@@ -27,6 +38,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=6)
     ap.add_argument("--variants", default="split,ds")
+    ap.add_argument("--timing", action="store_true")
     a = ap.parse_args()
     B, H, Hk, S, D = a.batch, 32, 8, 4096, 128
     dev = "cuda"
@@ -45,7 +57,7 @@ def main():
     outs = {}
 
     # backward form: 0 = split (dQ recomputes S / dP), 1 = dS through HBM + dQ GEMM
-    forms = {"split": 0, "ds": 1}
+    forms = {"split": 0, "ds": 1, **{f"ds{f}": f for f in range(2, 25)}}
     variants = a.variants.split(",")
 
     def run(variant):
@@ -81,6 +93,24 @@ def main():
         med = statistics.median(t)
         res[var] = {"median_ms": round(med, 3), "min_ms": round(min(t), 3),
                              "useful_PFps": round(2.5 * flops_fwd / med / 1e12, 3)}
+    if a.timing:
+        nblk = (S // 128) * B * Hk
+        for var in variants:
+            if forms[var] == 0:
+                continue
+            ts = torch.zeros(nblk * 8 * 4, device=dev, dtype=torch.int64)
+            _lib.call("toa_attn_set_bwd_timing", P(ts))
+            run(var)
+            torch.cuda.synchronize()
+            _lib.call("toa_attn_set_bwd_timing", None)
+            t = ts.view(nblk, 8, 4).double().cpu()
+            steps = t[..., 2].clamp(min=1)
+            per = {}
+            for m in (0, 1):
+                w = slice(4 * m, 4 * m + 4)
+                per[f"m{m}"] = {"issue_cyc_per_step": round(float((t[:, w, 0] / steps[:, w]).mean()), 1),
+                                "wait_cyc_per_step": round(float((t[:, w, 1] / steps[:, w]).mean()), 1)}
+            res[var]["timing"] = per
     _lib.call("toa_attn_set_bwd_variant", -1)
     print(json.dumps(res))
 

@@ -4,10 +4,13 @@ on random data (guide §5.4 rules 24/25):
 
     reg  K/V tiles staged through registers + ds_write (attn_fwd_kernel)
     gl   K/V tiles by LDS-DMA into two distinct LDS objects (attn_fwd_gl_kernel)
+    pipe gl with buffer-path DMA and every LDS fragment read one MFMA pair
+         ahead (attn_fwd_gl_kernel<D, 1>)
+    buf  gl with buffer-path DMA, hipcc's own schedule (attn_fwd_gl_kernel<D, 2>)
 
 and the max |difference| of O / lse between them (same arithmetic: 0 expected).
 
-    python scripts/attn_fwd_ab.py [--rounds 6] [--reps 10]
+    python scripts/attn_fwd_ab.py [--rounds 6] [--reps 10] [--forms gl,pipe]
 """
 import argparse
 import json
@@ -26,6 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=6)
+    ap.add_argument("--forms", default="reg,gl,pipe")
     a = ap.parse_args()
     B, H, Hk, S, D = a.batch, 32, 8, 4096, 128
     torch.manual_seed(0)
@@ -33,7 +37,7 @@ def main():
     k = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     v = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     P = _lib.ptr
-    forms = {"reg": 0, "gl": 1}
+    forms = {k: v for k, v in {"reg": 0, "gl": 1, "pipe": 2, "buf": 3}.items() if k in a.forms.split(",")}
     outs = {}
 
     def run(form):
@@ -47,8 +51,9 @@ def main():
     for f in forms:
         outs[f] = run(f)
     torch.cuda.synchronize()
-    diff = {"o": float((outs["gl"][0].float() - outs["reg"][0].float()).abs().max()),
-            "lse": float((outs["gl"][1] - outs["reg"][1]).abs().max())}
+    base = list(forms)[0]
+    diff = {f"{f}_vs_{base}": {"o": float((outs[f][0].float() - outs[base][0].float()).abs().max()),
+                               "lse": float((outs[f][1] - outs[base][1]).abs().max())} for f in list(forms)[1:]}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {f: [] for f in forms}
     for _ in range(a.rounds):
@@ -62,7 +67,7 @@ def main():
             times[f].append(ev[0].elapsed_time(ev[1]) / a.reps)
     _lib.call("toa_attn_set_fwd_variant", -1)
     flops = 4 * B * H * S * S * D / 2
-    res = {"shape": [B, H, Hk, S, D], "max_abs_diff_gl_vs_reg": diff}
+    res = {"shape": [B, H, Hk, S, D], "max_abs_diff": diff}
     for f, t in times.items():
         med = statistics.median(t)
         res[f] = {"median_ms": round(med, 4), "min_ms": round(min(t), 4), "PFps": round(flops / med / 1e12, 3)}

@@ -5,7 +5,8 @@ process (one model, one set of buffers): alternating timed windows of
     python scripts/wgrad_inmodel_ab.py [--rounds 3] [--steps 4] [--arms wgrad=asm+gemm=nosk,wgrad=hip+gemm=nosk]
 
 An arm is settings joined by '+': wgrad=asm|hip (ops.gemm.set_wgrad_kernel),
-gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy).  Same-process windows
+gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy), attnf=N /
+attnb=N (toa_attn_set_fwd_variant / toa_attn_set_bwd_variant forms).  Same-process windows
 remove the box-to-box spread (about +-2.5 %) from the comparison.
 """
 import argparse
@@ -17,7 +18,7 @@ import time
 import torch
 
 sys.path.insert(0, ".")
-from tf_operator_amd.ops import gemm  # noqa: E402
+from tf_operator_amd.ops import _lib, gemm  # noqa: E402
 from tf_operator_amd.train.llm import LlamaTrainer  # noqa: E402
 
 
@@ -29,6 +30,10 @@ def apply(arm: str):
             gemm.set_wgrad_kernel(val)
         elif key == "gemm":
             gemm.set_mode(val)
+        elif key == "attnf":
+            _lib.call("toa_attn_set_fwd_variant", int(val))
+        elif key == "attnb":
+            _lib.call("toa_attn_set_bwd_variant", int(val))
         else:
             raise SystemExit(f"unknown arm {arm}")
 

@@ -91,6 +91,7 @@ _SIGS = {
     "toa_gemm_asm_timing": [c_int, c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_probe": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_attn_set_bwd_variant": [c_int],
+    "toa_attn_set_bwd_timing": [c_p],
     "toa_norm_set_row": [c_int],
     "toa_attn_set_fwd_variant": [c_int],
     "toa_attn_bwd_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
