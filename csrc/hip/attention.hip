@@ -36,7 +36,6 @@
 // query (the diagonal mask removes it), a padded query's outputs are never
 // stored, and in dK/dV a padded query row gets lse = +inf, i.e. p = 0.
 #include <cstdlib>
-#include <type_traits>
 
 #include "toa_common.h"
 
@@ -412,10 +411,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
 // body as attn_fwd_kernel, the K / V tiles brought in by global_load_lds
 // into two distinct LDS objects instead of register staging + ds_write
 // (the change that took the dK/dV kernel from 2.19 to 1.97 ms).
-// VAR 1: tiles by buffer_load ... lds (counted lgkmcnt waits, see BUF_DMA) and
-// the compute with every LDS fragment read one MFMA pair ahead of its use
-// (the two S chains interleaved; same per-chain order, same results).
-template <int D, int VAR = 0>
+template <int D>
 __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int H, int Hk, int S,
@@ -479,16 +475,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __res
   auto stage = [&](int t, int buf) {
     char* st = buf ? kv1 : kv0;
     const bf16_t* base = (wave < 4 ? K : V) + koff + (int64_t)t * TK * D;
-    if constexpr (VAR != 0) {
-      const auto rs = buf_rsrc(base);
-#pragma unroll
-      for (int u = 0; u < PW; ++u) {
-        const int pt = PW * (wave & 3) + u;
-        const int col = wave < 4 ? (D == 128 ? kcol ^ ((4 * (pt & 3)) << 3) : kcol) : vcol;
-        BUF_DMA(16, rs, (uint32_t)((RPP * pt + lkey) * D + col) * 2, st + (wave < 4 ? 0 : TILEB) + pt * 1024);
-      }
-      return;
-    }
     if (wave < 4) {
 #pragma unroll
       for (int u = 0; u < PW; ++u) {
@@ -581,102 +567,10 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __res
         }
       }
   };
-  auto compute_pipe = [&](int t, int buf, bool mask) {
-    const char* kb = buf ? kv1 : kv0;
-    const char* vb = kb + TILEB;
-    // ---- S^T = K Q^T: the two 32-key chains interleaved, K fragments of
-    // k-step s + 1 read while the MFMAs of s issue
-    f32x16 sc[2] = {{}, {}};
-    bf16x8 kf[2][2];
-    auto ldk = [&](int s, bf16x8(&f)[2]) {
-      f[0] = as_bf16x8(*(const u32x4*)(kb + kro[s]));
-      f[1] = as_bf16x8(*(const u32x4*)(kb + kro[s] + 32 * ROWB));
-    };
-    ldk(0, kf[0]);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      if (s + 1 < NS) ldk(s + 1, kf[(s + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      sc[0] = mfma32(kf[s & 1][0], qf[s], sc[0]);
-      sc[1] = mfma32(kf[s & 1][1], qf[s], sc[1]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (mask) {
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int key = t * TK + 32 * n + (j & 3) + 8 * (j >> 2) + 4 * hh;
-          if (key > myq) sc[n][j] = -INFINITY;
-        }
-    }
-    float mx = rowmax32(sc[0], sc[1]);
-    mx = xhalf_max(mx) * scale_log2;
-    if (__any(mx > m_run + RESCALE_THR)) {
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = (m_run == -INFINITY) ? 0.f : EXP2(m_run - m_new);
-      l_run *= alpha;
-      m_run = m_new;
-#pragma unroll
-      for (int i = 0; i < ND; ++i)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[i][j] *= alpha;
-    }
-    f32x2 ls;
-    const f32x2 c2 = {scale_log2, scale_log2}, nm2 = {-m_run, -m_run};
-    uint32_t pw[2][8];
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int j = 0; j < 16; j += 2) {
-        f32x2 x = pk_fma(f32x2{sc[n][j], sc[n][j + 1]}, c2, nm2);
-        x[0] = EXP2(x[0]);
-        x[1] = EXP2(x[1]);
-        ls = (n == 0 && j == 0) ? x : ls + x;
-        pw[n][j >> 1] = cvt_pk(x[0], x[1]);
-      }
-    l_run += ls[0] + ls[1];
-    // ---- O^T += V^T P^T: 4 (n, s) x ND MFMAs in pairs, V^T fragments of the
-    // next pair read while a pair issues
-    constexpr int NP = 4 * ND / 2;
-    bf16x4 vf[2][4];
-    auto ldv = [&](int p, bf16x4(&f)[4]) {
-      const int ns = (2 * p) / ND, dt0 = (2 * p) % ND;
-      const int kb0 = (32 * (ns >> 1) + 16 * (ns & 1)) * ROWB;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        f[2 * e] = tr_read(vb, vro[dt0 + e] + kb0);
-        f[2 * e + 1] = tr_read(vb, vro[dt0 + e] + kb0 + 8 * ROWB);
-      }
-    };
-    ldv(0, vf[0]);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int ns = (2 * p) / ND, dt0 = (2 * p) % ND, n = ns >> 1, s2 = ns & 1;
-      u32x4 w;
-      w[0] = pw[n][4 * s2 + 0];
-      w[1] = pw[n][4 * s2 + 1];
-      w[2] = pw[n][4 * s2 + 2];
-      w[3] = pw[n][4 * s2 + 3];
-      const bf16x8 pf = as_bf16x8(w);
-      if (p + 1 < NP) ldv(p + 1, vf[(p + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-        acc[dt0 + e] = mfma32(__builtin_shufflevector(vf[p & 1][2 * e], vf[p & 1][2 * e + 1], 0, 1, 2, 3, 4, 5, 6, 7),
-                              pf, acc[dt0 + e]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
   auto step = [&](int t, int buf) {
     if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
-    if constexpr (VAR & 1) {
-      if (t < t_diag) compute_pipe(t, buf, false);
-      else if (t == t_diag) compute_pipe(t, buf, true);
-    } else {
-      if (t < t_diag) compute(t, buf, false);
-      else if (t == t_diag) compute(t, buf, true);
-    }
+    if (t < t_diag) compute(t, buf, false);
+    else if (t == t_diag) compute(t, buf, true);
     // my DMA retired, then everyone's (the next step reads buf ^ 1 and restages buf)
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
@@ -1260,10 +1154,7 @@ struct DQG {
 //    block's (key, 4-query) pieces gives the B operand (query on the lane, 4
 //    keys per read; the key order matches the K^T read's, as in the split
 //    kernel).
-// VAR 1: tiles by buffer_load ... lds (counted lgkmcnt waits, see BUF_DMA)
-// and the compute with each MFMA pair's transposed reads issued one pair
-// ahead (same per-accumulator order, same results).
-template <int D, bool ROPE = false, int VAR = 0>
+template <int D, bool ROPE = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __restrict__ K,
                                                               const bf16_t* __restrict__ dS, bf16_t* __restrict__ dQ,
                                                               int B, int H, int Hk, int S, float scale,
@@ -1312,12 +1203,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     dsg[half] = (32 * gq + (((lane & 31) - 4 * gq) & 31)) * 8;
   }
   auto stage_k = [&](int t, char* st) {  // this wave's pieces of K tile t (shared by the workgroup)
-    if constexpr (VAR != 0) {
-      const auto rs = buf_rsrc(kbase + (int64_t)t * TK * D);
-#pragma unroll
-      for (int u = 0; u < NKP; ++u) BUF_DMA(16, rs, (uint32_t)kgo[u] * 2, st + (wave * NKP + u) * 1024);
-      return;
-    }
 #pragma unroll
     for (int u = 0; u < NKP; ++u)
       __builtin_amdgcn_global_load_lds(
@@ -1325,16 +1210,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
           (__attribute__((address_space(3))) void*)(st + (wave * NKP + u) * 1024), 16, 0, 0);
   };
   auto stage_s = [&](int t, char* st) {  // this wave's own dS blocks 2t, 2t + 1 (clamped to the diagonal)
-    if constexpr (VAR != 0) {
-      const auto rs = buf_rsrc(dsrow);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int ki = min(2 * t + (v >> 1), qi);
-        // slc (aux bit 1): read once; leave L2 to the K tiles
-        buf_dma16(rs, (uint32_t)((ki << 10) + dsg[v & 1]) * 2, st + KT + wave * DQG<D>::DSW + v * 1024, 1);
-      }
-      return;
-    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int ki = min(2 * t + (v >> 1), qi);
@@ -1374,10 +1249,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
   // the epilogue's cos / sin rows loaded ahead of the main loop, so their
   // latency hides under it instead of following it
-  // (the pipelined form loads them after the loop: its fragments in flight
-  // leave no room for them)
   f32x4 rcs[D / 64][4], rsn[D / 64][4];
-  if constexpr (ROPE && (VAR & 1) == 0)
+  if constexpr (ROPE)
     rope_cs_load<D>(rcs, rsn, cosv + (int64_t)(qi * 32 + r) * (D / 2), sinv + (int64_t)(qi * 32 + r) * (D / 2), hh);
 
   auto compute = [&](int t, const char* st) {
@@ -1399,56 +1272,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
       }
     }
   };
-  // the same MFMAs, (n, s2, dt) flattened, the next pair's reads (dS^T
-  // operand when it changes, K^T fragments) issued before a pair's MFMAs
-  auto compute_pipe = [&](auto nn_tag, int t, const char* st) {
-    constexpr int NN = decltype(nn_tag)::value;  // 32-key halves of the tile below the diagonal
-    constexpr int NI = NN * 2 * ND, NP = NI / 2;
-    const char* dimg = st + KT + wave * DQG<D>::DSW;
-    bf16x4 sf[2][2], kf[2][4];
-    auto ld = [&](int p, int slot) {
-      const int i0 = 2 * p, ns = i0 / ND, dt0 = i0 % ND, n = ns >> 1, s2 = ns & 1;
-      if (dt0 == 0) {
-        sf[slot][0] = tr_read(dimg + n * 2048, dso[s2][0]);
-        sf[slot][1] = tr_read(dimg + n * 2048, dso[s2][1]);
-      }
-      const int rb = (32 * n + 16 * s2) * ROWB;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        kf[slot][2 * e] = tr_read(st, tro[dt0 + e] + rb);
-        kf[slot][2 * e + 1] = tr_read(st, tro8[dt0 + e] + rb);
-      }
-    };
-    ld(0, 0);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int i0 = 2 * p, dt0 = i0 % ND;
-      // the dS^T operand slot: pairs of one (n, s2) share it
-      const int sslot = ((i0 / ND) & 1);
-      if (p + 1 < NP) {
-        const int i1 = i0 + 2;
-        if (i1 % ND == 0) {  // next (n, s2): its dS^T operand into the other slot
-          const int ns = i1 / ND, n = ns >> 1, s2 = ns & 1;
-          sf[sslot ^ 1][0] = tr_read(dimg + n * 2048, dso[s2][0]);
-          sf[sslot ^ 1][1] = tr_read(dimg + n * 2048, dso[s2][1]);
-        }
-        const int ns = i1 / ND, n = ns >> 1, s2 = ns & 1, rb = (32 * n + 16 * s2) * ROWB;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          kf[(p + 1) & 1][2 * e] = tr_read(st, tro[i1 % ND + e] + rb);
-          kf[(p + 1) & 1][2 * e + 1] = tr_read(st, tro8[i1 % ND + e] + rb);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const bf16x8 sb = (bf16x8)__builtin_shufflevector(sf[sslot][0], sf[sslot][1], 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-        acc[dt0 + e] = mfma32(
-            (bf16x8)__builtin_shufflevector(kf[p & 1][2 * e], kf[p & 1][2 * e + 1], 0, 1, 2, 3, 4, 5, 6, 7), sb,
-            acc[dt0 + e]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
   auto sync = [&]() {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -1465,12 +1288,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
     __builtin_amdgcn_s_waitcnt(0x0F70 | (8 + NKP));
     sync();  // every wave's K pieces of t landed; every wave done with K t - 1
     stage_k(min(t + 2, ntiles - 1), kpre);
-    if constexpr (VAR & 1) {
-      if (t < tdiag || (t == tdiag && 2 * t + 1 <= qi)) compute_pipe(std::integral_constant<int, 2>{}, t, cur);
-      else if (t == tdiag) compute_pipe(std::integral_constant<int, 1>{}, t, cur);
-    } else {
-      if (t <= tdiag) compute(t, cur);
-    }
+    if (t <= tdiag) compute(t, cur);
     stage_s(min(t + 3, ntiles - 1), (char*)cur);
   };
   stage_s(0, s0);
@@ -1492,8 +1310,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
   bf16_t* qrow = dQ + ((int64_t)(b * H + h) * S + myq) * D;
   float osc = scale;
   if constexpr (ROPE) {  // rotate back and write the q part of d(qkv) row (b, myq)
-    if constexpr ((VAR & 1) != 0)
-      rope_cs_load<D>(rcs, rsn, cosv + (int64_t)(qi * 32 + r) * (D / 2), sinv + (int64_t)(qi * 32 + r) * (D / 2), hh);
     rope_bwd_acc<D>(acc, rcs, rsn, scale);
     qrow = dQ + ((int64_t)b * S + myq) * H3 * D + h * D;
     osc = 1.f;
@@ -1522,14 +1338,15 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
 //  * every (32-query, 32-key) dS block stored for the dQ GEMM (layout at
 //    attn_bwd_dqg_kernel), between the sub-tile's two MFMA halves so the
 //    stores drain under the second half.
-// Each step ends with its own DMA and stores retired (vmcnt(0)) and a
-// barrier.  LSE / DELTA here are the delta pass's -lse log2(e) / -delta rows.
-// S % 256 == 0 only (no ragged tiles).
-// VAR bit 0: the step-end wait retires the step's LDS-DMA only (vmcnt(2): the
-// wave's two dS stores, issued after it, drain under the next step).
-// VAR bit 1: s_setprio 1 for the younger half (waves 4-7) before the loop.
-// TIMED: per wave, s_memtime sums of issue time and step-end wait time.
-template <int D, bool ROPE = false, int VAR = 0, bool TIMED = false>
+// The sub-tile reads its LDS fragments one MFMA pair ahead of their use
+// (round 4: counted lgkmcnt waits, which the buffer-path DMA makes possible;
+// 2.13 -> 1.93 ms at the bench shape, profiles/r4_attn).  Each step ends with
+// its own DMA retired and a barrier; the wave's two dS stores, issued after
+// the DMA, drain under the next step (vmcnt(2)).  LSE / DELTA here are the
+// delta pass's -lse log2(e) / -delta rows.  S % 256 == 0 only (no ragged
+// tiles).  TIMED: per wave, s_memtime sums of issue time and step-end wait
+// time (scripts/attn_bwd_ab.py --timing).
+template <int D, bool ROPE = false, bool TIMED = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -1634,11 +1451,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     }
   };
 
-  // VAR bit 2: the sub-tile with its LDS operands read one MFMA pair ahead
-  // (two fragment sets; the waits become counted lgkmcnt instead of a
-  // lgkmcnt(0) before every MFMA) and the -lse rows read under the last
-  // S / dP pair.  Same arithmetic in the same order as `subtile`.
-  auto subtile_pipe = [&](int buf, int qs, bool mask, bf16_t* dsb) {
+  // one (32-query, 32-key) sub-tile: S / dP, P and dS, dV^T / dK^T, the dS
+  // block stored.  Two fragment sets per operand stream, so each LDS read is
+  // issued one MFMA pair before its MFMA (counted lgkmcnt waits instead of a
+  // lgkmcnt(0) before every MFMA); the -lse rows are read under the last
+  // S / dP pair.
+  auto subtile = [&](int buf, int qs, bool mask, bf16_t* dsb) {
     const char* qi = buf ? qd1 : qd0;
     const char* oi = qi + TILEB;
     const float* lb = (const float*)(qi + 2 * TILEB);
@@ -1756,72 +1574,6 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     }
   };
 
-  auto subtile = [&](int buf, int qs, bool mask, bf16_t* dsb) {
-    const char* qi = buf ? qd1 : qd0;
-    const char* oi = qi + TILEB;
-    const float* lb = (const float*)(qi + 2 * TILEB);
-    f32x16 nd;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 d4 = *(const f32x4*)(lb + 64 + 32 * m + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nd[4 * g4 + j] = d4[j];
-    }
-    const f32x16 z = {};
-    f32x16 sc = z, dp = nd;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const bf16x8 qa = as_bf16x8(*(const u32x4*)(qi + rro[s] + 32 * ROWB * m));
-      const bf16x8 kf = as_bf16x8(*(const u32x4*)(kimg + rro[s] + 32 * ROWB * kg));
-      sc = mfma32(qa, kf, sc);
-      const bf16x8 oa = as_bf16x8(*(const u32x4*)(oi + rro[s] + 32 * ROWB * m));
-      const bf16x8 vf = as_bf16x8(*(const u32x4*)(vimg + rro[s] + 32 * ROWB * kg));
-      dp = mfma32(oa, vf, dp);
-    }
-    // (scalar VALU here: the packed forms need aligned register pairs, and at
-    // 256 VGPRs with resident dK^T / dV^T accumulators that spills in the loop)
-    uint32_t pw[8], sw[8];
-#pragma unroll
-    for (int j = 0; j < 16; j += 2) {
-      const f32x4 l4 = *(const f32x4*)(lb + 32 * m + 8 * (j >> 2) + 4 * hh);  // -lse * log2(e)
-      float p0 = EXP2(fmaf(sc[j], scale_log2, l4[j & 3]));
-      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, l4[(j + 1) & 3]));
-      if (mask) {
-        const int q = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        if (q < mykey) p0 = 0.f;
-        if (q + 1 < mykey) p1 = 0.f;
-      }
-      pw[j >> 1] = pack2(p0, p1);
-      sw[j >> 1] = pack2(p0 * dp[j], p1 * dp[j + 1]);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      u32x4 a, c;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = pw[4 * s2 + i];
-        c[i] = sw[4 * s2 + i];
-      }
-      const bf16x8 pb = as_bf16x8(a), sb = as_bf16x8(c);
-      const int rb = (32 * m + 16 * s2) * ROWB;
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt) {
-        const bf16x4 o0 = tr_read(oi, tro[dt] + rb), o1 = tr_read(oi, tro8[dt] + rb);
-        dv[dt] = mfma32((bf16x8)__builtin_shufflevector(o0, o1, 0, 1, 2, 3, 4, 5, 6, 7), pb, dv[dt]);
-        const bf16x4 q0 = tr_read(qi, tro[dt] + rb), q1 = tr_read(qi, tro8[dt] + rb);
-        dk[dt] = mfma32((bf16x8)__builtin_shufflevector(q0, q1, 0, 1, 2, 3, 4, 5, 6, 7), sb, dk[dt]);
-      }
-      if (s2 == 0) {  // chunk (key r, queries 8g' .. + 7), g' = 2k + hh, at g' * 512 + r * 16 bytes
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const auto x = __builtin_amdgcn_permlane32_swap(sw[4 * k], sw[4 * k + 2], false, false);
-          const auto y = __builtin_amdgcn_permlane32_swap(sw[4 * k + 1], sw[4 * k + 3], false, false);
-          // streamed once, by the dQ GEMM: non-temporal
-          __builtin_nontemporal_store(u32x4{x[0], y[0], x[1], y[1]}, (u32x4*)(dsb + (2 * k + hh) * 256 + r * 8));
-        }
-      }
-    }
-  };
   unsigned long long t_issue = 0, t_wait = 0;
   auto stamp = [&]() { return memtime_sync(); };
   auto step = [&](int it, int buf) {
@@ -1831,20 +1583,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const int qs = (qt0 + it % nqt) * 64 + 32 * m;
     const int hq = hk * rep + it / nqt, qb32 = qs >> 5, nb = S >> 5;
     bf16_t* dsb = dS + (int64_t)(b * H + hq) * (nb * (nb + 1) / 2) * 1024 + ((uint32_t)(qb32 * (qb32 + 1) / 2 + (kw >> 5)) << 10);
-    if constexpr ((VAR & 4) != 0) {
-      if (qs > kw) subtile_pipe(buf, qs, false, dsb);
-      else if (qs == kw) subtile_pipe(buf, qs, true, dsb);
-    } else {
-      if (qs > kw) subtile(buf, qs, false, dsb);        // strictly below this wave's diagonal
-      else if (qs == kw) subtile(buf, qs, true, dsb);  // the diagonal sub-tile
-    }
+    if (qs > kw) subtile(buf, qs, false, dsb);        // strictly below this wave's diagonal
+    else if (qs == kw) subtile(buf, qs, true, dsb);  // the diagonal sub-tile
     if constexpr (TIMED) t1 = stamp();
-    if constexpr (VAR & 1) {
-      if (qs < kw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no stores this step
-      asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
+    if (qs < kw) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no stores this step
+    asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if constexpr (TIMED) {
       const unsigned long long t2 = stamp();
       t_issue += t1 - t0;
@@ -1854,16 +1597,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
 
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if constexpr ((VAR & 2) != 0) {
-    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  }
   int it = 0;
   for (; it + 1 < total; it += 2) {  // unrolled by 2: buffer offsets become immediates
     step(it, 0);
     step(it + 1, 1);
   }
   if (it < total) step(it, 0);
-  if constexpr (VAR & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last dS stores
   if constexpr (TIMED) {
     if (lane == 0) {
       unsigned long long* o = tstat + ((int64_t)blockIdx.x * 8 + wave) * 4;
@@ -1944,7 +1684,7 @@ static int attn_bwd_variant() {
   return g_bwd_variant;
 }
 extern "C" int toa_attn_set_bwd_variant(int v) {
-  if (v < -1 || v > 24) return (int)hipErrorInvalidValue;
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
   g_bwd_variant = v;
   return 0;
 }
@@ -1961,28 +1701,12 @@ static void dkdv_ds_launch(hipStream_t stream, const bf16_t* q, const bf16_t* k,
                            const float* nlse2, const float* delta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B, int H,
                            int Hk, int S, float scale, int o_bshd, const float* cosv, const float* sinv, int H3) {
   const dim3 grid((S / 128) * B * Hk), block(512);
-  const int var = g_bwd_variant >= 2 ? (g_bwd_variant - 1) & 7 : 0;  // forms 2..8 (10..16, 18..24) -> VAR 1..7
-#define TOA_DKDV(VV, TT)                                                                                            \
-  hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE, VV, TT>), grid, block, 0, stream, q, k, v, dout, nlse2,      \
-                     delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, cosv, sinv, H3, g_attn_tstat)
-#define TOA_DKDV_T(TT)                  \
-  switch (var) {                        \
-    case 1: TOA_DKDV(1, TT); break;     \
-    case 2: TOA_DKDV(2, TT); break;     \
-    case 3: TOA_DKDV(3, TT); break;     \
-    case 4: TOA_DKDV(4, TT); break;     \
-    case 5: TOA_DKDV(5, TT); break;     \
-    case 6: TOA_DKDV(6, TT); break;     \
-    case 7: TOA_DKDV(7, TT); break;     \
-    default: TOA_DKDV(0, TT); break;    \
-  }
-  if (g_attn_tstat) {
-    TOA_DKDV_T(true);
-  } else {
-    TOA_DKDV_T(false);
-  }
-#undef TOA_DKDV_T
-#undef TOA_DKDV
+  if (g_attn_tstat)
+    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE, true>), grid, block, 0, stream, q, k, v, dout, nlse2, delta,
+                       dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, cosv, sinv, H3, g_attn_tstat);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE>), grid, block, 0, stream, q, k, v, dout, nlse2, delta, dk,
+                       dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, cosv, sinv, H3, nullptr);
 }
 static bool attn_bwd_uses_ds(int S) { return attn_bwd_variant() >= 1 && S % FWD_QB == 0; }
 // [dS blocks][-lse log2e rows]; the -delta rows go to the caller's delta buffer
@@ -2019,7 +1743,7 @@ static void attn_set_lds_limits() {
 static int g_fwd_variant = 1;
 static int attn_fwd_variant() { return g_fwd_variant; }
 extern "C" int toa_attn_set_fwd_variant(int v) {
-  if (v < -1 || v > 3) return (int)hipErrorInvalidValue;
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
   g_fwd_variant = v < 0 ? 1 : v;
   return 0;
 }
@@ -2033,16 +1757,6 @@ static int attn_fwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf
     if (attn_fwd_variant() == 1) {
       hipLaunchKernelGGL((attn_fwd_gl_kernel<D>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o, lse,
                          B, H, Hk, S, scale * LOG2E, o_bshd);
-      return (int)hipGetLastError();
-    }
-    if (attn_fwd_variant() == 2) {
-      hipLaunchKernelGGL((attn_fwd_gl_kernel<D, 1>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o,
-                         lse, B, H, Hk, S, scale * LOG2E, o_bshd);
-      return (int)hipGetLastError();
-    }
-    if (attn_fwd_variant() == 3) {
-      hipLaunchKernelGGL((attn_fwd_gl_kernel<D, 2>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o,
-                         lse, B, H, Hk, S, scale * LOG2E, o_bshd);
       return (int)hipGetLastError();
     }
   }
@@ -2066,15 +1780,8 @@ static int attn_bwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
                          stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);
       dkdv_ds_launch<D, false>(stream, q, k, v, dout, nlse2, delta, dk, dv, ds, B, H, Hk, S, scale, o_bshd, nullptr,
                                nullptr, 0);
-      if (g_bwd_variant >= 17)
-        hipLaunchKernelGGL((attn_bwd_dqg_kernel<D, false, 2>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,
-                           ds, dq, B, H, Hk, S, scale, nullptr, nullptr, 0);
-      else if (g_bwd_variant >= 9)
-        hipLaunchKernelGGL((attn_bwd_dqg_kernel<D, false, 1>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,
-                           ds, dq, B, H, Hk, S, scale, nullptr, nullptr, 0);
-      else
-        hipLaunchKernelGGL((attn_bwd_dqg_kernel<D>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, dq, B,
-                           H, Hk, S, scale, nullptr, nullptr, 0);
+      hipLaunchKernelGGL((attn_bwd_dqg_kernel<D>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, dq, B, H,
+                         Hk, S, scale, nullptr, nullptr, 0);
       return (int)hipGetLastError();
     }
   }
@@ -2153,12 +1860,8 @@ extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t*
                        0, stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);                               \
     dkdv_ds_launch<DD, true>(stream, q, k, v, dout, nlse2, delta, dqkv, dqkv, ds, B, H, Hk, S, scale, o_bshd,  \
                              cosv, sinv, H3);                                                                   \
-    if (g_bwd_variant >= 9)                                                                                     \
-      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true, 1>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k,  \
-                         ds, dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                         \
-    else                                                                                                         \
-      hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \
-                         dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                             \
+    hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \
+                       dqkv, B, H, Hk, S, scale, cosv, sinv, H3);                                               \
   } while (0)
 #ifdef TOA_ATTN_D128_ONLY
   if (D != 128) return (int)hipErrorInvalidValue;

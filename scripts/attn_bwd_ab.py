@@ -4,21 +4,17 @@ rounds on random data (guide §5.4 rules 24/25):
 
     split   dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
-    ds2     ds with the dK/dV step-end wait retiring only the step's LDS-DMA
-            (the dS stores drain under the next step)
-    ds3     ds with s_setprio 1 for the younger half of the dK/dV workgroup
-    ds4     ds2 + ds3
-    ds5..8  ds1..4 with the pipelined sub-tile (LDS fragments read one MFMA
-            pair ahead under counted lgkmcnt waits)
-    ds9..16 ds1..8 with the pipelined dQ GEMM
-    ds17..24 ds1..8 with the dQ GEMM staged by buffer-path DMA (hipcc's schedule)
 
---timing: one extra run per ds form with the dK/dV kernel's s_memtime
+(Round-4 arms measured with this script and since removed -- store-aware
+step-end wait, static priority, pipelined sub-tile, pipelined / buffer-DMA
+dQ GEMM: profiles/r4_attn/.)
+
+--timing: one extra run of the ds form with the dK/dV kernel's s_memtime
 instrumentation (issue vs step-end wait cycles per step, per wave).
 
 Also checks every form agrees with the first.
 
-    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5] [--variants split,ds,ds2] [--timing]
+    python scripts/attn_bwd_ab.py [--rounds 6] [--reps 5] [--variants split,ds] [--timing]
 """
 import argparse
 import json
@@ -57,7 +53,7 @@ def main():
     outs = {}
 
     # backward form: 0 = split (dQ recomputes S / dP), 1 = dS through HBM + dQ GEMM
-    forms = {"split": 0, "ds": 1, **{f"ds{f}": f for f in range(2, 25)}}
+    forms = {"split": 0, "ds": 1}
     variants = a.variants.split(",")
 
     def run(variant):

@@ -4,13 +4,13 @@ on random data (guide §5.4 rules 24/25):
 
     reg  K/V tiles staged through registers + ds_write (attn_fwd_kernel)
     gl   K/V tiles by LDS-DMA into two distinct LDS objects (attn_fwd_gl_kernel)
-    pipe gl with buffer-path DMA and every LDS fragment read one MFMA pair
-         ahead (attn_fwd_gl_kernel<D, 1>)
-    buf  gl with buffer-path DMA, hipcc's own schedule (attn_fwd_gl_kernel<D, 2>)
+(Round 4 measured two more arms and removed them, both slower than gl:
+buffer-path DMA with fragments read one MFMA pair ahead 0.860 vs 0.798 ms,
+buffer-path DMA alone 0.838 vs 0.803 ms, profiles/r4_attn/.)
 
 and the max |difference| of O / lse between them (same arithmetic: 0 expected).
 
-    python scripts/attn_fwd_ab.py [--rounds 6] [--reps 10] [--forms gl,pipe]
+    python scripts/attn_fwd_ab.py [--rounds 6] [--reps 10] [--forms reg,gl]
 """
 import argparse
 import json
@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=6)
-    ap.add_argument("--forms", default="reg,gl,pipe")
+    ap.add_argument("--forms", default="reg,gl")
     a = ap.parse_args()
     B, H, Hk, S, D = a.batch, 32, 8, 4096, 128
     torch.manual_seed(0)
@@ -37,7 +37,7 @@ def main():
     k = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     v = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     P = _lib.ptr
-    forms = {k: v for k, v in {"reg": 0, "gl": 1, "pipe": 2, "buf": 3}.items() if k in a.forms.split(",")}
+    forms = {k: v for k, v in {"reg": 0, "gl": 1}.items() if k in a.forms.split(",")}
     outs = {}
 
     def run(form):

@@ -582,12 +582,10 @@ def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
     do = torch.randn_like(o)
     grads = {}
     try:
-        # 6: the pipelined dK/dV sub-tile with the store-aware step-end wait;
-        # 14: 6 + the pipelined dQ GEMM
-        for form in (0, 1, 6, 14):
+        for form in (0, 1):
             L.call("toa_attn_set_bwd_variant", form)
             nws = L.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D)
-            assert (nws > 0) == (form >= 1)
+            assert (nws > 0) == (form == 1)
             ws = torch.full((nws,), 0xFF, device=DEV, dtype=torch.uint8) if nws else None  # NaN-poisoned
             delta = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
             dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
@@ -598,9 +596,6 @@ def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
     finally:
         L.call("toa_attn_set_bwd_variant", -1)
     (dq0, dk0, dv0, de0), (dq1, dk1, dv1, de1) = grads[0], grads[1]
-    for f in (6, 14):
-        for a, b in zip(grads[f][:3], grads[1][:3]):  # same arithmetic in the same order
-            assert torch.equal(a, b), f
     assert torch.isfinite(dq1.float()).all()
     assert rel(-de1, de0) < 1e-5  # the dS form's delta pass leaves -delta (the dP accumulators' start)
     assert rel(dk1, dk0) < 1e-2 and rel(dv1, dv0) < 1e-2
@@ -615,9 +610,8 @@ def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
 @pytest.mark.parametrize("B,H,Hk,S,D,bshd", [(1, 4, 2, 512, 128, True), (2, 8, 2, 1024, 128, False),
                                               (1, 4, 1, 768, 64, True)])
 def test_flash_attention_fwd_forms_identical(B, H, Hk, S, D, bshd):
-    """The LDS-DMA-staged forward (default at S % 256 == 0), the register-
-    staged one and the pipelined one (buffer-path DMA, fragments read one
-    MFMA pair ahead) run the same arithmetic: O and lse bit-identical."""
+    """The LDS-DMA-staged forward (default at S % 256 == 0) and the
+    register-staged one run the same arithmetic: O and lse bit-identical."""
     L = _lib()
     torch.manual_seed(9)
     q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16)
@@ -625,7 +619,7 @@ def test_flash_attention_fwd_forms_identical(B, H, Hk, S, D, bshd):
     v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
     outs = []
     try:
-        for form in (0, 1, 2):
+        for form in (0, 1):
             L.call("toa_attn_set_fwd_variant", form)
             o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16) if bshd else torch.empty_like(q)
             lse = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
@@ -635,8 +629,7 @@ def test_flash_attention_fwd_forms_identical(B, H, Hk, S, D, bshd):
         torch.cuda.synchronize()
     finally:
         L.call("toa_attn_set_fwd_variant", -1)
-    for f in (1, 2):
-        assert torch.equal(outs[0][0], outs[f][0]) and torch.equal(outs[0][1], outs[f][1]), f
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
 @pytest.mark.parametrize("B,H,Hk,S,D", [(2, 8, 2, 512, 128), (1, 4, 1, 1024, 64), (1, 4, 2, 300, 128)])
