@@ -824,41 +824,6 @@ def test_first_step_gemms_run_on_the_assembly_kernel():
         gemm.set_mode(old)
 
 
-def test_mixed_policy_routes_by_role():
-    """TOA_GEMM=mixed: the assembly kernel takes the fused SwiGLU GEMMs and
-    the data gradients with a reduction >= MIXED_WIDE_K (bit-identical to a
-    direct toa_gemm_asm launch); a plain forward or a narrow data gradient
-    stays on the library."""
-    L = _lib()
-    from tf_operator_amd.ops import gemm
-
-    old = gemm.mode()
-    gemm.set_mode("mixed")
-    try:
-        torch.manual_seed(2)
-        K = gemm.MIXED_WIDE_K
-        dy = torch.randn(256, K, device=DEV, dtype=torch.bfloat16)
-        wt = torch.randn(256, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5  # W^T copy: [out, reduction]
-        w = wt.t().contiguous()
-        w._toa_wt = wt
-        direct = torch.empty(256, 256, device=DEV, dtype=torch.bfloat16)
-        L.call("toa_gemm_asm", L.ptr(dy), K, L.ptr(wt), K, L.ptr(direct), 256, 256, 256, K, L.stream(dy))
-        assert gemm._asm_shape_ok(dy, wt, role="dgrad")
-        dx = gemm.linear_dgrad(dy, w)
-        x = torch.randn(512, 384, device=DEV, dtype=torch.bfloat16)
-        w2 = torch.randn(768, 384, device=DEV, dtype=torch.bfloat16) / 384 ** 0.5
-        assert not gemm._asm_shape_ok(x, w2)  # plain forward: library
-        assert not gemm._asm_shape_ok(x, w2, role="dgrad")  # narrow reduction: library
-        assert gemm._asm_shape_ok(x, w2, role="swiglu")
-        y = gemm.linear_fwd(x, w2)
-        torch.cuda.synchronize()
-        assert torch.equal(dx, direct)
-        assert rel(dx, dy.float() @ w.float()) < 1e-2
-        assert rel(y, x.float() @ w2.float().t()) < 1e-2
-    finally:
-        gemm.set_mode(old)
-
-
 @pytest.mark.parametrize("B,H,Hk,S", [(2, 4, 2, 384), (1, 8, 2, 1024)])
 def test_flash_attention_bshd_output_layout(B, H, Hk, S):
     """O written / dO read as [B, S, H, D] (no transpose copies in the model)

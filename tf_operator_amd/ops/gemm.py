@@ -6,10 +6,8 @@
 
 The forward / data-gradient forms run on the hipBLASLt layer
 (csrc/hip/gemm.hip, one column-major call per form, see there for the
-transposition algebra) or on the hand-written assembly kernel
-(``TOA_GEMM=asm`` / ``mixed``); the weight gradient on the assembly NT kernel
-(csrc/asm/wgrad_gen.py), with the HIP NT kernel (csrc/hip/wgrad.hip) as its
-fallback.
+transposition algebra) or, under ``TOA_GEMM=asm``, on the hand-written
+assembly kernel; the weight gradient on the NT kernel (csrc/hip/wgrad.hip).
 The per-form solution tables measured by ``scripts/tune_gemm.py`` on an
 MI355X are stored next to this file, keyed by the hipBLASLt build.
 
@@ -23,11 +21,6 @@ Modes (``TOA_GEMM``):
   data gradient (``ops.llm.swiglu_mlp``); anything else as ``nosk``.  No
   hipBLASLt table to load, so nothing to prewarm for these forms.
   ``hip`` is an alias (it named the round-3 HIP TN kernel this replaced).
-* ``mixed``: the assembly kernel only where it measured ahead of the
-  library (profiles/r4_asm_gemm/diag4): the fused SwiGLU MLP (gate|up
-  forward with the SwiGLU epilogue, the down projection's data gradient with
-  the SwiGLU backward) and the data gradients with a wide reduction (gate|up
-  and lm_head, N >= 16384); every other form as ``nosk``.
 * ``torch``: torch.matmul, i.e. hipBLASLt's own heuristic.  Per-form
   winners picked in isolation were 2-22 % faster alone, yet the full
   Llama-3-8B step was ~1.3 % SLOWER with them (profiles/r1_gemm_*).
@@ -69,7 +62,7 @@ def mode() -> str:
 def set_mode(m: str):
     """Select the GEMM policy for this process (before the first GEMM)."""
     global _MODE, _installed
-    if m not in ("auto", "torch", "tuned", "nosk", "hip", "asm", "mixed"):
+    if m not in ("auto", "torch", "tuned", "nosk", "hip", "asm"):
         raise ValueError(f"unknown GEMM mode {m!r}")
     _MODE = "asm" if m == "hip" else m
     _installed = False
@@ -101,8 +94,8 @@ def _install():
         return
     _installed = True
     if _lib.has("toa_gemm_set_no_streamk"):
-        _lib.call("toa_gemm_set_no_streamk", int(_MODE in ("nosk", "asm", "mixed")))
-    table = TABLE_NOSK if _MODE in ("nosk", "asm", "mixed") else TABLE
+        _lib.call("toa_gemm_set_no_streamk", int(_MODE in ("nosk", "asm")))
+    table = TABLE_NOSK if _MODE in ("nosk", "asm") else TABLE
     if not os.path.exists(table):
         return
     with open(table) as f:
@@ -128,7 +121,7 @@ def prewarm(device=None, background: bool = True):
     thread is returned (the GEMM layer's lock orders the first real GEMM
     after it).  Idempotent; None when the policy uses no table."""
     global _prewarm_thread, _prewarm_dev
-    if _MODE not in ("tuned", "nosk", "mixed") or not _lib.has("toa_gemm_prewarm"):
+    if _MODE not in ("tuned", "nosk") or not _lib.has("toa_gemm_prewarm"):
         return None
     dev = None if device is None else torch.device(device).index
     dev = torch.cuda.current_device() if dev is None else dev
@@ -186,7 +179,7 @@ def prewarm_early():
 
 
 def _ok(*ts):
-    if _MODE not in ("tuned", "nosk", "asm", "mixed") or not _lib.has("toa_gemm"):
+    if _MODE not in ("tuned", "nosk", "asm") or not _lib.has("toa_gemm"):
         return False
     for t in ts:
         if not (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1):
@@ -214,7 +207,7 @@ class first_step:
     the policy)."""
 
     def __init__(self, on: bool = True):
-        self.on = bool(on) and _MODE in ("nosk", "tuned", "mixed") and _lib.has("toa_gemm_asm")
+        self.on = bool(on) and _MODE in ("nosk", "tuned") and _lib.has("toa_gemm_asm")
 
     def __enter__(self):
         global _asm_first
@@ -227,24 +220,12 @@ class first_step:
         return False
 
 
-# ``mixed``: the data gradients the assembly kernel takes from the library
-# are the ones with a reduction at least this wide (gate|up 28672, lm_head
-# 128256; the attention / down-projection forms reduce over 4096-14336)
-MIXED_WIDE_K = 16384
-
-
-def _asm_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256, role: str = "") -> bool:
+def _asm_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> bool:
     """Operands the assembly GEMM takes (csrc/hip/gemm_asm.hip checks the
     same and refuses anything else): bf16 GPU rows with unit column stride,
     16-byte aligned rows, M and N multiples of 256 (n_mult), K a multiple of
-    64 and >= 128.  role: "swiglu" (the fused MLP GEMMs) or "dgrad" (a data
-    gradient), for the ``mixed`` policy."""
-    if not _lib.has("toa_gemm_asm"):
-        return False
-    if _MODE == "mixed" and not _asm_first:
-        if not (role == "swiglu" or (role == "dgrad" and x2.shape[1] >= MIXED_WIDE_K)):
-            return False
-    elif not (_MODE == "asm" or _asm_first):
+    64 and >= 128."""
+    if not (_MODE == "asm" or _asm_first) or not _lib.has("toa_gemm_asm"):
         return False
     if not (x2.is_cuda and x2.dtype == w.dtype == torch.bfloat16 and x2.dim() == 2 and w.dim() == 2):
         return False
@@ -256,8 +237,8 @@ def _asm_shape_ok(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256, role: st
             and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and _lib.use_hip(x2))
 
 
-def linear_fwd(x2: torch.Tensor, w: torch.Tensor, role: str = "") -> torch.Tensor:
-    if _asm_shape_ok(x2, w, role=role):
+def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if _asm_shape_ok(x2, w):
         M, N = x2.shape[0], w.shape[0]
         y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
         _lib.call("toa_gemm_asm", _lib.ptr(x2), x2.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), N, M, N,
@@ -275,7 +256,7 @@ def linear_fwd(x2: torch.Tensor, w: torch.Tensor, role: str = "") -> torch.Tenso
 def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     wt = getattr(w, "_toa_wt", None)
     if wt is not None:  # W^T kept by ops.wt.TransposedWeights: dx = dy (W^T)^T, the forward's form
-        return linear_fwd(dy2, wt, role="dgrad")
+        return linear_fwd(dy2, wt)
     if not _ok(dy2, w):
         return torch.matmul(dy2, w)
     M, N = dy2.shape
@@ -288,7 +269,7 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 def swiglu_gate_up(x2: torch.Tensor, wgu: torch.Tensor):
     """(gu, s) = (x Wgu^T, silu(gate) * up) from ONE assembly GEMM with the
     SwiGLU in its epilogue; None when the kernel cannot take the shapes."""
-    if not (_asm_shape_ok(x2, wgu, n_mult=2, role="swiglu") and (wgu.shape[0] // 2) % 128 == 0):
+    if not (_asm_shape_ok(x2, wgu, n_mult=2) and (wgu.shape[0] // 2) % 128 == 0):
         return None
     M, F = x2.shape[0], wgu.shape[0] // 2
     gu = torch.empty(M, 2 * F, device=x2.device, dtype=x2.dtype)
@@ -303,7 +284,7 @@ def swiglu_down_dgrad(d2: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor):
     transposed weight copy (ops/wt.py) with the SwiGLU backward in its
     epilogue (ds is never stored); None when the kernel cannot take it."""
     wdt = getattr(wd, "_toa_wt", None)
-    if wdt is None or not (_asm_shape_ok(d2, wdt, role="swiglu") and gu.is_contiguous() and gu.shape[1] == 2 * wdt.shape[0]
+    if wdt is None or not (_asm_shape_ok(d2, wdt) and gu.is_contiguous() and gu.shape[1] == 2 * wdt.shape[0]
                            and gu.data_ptr() % 16 == 0):
         return None
     M, F = d2.shape[0], wdt.shape[0]

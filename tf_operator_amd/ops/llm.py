@@ -196,9 +196,9 @@ class _SwiGLUMLP(torch.autograd.Function):
 
 def swiglu_mlp(x, wgu, wd):
     """The Llama MLP, x -> swiglu(x Wgu^T) Wd^T, fused where the assembly
-    GEMM takes the shapes (TOA_GEMM=asm / mixed), else the two-GEMM +
+    GEMM takes the shapes (TOA_GEMM=asm, the default), else the two-GEMM +
     SwiGLU path."""
-    if gemm.mode() in ("asm", "mixed"):
+    if gemm.mode() == "asm":
         return _SwiGLUMLP.apply(x, wgu, wd)
     from .linear import linear
 
