@@ -1523,18 +1523,22 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       dp = mfma32(ov[s & 1][0], ov[s & 1][1], dp);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // P and dS on register pairs (v_pk_fma_f32 / v_pk_mul_f32: the same
+    // per-element operations as the scalar forms, half the issue slots)
     uint32_t pw[8], sw[8];
+    const f32x2 c2 = {scale_log2, scale_log2};
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
-      float p0 = EXP2(fmaf(sc[j], scale_log2, l4[j >> 2][j & 3]));
-      float p1 = EXP2(fmaf(sc[j + 1], scale_log2, l4[j >> 2][(j + 1) & 3]));
+      const f32x2 x = pk_fma(f32x2{sc[j], sc[j + 1]}, c2, f32x2{l4[j >> 2][j & 3], l4[j >> 2][(j + 1) & 3]});
+      f32x2 p = {EXP2(x[0]), EXP2(x[1])};
       if (mask) {
         const int q = qs + (j & 3) + 8 * (j >> 2) + 4 * hh;
-        if (q < mykey) p0 = 0.f;
-        if (q + 1 < mykey) p1 = 0.f;
+        if (q < mykey) p[0] = 0.f;
+        if (q + 1 < mykey) p[1] = 0.f;
       }
-      pw[j >> 1] = pack2(p0, p1);
-      sw[j >> 1] = pack2(p0 * dp[j], p1 * dp[j + 1]);
+      pw[j >> 1] = pack2(p[0], p[1]);
+      const f32x2 d = p * f32x2{dp[j], dp[j + 1]};
+      sw[j >> 1] = pack2(d[0], d[1]);
     }
     // dV^T / dK^T: 8 (s2, dt) pairs of MFMAs, the transposed reads one pair ahead
     bf16x4 ft[2][4];
