@@ -378,7 +378,10 @@ def epilogue(a: Asm):
     a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")             # 16 rows
     a(f"s_mov_b32 {sr(S_E0)}, 0")
     for i in range(8):
-        f, pk, old = V_E + 8, V_E + 40, V_E + 72
+        # pk alternates between two register sets and nothing waits for the
+        # stores (the TN epilogue re-uses its store registers at once: the
+        # data is read at issue); a row block's stores drain under the next
+        f, pk, old = V_E + 8, V_E + 40 + 16 * (i & 1), V_E + 72
         for j in range(8):
             G.read_acc4(a, f + 4 * j, 4 * (8 * i + j))
         a(f"s_cmp_eq_u32 {sr(S_BETA)}, 0")
@@ -395,19 +398,17 @@ def epilogue(a: Asm):
             G.cvt_pack(a, pk + 2 * j, f + 4 * j)
         for j in range(8):
             a(f"buffer_store_dwordx2 {vr(pk + 2 * j, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * j}")
-        a("s_waitcnt vmcnt(0)")                              # pk / old reused by the next row block
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
     a(f"s_branch {l_end}")
     # --- fp32 partials into the workspace tile (256 x 256 x 4 B, row-major)
     a.label(l_piece)
     a(f"s_mov_b32 {sr(S_E0)}, 0")
     for i in range(8):
-        f = V_E + 8
+        f = V_E + 8 + 32 * (i & 1)                           # two sets, as pk above
         for j in range(8):
             G.read_acc4(a, f + 4 * j, 4 * (8 * i + j))
         for j in range(8):
             a(f"buffer_store_dwordx4 {vr(f + 4 * j, 4)}, {vr(V_E + 1)}, {sr(SRD_WS, 4)}, {sr(S_E0)} offen offset:{64 * j}")
-        a("s_waitcnt vmcnt(0)")
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {16 * 1024}")
     a.label(l_end)
 
