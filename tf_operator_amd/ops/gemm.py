@@ -7,7 +7,9 @@
 The forward / data-gradient forms run on the hipBLASLt layer
 (csrc/hip/gemm.hip, one column-major call per form, see there for the
 transposition algebra) or, under ``TOA_GEMM=asm``, on the hand-written
-assembly kernel; the weight gradient on the NT kernel (csrc/hip/wgrad.hip).
+assembly kernel; the weight gradient on the assembly NT kernel
+(csrc/asm/wgrad_gen.py), with the HIP NT kernel (csrc/hip/wgrad.hip) as its
+fallback.
 The per-form solution tables measured by ``scripts/tune_gemm.py`` on an
 MI355X are stored next to this file, keyed by the hipBLASLt build.
 
@@ -71,8 +73,10 @@ def set_mode(m: str):
 def resolve_auto(world: int = 1) -> str:
     """``auto`` -> ``nosk`` (an explicit TOA_GEMM is kept).  Returns the mode
     in force.  ``asm`` stays opt-in until it wins in-model: the Llama-3-8B
-    step measured 1010.7 / 1014.8 ms on it against 977.2 / 978.4 ms on
-    ``nosk``, alternating on one box (profiles/r4_asm_gemm/ab1)."""
+    step measured 946.3 ms on it against 930.1 ms on ``nosk`` (one process,
+    alternating windows, profiles/r4_wgrad/inmodel_ab.log), and a policy
+    using it only for the forms it wins in isolation 940.7 vs 936.7 ms
+    (profiles/r4_mixed/inmodel_ab.log)."""
     del world
     if _MODE == "auto":
         set_mode("nosk")
