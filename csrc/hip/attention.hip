@@ -1524,11 +1524,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
     // P and dS on register pairs (v_pk_fma_f32 / v_pk_mul_f32: the same
-    // per-element operations as the scalar forms, half the issue slots)
+    // per-element operations as the scalar forms, half the issue slots).
+    // Elements 0-7 (the first 16-query half, s2 = 0) here; 8-15 between the
+    // s2 = 0 MFMAs below, whose issue they overlap.
     uint32_t pw[8], sw[8];
     const f32x2 c2 = {scale_log2, scale_log2};
-#pragma unroll
-    for (int j = 0; j < 16; j += 2) {
+    auto expair = [&](int j) {
       const f32x2 x = pk_fma(f32x2{sc[j], sc[j + 1]}, c2, f32x2{l4[j >> 2][j & 3], l4[j >> 2][(j + 1) & 3]});
       f32x2 p = {EXP2(x[0]), EXP2(x[1])};
       if (mask) {
@@ -1539,7 +1540,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       pw[j >> 1] = pack2(p[0], p[1]);
       const f32x2 d = p * f32x2{dp[j], dp[j + 1]};
       sw[j >> 1] = pack2(d[0], d[1]);
-    }
+    };
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) expair(j);
     // dV^T / dK^T: 8 (s2, dt) pairs of MFMAs, the transposed reads one pair ahead
     bf16x4 ft[2][4];
     auto ldt = [&](int i, bf16x4(&f)[4]) {
@@ -1566,6 +1569,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       const bf16x4* f = ft[i & 1];
       dv[dt] = mfma32((bf16x8)__builtin_shufflevector(f[0], f[1], 0, 1, 2, 3, 4, 5, 6, 7), as_bf16x8(a), dv[dt]);
       dk[dt] = mfma32((bf16x8)__builtin_shufflevector(f[2], f[3], 0, 1, 2, 3, 4, 5, 6, 7), as_bf16x8(c), dk[dt]);
+      if (i < ND) {  // elements 8-15, 4 / ND pairs under each s2 = 0 MFMA pair
+#pragma unroll
+        for (int e = 0; e < 4 / ND; ++e) expair(8 + 2 * (i * (4 / ND) + e));
+      }
       __builtin_amdgcn_sched_barrier(0);
       if (i == ND - 1) {  // dS chunks (as in `subtile`), draining under the second half
 #pragma unroll
