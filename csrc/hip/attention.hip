@@ -1346,7 +1346,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dqg_kernel(const bf16_t* __re
 // delta pass's -lse log2(e) / -delta rows.  S % 256 == 0 only (no ragged
 // tiles).  TIMED: per wave, s_memtime sums of issue time and step-end wait
 // time (scripts/attn_bwd_ab.py --timing).
-template <int D, bool ROPE = false, bool TIMED = false, bool EXPO = false>
+template <int D, bool ROPE = false, bool TIMED = false>
 __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
@@ -1524,9 +1524,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
     // P and dS (scalar VALU: a register-pair form measured 3 % slower per
-    // step, profiles/r4_attn/r4_batch).  EXPO: elements 0-7 (the first
-    // 16-query half, s2 = 0) here and 8-15 between the s2 = 0 MFMAs below,
-    // whose issue they overlap; else all 16 here.
+    // step, profiles/r4_attn/r4_batch): elements 0-7 (the first 16-query
+    // half, s2 = 0) here, 8-15 between the s2 = 0 MFMAs below, whose issue
+    // they overlap (1.2 % fewer cycles per step, profiles/r4_attn/r4_attn6).
     uint32_t pw[8], sw[8];
     auto expair = [&](int j) {
       float p0 = EXP2(fmaf(sc[j], scale_log2, l4[j >> 2][j & 3]));
@@ -1540,7 +1540,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       sw[j >> 1] = pack2(p0 * dp[j], p1 * dp[j + 1]);
     };
 #pragma unroll
-    for (int j = 0; j < (EXPO ? 8 : 16); j += 2) expair(j);
+    for (int j = 0; j < 8; j += 2) expair(j);
     // dV^T / dK^T: 8 (s2, dt) pairs of MFMAs, the transposed reads one pair ahead
     bf16x4 ft[2][4];
     auto ldt = [&](int i, bf16x4(&f)[4]) {
@@ -1567,7 +1567,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_dkdv_ds_kernel(
       const bf16x4* f = ft[i & 1];
       dv[dt] = mfma32((bf16x8)__builtin_shufflevector(f[0], f[1], 0, 1, 2, 3, 4, 5, 6, 7), as_bf16x8(a), dv[dt]);
       dk[dt] = mfma32((bf16x8)__builtin_shufflevector(f[2], f[3], 0, 1, 2, 3, 4, 5, 6, 7), as_bf16x8(c), dk[dt]);
-      if (EXPO && i < ND) {  // elements 8-15, 4 / ND pairs under each s2 = 0 MFMA pair
+      if (i < ND) {  // elements 8-15, 4 / ND pairs under each s2 = 0 MFMA pair
 #pragma unroll
         for (int e = 0; e < 4 / ND; ++e) expair(8 + 2 * (i * (4 / ND) + e));
       }
@@ -1693,7 +1693,7 @@ static int attn_bwd_variant() {
   return g_bwd_variant;
 }
 extern "C" int toa_attn_set_bwd_variant(int v) {
-  if (v < -1 || v > 2) return (int)hipErrorInvalidValue;
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
   g_bwd_variant = v;
   return 0;
 }
@@ -1710,16 +1710,12 @@ static void dkdv_ds_launch(hipStream_t stream, const bf16_t* q, const bf16_t* k,
                            const float* nlse2, const float* delta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B, int H,
                            int Hk, int S, float scale, int o_bshd, const float* cosv, const float* sinv, int H3) {
   const dim3 grid((S / 128) * B * Hk), block(512);
-#define TOA_DKDV(TT, EE)                                                                                          \
-  hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE, TT, EE>), grid, block, 0, stream, q, k, v, dout, nlse2,      \
-                     delta, dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, cosv, sinv, H3, g_attn_tstat)
-  const bool expo = g_bwd_variant == 2;
-  if (g_attn_tstat) {
-    if (expo) TOA_DKDV(true, true); else TOA_DKDV(true, false);
-  } else {
-    if (expo) TOA_DKDV(false, true); else TOA_DKDV(false, false);
-  }
-#undef TOA_DKDV
+  if (g_attn_tstat)
+    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE, true>), grid, block, 0, stream, q, k, v, dout, nlse2, delta,
+                       dk, dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, cosv, sinv, H3, g_attn_tstat);
+  else
+    hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE>), grid, block, 0, stream, q, k, v, dout, nlse2, delta, dk,
+                       dv, ds, B, H, Hk, S, scale, scale * LOG2E, o_bshd, cosv, sinv, H3, nullptr);
 }
 static bool attn_bwd_uses_ds(int S) { return attn_bwd_variant() >= 1 && S % FWD_QB == 0; }
 // [dS blocks][-lse log2e rows]; the -delta rows go to the caller's delta buffer

@@ -4,12 +4,11 @@ rounds on random data (guide §5.4 rules 24/25):
 
     split   dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
-    ds_expo ds with the second half of P / dS computed between the first
-            half's dV / dK MFMAs (A/B arm)
 
 (Round-4 arms measured with this script and since removed -- store-aware
 step-end wait, static priority, pipelined sub-tile, pipelined / buffer-DMA
-dQ GEMM: profiles/r4_attn/.)
+dQ GEMM, register-pair P / dS, P / dS overlapped with the first half's
+MFMAs (kept): profiles/r4_attn/.)
 
 --timing: one extra run of the ds form with the dK/dV kernel's s_memtime
 instrumentation (issue vs step-end wait cycles per step, per wave).
@@ -55,7 +54,7 @@ def main():
     outs = {}
 
     # backward form: 0 = split (dQ recomputes S / dP), 1 = dS through HBM + dQ GEMM
-    forms = {"split": 0, "ds": 1, "ds_expo": 2}
+    forms = {"split": 0, "ds": 1}
     variants = a.variants.split(",")
 
     def run(variant):
