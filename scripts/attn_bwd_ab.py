@@ -5,10 +5,10 @@ rounds on random data (guide §5.4 rules 24/25):
     split   dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
 
-(Round-4 arms measured with this script and since removed -- store-aware
-step-end wait, static priority, pipelined sub-tile, pipelined / buffer-DMA
-dQ GEMM, register-pair P / dS, P / dS overlapped with the first half's
-MFMAs (kept): profiles/r4_attn/.)
+(Round-4 arms measured with this script, profiles/r4_attn/: kept -- the
+pipelined sub-tile, the store-aware step-end wait, P / dS overlapped with the
+first half's MFMAs; removed -- static priority, pipelined or buffer-DMA dQ
+GEMM, register-pair P / dS.)
 
 --timing: one extra run of the ds form with the dK/dV kernel's s_memtime
 instrumentation (issue vs step-end wait cycles per step, per wave).
