@@ -411,11 +411,7 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_kernel(const bf16_t* __restri
 // body as attn_fwd_kernel, the K / V tiles brought in by global_load_lds
 // into two distinct LDS objects instead of register staging + ds_write
 // (the change that took the dK/dV kernel from 2.19 to 1.97 ms).
-// VAR (A/B arms): bit 0 tiles by buffer-path DMA (counted lgkmcnt), bit 1 S
-// with K fragments read one MFMA pair ahead (the two chains interleaved),
-// bit 2 the PV MFMAs of the first 32 keys issued between the exponentials of
-// the second 32.  Same arithmetic in the same order in every arm.
-template <int D, int VAR = 0>
+template <int D>
 __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
                                                           const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
                                                           float* __restrict__ LSE, int B, int H, int Hk, int S,
@@ -479,16 +475,6 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __res
   auto stage = [&](int t, int buf) {
     char* st = buf ? kv1 : kv0;
     const bf16_t* base = (wave < 4 ? K : V) + koff + (int64_t)t * TK * D;
-    if constexpr ((VAR & 1) != 0) {
-      const auto rs = buf_rsrc(base);
-#pragma unroll
-      for (int u = 0; u < PW; ++u) {
-        const int pt = PW * (wave & 3) + u;
-        const int col = wave < 4 ? (D == 128 ? kcol ^ ((4 * (pt & 3)) << 3) : kcol) : vcol;
-        BUF_DMA(16, rs, (uint32_t)((RPP * pt + lkey) * D + col) * 2, st + (wave < 4 ? 0 : TILEB) + pt * 1024);
-      }
-      return;
-    }
     if (wave < 4) {
 #pragma unroll
       for (int u = 0; u < PW; ++u) {
@@ -514,32 +500,13 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __res
     const char* vb = kb + TILEB;
     // ---- S^T = K Q^T : two 32-key halves (first MFMA of each chain starts from 0)
     f32x16 sc[2];
-    if constexpr ((VAR & 2) != 0) {
-      sc[0] = f32x16{};
-      sc[1] = f32x16{};
-      bf16x8 kf[2][2];
-      auto ldk = [&](int s, bf16x8(&f)[2]) {
-        f[0] = as_bf16x8(*(const u32x4*)(kb + kro[s]));
-        f[1] = as_bf16x8(*(const u32x4*)(kb + kro[s] + 32 * ROWB));
-      };
-      ldk(0, kf[0]);
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        if (s + 1 < NS) ldk(s + 1, kf[(s + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        sc[0] = mfma32(kf[s & 1][0], qf[s], sc[0]);
-        sc[1] = mfma32(kf[s & 1][1], qf[s], sc[1]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
+    for (int n = 0; n < 2; ++n) {
+      const f32x16 z = {};
+      sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[0] + 32 * ROWB * n)), qf[0], z);
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const f32x16 z = {};
-        sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[0] + 32 * ROWB * n)), qf[0], z);
-#pragma unroll
-        for (int s = 1; s < NS; ++s)
-          sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[s] + 32 * ROWB * n)), qf[s], sc[n]);
-      }
+      for (int s = 1; s < NS; ++s)
+        sc[n] = mfma32(as_bf16x8(*(const u32x4*)(kb + kro[s] + 32 * ROWB * n)), qf[s], sc[n]);
     }
     // ---- causal mask (diagonal tile only) and row max of the raw scores
     if (mask) {
@@ -568,50 +535,20 @@ __global__ __launch_bounds__(512, 1) void attn_fwd_gl_kernel(const bf16_t* __res
     f32x2 ls;
     const f32x2 c2 = {scale_log2, scale_log2}, nm2 = {-m_run, -m_run};
     uint32_t pw[2][8];
-    auto expair = [&](int n, int j) {
-      f32x2 x = pk_fma(f32x2{sc[n][j], sc[n][j + 1]}, c2, nm2);
-      x[0] = EXP2(x[0]);
-      x[1] = EXP2(x[1]);
-      ls = (n == 0 && j == 0) ? x : ls + x;
-      pw[n][j >> 1] = cvt_pk(x[0], x[1]);
-    };
-    if constexpr ((VAR & 4) != 0) {
-      // P of the first 32 keys, then its 2 x ND PV MFMAs with the second 32
-      // keys' exponentials between them (8 / (2 ND) pairs each)
 #pragma unroll
-      for (int j = 0; j < 16; j += 2) expair(0, j);
-      constexpr int PER = 8 / (2 * ND);
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        u32x4 w;
-        w[0] = pw[0][4 * s + 0];
-        w[1] = pw[0][4 * s + 1];
-        w[2] = pw[0][4 * s + 2];
-        w[3] = pw[0][4 * s + 3];
-        const bf16x8 pf = as_bf16x8(w);
-        const int kb0 = (16 * s) * ROWB;
-#pragma unroll
-        for (int dt = 0; dt < ND; ++dt) {
-          const bf16x4 va = tr_read(vb, vro[dt] + kb0);
-          const bf16x4 vbv = tr_read(vb, vro[dt] + kb0 + 8 * ROWB);
-#pragma unroll
-          for (int e = 0; e < PER; ++e) expair(1, 2 * ((s * ND + dt) * PER + e));
-          __builtin_amdgcn_sched_barrier(0);
-          acc[dt] = mfma32(__builtin_shufflevector(va, vbv, 0, 1, 2, 3, 4, 5, 6, 7), pf, acc[dt]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      for (int j = 0; j < 16; j += 2) {
+        f32x2 x = pk_fma(f32x2{sc[n][j], sc[n][j + 1]}, c2, nm2);
+        x[0] = EXP2(x[0]);
+        x[1] = EXP2(x[1]);
+        ls = (n == 0 && j == 0) ? x : ls + x;
+        pw[n][j >> 1] = cvt_pk(x[0], x[1]);
       }
-      l_run += ls[0] + ls[1];
-    } else {
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int j = 0; j < 16; j += 2) expair(n, j);
-      l_run += ls[0] + ls[1];
-    }
+    l_run += ls[0] + ls[1];
     // ---- O^T += V^T P^T (k permutation of the accumulator handled by the V^T read order)
 #pragma unroll
-    for (int n = ((VAR & 4) != 0 ? 1 : 0); n < 2; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         u32x4 w;
@@ -1815,7 +1752,7 @@ static void attn_set_lds_limits() {
 static int g_fwd_variant = 1;
 static int attn_fwd_variant() { return g_fwd_variant; }
 extern "C" int toa_attn_set_fwd_variant(int v) {
-  if (v < -1 || v > 8) return (int)hipErrorInvalidValue;
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
   g_fwd_variant = v < 0 ? 1 : v;
   return 0;
 }
@@ -1826,20 +1763,9 @@ static int attn_fwd_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf
   attn_set_lds_limits<D, TAIL>();
   const int nqb = (S + FWD_QB - 1) / FWD_QB;
   if constexpr (!TAIL) {
-    const int fv = attn_fwd_variant();
-    if (fv >= 1) {
-#define TOA_FWD_GL(VV)                                                                                              \
-  hipLaunchKernelGGL((attn_fwd_gl_kernel<D, VV>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o, lse, \
-                     B, H, Hk, S, scale * LOG2E, o_bshd)
-      switch (fv - 1) {
-        case 2: TOA_FWD_GL(2); break;
-        case 3: TOA_FWD_GL(3); break;
-        case 4: TOA_FWD_GL(4); break;
-        case 5: TOA_FWD_GL(5); break;
-        case 7: TOA_FWD_GL(7); break;
-        default: TOA_FWD_GL(0); break;
-      }
-#undef TOA_FWD_GL
+    if (attn_fwd_variant() == 1) {
+      hipLaunchKernelGGL((attn_fwd_gl_kernel<D>), dim3(nqb * H * B), dim3(64 * FWD_WAVES), 0, stream, q, k, v, o, lse,
+                         B, H, Hk, S, scale * LOG2E, o_bshd);
       return (int)hipGetLastError();
     }
   }

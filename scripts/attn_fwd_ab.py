@@ -4,13 +4,6 @@ on random data (guide §5.4 rules 24/25):
 
     reg  K/V tiles staged through registers + ds_write (attn_fwd_kernel)
     gl   K/V tiles by LDS-DMA into two distinct LDS objects (attn_fwd_gl_kernel)
-Round-4 A/B arms of the LDS-DMA kernel (attn_fwd_gl_kernel<D, VAR>):
-    s_pipe   K fragments read one MFMA pair ahead, the two S chains interleaved
-    buf_s    s_pipe with buffer-path DMA (counted lgkmcnt waits)
-    expo     the first 32 keys' PV MFMAs between the second 32's exponentials
-    buf_expo expo with buffer-path DMA
-    all      buffer-path DMA + s_pipe + expo
-
 (Round 4 measured two more arms and removed them, both slower than gl:
 buffer-path DMA with fragments read one MFMA pair ahead 0.860 vs 0.798 ms,
 buffer-path DMA alone 0.838 vs 0.803 ms, profiles/r4_attn/.)
@@ -44,8 +37,7 @@ def main():
     k = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     v = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     P = _lib.ptr
-    arms = {"reg": 0, "gl": 1, "s_pipe": 3, "buf_s": 4, "expo": 5, "buf_expo": 6, "all": 8}
-    forms = {k: arms[k] for k in a.forms.split(",")}
+    forms = {k: v for k, v in {"reg": 0, "gl": 1}.items() if k in a.forms.split(",")}
     outs = {}
 
     def run(form):
