@@ -4,9 +4,13 @@ on random data (guide §5.4 rules 24/25):
 
     reg  K/V tiles staged through registers + ds_write (attn_fwd_kernel)
     gl   K/V tiles by LDS-DMA into two distinct LDS objects (attn_fwd_gl_kernel)
-(Round 4 measured two more arms and removed them, both slower than gl:
-buffer-path DMA with fragments read one MFMA pair ahead 0.860 vs 0.798 ms,
-buffer-path DMA alone 0.838 vs 0.803 ms, profiles/r4_attn/.)
+(Round 4 measured more arms of the LDS-DMA kernel and removed them, all
+slower than gl and bit-identical to it, profiles/r4_attn/: buffer-path DMA
+with fragments read one MFMA pair ahead 0.860 vs 0.798 ms, buffer-path DMA
+alone 0.838 vs 0.803 ms; then against gl's 0.805 ms (r4_fwd): K fragments
+one pair ahead 0.815, the same with buffer-path DMA 0.833, the first 32 keys'
+PV MFMAs between the second 32's exponentials 0.838, that with buffer-path
+DMA 0.894, all three 0.876.)
 
 and the max |difference| of O / lse between them (same arithmetic: 0 expected).
 
