@@ -5,6 +5,11 @@ a warm-up, random operands.
 
     rocprofv3 --pmc ... -- python3 scripts/probes/asm_pmc.py
     python scripts/pmc_summary.py <out> toa_gemm_tn_asm Cijk
+
+ASM_PMC_ORDER=interleave alternates the two kernels call by call (same
+thermal state for both); ASM_PMC_WGRAD=1 measures the weight-gradient form
+instead: the assembly NT kernel (toa_wgrad_nt_asm) against the HIP one
+(wgrad_nt_kernel) at dW[N, K] = dY^T X over T tokens.
 """
 import os
 import sys
@@ -27,14 +32,36 @@ def main():
     def asm():
         _lib.call("toa_gemm_asm", _lib.ptr(x), K, _lib.ptr(w), K, _lib.ptr(y), N, T, N, K, _lib.stream(x))
 
+    def other():
+        gemm.linear_fwd(x, w)
+
+    if os.environ.get("ASM_PMC_WGRAD") == "1":
+        dy = (torch.rand(T, N, device="cuda") - 0.5).to(torch.bfloat16)
+        g = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+        ws = torch.empty(max(int(_lib.call_ret("toa_wgrad_workspace", N, K, T, 0)), 16) // 4, device="cuda",
+                         dtype=torch.float32)
+
+        def asm():  # noqa: F811
+            _lib.call("toa_wgrad_asm", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g), K, _lib.ptr(ws), N, K, T, 0, 0,
+                      _lib.stream(dy))
+
+        def other():  # noqa: F811
+            _lib.call("toa_wgrad", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g), K, _lib.ptr(ws), N, K, T, 0, 0,
+                      _lib.stream(dy))
+
     for _ in range(2):
         asm()
-        gemm.linear_fwd(x, w)
+        other()
     torch.cuda.synchronize()
-    for _ in range(5):
-        asm()
-    for _ in range(5):
-        gemm.linear_fwd(x, w)
+    if os.environ.get("ASM_PMC_ORDER") == "interleave":
+        for _ in range(5):
+            asm()
+            other()
+    else:
+        for _ in range(5):
+            asm()
+        for _ in range(5):
+            other()
     torch.cuda.synchronize()
     print("ok", flush=True)
 
