@@ -258,6 +258,18 @@ def wgrad(a):
                       _lib.stream(dy))
 
         arms = [("asm", asm_), ("hip", hip), ("blt", lambda: torch.mm(dy.t(), x))]
+        for sp in (int(v) for v in a.wgrad_splits.split(",") if v):
+            # every tile cut into `sp` K-pieces (1: none) instead of the auto plan
+            if sp * (N // 256) * (K // 256) >= (1 << 14) or T % (64 * sp):
+                continue
+            need = int(_lib.call_ret("toa_wgrad_workspace", N, K, T, sp))
+            wsp = torch.empty(max(need, 16) // 4, device="cuda", dtype=torch.float32)
+
+            def forced(sp=sp, wsp=wsp):
+                _lib.call("toa_wgrad_asm", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g2), K, _lib.ptr(wsp), N, K, T,
+                          sp, 0, _lib.stream(dy))
+
+            arms.append((f"asm_split{sp}", forced))
         ts = {k: [] for k, _ in arms}
         for _ in range(a.rounds):
             for k, f in arms:
@@ -359,6 +371,7 @@ def main():
     ap.add_argument("--variants", default="", help="plain-kernel A/B arms to add, e.g. 1,2,3")
     ap.add_argument("--timing", action="store_true", help="wait-cycle breakdown of the product kernel (--forms)")
     ap.add_argument("--wgrad", action="store_true", help="weight-gradient forms: asm NT vs HIP vs hipBLASLt")
+    ap.add_argument("--wgrad-splits", default="", help="extra asm arms with every tile cut into S K-pieces, e.g. 1,2,3")
     a = ap.parse_args()
     if a.probe:
         probe()
