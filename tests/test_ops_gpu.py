@@ -607,6 +607,47 @@ def test_flash_attention_bwd_ds_form(B, H, Hk, S, D, bshd):
         assert rel(got, ref) < 3e-2, rel(got, ref)
 
 
+def test_attention_bwd_timing_instrumentation():
+    """toa_attn_set_bwd_timing: the dS-form dK/dV kernel's s_memtime
+    instrumentation (scripts/attn_bwd_ab.py --timing) runs, writes one
+    {issue, wait, steps, 0} record per wave, and leaves the gradients
+    bit-identical to the uninstrumented kernel."""
+    L = _lib()
+    torch.manual_seed(3)
+    B, H, Hk, S, D = 1, 4, 2, 512, 128
+    scale = 1.0 / math.sqrt(D)
+    q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    o = torch.empty(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
+    P = L.ptr
+    L.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, 3, scale, L.stream(q))
+    do = torch.randn_like(o)
+    nws = L.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D)
+    assert nws > 0
+    nblk = (S // 128) * B * Hk
+    ts = torch.zeros(nblk * 8 * 4, device=DEV, dtype=torch.int64)
+    outs = []
+    for timed in (False, True):
+        ws = torch.empty(nws, device=DEV, dtype=torch.uint8)
+        delta = torch.empty(B, H, S, device=DEV, dtype=torch.float32)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        L.call("toa_attn_set_bwd_timing", P(ts) if timed else None)
+        try:
+            L.call("toa_attn_bwd", P(q), P(k), P(v), P(o), P(do), P(lse), P(delta), P(ws), P(dq), P(dk), P(dv),
+                   B, H, Hk, S, D, 3, scale, L.stream(q))
+            torch.cuda.synchronize()
+        finally:
+            L.call("toa_attn_set_bwd_timing", None)
+        outs.append((dq, dk, dv))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    t = ts.view(nblk, 8, 4).cpu()
+    assert (t[..., 2] > 0).all()  # every wave records its step count
+    assert (t[..., 0] > 0).all() and (t[..., 3] == 0).all()
+
+
 @pytest.mark.parametrize("B,H,Hk,S,D,bshd", [(1, 4, 2, 512, 128, True), (2, 8, 2, 1024, 128, False),
                                               (1, 4, 1, 768, 64, True)])
 def test_flash_attention_fwd_forms_identical(B, H, Hk, S, D, bshd):
