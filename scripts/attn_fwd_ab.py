@@ -10,7 +10,12 @@ with fragments read one MFMA pair ahead 0.860 vs 0.798 ms, buffer-path DMA
 alone 0.838 vs 0.803 ms; then against gl's 0.805 ms (r4_fwd): K fragments
 one pair ahead 0.815, the same with buffer-path DMA 0.833, the first 32 keys'
 PV MFMAs between the second 32's exponentials 0.838, that with buffer-path
-DMA 0.894, all three 0.876.)
+DMA 0.894, all three 0.876.  Then the stagger, profiles/r4_fwd_stagger/:
+the two waves of each SIMD half a tile apart (waves 4-7 run O += V P(t-1)
+before scoring tile t, three K/V buffers) 0.846 vs 0.809 ms, that with
+s_setprio 1 around every MFMA run 0.859, and three buffers without the lag
+0.834 -- the third buffer's code alone costs 3 %, the lag another 1.5 %, so
+the waves' shared phase is not what holds the forward at 47 % MFMA busy.)
 
 and the max |difference| of O / lse between them (same arithmetic: 0 expected).
 
