@@ -15,7 +15,8 @@ the two waves of each SIMD half a tile apart (waves 4-7 run O += V P(t-1)
 before scoring tile t, three K/V buffers) 0.846 vs 0.809 ms, that with
 s_setprio 1 around every MFMA run 0.859, and three buffers without the lag
 0.834 -- the third buffer's code alone costs 3 %, the lag another 1.5 %, so
-the waves' shared phase is not what holds the forward at 47 % MFMA busy.)
+the waves' shared phase is not what holds the forward at 47 % MFMA busy.
+Static s_setprio 1 for waves 4-7 before the loop: 0.826 vs 0.814 ms.)
 
 and the max |difference| of O / lse between them (same arithmetic: 0 expected).
 
