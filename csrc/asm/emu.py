@@ -309,6 +309,15 @@ class Emu:
     def op_s_branch(self, w, a, m):
         w.pc = self.labels[a[0]]
 
+    def op_s_getreg_b32(self, w, a, m):
+        """hwreg(HW_REG_HW_ID, offset, size) only: wave id in [3:0], SIMD id
+        in [5:4].  Waves 0..3 sit on SIMDs 0, 2, 1, 3 (the hardware's cyclic
+        placement from SIMD 0), so both SIMD-parity paths of a kernel run."""
+        assert a[1].replace(" ", "") == "hwreg(HW_REG_HW_ID", a
+        off, size = int(a[2]), int(a[3].rstrip(")"))
+        hw_id = ([0, 2, 1, 3][w.wid % 4] << 4) | w.wid
+        self.sset(w, a[0], (hw_id >> off) & ((1 << size) - 1))
+
     def op_s_waitcnt(self, w, a, m):
         pass
 

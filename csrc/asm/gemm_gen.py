@@ -418,7 +418,7 @@ def mfma(i: int, j: int, sub: int) -> str:
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
-         "align": True, "drain_end": False, "map": "spread", "persist": False}
+         "align": True, "drain_end": False, "map": "spread", "persist": False, "dual": ""}
 
 
 def _stamp(k: int) -> str:
@@ -551,6 +551,20 @@ SLOT_MAPS = {
     "spread3": {"x1": [0, 2, 4, 6, 8, 10, 12, 14], "xbar": 20, "w1": [24, 27, 30, 33, 36, 38, 40, 42],
                 "wbar": 50, "xdma": [22, 26, 30, 34, 38, 44, 52, 58], "wdma": [64, 76, 93, 99, 105, 111, 117, 123],
                 "wait": 91, "x0": [94, 95, 96, 97, 98, 100, 101, 102], "w0": [103, 104, 106, 108, 110, 113, 116, 119]},
+    # "spread" as the library's main 256 x 256 kernel actually issues it:
+    # every barrier one MFMA after its wait, M0 advanced one MFMA after each
+    # piece, the resource advances a few MFMAs after the last piece
+    "lib0": {"x1": [0, 2, 4, 6, 8, 10, 12, 14], "xbar": 20, "w1": [24, 27, 30, 33, 36, 38, 40, 42], "wbar": 50,
+             "xdma": [22, 25, 28, 31, 34, 52, 55, 58], "wdma": [61, 64, 85, 87, 89, 96, 100, 124], "wait": 91,
+             "x0": [93, 94, 95, 97, 98, 102, 103, 104], "w0": [105, 106, 109, 112, 114, 117, 120, 123],
+             "split": 1, "m0_lag": 1, "adv": {"x": 65, "w": 125}},
+    # its partner for the waves on odd SIMDs (the library selects one of two
+    # loop bodies by the SIMD id): X pieces and W reads one MFMA apart from
+    # lib0's, the last four W pieces non-temporal
+    "lib1": {"x1": [0, 2, 4, 6, 8, 10, 12, 14], "xbar": 20, "w1": [22, 25, 28, 31, 34, 38, 40, 42], "wbar": 50,
+             "xdma": [23, 26, 29, 32, 35, 53, 56, 59], "wdma": [62, 65, 84, 86, 88, 95, 99, 123], "wait": 91,
+             "x0": [93, 94, 96, 97, 98, 102, 103, 104], "w0": [105, 106, 109, 112, 114, 117, 120, 122],
+             "split": 1, "m0_lag": 1, "adv": {"x": 66, "w": 125}, "nt_w": [4, 5, 6, 7]},
 }
 
 
@@ -568,34 +582,53 @@ def span_mfmas(m: dict) -> list[int]:
     return [hi - lo for lo, hi in span_slots(m)]
 
 
-def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0):
-    m = SLOT_MAPS[SCHED["map"]]
+def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0,
+                  mapname: str = ""):
+    """One 64-k tile placed by an explicit slot map (SLOT_MAPS).  Map keys
+    beyond the placements: `split` puts each barrier that many MFMAs after
+    its wait (the MFMA issued in between runs while the wave waits at the
+    barrier); `m0_lag` advances M0 that many MFMAs after each piece instead
+    of right behind it; `adv` gives the slots of the X / W resource advances
+    (default: with the last piece of the half); `nt_w` the W pieces loaded
+    non-temporal."""
+    m = SLOT_MAPS[mapname or SCHED["map"]]
+    split, lag = m.get("split", 0), m.get("m0_lag", 0)
+    nt_w = set(m.get("nt_w", ()))
     slots: dict[int, list[str]] = {n: [] for n in range(128)}
     for j, n in enumerate(m["x1"]):
         slots[n].append(frag_read("x", j, 1))
     for i, n in enumerate(m["w1"]):
         slots[n].append(frag_read("w", i, 1))
     assert max(m["x1"]) < m["xbar"] and max(m["w1"]) < m["wbar"] and max(m["x1"] + m["w1"]) < 63
+    tm, sp = SCHED["timing"] == 1, SCHED["timing"] == 2
+    assert not (split and tm), "the wait-timing kernel stamps an unsplit wait + barrier"
     if with_dma:
-        slots[m["xbar"]] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
-        slots[m["wbar"]] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
+        for bar in (m["xbar"], m["wbar"]):
+            slots[bar].append("s_waitcnt lgkmcnt(0)")
+            slots[bar + split].append("s_barrier")
         for half, key, bar in (("x", "xdma", m["xbar"]), ("w", "wdma", m["wbar"])):
             srd_, vo, so, m0 = (SRD_X, V_DX, S_SOX, S_M0X) if half == "x" else (SRD_W, V_DW, S_SOW, S_M0W)
             pos = m[key]
-            assert sorted(pos) == pos and pos[0] > bar and len(set(pos)) == 8
+            assert sorted(pos) == pos and pos[0] > bar + split and len(set(pos)) == 8
             slots[pos[0] - 1].append(f"s_mov_b32 m0, {sr(m0)}")
             for j, n in enumerate(pos):
                 soff = "0" if j == 0 else sr(so + j - 1)
-                slots[n].append(f"buffer_load_dwordx4 {vr(vo)}, {sr(srd_, 4)}, {soff} offen lds")
+                nt = " nt" if half == "w" and j in nt_w else ""
+                slots[n].append(f"buffer_load_dwordx4 {vr(vo)}, {sr(srd_, 4)}, {soff} offen{nt} lds")
                 if j < 7:
-                    slots[n].append(f"s_add_u32 m0, m0, {4 * LINE}")
-            slots[pos[-1]] += advance(half) + [f"s_xor_b32 {sr(m0)}, {sr(m0)}, {sr(m0 + 1)}"]
+                    # an MFMA between every M0 write and the next piece (the
+                    # M0 -> LDS-DMA hazard wants one wait state)
+                    assert pos[j + 1] > n + lag
+                    slots[n + lag].append(f"s_add_u32 m0, m0, {4 * LINE}")
+            adv = m.get("adv", {}).get(half, pos[-1])
+            assert adv >= pos[-1]
+            slots[adv] += advance(half) + [f"s_xor_b32 {sr(m0)}, {sr(m0)}, {sr(m0 + 1)}"]
         # the two halves' pieces must not interleave (one running M0)
-        assert max(m["xdma"]) < min(m["wdma"]) - 1
+        assert max(m["xdma"]) + lag < min(m["wdma"]) - 1
+        assert m.get("adv", {}).get("x", 0) < 128 and m.get("adv", {}).get("w", 0) < 128
         vm = sum(1 for n in m["xdma"] + m["wdma"] if n < m["wait"])
     else:
         vm = 0
-    tm, sp = SCHED["timing"] == 1, SCHED["timing"] == 2
     if with_dma and tm:  # waits: X-free and W-free barriers (the vm wait below)
         for k, bar in ((2, m["xbar"]), (4, m["wbar"])):
             slots[bar].insert(0, _stamp(k))
@@ -607,11 +640,16 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
             slots[hi].append(_stamp(2 * k + 1))
     if next_reads:
         w = m["wait"]
-        slots[w] += ([_stamp(0)] if (tm and with_dma) else []) + [
-                     f"s_waitcnt vmcnt({vm if with_dma else vm_after_dma})", "s_barrier"] + (
-                     [_stamp(1)] if (tm and with_dma) else []) + [
-                     f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
-                     f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
+        wait = [f"s_waitcnt vmcnt({vm if with_dma else vm_after_dma})"]
+        toggles = [f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
+                   f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
+        if split:
+            slots[w] += wait
+            slots[w + split] += ["s_barrier"] + toggles
+            assert min(m["x0"] + m["w0"]) > w + split
+        else:
+            slots[w] += ([_stamp(0)] if (tm and with_dma) else []) + wait + ["s_barrier"] + (
+                [_stamp(1)] if (tm and with_dma) else []) + toggles
         assert min(m["x0"] + m["w0"]) > w and max(m["x0"] + m["w0"]) < 126
         for j, n in enumerate(m["x0"]):
             slots[n].append(frag_read("x", j, 0))
@@ -886,6 +924,17 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     l_loop, l_tail = a.fresh("loop"), a.fresh("tail")
     a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
     a(f"s_cbranch_scc1 {l_tail}")
+    dual = SCHED["dual"]
+    if dual:
+        # two loop bodies, picked by the SIMD id's low bit (HW_ID[4]): the
+        # waves of SIMDs 1 and 3 run the `dual` map, whose DMA pieces and
+        # reads sit one MFMA away from the others'.  Both bodies have the
+        # same barriers, so the workgroup stays in step.
+        assert SCHED["map"] and not SCHED["timing"]
+        l_loop1 = a.fresh("loop1")
+        a(f"s_getreg_b32 {sr(S_T0)}, hwreg(HW_REG_HW_ID, 4, 1)")
+        a(f"s_cmp_eq_u32 {sr(S_T0)}, 0")
+        a(f"s_cbranch_scc0 {l_loop1}")
     if SCHED["align"]:
         a(".p2alignl 6, 0xbf800000")   # loop head on a 64-byte boundary (s_nop padding)
     a.label(l_loop)
@@ -894,6 +943,15 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_LOOP)}, 1")
     a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
     a(f"s_cbranch_scc0 {l_loop}")
+    if dual:
+        a(f"s_branch {l_tail}")
+        if SCHED["align"]:
+            a(".p2alignl 6, 0xbf800000")
+        a.label(l_loop1)
+        iteration_map(a, with_dma=True, next_reads=True, vm_after_dma=16, mapname=dual)
+        a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_LOOP)}, 1")
+        a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
+        a(f"s_cbranch_scc0 {l_loop1}")
     a.label(l_tail)
     it(a, with_dma=False, next_reads=True, vm_after_dma=0, trace_base=tb(200))
     it(a, with_dma=False, next_reads=False, vm_after_dma=0, trace_base=tb(300))
@@ -1146,6 +1204,10 @@ PLAIN_VARIANTS = (
     ("v3", {"map": "spread3"}),
     ("v4", {"group": 2}),
     ("v5", {"persist": True}),              # persistent: a workgroup per CU walks its tiles, next tile staged under the epilogue
+    ("v6", {"map": "lib0"}),                # split waits, lagged M0 / resource advances
+    ("v7", {"map": "lib0", "dual": "lib1"}),  # + the odd-SIMD body
+    ("v8", {"map": "lib0", "dual": "lib1", "align": False}),  # + MFMAs where they fall (no s_nop padding)
+    ("v9", {"map": "lib0", "align": False}),
 )
 # measured (profiles/r4_asm_gemm/ab1..diag2): MFMAs on 8-byte boundaries, ending
 # with the epilogue's stores in flight, two barriers per tile and the wait 16

@@ -40,7 +40,30 @@
 //     TOA_DEVICE_SOURCE=pod-resources;
 //   * the annotation amd.com/gpu-visibility=node, which the local kubelet
 //     (localkubelet/kubelet.py) honours only for a privileged container with
-//     hostIPC -- the same rule a real node enforces.
+//     hostIPC -- the same rule a real node enforces;
+//   * RCCL host identity: NCCL_HOSTID from the downward API (spec.nodeName).
+//     Every rank pod has its own UTS namespace, so its hostname is the pod
+//     name; RCCL (like NCCL) hashes gethostname() + boot_id into hostHash
+//     unless NCCL_HOSTID is set, and its P2P / SHM transports refuse a peer
+//     with another hostHash ("different node").  Without this value the
+//     co-located ranks would form an 8-node communicator over the socket
+//     transport -- the degradation this layout exists to prevent.  The
+//     required podAffinity puts every rank on one node, so spec.nodeName is
+//     the same string in all of them.  A container that sets NCCL_HOSTID
+//     itself keeps its own value;
+//   * IPC mode: hostPID.  The MI355X hosts support DMA-BUF IPC only
+//     (HSA_ENABLE_IPC_MODE_LEGACY=0, kRcclDefaults in envgen.cc; the legacy
+//     KFD handles are refused by their driver).  A DMA-BUF handle is an fd
+//     of the exporting process that ROCr hands to the importer through the
+//     exporter's process (its runtime uses sendmsg / recvmsg and a raw
+//     syscall for the transfer), so the ranks must see each other's
+//     processes: hostPID puts every rank in the node's PID namespace, and
+//     privileged already grants the ptrace-level access such a transfer
+//     checks.  scripts/ipc_namespace_probe.py opens a HIP IPC handle from
+//     an importer started in its own PID / network / IPC / mount namespace
+//     and records which of them the transfer crosses
+//     (profiles/r5_ipcns/); hostIPC stays for the one-shot all-reduce's
+//     shared-memory rendezvous.
 //
 // Cost, to be accepted explicitly: privileged pods and hostIPC are rejected by
 // the PodSecurity "baseline" and "restricted" levels.  The namespace needs the
@@ -116,6 +139,7 @@ void apply_node_local(const Json& job, const std::string& rtype, Json& tpl, cons
 
   Json& ps = tpl["spec"];
   ps.set("hostIPC", true);
+  ps.set("hostPID", true);  // DMA-BUF IPC handles cross processes by PID (header)
   // co-locate with the job's other rank pods
   Json sel = Json::object();
   sel.set(kLabelGroupName, labels.get(kLabelGroupName).str("kubeflow.org"));
@@ -157,10 +181,12 @@ void apply_node_local(const Json& job, const std::string& rtype, Json& tpl, cons
   Json sc = c.get("securityContext").is_object() ? c.get("securityContext") : Json::object();
   sc.set("privileged", true);
   c.set("securityContext", sc);
-  // the pod's own identity, for the pod-resources lookup
+  // the pod's own identity, for the pod-resources lookup; the node's name as
+  // RCCL's host identity (header: one hostHash for every rank of the node)
   Json env = c.get("env").is_array() ? c.get("env") : Json::array();
-  static const char* const kDownward[2][2] = {{"TOA_POD_NAME", "metadata.name"},
-                                              {"TOA_POD_NAMESPACE", "metadata.namespace"}};
+  static const char* const kDownward[3][2] = {{"TOA_POD_NAME", "metadata.name"},
+                                              {"TOA_POD_NAMESPACE", "metadata.namespace"},
+                                              {"NCCL_HOSTID", "spec.nodeName"}};
   for (const auto& d : kDownward) {
     bool have = false;
     for (size_t i = 0; i < env.size(); ++i) have = have || env.at(i).get("name").str() == d[0];

@@ -32,13 +32,14 @@ namespace {
 
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
-       K_WGRAD = 7, K_V1 = 8, K_N = 13 };
+       K_WGRAD = 7, K_V1 = 8, K_N = 17 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
                            "toa_gemm_tn_asm_timing2",  "toa_wgrad_nt_asm",           "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
-                           "toa_gemm_tn_asm_plain_v5"};
+                           "toa_gemm_tn_asm_plain_v5", "toa_gemm_tn_asm_plain_v6", "toa_gemm_tn_asm_plain_v7",
+                           "toa_gemm_tn_asm_plain_v8", "toa_gemm_tn_asm_plain_v9"};
 
 struct DevModule {
   std::once_flag once;
@@ -77,7 +78,7 @@ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // A/B arms that walk several tiles per workgroup (gemm_gen.py SCHED
 // "persist"), by variant number 1..: their grid is one workgroup per CU.
-constexpr bool kVariantPersist[K_N - K_V1] = {false, false, false, false, true};
+constexpr bool kVariantPersist[K_N - K_V1] = {false, false, false, false, true, false, false, false, false};
 constexpr unsigned kPersistGrid = 256;
 
 int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {

@@ -542,6 +542,8 @@ def test_node_local_pod_spec_and_env():
     w3 = pods["test-tfjob-worker-3"]
     spec = w3["spec"]
     assert spec["hostIPC"] is True
+    # DMA-BUF IPC handles travel between rank processes by PID (nodelocal.cc)
+    assert spec["hostPID"] is True
     term = spec["affinity"]["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][0]
     assert term["topologyKey"] == "kubernetes.io/hostname"
     assert term["labelSelector"]["matchLabels"] == {"group-name": "kubeflow.org", "job-name": "test-tfjob",
@@ -556,15 +558,19 @@ def test_node_local_pod_spec_and_env():
                                   "readOnly": True}]
     env = {e["name"]: e.get("value") for e in c["env"]}
     downward = {e["name"]: e["valueFrom"]["fieldRef"]["fieldPath"] for e in c["env"] if "valueFrom" in e}
-    assert downward == {"TOA_POD_NAME": "metadata.name", "TOA_POD_NAMESPACE": "metadata.namespace"}
+    # NCCL_HOSTID = the node's name: one RCCL hostHash for every co-located rank
+    # (each pod has its own hostname), so RCCL takes P2P / SHM, not the socket transport
+    assert downward == {"TOA_POD_NAME": "metadata.name", "TOA_POD_NAMESPACE": "metadata.namespace",
+                        "NCCL_HOSTID": "spec.nodeName"}
     assert env["RANK"] == "4" and env["LOCAL_RANK"] == "4"  # chief is rank 0
     assert env["LOCAL_WORLD_SIZE"] == "8" and env["WORLD_SIZE"] == "8" and env["TOA_NODE_LOCAL"] == "1"
     assert env["TOA_DEVICE_SOURCE"] == "pod-resources"
     chief = {e["name"]: e.get("value") for e in pods["test-tfjob-chief-0"]["spec"]["containers"][0]["env"]}
     assert chief["LOCAL_RANK"] == "0" and chief["LOCAL_WORLD_SIZE"] == "8"
     ps = pods["test-tfjob-ps-0"]  # outside the RCCL world: unchanged
-    assert "hostIPC" not in ps["spec"] and "affinity" not in ps["spec"]
+    assert "hostIPC" not in ps["spec"] and "affinity" not in ps["spec"] and "hostPID" not in ps["spec"]
     assert "securityContext" not in ps["spec"]["containers"][0]
+    assert "NCCL_HOSTID" not in {e["name"] for e in ps["spec"]["containers"][0]["env"]}
     assert "LOCAL_RANK" not in {e["name"] for e in ps["spec"]["containers"][0]["env"]}
 
 
@@ -578,6 +584,19 @@ def test_node_local_keeps_user_security_context_and_env():
     assert c["securityContext"] == {"runAsUser": 1000, "privileged": True}
     names = [e["name"] for e in c["env"]]
     assert names.count("TOA_POD_NAME") == 1 and names.count("TOA_POD_NAMESPACE") == 1
+    assert names.count("NCCL_HOSTID") == 1
+
+
+def test_node_local_keeps_operator_nccl_hostid():
+    """An NCCL_HOSTID the operator's --nccl-env sets wins over the downward-API
+    default; without the annotation no rank pod gets NCCL_HOSTID or hostPID."""
+    job = _gpu_job(2, annotation="privileged")
+    pod = ops(run(job, nccl_env={"NCCL_HOSTID": "rack7-node3"}), "create_pod")[0]["pod"]
+    env = [e for e in pod["spec"]["containers"][0]["env"] if e["name"] == "NCCL_HOSTID"]
+    assert env == [{"name": "NCCL_HOSTID", "value": "rack7-node3"}]
+    plain = ops(run(_gpu_job(2)), "create_pod")[0]["pod"]
+    assert "hostPID" not in plain["spec"]
+    assert "NCCL_HOSTID" not in {e["name"] for e in plain["spec"]["containers"][0]["env"]}
 
 
 @pytest.mark.parametrize("workers,gpus,annotation,gang,expected", [

@@ -131,3 +131,49 @@ async def _put_namespace(c, name, level):
 def test_bench_flags_a_degraded_one_node_transport(trans, n, ok):
     assert transport_ok({"channel_connections_by_transport": trans}, n) is ok
     assert transport_ok(None, 8) is None
+
+
+def _kubelet():
+    from tf_operator_amd.localkubelet.kubelet import LocalKubelet
+
+    kl = LocalKubelet.__new__(LocalKubelet)
+    kl.device_visibility = None
+    kl.node = "node-a"
+    kl._rewrite_env = lambda pod, env: env
+    kl.service_port = lambda ns, name: 2222
+    return kl
+
+
+def test_kubelet_gives_each_pod_its_own_rccl_host_identity():
+    """On a real node every pod has its own hostname, which RCCL hashes into
+    its host identity: the one-host local kubelet emulates that with a
+    per-pod NCCL_HOSTID, so a job that needs one identity for its ranks must
+    say so (the operator's node-local layout: spec.nodeName)."""
+    kl = _kubelet()
+    a = {"metadata": {"name": "job-worker-0", "namespace": "ns"}, "spec": {"containers": [{"name": "c"}]}}
+    b = {"metadata": {"name": "job-worker-1", "namespace": "ns"}, "spec": {"containers": [{"name": "c"}]}}
+    ea = kl._build_env(a, a["spec"]["containers"][0], [])
+    eb = kl._build_env(b, b["spec"]["containers"][0], [])
+    assert ea["NCCL_HOSTID"] == "job-worker-0" and eb["NCCL_HOSTID"] == "job-worker-1"
+    hn = {"metadata": {"name": "h", "namespace": "ns"}, "spec": {"hostNetwork": True, "containers": [{"name": "c"}]}}
+    assert kl._build_env(hn, hn["spec"]["containers"][0], []).get("NCCL_HOSTID") != "h"  # shares the node's hostname
+
+
+def test_kubelet_operator_node_local_env_overrides_the_per_pod_identity():
+    """The node-local rank pods the C++ core builds carry NCCL_HOSTID from
+    spec.nodeName: the kubelet resolves that fieldRef, so every rank reports
+    the node, and RCCL sees one host."""
+    from tf_operator_amd import core
+    from tf_operator_amd.testing import fixtures as fx
+
+    job = fx.new_tfjob(3, 0)
+    for s in job["spec"]["tfReplicaSpecs"].values():
+        s["template"]["spec"]["containers"][0]["resources"] = {"limits": {"amd.com/gpu": 1}}
+    job["metadata"]["annotations"] = {"amd.com/node-local": "privileged"}
+    res = core.reconcile(job, [], [], now=0.0, options={})
+    pods = [a["pod"] for a in res["actions"] if a["op"] == "create_pod"]
+    assert len(pods) == 3
+    kl = _kubelet()
+    ids = {kl._build_env(p, p["spec"]["containers"][0], [0])["NCCL_HOSTID"] for p in pods}
+    assert ids == {"node-a"}
+    assert all(p["spec"]["hostPID"] is True for p in pods)

@@ -186,6 +186,7 @@ POD_TEMPLATE = {
                 "priorityClassName": _STR,
                 "hostNetwork": {"type": "boolean"},
                 "hostIPC": {"type": "boolean"},
+                "hostPID": {"type": "boolean"},
                 "shareProcessNamespace": {"type": "boolean"},
                 "terminationGracePeriodSeconds": _int("Grace period before SIGKILL.", "int64", 0),
                 "activeDeadlineSeconds": _int("Pod deadline.", "int64", 1),

@@ -385,11 +385,24 @@ class LocalKubelet:
                 and bool(spec.get("hostIPC"))
                 and (container.get("securityContext") or {}).get("privileged") is True)
 
+    def _field_ref(self, pod, path: str):
+        """Downward API fieldRef values this kubelet can answer."""
+        md = pod.get("metadata") or {}
+        return {"metadata.name": md.get("name"), "metadata.namespace": md.get("namespace", "default"),
+                "metadata.uid": md.get("uid"), "spec.nodeName": self.node,
+                "spec.serviceAccountName": (pod.get("spec") or {}).get("serviceAccountName", "default"),
+                "status.hostIP": "127.0.0.1", "status.podIP": "127.0.0.1"}.get(path)
+
     def _build_env(self, pod, container, gpus):
         env = {}
         for e in container.get("env") or []:
             if "value" in e:
                 env[e["name"]] = str(e["value"])
+            else:
+                ref = ((e.get("valueFrom") or {}).get("fieldRef") or {}).get("fieldPath")
+                val = self._field_ref(pod, ref) if ref else None
+                if val is not None:
+                    env[e["name"]] = str(val)
         env = self._rewrite_env(pod, env)
         ns = pod["metadata"].get("namespace", "default")
         # a real kubelet starts containers from the image's env, not its own:
@@ -399,6 +412,16 @@ class LocalKubelet:
         base = {k: v for k, v in os.environ.items() if not _inherited_rendezvous(k)}
         base.update(env)
         base["HOSTNAME"] = pod["metadata"]["name"]
+        # Every pod of a real node has its own UTS namespace, i.e. its own
+        # hostname, and RCCL derives its host identity from the hostname
+        # unless NCCL_HOSTID is set: two "pods" of this one-host kubelet would
+        # otherwise share an identity a real cluster never grants them.  The
+        # pod's own name stands in for its hostname; a value the pod spec
+        # provides (the operator's node-local layout: spec.nodeName,
+        # csrc/core/nodelocal.cc) overrides it.  A hostNetwork pod shares the
+        # node's hostname, so it gets none.
+        if not (pod.get("spec") or {}).get("hostNetwork") and "NCCL_HOSTID" not in env:
+            base["NCCL_HOSTID"] = pod["metadata"]["name"]
         base["PORT"] = str(self.service_port(ns, pod["metadata"]["name"]))
         base["TOA_POD_NAME"] = pod["metadata"]["name"]
         base["TOA_POD_NAMESPACE"] = ns

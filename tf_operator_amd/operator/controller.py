@@ -354,12 +354,12 @@ class JobController:
                     pname = pod.get("metadata", {}).get("name", "")
                     nl = (pod.get("metadata", {}).get("labels") or {}).get("training.amd.com/node-local") == "true"
                     if e.status == 403 and nl and "PodSecurity" in str(e):
-                        # the node-local layout needs a privileged pod + hostIPC
+                        # the node-local layout needs a privileged pod + hostIPC + hostPID
                         # (csrc/core/nodelocal.cc): say so instead of a silent Pending
                         await self._emit_events(job, [{
                             "type": "Warning", "reason": "NodeLocalForbidden",
                             "message": f"Error creating pod {pname}: the node-local xGMI layout "
-                                       f"(annotation amd.com/node-local) needs a privileged container and hostIPC, "
+                                       f"(annotation amd.com/node-local) needs a privileged container, hostIPC and hostPID, "
                                        f"which this namespace's PodSecurity level rejects; label the namespace "
                                        f"pod-security.kubernetes.io/enforce=privileged or remove the annotation: "
                                        f"{e}"}], job.get("kind"))
