@@ -74,6 +74,8 @@ def parser() -> argparse.ArgumentParser:
     ap.add_argument("--result-file", default=None, help=argparse.SUPPRESS)  # replica -> launcher
     ap.add_argument("--rccl-log", choices=("auto", "0", "1"), default="auto",
                     help="capture RCCL's transport selection (NCCL_DEBUG=INFO to a file) into the JSON line")
+    ap.add_argument("--calibrate", choices=("0", "1"), default="1",
+                    help="box-speed record: fixed-shape GEMM rates around the timed region, clock during it")
     return ap
 
 
@@ -447,6 +449,7 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
     from ..train import dist as tdist
     from ..train.llm import LlamaTrainer
     from ..train.runtime import Runtime
+    from .calibrate import Calibration
 
     phases["imports"] = time.time()
     from ..ops import gemm as _gemm
@@ -486,9 +489,14 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
     rt.first_step_done()  # -> operator (TFJob launches): the submit->first-step clock of this job
     for _ in range(max(args.warmup - 1, 0)):
         loss = tr.step(batches)
+    # box-speed evidence (bench/calibrate.py): fixed-shape GEMM rates just
+    # before and just after the timed region, clock sampled during it
+    cal = Calibration(dev, enabled=args.calibrate == "1")
+    cal.before()
     tdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    cal.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = tr.step(batches)
@@ -498,6 +506,8 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    cal.stop()
+    cal.after()
     dt = tdist.all_max(dt, dev)
     loss_v = float(loss)
     # data parallelism keeps every replica's weights identical: check it
@@ -561,6 +571,9 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
             "replicas_identical": bool(in_sync),
             "peak_mem_gib": round(peak_mem, 1),
         }
+        cr = cal.record()
+        if cr is not None:
+            out["calibration"] = cr
         rl = summarize_rccl_log(rccl_log)
         if rl:
             out["rccl"] = rl
@@ -620,7 +633,8 @@ def run_launcher(args) -> int:
                str(args.warmup), "--model", args.model, "--seq-len", str(args.seq_len), "--micro-batch",
                str(args.micro_batch), "--grad-accum", str(args.grad_accum), "--zero", args.zero,
                "--warm-start", args.warm_start,
-               "--rccl-log", args.rccl_log, "--latency-probes", "0", "--result-file", res_file]
+               "--rccl-log", args.rccl_log, "--latency-probes", "0", "--result-file", res_file,
+               "--calibrate", args.calibrate]
         if args.bucket_mb is not None:
             cmd += ["--bucket-mb", str(args.bucket_mb)]
         timeout = args.probe_timeout + 60 + 30 * (args.steps + args.warmup)
