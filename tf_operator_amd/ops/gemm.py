@@ -175,8 +175,8 @@ def prewarm_early():
 
     try:
         local = tdist.local_device_index()
-    except (ValueError, RuntimeError, LookupError):
-        return None  # the trainer's own init reports the binding error
+    except Exception:  # noqa: BLE001 - e.g. grpc.RpcError (kubelet socket down), ImportError (no grpcio)
+        return None  # the trainer's own init (train/dist.py) hits the same lookup and reports it
     if local >= torch.cuda.device_count():
         return None
     return prewarm(torch.device("cuda", local))
@@ -211,7 +211,9 @@ class first_step:
     the policy)."""
 
     def __init__(self, on: bool = True):
-        self.on = bool(on) and _MODE in ("nosk", "tuned") and _lib.has("toa_gemm_asm")
+        # TOA_GEMM_TN_FIRST=0: the first step stays on the steady-state policy
+        self.on = (bool(on) and _MODE in ("nosk", "tuned") and _lib.has("toa_gemm_asm")
+                   and os.environ.get("TOA_GEMM_TN_FIRST", "1") != "0")
 
     def __enter__(self):
         global _asm_first
@@ -299,6 +301,7 @@ def swiglu_down_dgrad(d2: torch.Tensor, wd: torch.Tensor, gu: torch.Tensor):
 
 
 _ws = {}
+HIP_ERROR_INVALID_VALUE = 1
 # weight-gradient kernel: the assembly NT kernel (csrc/asm/wgrad_gen.py;
 # 1.30-1.50 PF/s at the Llama forms, 1-12 % faster than the HIP kernel and
 # bit-identical to it, profiles/r4_wgrad/) where the library carries it, else
@@ -308,9 +311,14 @@ _WGRAD_KERNEL = None
 
 
 def wgrad_kernel() -> str:
+    """``asm`` (default where the library carries it) or ``hip``;
+    ``TOA_WGRAD=hip`` forces the HIP kernel without a code change."""
     global _WGRAD_KERNEL
     if _WGRAD_KERNEL is None:
-        _WGRAD_KERNEL = "asm" if _lib.has("toa_wgrad_asm") else "hip"
+        forced = os.environ.get("TOA_WGRAD", "")
+        if forced not in ("", "asm", "hip"):
+            raise ValueError(f"TOA_WGRAD={forced!r}: expected asm or hip")
+        _WGRAD_KERNEL = forced or ("asm" if _lib.has("toa_wgrad_asm") else "hip")
     return _WGRAD_KERNEL
 
 
@@ -355,9 +363,17 @@ def wgrad_hip_(g, dy2, x2, beta=1.0, split=None):
     split = 0 if split is None else int(split)
     nbytes = int(_lib.call_ret("toa_wgrad_workspace", N, K, T, split))
     ws = _workspace(dy2.device, nbytes) if nbytes > 0 else None
-    fn = "toa_wgrad_asm" if wgrad_kernel() == "asm" else "toa_wgrad"
-    _lib.call(fn, _lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(g), K, _lib.ptr(ws),
-              N, K, T, int(split), int(beta != 0.0), _lib.stream(dy2))
+    args = (_lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(g), K, _lib.ptr(ws),
+            N, K, T, int(split), int(beta != 0.0), _lib.stream(dy2))
+    if wgrad_kernel() == "asm":
+        rc = _lib.call_ret("toa_wgrad_asm", *args)
+        if rc == 0:
+            return g
+        if rc != HIP_ERROR_INVALID_VALUE:
+            raise RuntimeError(f"toa_wgrad_asm failed: hipError {rc}")
+        # a shape / layout the assembly kernel's launcher refuses (it checks
+        # before launching): the HIP kernel shares its split plan and reduce
+    _lib.call("toa_wgrad", *args)
     return g
 
 

@@ -15,6 +15,8 @@ import dataclasses
 import datetime
 import json
 import os
+import sys
+import threading
 
 import torch
 import torch.distributed as dist
@@ -95,7 +97,11 @@ def init(backend=None, timeout_s=1800) -> DistInfo:
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
         # a group still alive when the interpreter exits can abort in its
         # destructor ("terminate called without an active exception") and turn
-        # a finished replica into a failed one: tear it down at exit
+        # a finished replica into a failed one: tear it down at exit --
+        # gracefully after a clean run, by abort after an uncaught exception
+        # (a graceful destroy can block on collectives a dead peer never
+        # completes, and the operator would never see the failure)
+        _install_failure_hook()
         atexit.register(_shutdown_quietly)
     return DistInfo(rank, world, local_rank, device, backend if world > 1 else None)
 
@@ -121,11 +127,61 @@ def shutdown():
         dist.destroy_process_group()
 
 
+_FAILED = []          # set by the excepthook: the interpreter is exiting on an uncaught exception
+EXIT_TEARDOWN_S = 20.0
+
+
+def _install_failure_hook():
+    prev = sys.excepthook
+    if getattr(prev, "_toa_failure_hook", False):
+        return
+
+    def hook(tp, val, tb):
+        _FAILED.append(tp)
+        prev(tp, val, tb)
+
+    hook._toa_failure_hook = True
+    sys.excepthook = hook
+
+
+def _bounded(fn, timeout: float) -> bool:
+    """Run fn on a helper thread; False if it did not return in time."""
+    t = threading.Thread(target=fn, name="toa-pg-teardown", daemon=True)
+    t.start()
+    t.join(timeout)
+    return not t.is_alive()
+
+
 def _shutdown_quietly():
-    try:
-        shutdown()
-    except Exception:  # pragma: no cover - a peer already gone
-        pass
+    """atexit teardown of the process group.  After a clean run: graceful
+    destroy.  After an uncaught exception: abort the group (no waiting on
+    outstanding collectives), and if even that does not return within
+    EXIT_TEARDOWN_S, leave with status 1 right away, so a failed replica
+    always exits non-zero and the operator can restart it."""
+    if not dist.is_initialized():
+        return
+
+    def graceful():
+        try:
+            shutdown()
+        except Exception:  # pragma: no cover - a peer already gone
+            pass
+
+    def abort():
+        try:
+            dist.distributed_c10d._abort_process_group()
+        except Exception:  # noqa: BLE001 - fall back to the graceful path, still bounded
+            graceful()
+
+    if _FAILED:
+        if not _bounded(abort, EXIT_TEARDOWN_S):
+            sys.stderr.write("[dist] process group teardown did not finish after a failure; exiting 1\n")
+            sys.stderr.flush()
+            os._exit(1)
+    elif not _bounded(graceful, 3 * EXIT_TEARDOWN_S):
+        sys.stderr.write("[dist] process group teardown hung after a clean run; exiting 0\n")
+        sys.stderr.flush()
+        os._exit(0)
 
 
 def resolve_endpoint(addr: str) -> tuple[str, int]:
