@@ -53,17 +53,18 @@
 //     itself keeps its own value;
 //   * IPC mode: hostPID.  The MI355X hosts support DMA-BUF IPC only
 //     (HSA_ENABLE_IPC_MODE_LEGACY=0, kRcclDefaults in envgen.cc; the legacy
-//     KFD handles are refused by their driver).  A DMA-BUF handle is an fd
-//     of the exporting process that ROCr hands to the importer through the
-//     exporter's process (its runtime uses sendmsg / recvmsg and a raw
-//     syscall for the transfer), so the ranks must see each other's
-//     processes: hostPID puts every rank in the node's PID namespace, and
-//     privileged already grants the ptrace-level access such a transfer
-//     checks.  scripts/ipc_namespace_probe.py opens a HIP IPC handle from
-//     an importer started in its own PID / network / IPC / mount namespace
-//     and records which of them the transfer crosses
-//     (profiles/r5_ipcns/); hostIPC stays for the one-shot all-reduce's
-//     shared-memory rendezvous.
+//     KFD handles are refused by their driver).  A DMA-BUF IPC handle
+//     carries the exporter's PID and fd number, and the importer opens
+//     /proc/<pid>/fd/<fd> (ROCm 7.2's libhsa-runtime64: "PID: %jd; fd: %d;
+//     /proc/%jd/fd/%d").  So the ranks must see each other's processes:
+//     hostPID puts every rank in the node's PID namespace (a per-pod PID
+//     namespace would resolve the exporter's PID to nothing or to another
+//     process), and the privileged container passes the ptrace-read check
+//     that opening another process's fd link makes.  hostIPC stays for the
+//     one-shot all-reduce's IPC rendezvous (parallel/ipc.py).  The GPU box
+//     refuses unprivileged user namespaces, so
+//     scripts/ipc_namespace_probe.py could only run its same-namespace arm
+//     there (profiles/r5_ipcns/).
 //
 // Cost, to be accepted explicitly: privileged pods and hostIPC are rejected by
 // the PodSecurity "baseline" and "restricted" levels.  The namespace needs the

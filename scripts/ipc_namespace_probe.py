@@ -9,6 +9,12 @@ those namespaces that transfer crosses.
 
     python scripts/ipc_namespace_probe.py [--modes same,userns,pidns,netns,ipcns]
 
+ROCm 7.2's runtime imports a DMA-BUF handle by opening /proc/<exporter
+pid>/fd/<fd>, so the PID namespace is the one expected to matter.  Creating
+the namespaces needs unprivileged user namespaces; where the host forbids
+them (`unshare: ... No space left on device`, max_user_namespaces = 0) only
+the `same` arm runs.
+
 The driver (this process) never touches the GPU.  It starts the exporter as a
 child, then one importer per mode, each under `unshare` (the exec happens
 before the importer's first HIP call), and prints one JSON line per mode:
@@ -26,6 +32,11 @@ import time
 
 N = 1 << 20
 PATTERN = 0x5A
+
+
+class IpcHandle(ctypes.Structure):
+    """hipIpcMemHandle_t: 64 bytes, passed BY VALUE to hipIpcOpenMemHandle."""
+    _fields_ = [("reserved", ctypes.c_char * 64)]
 
 
 def _hip():
@@ -49,8 +60,8 @@ def exporter(handle_path: str, done_path: str, timeout: float):
     _check(hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(N)), "hipMalloc")
     _check(hip.hipMemset(ptr, PATTERN, ctypes.c_size_t(N)), "hipMemset")
     _check(hip.hipDeviceSynchronize(), "hipDeviceSynchronize")
-    handle = (ctypes.c_char * 64)()
-    _check(hip.hipIpcGetMemHandle(handle, ptr), "hipIpcGetMemHandle")
+    handle = IpcHandle()
+    _check(hip.hipIpcGetMemHandle(ctypes.byref(handle), ptr), "hipIpcGetMemHandle")
     tmp = handle_path + ".tmp"
     with open(tmp, "wb") as f:
         f.write(bytes(handle))
@@ -65,8 +76,9 @@ def importer(handle_path: str):
     hip = _hip()
     _check(hip.hipSetDevice(0), "hipSetDevice")
     raw = open(handle_path, "rb").read()
-    handle = (ctypes.c_char * 64).from_buffer_copy(raw)
+    handle = IpcHandle.from_buffer_copy(raw)
     dptr = ctypes.c_void_p()
+    hip.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), IpcHandle, ctypes.c_uint]
     _check(hip.hipIpcOpenMemHandle(ctypes.byref(dptr), handle, ctypes.c_uint(1)), "hipIpcOpenMemHandle")
     host = (ctypes.c_ubyte * N)()
     _check(hip.hipMemcpy(host, dptr, ctypes.c_size_t(N), ctypes.c_int(2)), "hipMemcpy D2H")
