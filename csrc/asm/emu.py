@@ -203,6 +203,9 @@ class Emu:
     def op_s_load_dwordx4(self, w, a, m):
         self._sload(w, a, 4)
 
+    def op_s_load_dwordx2(self, w, a, m):
+        self._sload(w, a, 2)
+
     def op_s_memtime(self, w, a, m):
         """A monotonically increasing stand-in for the shader clock: this
         wave's instruction count (the timing kernel's records stay ordered)."""

@@ -76,15 +76,20 @@ LINE = 1056              # one LDS line: 8 tile rows x 128 B + 32 B pad
 HALF = 32 * LINE         # 256 rows of one operand = 33792 B
 STAGE = 2 * HALF         # X half + W half = 67584 B
 LDS_BYTES = 2 * STAGE    # 135168 B
-KARG_BYTES = 80
+KARG_BYTES = 96
 
-# kernarg layout (byte offsets; mirrored by csrc/hip/gemm_asm.hip)
+# kernarg layout (byte offsets; mirrored by csrc/hip/gemm_asm.hip).  `map`:
+# the tile order, bits [3:0] log2 of the group size, bit 4 set = groups of
+# COLUMN tiles walk the row tiles (clear: groups of row tiles walk the
+# column tiles); `grid`: a persistent kernel's workgroup count.
 KARG = {
     "X": 0, "W": 8, "C": 16, "S": 24,
     "ldx": 32, "ldw": 36, "ldc": 40, "lds": 44,
     "ktiles": 48, "tiles_m": 52, "tiles_n": 56, "xq": 60, "xr": 64,
-    "per_group": 68, "fw": 72, "fc": 76,
+    "per_group": 68, "fw": 72, "fc": 76, "map": 80, "grid": 84,
 }
+MAP_WALK_COLS = 16
+MAP_DEFAULT = 2          # groups of 4 row tiles walk the column tiles
 
 EPIS = ("plain", "swiglu_fwd", "swiglu_bwd")
 
@@ -109,7 +114,9 @@ S_Q, S_R = 69, 70   # division results
 # barrier, W-free barrier), s88..s89 the kernel's start stamp
 S_TMT, S_ACC, S_T_START = 72, 84, 88
 S_ITER, S_GRID = 90, 91   # persistent arms: this workgroup's tile-order index, the grid size
-N_SGPR = 92
+S_MAP, S_KGRID = 92, 93   # kernarg map / grid words (s94, s95: the map's decoded log2 group, walk flag)
+S_LG, S_WALK = 94, 95
+N_SGPR = 96
 
 # VGPRs
 V_TID = 132
@@ -213,6 +220,7 @@ def mul64(a: Asm, lo: int, hi: int, x: int, y: int):
 def prologue_args(a: Asm):
     a(f"s_load_dwordx16 {sr(S_ARGS, 16)}, s[0:1], 0x0")
     a(f"s_load_dwordx4 {sr(S_ARGS + 16, 4)}, s[0:1], 0x40")
+    a(f"s_load_dwordx2 {sr(S_MAP, 2)}, s[0:1], 0x50")
     a("s_mov_b32 m0, 0")
     a(f"v_mov_b32 {vr(V_TID)}, v0")
     a("s_waitcnt lgkmcnt(0)")
@@ -229,8 +237,18 @@ def prologue_args(a: Asm):
     a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_XR)}")
     a(f"s_cmp_lg_u32 {sr(S_T1)}, {sr(S_T0)}")
     a(f"s_cbranch_scc1 {a.abort}")
+    # tile order: log2 group <= 6, nothing above the walk bit
+    a(f"s_and_b32 {sr(S_LG)}, {sr(S_MAP)}, 15")
+    a(f"s_cmp_gt_u32 {sr(S_LG)}, 6")
+    a(f"s_cbranch_scc1 {a.abort}")
+    a(f"s_cmp_ge_u32 {sr(S_MAP)}, {2 * MAP_WALK_COLS}")
+    a(f"s_cbranch_scc1 {a.abort}")
+    a(f"s_lshr_b32 {sr(S_WALK)}, {sr(S_MAP)}, 4")
     if SCHED["persist"]:
-        a(f"s_mov_b32 {sr(S_GRID)}, {sr(S_PG)}")        # persistent: the grid size (per_group slot)
+        # persistent: the grid size; 0 would walk one tile forever
+        a(f"s_cmp_eq_u32 {sr(S_KGRID)}, 0")
+        a(f"s_cbranch_scc1 {a.abort}")
+        a(f"s_mov_b32 {sr(S_GRID)}, {sr(S_KGRID)}")
         a(f"s_mov_b32 {sr(S_ITER)}, s2")
 
 
@@ -249,19 +267,24 @@ def tile_setup(a: Asm, epi: str, bid: str = "s2"):
     a(f"s_cmp_lt_u32 {sr(S_T0)}, {sr(S_XR)}")
     a(f"s_cselect_b32 {sr(S_TILE)}, {sr(S_T3)}, {sr(S_TILE)}")
     a(f"s_add_u32 {sr(S_TILE)}, {sr(S_TILE)}, {sr(S_T1)}")
-    # --- tile -> (tm, tn): groups of `group` row tiles walk the column tiles
-    grp = SCHED["group"]
-    lg = grp.bit_length() - 1
-    assert grp == 1 << lg
-    a(f"s_lshl_b32 {sr(S_PG)}, {sr(S_TN_N)}, {lg}")   # tiles per group (the kernarg's is not used)
-    udiv(a, S_Q, S_R, S_TILE, S_PG)                   # group, within
-    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, {lg}")      # first_m
-    a(f"s_sub_u32 {sr(S_T1)}, {sr(S_TM_N)}, {sr(S_T0)}")
-    a(f"s_min_u32 {sr(S_T1)}, {sr(S_T1)}, {grp}")     # gsz
+    # --- tile -> (tm, tn) by the kernarg map: groups of 2^lg tiles of the
+    # grouped dimension (rows; columns when the walk bit is set) walk the
+    # other dimension's tiles.  A = grouped tile count (S_E0), B = walked (S_E1)
+    a(f"s_cmp_eq_u32 {sr(S_WALK)}, 0")
+    a(f"s_cselect_b32 {sr(S_E0)}, {sr(S_TM_N)}, {sr(S_TN_N)}")
+    a(f"s_cselect_b32 {sr(S_E1)}, {sr(S_TN_N)}, {sr(S_TM_N)}")
+    a(f"s_lshl_b32 {sr(S_PG)}, {sr(S_E1)}, {sr(S_LG)}")   # tiles per group (the kernarg's is not used)
+    udiv(a, S_Q, S_R, S_TILE, S_PG)                     # group, within
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, {sr(S_LG)}")  # first tile of the group
+    a(f"s_sub_u32 {sr(S_T1)}, {sr(S_E0)}, {sr(S_T0)}")
+    a(f"s_lshl_b32 {sr(S_T2)}, 1, {sr(S_LG)}")
+    a(f"s_min_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_T2)}")  # gsz
     a(f"s_mov_b32 {sr(S_T2)}, {sr(S_R)}")
-    udiv(a, S_Q, S_R, S_T2, S_T1)                     # within / gsz, within % gsz
-    a(f"s_add_u32 {sr(S_TM)}, {sr(S_T0)}, {sr(S_R)}")
-    a(f"s_mov_b32 {sr(S_TN)}, {sr(S_Q)}")
+    udiv(a, S_Q, S_R, S_T2, S_T1)                       # within / gsz, within % gsz
+    a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_R)}")   # grouped-dimension tile
+    a(f"s_cmp_eq_u32 {sr(S_WALK)}, 0")
+    a(f"s_cselect_b32 {sr(S_TM)}, {sr(S_T0)}, {sr(S_Q)}")
+    a(f"s_cselect_b32 {sr(S_TN)}, {sr(S_Q)}, {sr(S_T0)}")
 
     # --- buffer resources at the tile's first row / column
     # X: rows tm*256 .. +255, every k
@@ -370,7 +393,8 @@ def prologue_lanes(a: Asm, epi: str):
     a(f"v_xor_b32 {vr(V_RXT)}, {vr(V_RXT)}, {vr(V_RX)}")
     a(f"v_add_u32 {vr(V_RWT)}, {STAGE}, {vr(V_RW)}")
     a(f"v_xor_b32 {vr(V_RWT)}, {vr(V_RWT)}, {vr(V_RW)}")
-    zero_acc(a)
+    if not SCHED["zero_late"]:
+        zero_acc(a)
 
 
 def zero_acc(a: Asm):
@@ -418,7 +442,8 @@ def mfma(i: int, j: int, sub: int) -> str:
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
-         "align": True, "drain_end": False, "map": "spread", "persist": False, "dual": ""}
+         "align": True, "drain_end": False, "map": "lib0", "persist": False, "dual": "", "zero_late": True,
+         "nostore": False}
 
 
 def _stamp(k: int) -> str:
@@ -601,7 +626,6 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
         slots[n].append(frag_read("w", i, 1))
     assert max(m["x1"]) < m["xbar"] and max(m["w1"]) < m["wbar"] and max(m["x1"] + m["w1"]) < 63
     tm, sp = SCHED["timing"] == 1, SCHED["timing"] == 2
-    assert not (split and tm), "the wait-timing kernel stamps an unsplit wait + barrier"
     if with_dma:
         for bar in (m["xbar"], m["wbar"]):
             slots[bar].append("s_waitcnt lgkmcnt(0)")
@@ -629,10 +653,16 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
         vm = sum(1 for n in m["xdma"] + m["wdma"] if n < m["wait"])
     else:
         vm = 0
+    def stamp_around(k, n):
+        """stamp k before the wait in slot n, stamp k+1 right after its
+        barrier (slot n + split; with a split the MFMA between them counts)"""
+        slots[n].insert(slots[n].index(next(x for x in slots[n] if x.startswith("s_waitcnt"))), _stamp(k))
+        b = slots[n + split]
+        b.insert(b.index("s_barrier") + 1, _stamp(k + 1))
+
     if with_dma and tm:  # waits: X-free and W-free barriers (the vm wait below)
         for k, bar in ((2, m["xbar"]), (4, m["wbar"])):
-            slots[bar].insert(0, _stamp(k))
-            slots[bar].insert(3, _stamp(k + 1))
+            stamp_around(k, bar)
     if with_dma and sp:  # stretches: X pieces, W pieces before the wait, W pieces after it
         (x0, x1), (w0, w1), (v0, v1) = span_slots(m)
         for k, (lo, hi) in enumerate(((x0, x1), (w0, w1), (v0, v1))):
@@ -643,13 +673,11 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
         wait = [f"s_waitcnt vmcnt({vm if with_dma else vm_after_dma})"]
         toggles = [f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}",
                    f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}"]
-        if split:
-            slots[w] += wait
-            slots[w + split] += ["s_barrier"] + toggles
-            assert min(m["x0"] + m["w0"]) > w + split
-        else:
-            slots[w] += ([_stamp(0)] if (tm and with_dma) else []) + wait + ["s_barrier"] + (
-                [_stamp(1)] if (tm and with_dma) else []) + toggles
+        slots[w] += wait
+        slots[w + split] += ["s_barrier"] + toggles
+        assert min(m["x0"] + m["w0"]) > w + split
+        if tm and with_dma:
+            stamp_around(0, w)
         assert min(m["x0"] + m["w0"]) > w and max(m["x0"] + m["w0"]) < 126
         for j, n in enumerate(m["x0"]):
             slots[n].append(frag_read("x", j, 0))
@@ -759,7 +787,8 @@ def epilogue_plain(a: Asm):
         for p in range(4):
             cvt_pack8(a, pk + 4 * p, f + 8 * p)
         for p in range(4):
-            store16(a, pk + 4 * p, V_E, SRD_C, S_E0, p)
+            if not SCHED["nostore"]:
+                store16(a, pk + 4 * p, V_E, SRD_C, S_E0, p)
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
 
 
@@ -902,6 +931,10 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
             a(ins)
     # --- prologue DMA: tile 0 -> stage 0, tile 1 -> stage 1
     prologue_dma(a)
+    if SCHED["zero_late"]:
+        # 256 accumulator writes while the first tiles are in flight, not
+        # ahead of their DMA (~1k issue cycles per tile off the critical path)
+        zero_acc(a)
     # both stages toggled twice: M0 bases are back at stage 0 for tile 2
     a("s_waitcnt vmcnt(16)")                       # own tile-0 pieces
     a("s_barrier")                                 # everyone's
@@ -1199,15 +1232,11 @@ PROBE_WORDS = PROBE_VBASE + 8 * 256
 # (scripts/asm_gemm_bench.py --variants): layout / schedule knobs against the
 # product kernel, measured in one process.  Index 0 is the product kernel.
 PLAIN_VARIANTS = (
-    ("v1", {"map": ""}),                    # round-4 slot schedule (pieces bunched after each barrier)
-    ("v2", {"map": "spread2"}),
-    ("v3", {"map": "spread3"}),
-    ("v4", {"group": 2}),
-    ("v5", {"persist": True}),              # persistent: a workgroup per CU walks its tiles, next tile staged under the epilogue
-    ("v6", {"map": "lib0"}),                # split waits, lagged M0 / resource advances
-    ("v7", {"map": "lib0", "dual": "lib1"}),  # + the odd-SIMD body
-    ("v8", {"map": "lib0", "dual": "lib1", "align": False}),  # + MFMAs where they fall (no s_nop padding)
-    ("v9", {"map": "lib0", "align": False}),
+    ("v1", {"map": "spread", "zero_late": False}),   # the round-4 product kernel
+    ("v2", {"zero_late": False}),           # accumulators zeroed ahead of the prologue DMA (round 4)
+    ("v3", {"persist": True}),              # persistent: a workgroup per CU walks its tiles, next tile staged under the epilogue
+    ("v4", {"nostore": True, "diag": True}),  # DIAGNOSTIC: no C stores (what the epilogue's stores cost); C is not written
+    ("v5", {"dual": "lib1"}),               # the library's second loop body on odd SIMDs
 )
 # measured (profiles/r4_asm_gemm/ab1..diag2): MFMAs on 8-byte boundaries, ending
 # with the epilogue's stores in flight, two barriers per tile and the wait 16
@@ -1217,7 +1246,11 @@ PLAIN_VARIANTS = (
 # next-tile wait at MFMA 95 and the X-free barrier 16 MFMAs after the last X
 # read taken into the product kernel (+1..+4 %); an L2 prefetch of the tile two
 # beyond the DMA (one 4-B load per line, its own bounded resources) -16..-24 %
-# (profiles/r4_asm_gemm/ab3): the extra loads share the counted vmcnt waits
+# (profiles/r4_asm_gemm/ab3): the extra loads share the counted vmcnt waits.
+# Round 5 (profiles/r5_lib/forms.log): the "lib0" placement (barriers one MFMA
+# after their waits, M0 / resource advances one MFMA after the pieces) +0.5..2 %
+# over "spread" at every form, taken into the product kernel; the library's
+# second loop body for odd SIMDs (with and without MFMA alignment) -1..-3 %.
 
 
 def _with_knobs(knobs: dict, fn):

@@ -5,7 +5,7 @@ from __future__ import annotations
 
 import struct
 
-from gemm_gen import KARG, KARG_BYTES  # noqa: E402  (csrc/asm on sys.path)
+from gemm_gen import KARG, KARG_BYTES, MAP_DEFAULT  # noqa: E402  (csrc/asm on sys.path)
 
 
 def grid_params(tiles_m: int, tiles_n: int):
@@ -13,18 +13,38 @@ def grid_params(tiles_m: int, tiles_n: int):
     return nwg, nwg >> 3, nwg & 7, 8 * tiles_n
 
 
-def pack(X, W, C, S, ldx_b, ldw_b, ldc_b, lds_b, K, tiles_m, tiles_n, fw_b=0, fc_b=0, grid=None) -> bytes:
-    """grid: a persistent kernel's workgroup count (in the per_group slot,
-    which the non-persistent kernels do not read)."""
+def pack(X, W, C, S, ldx_b, ldw_b, ldc_b, lds_b, K, tiles_m, tiles_n, fw_b=0, fc_b=0, grid=None,
+         tile_map=MAP_DEFAULT) -> bytes:
+    """grid: a persistent kernel's workgroup count; tile_map: the tile order
+    (gemm_gen.KARG "map": log2 group | 16 for column groups)."""
     nwg, xq, xr, pg = grid_params(tiles_m, tiles_n)
-    if grid is not None:
-        pg = grid
     buf = bytearray(KARG_BYTES)
     struct.pack_into("<QQQQ", buf, KARG["X"], X, W, C, S)
     struct.pack_into("<IIII", buf, KARG["ldx"], ldx_b, ldw_b, ldc_b, lds_b)
     struct.pack_into("<IIIIII", buf, KARG["ktiles"], K // 64, tiles_m, tiles_n, xq, xr, pg)
     struct.pack_into("<II", buf, KARG["fw"], fw_b, fc_b)
+    struct.pack_into("<II", buf, KARG["map"], tile_map, grid or 0)
     return bytes(buf)
+
+
+def tile_order(tiles_m: int, tiles_n: int, tile_map: int = MAP_DEFAULT) -> list[tuple[int, int]]:
+    """(tm, tn) of workgroups 0, 1, ... as the prologue computes them: the
+    XCD remap (workgroups b, b + 8, ... share an XCD; each XCD gets a
+    contiguous range of the tile order), then groups of 2^lg tiles of the
+    grouped dimension walking the other one."""
+    nwg, xq, xr, _ = grid_params(tiles_m, tiles_n)
+    lg, walk = tile_map & 15, tile_map >> 4
+    a_n, b_n = (tiles_n, tiles_m) if walk else (tiles_m, tiles_n)
+    out = []
+    for b in range(nwg):
+        xcd, bq = b & 7, b >> 3
+        tile = (xcd * (xq + 1) if xcd < xr else xr * (xq + 1) + (xcd - xr) * xq) + bq
+        group, within = divmod(tile, b_n << lg)
+        first = group << lg
+        gsz = min(a_n - first, 1 << lg)
+        ta, tb = first + within % gsz, within // gsz
+        out.append((tb, ta) if walk else (ta, tb))
+    return out
 
 
 def wgrad_plan(M: int, N: int, K: int) -> tuple[int, int]:

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -32,14 +33,13 @@ namespace {
 
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
-       K_WGRAD = 7, K_V1 = 8, K_N = 17 };
+       K_WGRAD = 7, K_V1 = 8, K_N = 13 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
                            "toa_gemm_tn_asm_timing2",  "toa_wgrad_nt_asm",           "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
-                           "toa_gemm_tn_asm_plain_v5", "toa_gemm_tn_asm_plain_v6", "toa_gemm_tn_asm_plain_v7",
-                           "toa_gemm_tn_asm_plain_v8", "toa_gemm_tn_asm_plain_v9"};
+                           "toa_gemm_tn_asm_plain_v5"};
 
 struct DevModule {
   std::once_flag once;
@@ -70,15 +70,21 @@ struct __attribute__((packed)) Args {
   uint32_t ldx, ldw, ldc, lds;  // bytes
   uint32_t ktiles, tiles_m, tiles_n, xq, xr, per_group;
   uint32_t fw, fc;  // swiglu: up-half row offset in W (bytes) / column offset in gu (bytes)
+  uint32_t map;     // tile order: log2 group | 16 = column groups walk the rows (gemm_gen.py KARG)
+  uint32_t grid;    // persistent kernels: the workgroup count
+  uint32_t pad[2];
 };
-static_assert(sizeof(Args) == 80, "kernarg block must match csrc/asm/gemm_gen.py KARG_BYTES");
+static_assert(sizeof(Args) == 96, "kernarg block must match csrc/asm/gemm_gen.py KARG_BYTES");
+
+constexpr uint32_t kMapDefault = 2;  // groups of 4 row tiles walk the column tiles
+constexpr uint32_t kMapWalkCols = 16;
 
 bool ld_ok(int64_t ld, int64_t min_cols) { return ld >= min_cols && ld % 8 == 0 && ld * 2 * 256 < (1ll << 32); }
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // A/B arms that walk several tiles per workgroup (gemm_gen.py SCHED
 // "persist"), by variant number 1..: their grid is one workgroup per CU.
-constexpr bool kVariantPersist[K_N - K_V1] = {false, false, false, false, true, false, false, false, false};
+constexpr bool kVariantPersist[K_N - K_V1] = {false, false, true, false, false};
 constexpr unsigned kPersistGrid = 256;
 
 int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
@@ -89,8 +95,33 @@ int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
   size_t sz = sizeof(k);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned nwg = grid ? grid : a.tiles_m * a.tiles_n;
-  if (grid) k.per_group = grid;  // the persistent kernels read their grid size here
+  if (grid) k.grid = grid;  // the persistent kernels read their grid size here
   return (int)hipModuleLaunchKernel(fn, nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
+}
+
+// Tile order (kernarg `map`) per shape.  The 256 workgroups in flight walk K
+// in step, so what they share is re-read from L2 / the Infinity Cache, and what
+// a group order makes them re-read from HBM is the cost: with row groups of G
+// tiles, all of W is streamed once per group (tiles_m / G times); with column
+// groups, all of X once per column group.  Where the streamed operand does not
+// fit the 256 MiB Infinity Cache next to the other (W of the LM head: 1 GiB),
+// take the order that re-streams fewer bytes.  Override: TOA_ASM_TILE_MAP.
+uint32_t tile_map(uint32_t tiles_m, uint32_t tiles_n, uint32_t ktiles, int64_t ldx, int64_t ldw) {
+  static const int forced = [] {
+    const char* e = getenv("TOA_ASM_TILE_MAP");
+    return (e && *e) ? atoi(e) : -1;
+  }();
+  if (forced >= 0 && forced < 32 && (forced & 15) <= 6) return (uint32_t)forced;
+  (void)ldx;
+  (void)ldw;
+  const double kb = (double)ktiles * 64 * 2;             // bytes per row of an operand
+  const double x_bytes = (double)tiles_m * 256 * kb;     // X rows of this GEMM
+  const double w_bytes = (double)tiles_n * 256 * kb;
+  const double rows_walk = x_bytes + w_bytes * ((tiles_m + 3) / 4);        // row groups of 4
+  const double cols_walk = w_bytes + x_bytes * ((tiles_n + 15) / 16);      // column groups of 16
+  const double mall = 192.0 * (1 << 20);
+  if (w_bytes > mall && cols_walk < rows_walk) return kMapWalkCols | 4;
+  return kMapDefault;
 }
 
 Args base_args(const void* X, int64_t ldx, const void* W, int64_t ldw, void* C, int64_t ldc, int M, int tiles_n,
@@ -110,6 +141,7 @@ Args base_args(const void* X, int64_t ldx, const void* W, int64_t ldw, void* C, 
   a.xq = nwg >> 3;
   a.xr = nwg & 7;
   a.per_group = 8 * a.tiles_n;
+  a.map = tile_map(a.tiles_m, a.tiles_n, a.ktiles, ldx, ldw);
   return a;
 }
 
@@ -145,6 +177,18 @@ extern "C" int toa_gemm_asm_variant(int v, const bf16_t* X, int64_t ldx, const b
     return launch(K_V1 + v - 1, a, stream, tiles < kPersistGrid ? tiles : kPersistGrid);
   }
   return launch(v == 0 ? K_PLAIN : K_V1 + v - 1, a, stream);
+}
+
+// A/B: the product kernel with an explicit tile order (kernarg `map`, see
+// tile_map) instead of the per-shape choice.
+extern "C" int toa_gemm_asm_map(int map, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C,
+                                int64_t ldc, int M, int N, int K, hipStream_t stream) {
+  if (map < 0 || map >= 32 || (map & 15) > 6 || !common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 ||
+      !ld_ok(ldc, N) || !al16(C))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  a.map = (uint32_t)map;
+  return launch(K_PLAIN, a, stream);
 }
 
 // Diagnostic: the product kernel with s_memtime stamps (csrc/asm/gemm_gen.py

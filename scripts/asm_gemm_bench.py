@@ -56,6 +56,13 @@ def asm_variant(v, x, w, y):
               M, N, K, _lib.stream(x))
 
 
+def asm_map(tmap, x, w, y):
+    M, K = x.shape
+    N = w.shape[0]
+    _lib.call("toa_gemm_asm_map", tmap, _lib.ptr(x), x.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), y.stride(0),
+              M, N, K, _lib.stream(x))
+
+
 def rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm())
 
@@ -304,6 +311,7 @@ def bench(a):
     torch.manual_seed(0)
     out = {"tokens": T, "forms": {}}
     variants = [int(v) for v in a.variants.split(",") if v]
+    maps = [int(v) for v in a.maps.split(",") if v]
     for name, (K, N) in FORMS.items():
         for kind, (kk, nn) in (("fwd", (K, N)), ("dgrad_wt", (N, K))):
             if a.forms and f"{name}.{kind}" not in a.forms.split(","):
@@ -317,6 +325,8 @@ def bench(a):
             yv = torch.empty_like(y)
             for v in variants:
                 arms.append((f"asm_v{v}", lambda v=v: asm_variant(v, x, w, yv)))
+            for tm_ in maps:
+                arms.append((f"asm_map{tm_}", lambda tm_=tm_: asm_map(tm_, x, w, yv)))
             ts = {k: [] for k, _ in arms}
             for _ in range(a.rounds):
                 for k, f in arms:
@@ -326,6 +336,9 @@ def bench(a):
             for v in variants:
                 asm_variant(v, x, w, yv)
                 same[f"asm_v{v}"] = bool(torch.equal(y, yv))
+            for tm_ in maps:
+                asm_map(tm_, x, w, yv)
+                same[f"asm_map{tm_}"] = bool(torch.equal(y, yv))
             err = rel(y, x.float() @ w.float().t()) if T * nn <= 24576 * 28672 else -1.0
             fl = 2.0 * T * nn * kk
             rec = {k: {"ms": round(statistics.median(v), 4), "TFps": round(fl / statistics.median(v) / 1e9, 1)}
@@ -369,6 +382,7 @@ def main():
     ap.add_argument("--forms", default="")
     ap.add_argument("--mlp", type=int, default=1)
     ap.add_argument("--variants", default="", help="plain-kernel A/B arms to add, e.g. 1,2,3")
+    ap.add_argument("--maps", default="", help="tile orders to add as arms (kernarg map words, e.g. 2,3,18,20)")
     ap.add_argument("--timing", action="store_true", help="wait-cycle breakdown of the product kernel (--forms)")
     ap.add_argument("--wgrad", action="store_true", help="weight-gradient forms: asm NT vs HIP vs hipBLASLt")
     ap.add_argument("--wgrad-splits", default="", help="extra asm arms with every tile cut into S K-pieces, e.g. 1,2,3")

@@ -60,7 +60,7 @@ def test_asm_gemm_plain_emulated(M, N, K):
     assert np.mean(np.abs(C - tof(bf16(ref))) <= np.abs(ref) * 2 ** -7) > 0.999
 
 
-@pytest.mark.parametrize("variant", [v for v, _ in gemm_gen.PLAIN_VARIANTS])
+@pytest.mark.parametrize("variant", [v for v, k in gemm_gen.PLAIN_VARIANTS if not k.get("diag")])
 def test_asm_gemm_variants_match_product_kernel(variant):
     """Each A/B arm of the plain kernel (other LDS pad, DMA spacing, wait slot,
     row-group size) writes exactly the product kernel's C on a 5 x 2 grid."""
@@ -69,11 +69,14 @@ def test_asm_gemm_variants_match_product_kernel(variant):
     X = bf16(rng.standard_normal((M, K)))
     W = bf16(rng.standard_normal((N, K)))
     out = []
+    persist = dict(gemm_gen.PLAIN_VARIANTS)[variant].get("persist")
     for name in ("toa_gemm_tn_asm_plain", f"toa_gemm_tn_asm_plain_{variant}"):
         mem = emu.Memory()
         ax, aw, ac = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16))
-        karg = host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256)
-        run_all(name, karg, (M // 256) * (N // 256), mem)
+        nwg = (M // 256) * (N // 256)
+        karg = host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256,
+                              grid=nwg if persist else None)
+        run_all(name, karg, nwg, mem)
         out.append(mem.bufs[2][1].view(np.uint16).reshape(M, N).copy())
     assert np.array_equal(out[0], out[1])
     close(tof(out[0]), tof(X) @ tof(W).T)
@@ -171,23 +174,60 @@ def test_asm_gemm_swiglu_bwd_emulated():
     close(dgu[:, F:], ds * g * sg)
 
 
-@pytest.mark.parametrize("grp", [2, 4, 8, 16])
-def test_asm_gemm_tile_order_is_a_bijection(grp):
-    """The XCD remap + row-group walk visits every (tm, tn) exactly once, for
-    grids that are and are not multiples of 8 and of the group size (the
-    formulas the prologue implements)."""
+@pytest.mark.parametrize("tile_map", [0, 1, 2, 3, 4, 16, 17, 18, 19, 20])
+def test_asm_gemm_tile_order_is_a_bijection(tile_map):
+    """The XCD remap + group walk (row groups, or column groups with the walk
+    bit) visits every (tm, tn) exactly once, for grids that are and are not
+    multiples of 8 and of the group size (the formulas the prologue
+    implements, host_args.tile_order)."""
     for tm_n, tn_n in ((1, 1), (3, 5), (96, 16), (7, 9), (96, 501)):
-        nwg, xq, xr, _ = host_args.grid_params(tm_n, tn_n)
-        pg = grp * tn_n
-        seen = set()
-        for b in range(nwg):
-            xcd, bq = b & 7, b >> 3
-            tile = (xcd * (xq + 1) if xcd < xr else xr * (xq + 1) + (xcd - xr) * xq) + bq
-            group, within = divmod(tile, pg)
-            first = group * grp
-            gsz = min(tm_n - first, grp)
-            seen.add((first + within % gsz, within // gsz))
-        assert seen == {(i, j) for i in range(tm_n) for j in range(tn_n)}
+        seen = host_args.tile_order(tm_n, tn_n, tile_map)
+        assert len(seen) == tm_n * tn_n
+        assert set(seen) == {(i, j) for i in range(tm_n) for j in range(tn_n)}
+
+
+@pytest.mark.parametrize("tile_map", [0, 18, 20])
+def test_asm_gemm_tile_maps_emulated(tile_map):
+    """Other tile orders (single row tiles; column groups of 4 and 16) write
+    the default order's C bit for bit: each tile's arithmetic is the same,
+    only which workgroup computes it changes."""
+    rng = np.random.default_rng(17)
+    M, N, K = 768, 1280, 128
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)))
+    outs = []
+    for tmap in (gemm_gen.MAP_DEFAULT, tile_map):
+        mem = emu.Memory()
+        ax, aw, ac = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16))
+        karg = host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256, tile_map=tmap)
+        run_all("toa_gemm_tn_asm_plain", karg, (M // 256) * (N // 256), mem)
+        outs.append(mem.bufs[2][1].view(np.uint16).reshape(M, N).copy())
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_asm_gemm_persistent_refuses_zero_grid():
+    """A persistent arm given grid 0 (it would walk its first tile forever)
+    ends before any memory access."""
+    name = next(f"toa_gemm_tn_asm_plain_{v}" for v, k in gemm_gen.PLAIN_VARIANTS if k.get("persist"))
+    M, N, K = 256, 256, 128
+    mem = emu.Memory()
+    ax, aw = mem.add(np.ones((M, K), np.uint16)), mem.add(np.ones((N, K), np.uint16))
+    ac = mem.add(np.full((M, N), 7, np.uint16))
+    run_all(name, host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, 1, 1, grid=0), 1, mem)
+    assert (mem.bufs[2][1].view(np.uint16) == 7).all()
+
+
+def test_asm_gemm_rejects_bad_tile_map():
+    """A map word the host never packs (log2 group > 6, bits above the walk
+    flag) ends every workgroup before any memory access: C untouched."""
+    M, N, K = 256, 256, 128
+    for bad in (7, 15, 32, 1 << 20):
+        mem = emu.Memory()
+        ax, aw = mem.add(np.ones((M, K), np.uint16)), mem.add(np.ones((N, K), np.uint16))
+        ac = mem.add(np.full((M, N), 7, np.uint16))
+        karg = host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, 1, 1, tile_map=bad)
+        run_all("toa_gemm_tn_asm_plain", karg, 1, mem)
+        assert (mem.bufs[2][1].view(np.uint16) == 7).all()
 
 
 def test_host_kernel_table_matches_generator():
