@@ -88,6 +88,7 @@ _SIGS = {
     "toa_host_free": [c_p],
     "toa_gemm_asm_stage": [c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_variant": [c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
+    "toa_gemm_asm_map": [c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_timing": [c_int, c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_probe": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_attn_set_bwd_variant": [c_int],
@@ -158,10 +159,22 @@ def has(name: str) -> bool:
     return available() and hasattr(_lib, name)
 
 
+# launchers whose argument / result types _load sets outside _SIGS
+_TYPED_ELSEWHERE = {"toa_bn_ws_floats", "toa_attn_bwd_ws_bytes", "toa_host_coherent_alloc", "toa_wgrad_workspace"}
+
+
+def _fn(name: str):
+    """The launcher, refusing one without declared argument types: ctypes
+    would pass Python ints as 32-bit C ints, and a 64-bit parameter (a row
+    stride) would arrive with garbage in its upper half."""
+    if name not in _SIGS and name not in _TYPED_ELSEWHERE:
+        raise KeyError(f"{name}: no ctypes signature in ops/_lib.py _SIGS")
+    return getattr(lib(), name)
+
+
 def call(name: str, *args):
     """Invoke launcher `name`; raise on a non-zero hipError_t."""
-    fn = getattr(lib(), name)
-    rc = fn(*args)
+    rc = _fn(name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")
     return rc
@@ -169,7 +182,7 @@ def call(name: str, *args):
 
 def call_ret(name: str, *args) -> int:
     """Invoke `name` and return its int result (no error check)."""
-    return getattr(lib(), name)(*args)
+    return _fn(name)(*args)
 
 
 def stream(t: torch.Tensor | None = None):
