@@ -305,6 +305,9 @@ def tile_setup(a: Asm, epi: str, bid: str = "s2"):
 def tile_c(a: Asm, epi: str):
     """SRD_C (and SRD_S) of the tile at (S_TM, S_TN)."""
     # C (and S): rows tm*256, columns tn*256 (tn*128 for the gate|up epilogue)
+    if SCHED["store_same"]:   # DIAGNOSTIC arm: every workgroup stores tile (0, 0)
+        a(f"s_mov_b32 {sr(S_TM)}, 0")
+        a(f"s_mov_b32 {sr(S_TN)}, 0")
     a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
     mul64(a, S_T2, S_T3, S_T0, S_LDC)
     a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TN)}, {8 if epi == 'swiglu_fwd' else 9}")  # column bytes
@@ -443,7 +446,7 @@ def mfma(i: int, j: int, sub: int) -> str:
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
          "align": True, "drain_end": False, "map": "lib0", "persist": False, "dual": "", "zero_late": True,
-         "nostore": False}
+         "nostore": False, "store_nt": True, "store_same": False}
 
 
 def _stamp(k: int) -> str:
@@ -774,7 +777,8 @@ def unpack8(a: Asm, dst: int, src: int):
 
 
 def store16(a: Asm, data: int, voff: int, srd_: int, soff: int, p: int):
-    a(f"buffer_store_dwordx4 {vr(data, 4)}, {vr(voff)}, {sr(srd_, 4)}, {sr(soff)} offen offset:{64 * p} nt")
+    nt = " nt" if SCHED["store_nt"] else ""
+    a(f"buffer_store_dwordx4 {vr(data, 4)}, {vr(voff)}, {sr(srd_, 4)}, {sr(soff)} offen offset:{64 * p}{nt}")
 
 
 def epilogue_plain(a: Asm):
@@ -1237,6 +1241,9 @@ PLAIN_VARIANTS = (
     ("v3", {"persist": True}),              # persistent: a workgroup per CU walks its tiles, next tile staged under the epilogue
     ("v4", {"nostore": True, "diag": True}),  # DIAGNOSTIC: no C stores (what the epilogue's stores cost); C is not written
     ("v5", {"dual": "lib1"}),               # the library's second loop body on odd SIMDs
+    ("v6", {"store_same": True, "diag": True}),  # DIAGNOSTIC: every workgroup stores tile (0, 0) (L2-hot writes)
+    ("v7", {"store_nt": False}),            # C stores without the non-temporal hint
+    ("v8", {"persist": True, "store_nt": False}),
 )
 # measured (profiles/r4_asm_gemm/ab1..diag2): MFMAs on 8-byte boundaries, ending
 # with the epilogue's stores in flight, two barriers per tile and the wait 16

@@ -33,13 +33,14 @@ namespace {
 
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
-       K_WGRAD = 7, K_V1 = 8, K_N = 13 };
+       K_WGRAD = 7, K_V1 = 8, K_N = 16 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
                            "toa_gemm_tn_asm_timing2",  "toa_wgrad_nt_asm",           "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
-                           "toa_gemm_tn_asm_plain_v5"};
+                           "toa_gemm_tn_asm_plain_v5", "toa_gemm_tn_asm_plain_v6", "toa_gemm_tn_asm_plain_v7",
+                           "toa_gemm_tn_asm_plain_v8"};
 
 struct DevModule {
   std::once_flag once;
@@ -84,7 +85,7 @@ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // A/B arms that walk several tiles per workgroup (gemm_gen.py SCHED
 // "persist"), by variant number 1..: their grid is one workgroup per CU.
-constexpr bool kVariantPersist[K_N - K_V1] = {false, false, true, false, false};
+constexpr bool kVariantPersist[K_N - K_V1] = {false, false, true, false, false, false, false, true};
 constexpr unsigned kPersistGrid = 256;
 
 int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
@@ -99,29 +100,24 @@ int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
   return (int)hipModuleLaunchKernel(fn, nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
 }
 
-// Tile order (kernarg `map`) per shape.  The 256 workgroups in flight walk K
-// in step, so what they share is re-read from L2 / the Infinity Cache, and what
-// a group order makes them re-read from HBM is the cost: with row groups of G
-// tiles, all of W is streamed once per group (tiles_m / G times); with column
-// groups, all of X once per column group.  Where the streamed operand does not
-// fit the 256 MiB Infinity Cache next to the other (W of the LM head: 1 GiB),
-// take the order that re-streams fewer bytes.  Override: TOA_ASM_TILE_MAP.
-uint32_t tile_map(uint32_t tiles_m, uint32_t tiles_n, uint32_t ktiles, int64_t ldx, int64_t ldw) {
+// Tile order (kernarg `map`) per shape, from the in-process form sweeps
+// (profiles/r5_lib2, r5_lib3; scripts/asm_gemm_bench.py --maps).  Both orders
+// keep 256 tiles in flight that share their operand strips through each
+// XCD's L2 and the Infinity Cache; what differs is how many distinct strips
+// the chip streams per k-step.  With a long reduction (K >= 8192: the down
+// projection, the wide data gradients) a strip is 4-65 MB, and column groups
+// of 4 tiles walking the rows (map 18) stream fewer of them: +1.5..3 % at
+// down.fwd / gate_up.dgrad / lm_head.dgrad.  At K = 4096..6144 row groups of
+// 4 (map 2) are as fast or 0.5..1 % faster.  Override: TOA_ASM_TILE_MAP.
+uint32_t tile_map(uint32_t tiles_m, uint32_t tiles_n, uint32_t ktiles) {
   static const int forced = [] {
     const char* e = getenv("TOA_ASM_TILE_MAP");
     return (e && *e) ? atoi(e) : -1;
   }();
   if (forced >= 0 && forced < 32 && (forced & 15) <= 6) return (uint32_t)forced;
-  (void)ldx;
-  (void)ldw;
-  const double kb = (double)ktiles * 64 * 2;             // bytes per row of an operand
-  const double x_bytes = (double)tiles_m * 256 * kb;     // X rows of this GEMM
-  const double w_bytes = (double)tiles_n * 256 * kb;
-  const double rows_walk = x_bytes + w_bytes * ((tiles_m + 3) / 4);        // row groups of 4
-  const double cols_walk = w_bytes + x_bytes * ((tiles_n + 15) / 16);      // column groups of 16
-  const double mall = 192.0 * (1 << 20);
-  if (w_bytes > mall && cols_walk < rows_walk) return kMapWalkCols | 4;
-  return kMapDefault;
+  (void)tiles_m;
+  (void)tiles_n;
+  return ktiles >= 128 ? (kMapWalkCols | 2) : kMapDefault;
 }
 
 Args base_args(const void* X, int64_t ldx, const void* W, int64_t ldw, void* C, int64_t ldc, int M, int tiles_n,
@@ -141,7 +137,7 @@ Args base_args(const void* X, int64_t ldx, const void* W, int64_t ldw, void* C, 
   a.xq = nwg >> 3;
   a.xr = nwg & 7;
   a.per_group = 8 * a.tiles_n;
-  a.map = tile_map(a.tiles_m, a.tiles_n, a.ktiles, ldx, ldw);
+  a.map = tile_map(a.tiles_m, a.tiles_n, a.ktiles);
   return a;
 }
 
