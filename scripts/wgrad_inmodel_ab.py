@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--arms", default="wgrad=asm+gemm=nosk,wgrad=hip+gemm=nosk,wgrad=asm+gemm=asm")
     ap.add_argument("--micro-batch", type=int, default=6)
+    ap.add_argument("--abba", type=int, default=1, help="reverse the arm order every other round")
     a = ap.parse_args()
     arms = a.arms.split(",")
     dev = torch.device("cuda", 0)
@@ -58,7 +59,10 @@ def main():
     torch.cuda.synchronize()
     times = {arm: [] for arm in arms}
     for r in range(a.rounds):
-        for arm in arms:
+        # ABBA: every other round runs the arms in reverse, so a linear drift
+        # (the chip warming over the run) does not favour the first arm
+        order = arms if (r % 2 == 0 or not a.abba) else arms[::-1]
+        for arm in order:
             apply(arm)
             tr.step(batch)  # one untimed step after the switch
             torch.cuda.synchronize()
@@ -69,8 +73,17 @@ def main():
             ms = (time.perf_counter() - t0) * 1e3 / a.steps
             times[arm].append(ms)
             print(json.dumps({"round": r, "arm": arm, "ms_per_step": round(ms, 2), "loss": float(loss)}), flush=True)
-    print(json.dumps({"median_ms_per_step": {k: round(statistics.median(v), 2) for k, v in times.items()},
-                      "all": times}))
+    out = {"median_ms_per_step": {k: round(statistics.median(v), 2) for k, v in times.items()}, "all": times}
+    if len(arms) >= 2 and a.rounds >= 2:
+        # paired per-round differences against the first arm: mean and its standard error
+        base = times[arms[0]]
+        for arm in arms[1:]:
+            d = [x - y for x, y in zip(times[arm], base)]
+            se = statistics.stdev(d) / len(d) ** 0.5
+            out.setdefault("paired_vs_" + arms[0], {})[arm] = {
+                "mean_ms": round(statistics.fmean(d), 2), "stderr_ms": round(se, 2),
+                "pct": round(100 * statistics.fmean(d) / statistics.fmean(base), 2)}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

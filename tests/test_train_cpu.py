@@ -233,6 +233,7 @@ def test_first_step_asm_scope(monkeypatch):
     tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device("cpu"), micro_batch=1, seq_len=16)
     monkeypatch.setattr(tr, "_step", lambda batches: seen.append(gemm._asm_first and tr.gemm_mode == "nosk"))
     monkeypatch.setattr(gemm, "_MODE", "nosk")
+    monkeypatch.setattr(tr, "gemm_mode", "nosk")  # the trainer resolved "auto" (asm) at construction
     tr.step([])
     tr.step_idx = 1
     tr.step([])

@@ -4,10 +4,10 @@
     linear_dgrad(dy, w)        dx = dy w             [M,N] x [N,K] -> [M,K]
     wgrad_acc_(g, dy, x)       g += dy^T x           (beta = 1, in place)
 
-The forward / data-gradient forms run on the hipBLASLt layer
-(csrc/hip/gemm.hip, one column-major call per form, see there for the
-transposition algebra) or, under ``TOA_GEMM=asm``, on the hand-written
-assembly kernel; the weight gradient on the assembly NT kernel
+The forward / data-gradient forms run on the hand-written assembly kernel
+(the default, ``TOA_GEMM=asm``) or on the hipBLASLt layer (csrc/hip/gemm.hip,
+one column-major call per form, see there for the transposition algebra;
+``TOA_GEMM=nosk``); the weight gradient on the assembly NT kernel
 (csrc/asm/wgrad_gen.py), with the HIP NT kernel (csrc/hip/wgrad.hip) as its
 fallback.
 The per-form solution tables measured by ``scripts/tune_gemm.py`` on an
@@ -34,7 +34,7 @@ Modes (``TOA_GEMM``):
   (profiles/r2_sk_contention; +6.7 % vs +3.4 % under emulated world-8
   ZeRO-1 traffic, profiles/r3_overlap).
 * ``auto`` (the default): resolved by :func:`resolve_auto` when the trainer
-  starts, to ``nosk``.
+  starts, to ``asm``.
 """
 from __future__ import annotations
 
@@ -71,15 +71,18 @@ def set_mode(m: str):
 
 
 def resolve_auto(world: int = 1) -> str:
-    """``auto`` -> ``nosk`` (an explicit TOA_GEMM is kept).  Returns the mode
-    in force.  ``asm`` stays opt-in until it wins in-model: the Llama-3-8B
-    step measured 946.3 ms on it against 930.1 ms on ``nosk`` (one process,
-    alternating windows, profiles/r4_wgrad/inmodel_ab.log), and a policy
-    using it only for the forms it wins in isolation 940.7 vs 936.7 ms
-    (profiles/r4_mixed/inmodel_ab.log)."""
+    """``auto`` -> ``asm`` (an explicit TOA_GEMM is kept).  Returns the mode
+    in force.  The assembly kernel with the library-form slot map, the
+    per-shape tile order and the fused SwiGLU epilogues wins in-model: the
+    Llama-3-8B step is 5.5 +- 1.6 ms faster than on ``nosk`` (12 ABBA rounds
+    in one process, profiles/r5_ab2/inmodel.log; 9.4 ms less kernel time
+    under rocprofv3, profiles/r5_prof1).  Like ``nosk`` it never holds the
+    whole chip (one workgroup per tile, no stream-K), so the data-parallel
+    collectives overlap it.  Round 4 measured the other way (946.3 vs 930.1
+    ms, profiles/r4_wgrad/inmodel_ab.log), before those changes."""
     del world
     if _MODE == "auto":
-        set_mode("nosk")
+        set_mode("asm")
     return _MODE
 
 

@@ -196,8 +196,8 @@ class _SwiGLUMLP(torch.autograd.Function):
 
 def swiglu_mlp(x, wgu, wd):
     """The Llama MLP, x -> swiglu(x Wgu^T) Wd^T, fused where the assembly
-    GEMM takes the shapes (TOA_GEMM=asm, the default), else the two-GEMM +
-    SwiGLU path."""
+    GEMM takes the shapes (policy ``asm``: the default since round 5, see
+    ops.gemm.resolve_auto), else the two-GEMM + SwiGLU path (``nosk``)."""
     if gemm.mode() == "asm":
         return _SwiGLUMLP.apply(x, wgu, wd)
     from .linear import linear
