@@ -1292,7 +1292,16 @@ def generate() -> str:
         metas.append(meta)
     import wgrad_gen  # the weight-gradient kernel shares this code object (lazy: it imports this module)
 
-    for body, meta in (wgrad_gen.kernel(), probe_kernel(), kernel("plain", trace=True),
+    def wgrad_round4():
+        saved = dict(wgrad_gen.KNOBS)
+        wgrad_gen.KNOBS.update(map="spread", zero_late=False)
+        try:
+            return wgrad_gen.kernel("v1")
+        finally:
+            wgrad_gen.KNOBS.clear()
+            wgrad_gen.KNOBS.update(saved)
+
+    for body, meta in (wgrad_gen.kernel(), wgrad_round4(), probe_kernel(), kernel("plain", trace=True),
                        _with_knobs({"timing": 1}, lambda: kernel("plain", variant="timing")),
                        _with_knobs({"timing": 2}, lambda: kernel("plain", variant="timing2"))):
         parts.append(body)

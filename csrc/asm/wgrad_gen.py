@@ -96,8 +96,10 @@ V_T = 136                                        # 136..139 scratch
 V_TGALO, V_TGAHI, V_TGBLO, V_TGBHI = 140, 141, 142, 143
 V_E = 144                                        # 144..255 epilogue scratch
 
-# slot map: the forward kernel's "spread" placement (gemm_gen.SLOT_MAPS)
-MAP = G.SLOT_MAPS["spread"]
+# slot map: the forward kernel's product placement (gemm_gen.SLOT_MAPS
+# "lib0": barriers one MFMA after their waits, M0 / resource advances one
+# MFMA behind the pieces); KNOBS["map"] selects another for an A/B arm
+KNOBS = {"map": "lib0", "zero_late": True}
 
 
 def prologue(a: Asm):
@@ -239,6 +241,11 @@ def prologue(a: Asm):
     for base, tg in ((V_RALO, V_TGALO), (V_RAHI, V_TGAHI), (V_RBLO, V_TGBLO), (V_RBHI, V_TGBHI)):
         a(f"v_add_u32 {vr(tg)}, {STAGE}, {vr(base)}")
         a(f"v_xor_b32 {vr(tg)}, {vr(tg)}, {vr(base)}")
+    if not KNOBS["zero_late"]:
+        zero_acc(a)
+
+
+def zero_acc(a: Asm):
     for i in range(256):
         a(f"v_accvgpr_write_b32 {ar(i)}, 0")
 
@@ -311,7 +318,10 @@ def mfma(i: int, j: int, sub: int) -> str:
 
 
 def iteration(a: Asm, with_dma: bool, next_reads: bool):
-    m = MAP
+    """One 64-row (t) tile on the forward kernel's slot map (the same keys:
+    split / m0_lag / adv, gemm_gen.iteration_map)."""
+    m = G.SLOT_MAPS[KNOBS["map"]]
+    split, lag = m.get("split", 0), m.get("m0_lag", 0)
     slots: dict[int, list[str]] = {n: [] for n in range(128)}
     for j, n in enumerate(m["x1"]):
         slots[n] += frag_reads("a", j, 1)
@@ -319,24 +329,30 @@ def iteration(a: Asm, with_dma: bool, next_reads: bool):
         slots[n] += frag_reads("b", i, 1)
     vm = 0
     if with_dma:
-        slots[m["xbar"]] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
-        slots[m["wbar"]] += ["s_waitcnt lgkmcnt(0)", "s_barrier"]
-        for half, key in (("a", "xdma"), ("b", "wdma")):
+        for bar in (m["xbar"], m["wbar"]):
+            slots[bar].append("s_waitcnt lgkmcnt(0)")
+            slots[bar + split].append("s_barrier")
+        for half, key, bar in (("a", "xdma", m["xbar"]), ("b", "wdma", m["wbar"])):
             srd_, vo, so, m0 = dma_pieces(half)
             p = m[key]
+            assert p[0] > bar + split
             slots[p[0] - 1].append(f"s_mov_b32 m0, {sr(m0)}")
             for j, n in enumerate(p):
                 soff = "0" if j == 0 else sr(so + j - 1)
                 slots[n].append(f"buffer_load_dwordx4 {vr(vo)}, {sr(srd_, 4)}, {soff} offen lds")
                 if j < 7:
-                    slots[n].append(f"s_add_u32 m0, m0, {blockbase(j + 1) - blockbase(j)}")
-            slots[p[-1]] += advance(half) + [f"s_xor_b32 {sr(m0)}, {sr(m0)}, {sr(m0 + 1)}"]
+                    assert p[j + 1] > n + lag
+                    slots[n + lag].append(f"s_add_u32 m0, m0, {blockbase(j + 1) - blockbase(j)}")
+            adv = m.get("adv", {}).get("x" if half == "a" else "w", p[-1])
+            slots[adv] += advance(half) + [f"s_xor_b32 {sr(m0)}, {sr(m0)}, {sr(m0 + 1)}"]
         vm = sum(1 for n in m["xdma"] + m["wdma"] if n < m["wait"])
     if next_reads:
         w = m["wait"]
-        slots[w] += [f"s_waitcnt vmcnt({vm})", "s_barrier"] + [
+        slots[w].append(f"s_waitcnt vmcnt({vm})")
+        slots[w + split] += ["s_barrier"] + [
             f"v_xor_b32 {vr(b)}, {vr(b)}, {vr(t)}" for b, t in ((V_RALO, V_TGALO), (V_RAHI, V_TGAHI),
                                                                   (V_RBLO, V_TGBLO), (V_RBHI, V_TGBHI))]
+        assert min(m["x0"] + m["w0"]) > w + split
         for j, n in enumerate(m["x0"]):
             slots[n] += frag_reads("a", j, 0)
         for i, n in enumerate(m["w0"]):
@@ -413,9 +429,9 @@ def epilogue(a: Asm):
     a.label(l_end)
 
 
-def kernel() -> tuple[str, str]:
-    name = "toa_wgrad_nt_asm"
-    a = Asm(prefix="nt_")
+def kernel(variant: str = "") -> tuple[str, str]:
+    name = "toa_wgrad_nt_asm" + (f"_{variant}" if variant else "")
+    a = Asm(prefix="nt_" + (variant + "_" if variant else ""))
     a.raw(f".globl {name}")
     a.raw(".p2align 8")
     a.raw(f".type {name},@function")
@@ -433,6 +449,8 @@ def kernel() -> tuple[str, str]:
             a(ins)
     a(f"s_xor_b32 {sr(S_M0A)}, {sr(S_M0A)}, {sr(S_M0AT)}")
     a(f"s_xor_b32 {sr(S_M0B)}, {sr(S_M0B)}, {sr(S_M0BT)}")
+    if KNOBS["zero_late"]:
+        zero_acc(a)                             # under the first tiles' DMA flight
     a("s_waitcnt vmcnt(16)")                    # own tile-0 pieces
     a("s_barrier")
     for j in range(8):

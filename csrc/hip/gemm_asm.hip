@@ -33,14 +33,14 @@ namespace {
 
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
-       K_WGRAD = 7, K_V1 = 8, K_N = 16 };
+       K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_N = 17 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
                            "toa_gemm_tn_asm_timing2",  "toa_wgrad_nt_asm",           "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
                            "toa_gemm_tn_asm_plain_v5", "toa_gemm_tn_asm_plain_v6", "toa_gemm_tn_asm_plain_v7",
-                           "toa_gemm_tn_asm_plain_v8"};
+                           "toa_gemm_tn_asm_plain_v8", "toa_wgrad_nt_asm_v1"};
 
 struct DevModule {
   std::once_flag once;
@@ -85,7 +85,7 @@ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // A/B arms that walk several tiles per workgroup (gemm_gen.py SCHED
 // "persist"), by variant number 1..: their grid is one workgroup per CU.
-constexpr bool kVariantPersist[K_N - K_V1] = {false, false, true, false, false, false, false, true};
+constexpr bool kVariantPersist[K_WGRAD_V1 - K_V1] = {false, false, true, false, false, false, false, true};
 constexpr unsigned kPersistGrid = 256;
 
 int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
@@ -269,8 +269,25 @@ extern "C" int toa_wgrad_split(int M, int N, int K);
 extern "C" int toa_wgrad_reduce(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem, int split,
                                 int beta, hipStream_t stream);
 
+static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C,
+                            int64_t ldc, float* W, int M, int N, int K, int split, int beta, hipStream_t stream);
+
 extern "C" int toa_wgrad_asm(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc,
                              float* W, int M, int N, int K, int split, int beta, hipStream_t stream) {
+  return wgrad_asm_launch(K_WGRAD, A, lda, B, ldb, C, ldc, W, M, N, K, split, beta, stream);
+}
+
+// A/B: variant v of the weight-gradient kernel (0 = product, 1 = the round-4
+// schedule: "spread" slot map, accumulators zeroed before the prologue DMA).
+extern "C" int toa_wgrad_asm_variant(int v, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C,
+                                     int64_t ldc, float* W, int M, int N, int K, int split, int beta,
+                                     hipStream_t stream) {
+  if (v < 0 || v > 1) return (int)hipErrorInvalidValue;
+  return wgrad_asm_launch(v ? K_WGRAD_V1 : K_WGRAD, A, lda, B, ldb, C, ldc, W, M, N, K, split, beta, stream);
+}
+
+static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C,
+                            int64_t ldc, float* W, int M, int N, int K, int split, int beta, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % 256 || N % 256 || split < 0 || split > 4 || !ld_ok(lda, M) ||
       !ld_ok(ldb, N) || !ld_ok(ldc, N) || !al16(A) || !al16(B) || !al16(C) || (lda * 2) * 64 >= (1ll << 31) ||
       (ldb * 2) * 64 >= (1ll << 31))
@@ -304,7 +321,7 @@ extern "C" int toa_wgrad_asm(const bf16_t* A, int64_t lda, const bf16_t* B, int6
   a.xr = (uint32_t)rem;
   a.per_group = (uint32_t)split;
   hipError_t err;
-  hipFunction_t fn = get_fn(K_WGRAD, &err);
+  hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};

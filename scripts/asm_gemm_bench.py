@@ -264,7 +264,13 @@ def wgrad(a):
             _lib.call("toa_wgrad_asm", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g), K, _lib.ptr(ws), N, K, T, 0, 0,
                       _lib.stream(dy))
 
-        arms = [("asm", asm_), ("hip", hip), ("blt", lambda: torch.mm(dy.t(), x))]
+        g3 = torch.empty_like(g)
+
+        def asm_v1():  # the round-4 schedule of the same kernel
+            _lib.call("toa_wgrad_asm_variant", 1, _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g3), K, _lib.ptr(ws), N,
+                      K, T, 0, 0, _lib.stream(dy))
+
+        arms = [("asm", asm_), ("asm_v1", asm_v1), ("hip", hip), ("blt", lambda: torch.mm(dy.t(), x))]
         for sp in (int(v) for v in a.wgrad_splits.split(",") if v):
             # every tile cut into `sp` K-pieces (1: none) instead of the auto plan
             if sp * (N // 256) * (K // 256) >= (1 << 14) or T % (64 * sp):
@@ -288,6 +294,9 @@ def wgrad(a):
         rec = {k: {"ms": round(statistics.median(v), 4), "TFps": round(fl / statistics.median(v) / 1e9, 1)}
                for k, v in ts.items()}
         rec["asm_vs_hip_rel"] = round(rel(g, g2), 6)
+        asm_v1()
+        torch.cuda.synchronize()
+        rec["asm_v1_bit_identical"] = bool(torch.equal(g, g3))
         res[f"{name}.wgrad"] = rec
         print(json.dumps({f"{name}.wgrad": rec}), flush=True)
         del dy, x, g, g2, ws

@@ -92,3 +92,27 @@ def test_wgrad_asm_k_pieces_emulated():
     tot = ws[:65536].reshape(256, 256).astype(np.float64) + ws[65536:131072].reshape(256, 256)
     err = np.abs(tot - ref).max() / np.abs(ref).max()
     assert err < 1e-5, err
+
+
+def test_wgrad_round4_arm_matches_product_kernel():
+    """The A/B arm with the round-4 schedule (toa_wgrad_nt_asm_v1: "spread"
+    slot map, accumulators zeroed before the prologue DMA) writes the product
+    kernel's C bit for bit, whole-K tiles and k-pieces."""
+    import gemm_gen
+
+    text = gemm_gen.generate()
+    M, N, T = 256, 512, 384
+    rng = np.random.default_rng(9)
+    A = bf16(rng.standard_normal((T, M)))
+    B = bf16(rng.standard_normal((T, N)))
+    outs = []
+    for name in ("toa_wgrad_nt_asm", "toa_wgrad_nt_asm_v1"):
+        mem = emu.Memory()
+        aa, ab, ac = mem.add(A), mem.add(B), mem.add(np.zeros((M, N), np.uint16))
+        aw = mem.add(np.zeros(65536 * 4, np.float32))
+        karg = host_args.pack_nt(aa, ab, ac, aw, 2 * M, 2 * N, 2 * N, 0, T, M // 256, N // 256, 0, 2)
+        e = emu.Emu(text, name)
+        for wg in range(4):
+            e.run(karg, wg, mem)
+        outs.append(mem.bufs[3][1].copy())
+    assert np.array_equal(outs[0], outs[1])

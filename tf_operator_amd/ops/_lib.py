@@ -68,6 +68,8 @@ _SIGS = {
     "toa_wgrad": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
     "toa_wgrad_split": [c_int, c_int, c_int],
     "toa_wgrad_asm": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
+    "toa_wgrad_asm_variant": [c_int, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_int,
+                              c_p],
     "toa_wgrad_reduce": [c_p, c_p, c_i64, c_int, c_int, c_int, c_int, c_int, c_int, c_p],
     "toa_transpose_bf16": [c_p, c_i64, c_p, c_i64, c_int, c_int, c_p],
     "toa_gemm": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p],
