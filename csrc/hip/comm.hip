@@ -200,3 +200,13 @@ extern "C" int toa_emulate_xfer(const void* src, void* dst, int64_t nbytes, int 
                      nbytes / 16, ticks_per_mib);
   return (int)hipGetLastError();
 }
+
+// One-GPU emulation of a CU-free all-gather (verdict r4 item 5): the bytes a
+// rank pulls from its peers, moved by a copy engine (hipMemcpyDeviceToDeviceNoCU:
+// SDMA, no workgroup on any CU) instead of a ring kernel's workgroups.  A copy
+// engine cannot be paced: it runs at its own rate, which
+// scripts/overlap_emulation.py reports next to the assumed bus rate.
+extern "C" int toa_emulate_copy_nocu(const void* src, void* dst, int64_t nbytes, hipStream_t stream) {
+  if (nbytes <= 0) return 0;
+  return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDeviceNoCU, stream);
+}

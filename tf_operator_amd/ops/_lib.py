@@ -100,6 +100,7 @@ _SIGS = {
     "toa_attn_bwd_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
                           c_int, c_f, c_p],
     "toa_emulate_xfer": [c_p, c_p, c_i64, c_int, ctypes.c_double, c_p],
+    "toa_emulate_copy_nocu": [c_p, c_p, c_i64, c_p],
     "toa_gemm_tune": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p, c_p, c_p,
                       c_p, c_p, c_int],
     "toa_gemm_kernel_name": [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_p, c_int],

@@ -18,7 +18,10 @@ trainer runs exactly rank 0's world-N step --
 on a high-priority side stream (bench.py runs RCCL's streams at high
 priority too): (N-1)/N x bucket bytes, paced to ``TOA_EMULATE_GBPS`` GB/s
 (default 350, an assumed RCCL bus bandwidth for 8 x MI355X over xGMI)
-on ``TOA_EMULATE_CHANNELS`` workgroups (default 32).
+on ``TOA_EMULATE_CHANNELS`` workgroups (default 32).  ``TOA_EMULATE_AG=sdma``
+moves the all-gathers' bytes with a copy engine instead
+(``toa_emulate_copy_nocu``: no workgroup on any CU, unpaced), the stand-in
+for pulling the peers' weight shards over xGMI by SDMA.
 
 The other ranks' shards are never updated (their "gathered" weights stay
 as they were), so the loss is meaningless; the TIME is rank 0's.  Compare
@@ -67,6 +70,9 @@ class CommEmulator:
         self.gbps = float(os.environ.get("TOA_EMULATE_GBPS", "350")) if gbps is None else float(gbps)
         self.channels = int(os.environ.get("TOA_EMULATE_CHANNELS", "32")) if channels is None else int(channels)
         self.move = (os.environ.get("TOA_EMULATE_BYTES", "1") != "0") if move_bytes is None else bool(move_bytes)
+        self.ag_mode = os.environ.get("TOA_EMULATE_AG", "ring")
+        if self.ag_mode not in ("ring", "sdma"):
+            raise ValueError(f"TOA_EMULATE_AG={self.ag_mode!r}: expected ring or sdma")
         self.stream = torch.cuda.Stream(device=self.device, priority=-1) if self.device.type == "cuda" else None
         self.scratch = None
         self.calls = 0
@@ -77,9 +83,10 @@ class CommEmulator:
             self.scratch = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         return self.scratch
 
-    def collective(self, buf: torch.Tensor):
+    def collective(self, buf: torch.Tensor, kind: str = "reduce_scatter"):
         """Emulate one rank's share of a reduce-scatter / all-gather of
-        `buf` (the whole bucket): (N-1)/N of its bytes, paced."""
+        `buf` (the whole bucket): (N-1)/N of its bytes, paced (an all-gather
+        under TOA_EMULATE_AG=sdma: by a copy engine, unpaced)."""
         nbytes = buf.numel() * buf.element_size() * (self.world - 1) // self.world // 16 * 16
         self.calls += 1
         if self.stream is None:
@@ -90,8 +97,11 @@ class CommEmulator:
             if self.move and nbytes > 0:
                 dst = self._scratch(nbytes)
                 buf.record_stream(self.stream)
-                _lib.call("toa_emulate_xfer", _lib.ptr(buf), _lib.ptr(dst), int(nbytes), self.channels,
-                          float(self.gbps), _lib.stream(dst))
+                if kind == "all_gather" and self.ag_mode == "sdma":
+                    _lib.call("toa_emulate_copy_nocu", _lib.ptr(buf), _lib.ptr(dst), int(nbytes), _lib.stream(dst))
+                else:
+                    _lib.call("toa_emulate_xfer", _lib.ptr(buf), _lib.ptr(dst), int(nbytes), self.channels,
+                              float(self.gbps), _lib.stream(dst))
                 self.bytes += nbytes
             ev = torch.cuda.Event()
             ev.record(self.stream)

@@ -98,7 +98,7 @@ class ParamGather:
         current stream already: the collective waits for that stream)."""
         lo, hi = self.ranges[b]
         if self.emu is not None:
-            self.works[b] = self.emu.collective(self.flat.param[lo:hi])
+            self.works[b] = self.emu.collective(self.flat.param[lo:hi], kind="all_gather")
         else:
             self.works[b] = all_gather_(self.flat.param[lo:hi], self.rank, self.world, self.group)
 
