@@ -66,6 +66,15 @@ class Memory:
         raise IndexError(f"address range {hex(int(addr.min()))}..{hex(int(addr.max()))} outside every buffer")
 
 
+# v_mfma_f32_32x32x16_bf16 D layout: register r of lane l holds row
+# (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31
+_LANES = np.arange(64)
+_ROW32 = np.array([(r & 3) + 8 * (r >> 2) + 4 * (_LANES >> 5) for r in range(16)])
+_COL32 = np.broadcast_to(_LANES & 31, (16, 64))
+# ds_read_b64_tr_b16: lane 16 G + i takes element i & 3 of lane 16 G + 4 q + (i >> 2)
+_TR_SRC = np.array([[16 * (l >> 4) + 4 * q + ((l & 15) >> 2) for q in range(4)] for l in range(64)])
+_TR_ELT = np.broadcast_to((_LANES & 3)[:, None], (64, 4))
+
 _REG = re.compile(r"^([vsa])(?:\[(\d+):(\d+)\]|(\d+))$")
 
 
@@ -365,10 +374,6 @@ class Emu:
     def op_v_sub_f32(self, w, a, m):
         self._vbin(w, a, lambda x, y: f2u(u2f(x) - u2f(y)))
 
-    def op_v_fma_f32(self, w, a, m):
-        x, y, z = (u2f(self.vget(w, t)).astype(np.float64) for t in a[1:4])
-        self.vset(w, a[0], f2u((x * y + z).astype(np.float32)))
-
     def op_v_exp_f32(self, w, a, m):
         self.vset(w, a[0], f2u(np.exp2(u2f(self.vget(w, a[1]))).astype(np.float32)))
 
@@ -403,6 +408,131 @@ class Emu:
     def op_v_lshl_add_u32(self, w, a, m):
         x, s, y = (self.vget(w, t) for t in a[1:4])
         self.vset(w, a[0], ((x.astype(np.uint64) << (s & 31)) + y) & M32)
+
+    # --- attention-forward subset (csrc/asm/attn_gen.py)
+    def op_v_max_f32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: f2u(np.maximum(u2f(x), u2f(y))))
+
+    def op_v_max3_f32(self, w, a, m):
+        x, y, z = (u2f(self.vget(w, t)) for t in a[1:4])
+        self.vset(w, a[0], f2u(np.maximum(np.maximum(x, y), z)))
+
+    def op_v_log_f32(self, w, a, m):
+        with np.errstate(divide="ignore"):
+            self.vset(w, a[0], f2u(np.log2(u2f(self.vget(w, a[1]))).astype(np.float32)))
+
+    def _fop(self, w, tok):
+        """A float operand with an optional leading '-' (VOP3 neg modifier)."""
+        if tok.startswith("-") and self._reg(w, tok[1:]) is not None:
+            return -u2f(self.vget(w, tok[1:]))
+        return u2f(self.vget(w, tok))
+
+    def op_v_fma_f32(self, w, a, m):
+        x, y, z = (self._fop(w, t).astype(np.float64) for t in a[1:4])
+        self.vset(w, a[0], f2u((x * y + z).astype(np.float32)))
+
+    def op_v_sub_u32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: (x.astype(np.int64) - y.astype(np.int64)) & M32)
+
+    def op_v_subrev_u32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: (y.astype(np.int64) - x.astype(np.int64)) & M32)
+
+    def op_v_or_b32(self, w, a, m):
+        self._vbin(w, a, lambda x, y: x | y)
+
+    def op_v_permlane32_swap_b32(self, w, a, m):
+        """lanes 32..63 of vdst <-> lanes 0..31 of vsrc."""
+        d0, _ = self.vrange(w, a[0])
+        s0, _ = self.vrange(w, a[1])
+        hi = w.v[d0, 32:].copy()
+        w.v[d0, 32:] = w.v[s0, :32]
+        w.v[s0, :32] = hi
+
+    def _mask(self, w, tok) -> np.ndarray:
+        if tok == "vcc":
+            v = w.vcc
+        else:
+            kind, lo, hi = self._reg(w, tok)
+            v = (int(w.s[lo]) & M32) | ((int(w.s[lo + 1]) & M32) << 32)
+        return np.array([(v >> l) & 1 for l in range(64)], dtype=bool)
+
+    def _set_mask(self, w, tok, bits: np.ndarray):
+        v = int(sum(1 << l for l in range(64) if bits[l]))
+        if tok == "vcc":
+            w.vcc = v
+        else:
+            kind, lo, hi = self._reg(w, tok)
+            w.s[lo], w.s[lo + 1] = v & M32, v >> 32
+
+    def op_v_cmp_gt_f32(self, w, a, m):
+        self._set_mask(w, a[0], u2f(self.vget(w, a[1])) > u2f(self.vget(w, a[2])))
+
+    def op_v_cmp_gt_i32(self, w, a, m):
+        x = self.vget(w, a[1]).view(np.int32)
+        y = self.vget(w, a[2]).view(np.int32)
+        self._set_mask(w, a[0], x > y)
+
+    def op_v_cmp_lt_i32(self, w, a, m):
+        x = self.vget(w, a[1]).view(np.int32)
+        y = self.vget(w, a[2]).view(np.int32)
+        self._set_mask(w, a[0], x < y)
+
+    def op_v_cndmask_b32(self, w, a, m):
+        """vdst = mask ? src1 : src0"""
+        sel = self._mask(w, a[3])
+        self.vset(w, a[0], np.where(sel, self.vget(w, a[2]), self.vget(w, a[1])))
+
+    def op_s_or_b64(self, w, a, m):
+        bits = self._mask(w, a[1]) | self._mask(w, a[2])
+        self._set_mask(w, a[0], bits)
+        w.scc = int(bits.any())
+
+    def op_s_mov_b64(self, w, a, m):
+        if a[1] == "vcc" or a[1].startswith("s["):
+            bits = self._mask(w, a[1])
+        else:
+            v = int(a[1], 0) & ((1 << 64) - 1)
+            bits = np.array([(v >> l) & 1 for l in range(64)], dtype=bool)
+        self._set_mask(w, a[0], bits)
+
+    def op_s_cmp_eq_u64(self, w, a, m):
+        x = self._mask(w, a[0])
+        v = int(a[1], 0)
+        y = np.array([(v >> l) & 1 for l in range(64)], dtype=bool)
+        w.scc = int((x == y).all())
+
+    def op_s_cbranch_vccz(self, w, a, m):
+        if w.vcc == 0:
+            w.pc = self.labels[a[0]]
+
+    def op_v_mfma_f32_32x32x16_bf16(self, w, a, m):
+        """D[32x32] = A[32x16] B[16x32] + C.  Lane l: A row l&31, k 8(l>>5)..+7;
+        B k 8(l>>5)..+7, column l&31; D/C register r: row (r&3) + 8(r>>2) +
+        4(l>>5), column l&31.  srcC may be the inline constant 0."""
+        d0, d1 = self.vrange(w, a[0])
+        a0, a1 = self.vrange(w, a[1])
+        b0, b1 = self.vrange(w, a[2])
+        assert d1 - d0 == 16 and a1 - a0 == 4 and b1 - b0 == 4
+
+        def elems(r0):
+            regs = w.v[r0:r0 + 4].T
+            out = np.empty((64, 8), dtype=np.uint32)
+            out[:, 0::2] = (regs & 0xFFFF) << 16
+            out[:, 1::2] = regs & 0xFFFF0000
+            return u2f(out)
+
+        ea, eb = elems(a0).astype(np.float64), elems(b0).astype(np.float64)
+        A = np.concatenate([ea[:32], ea[32:]], axis=1)        # [32 rows, 16 k]
+        B = np.concatenate([eb[:32], eb[32:]], axis=1).T      # [16 k, 32 cols]
+        D = A @ B
+        if a[3] == "0":
+            C = np.zeros((16, 64), np.float64)
+        else:
+            c0, c1 = self.vrange(w, a[3])
+            assert c1 - c0 == 16
+            C = u2f(w.v[c0:c0 + 16]).astype(np.float64)
+        out = C + D[_ROW32, _COL32]
+        w.v[d0:d0 + 16] = f2u(out.astype(np.float32))
 
     def op_v_accvgpr_write_b32(self, w, a, m):
         self.vset(w, a[0], self.vget(w, a[1]))
@@ -548,11 +678,7 @@ class Emu:
         if addr.max() + 8 > self.lds.size:
             raise IndexError("ds_read past the LDS")
         src = np.stack([self.lds[x:x + 8] for x in addr]).view(np.uint16).reshape(64, 4)
-        out = np.empty((64, 4), np.uint16)
-        for lane in range(64):
-            g, i = lane >> 4, lane & 15
-            for q in range(4):
-                out[lane, q] = src[16 * g + 4 * q + (i >> 2), i & 3]
+        out = np.ascontiguousarray(src[_TR_SRC, _TR_ELT])
         lo, hi = self.vrange(w, a[0])
         w.v[lo:hi] = out.view(np.uint32).reshape(64, 2).T
 

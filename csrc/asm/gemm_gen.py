@@ -1124,9 +1124,11 @@ def stage_exit(a: Asm, stage: int):
     a(f"s_cbranch_scc1 {a.stage_exit}")
 
 
-def _descriptor(name: str, lds_bytes: int | None = None, n_sgpr: int | None = None) -> tuple[str, str]:
+def _descriptor(name: str, lds_bytes: int | None = None, n_sgpr: int | None = None,
+                karg_bytes: int | None = None) -> tuple[str, str]:
     LDS_BYTES = globals()["LDS_BYTES"] if lds_bytes is None else lds_bytes  # noqa: N806
     N_SGPR = globals()["N_SGPR"] if n_sgpr is None else n_sgpr  # noqa: N806
+    KARG_BYTES = globals()["KARG_BYTES"] if karg_bytes is None else karg_bytes  # noqa: N806
     desc = f"""
 .rodata
 .p2align 6
@@ -1290,7 +1292,8 @@ def generate() -> str:
         body, meta = _with_knobs(knobs, lambda: kernel("plain", variant=vname))
         parts.append(body)
         metas.append(meta)
-    import wgrad_gen  # the weight-gradient kernel shares this code object (lazy: it imports this module)
+    import attn_gen   # the attention forward and the weight-gradient kernel share this code object
+    import wgrad_gen  # (lazy: both import this module)
 
     def wgrad_round4():
         saved = dict(wgrad_gen.KNOBS)
@@ -1301,7 +1304,7 @@ def generate() -> str:
             wgrad_gen.KNOBS.clear()
             wgrad_gen.KNOBS.update(saved)
 
-    for body, meta in (wgrad_gen.kernel(), wgrad_round4(), probe_kernel(), kernel("plain", trace=True),
+    for body, meta in (wgrad_gen.kernel(), wgrad_round4(), attn_gen.kernel(), probe_kernel(), kernel("plain", trace=True),
                        _with_knobs({"timing": 1}, lambda: kernel("plain", variant="timing")),
                        _with_knobs({"timing": 2}, lambda: kernel("plain", variant="timing2"))):
         parts.append(body)

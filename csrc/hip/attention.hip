@@ -36,6 +36,7 @@
 // query (the diagonal mask removes it), a padded query's outputs are never
 // stored, and in dK/dV a padded query row gets lse = +inf, i.e. p = 0.
 #include <cstdlib>
+#include <cstring>
 
 #include "toa_common.h"
 
@@ -1747,13 +1748,15 @@ static void attn_set_lds_limits() {
 
 // Forward form: 1 = LDS-DMA staged K/V (where S % 256 == 0: 0.868 -> 0.811
 // ms at the bench shape, bit-identical, profiles/r3_attn_ds), 0 = register
-// staged (ragged S always).  toa_attn_set_fwd_variant pins the full-tile
-// form for in-process tests (-1: back to the default).
-static int g_fwd_variant = 1;
-static int attn_fwd_variant() { return g_fwd_variant; }
+// staged (ragged S always), 2 = the assembly kernel (csrc/asm/attn_gen.py;
+// D = 128, S % 256 == 0 -- the default there unless TOA_ATTN_FWD=hip).
+// toa_attn_set_fwd_variant pins a form for in-process tests / A/B (-1: back
+// to the default).
+static int g_fwd_variant = -1;
+static int attn_fwd_variant() { return g_fwd_variant == 0 ? 0 : 1; }
 extern "C" int toa_attn_set_fwd_variant(int v) {
-  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
-  g_fwd_variant = v < 0 ? 1 : v;
+  if (v < -1 || v > 2) return (int)hipErrorInvalidValue;
+  g_fwd_variant = v;
   return 0;
 }
 
@@ -1807,10 +1810,24 @@ static bool attn_shape_ok(int B, int H, int Hk, int S, int D, int flags) {
   return (D == 64 || D == 128) && B > 0 && S > 0 && Hk > 0 && H % Hk == 0 && (flags & 1);
 }
 
+// The assembly forward (csrc/asm/attn_gen.py, host side csrc/hip/gemm_asm.hip)
+// takes D = 128, S % 256 == 0; TOA_ATTN_FWD=hip keeps the HIP kernel (A/B).
+extern "C" int toa_attn_fwd_asm(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
+                                int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream);
+static bool attn_fwd_asm_on() {
+  static const bool env_on = [] {
+    const char* e = getenv("TOA_ATTN_FWD");
+    return !(e && strcmp(e, "hip") == 0);
+  }();
+  return g_fwd_variant == 2 || (g_fwd_variant < 0 && env_on);
+}
+
 // flags: bit 0 causal (required), bit 1 O / dO in [B, S, H, D] (else [B, H, S, D]).
 extern "C" int toa_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int H,
                             int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
   if (!attn_shape_ok(B, H, Hk, S, D, flags)) return (int)hipErrorInvalidValue;
+  if (D == 128 && S % 256 == 0 && attn_fwd_asm_on())
+    return toa_attn_fwd_asm(q, k, v, o, lse, B, H, Hk, S, D, flags, scale, stream);
   const int o_bshd = (flags >> 1) & 1;
   // S % 256 == 0: every 256-row block and 64-key tile is full, no clamping
   const bool tail = S % FWD_QB != 0;

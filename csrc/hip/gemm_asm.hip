@@ -33,14 +33,14 @@ namespace {
 
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
-       K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_N = 17 };
+       K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_N = 18 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
                            "toa_gemm_tn_asm_timing2",  "toa_wgrad_nt_asm",           "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
                            "toa_gemm_tn_asm_plain_v5", "toa_gemm_tn_asm_plain_v6", "toa_gemm_tn_asm_plain_v7",
-                           "toa_gemm_tn_asm_plain_v8", "toa_wgrad_nt_asm_v1"};
+                           "toa_gemm_tn_asm_plain_v8", "toa_wgrad_nt_asm_v1",       "toa_attn_fwd_asm"};
 
 struct DevModule {
   std::once_flag once;
@@ -330,6 +330,53 @@ static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_
   if (err != hipSuccess) return (int)err;
   if (split > 1 && rem > 0) return toa_wgrad_reduce(W, C, ldc, M, N, full, rem, split, beta, stream);
   return 0;
+}
+
+// Causal flash-attention forward (csrc/asm/attn_gen.py), the contract of
+// toa_attn_fwd (csrc/hip/attention.hip) for the shapes this kernel takes:
+// head dim 128, S % 256 == 0, causal (flags bit 0), flags bit 1 = O as
+// [B, S, H, D].  One workgroup of 4 waves per (256-row query block, head,
+// batch); the 80-byte argument block matches attn_gen.py KARG.
+struct __attribute__((packed)) AttnArgs {
+  uint64_t q, k, v, o, lse;
+  uint32_t B, H, Hk, S;
+  float c;  // scale * log2(e)
+  uint32_t flags, nqb, rep, g8, pad;
+};
+static_assert(sizeof(AttnArgs) == 80, "kernarg block must match csrc/asm/attn_gen.py KARG_BYTES");
+
+extern "C" int toa_attn_fwd_asm(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
+                                int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
+  if (D != 128 || !(flags & 1) || B <= 0 || H <= 0 || Hk <= 0 || H % Hk || S <= 0 || S % 256 || !al16(q) ||
+      !al16(k) || !al16(v) || !al16(o) || ((uintptr_t)lse & 3))
+    return (int)hipErrorInvalidValue;
+  const int64_t nwg = (int64_t)(S / 256) * H * B;
+  // the kernel's block-coordinate division works below 2^24; row indices
+  // (b H + h) S + q and (b S + q) H + h are 32-bit
+  if (nwg >= (1 << 24) || (int64_t)B * H * S >= (1ll << 32) || (int64_t)S * 256 >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  hipError_t err;
+  hipFunction_t fn = get_fn(K_ATTN_FWD, &err);
+  if (!fn) return (int)err;
+  AttnArgs a;
+  memset(&a, 0, sizeof(a));
+  a.q = (uint64_t)q;
+  a.k = (uint64_t)k;
+  a.v = (uint64_t)v;
+  a.o = (uint64_t)o;
+  a.lse = (uint64_t)lse;
+  a.B = (uint32_t)B;
+  a.H = (uint32_t)H;
+  a.Hk = (uint32_t)Hk;
+  a.S = (uint32_t)S;
+  a.c = scale * 1.4426950408889634f;
+  a.flags = (uint32_t)(flags & 3);
+  a.nqb = (uint32_t)(S / 256);
+  a.rep = (uint32_t)(H / Hk);
+  a.g8 = ((int64_t)B * Hk) % 8 == 0 ? 1u : 0u;
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  return (int)hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
 }
 
 extern "C" int toa_gemm_asm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* Wgu, int64_t ldw, bf16_t* GU,

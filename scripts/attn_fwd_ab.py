@@ -4,6 +4,8 @@ on random data (guide §5.4 rules 24/25):
 
     reg  K/V tiles staged through registers + ds_write (attn_fwd_kernel)
     gl   K/V tiles by LDS-DMA into two distinct LDS objects (attn_fwd_gl_kernel)
+    asm  the generated gfx950 assembly kernel (csrc/asm/attn_gen.py; default
+         since round 5)
 (Round 4 measured more arms of the LDS-DMA kernel and removed them, all
 slower than gl and bit-identical to it, profiles/r4_attn/: buffer-path DMA
 with fragments read one MFMA pair ahead 0.860 vs 0.798 ms, buffer-path DMA
@@ -20,7 +22,7 @@ Static s_setprio 1 for waves 4-7 before the loop: 0.826 vs 0.814 ms.)
 
 and the max |difference| of O / lse between them (same arithmetic: 0 expected).
 
-    python scripts/attn_fwd_ab.py [--rounds 6] [--reps 10] [--forms reg,gl]
+    python scripts/attn_fwd_ab.py [--rounds 6] [--reps 10] [--forms gl,asm]
 """
 import argparse
 import json
@@ -39,7 +41,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=6)
-    ap.add_argument("--forms", default="reg,gl")
+    ap.add_argument("--forms", default="gl,asm")
     a = ap.parse_args()
     B, H, Hk, S, D = a.batch, 32, 8, 4096, 128
     torch.manual_seed(0)
@@ -47,7 +49,7 @@ def main():
     k = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     v = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     P = _lib.ptr
-    forms = {k: v for k, v in {"reg": 0, "gl": 1}.items() if k in a.forms.split(",")}
+    forms = {k: v for k, v in {"reg": 0, "gl": 1, "asm": 2}.items() if k in a.forms.split(",")}
     outs = {}
 
     def run(form):
@@ -63,6 +65,8 @@ def main():
     torch.cuda.synchronize()
     base = list(forms)[0]
     diff = {f"{f}_vs_{base}": {"o": float((outs[f][0].float() - outs[base][0].float()).abs().max()),
+                               "o_rel": float((outs[f][0].float() - outs[base][0].float()).norm()
+                                              / outs[base][0].float().norm()),
                                "lse": float((outs[f][1] - outs[base][1]).abs().max())} for f in list(forms)[1:]}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {f: [] for f in forms}

@@ -673,6 +673,47 @@ def test_flash_attention_fwd_forms_identical(B, H, Hk, S, D, bshd):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("B,H,Hk,S,bshd,spike", [(1, 2, 1, 256, False, False), (2, 4, 2, 512, True, False),
+                                                   (1, 16, 8, 1024, True, False), (1, 4, 1, 768, False, True),
+                                                   (2, 8, 2, 2048, True, True), (6, 32, 8, 4096, True, False)])
+def test_attn_fwd_asm(B, H, Hk, S, bshd, spike):
+    """The assembly forward (csrc/asm/attn_gen.py, forward variant 2) against
+    the HIP LDS-DMA kernel (variant 1) and fp32: O to bf16 rounding, lse to
+    the bf16 P the row sums are taken from.  `spike`: late keys dominate, so
+    the deferred rescale runs (guide rule 26); B Hk % 8 == 0 takes the
+    XCD-grouped block order."""
+    L = _lib()
+    torch.manual_seed(21)
+    D = 128
+    scale = 1.0 / math.sqrt(D)
+    q = torch.randn(B, H, S, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, Hk, S, D, device=DEV, dtype=torch.bfloat16)
+    if spike:
+        k[:, :, S // 2:] *= 6.0
+        k[:, :, S - 37] = 4.0 * q[0, 0, S - 20]
+    outs = {}
+    try:
+        for form in (1, 2):
+            L.call("toa_attn_set_fwd_variant", form)
+            o = torch.full((B, S, H, D) if bshd else (B, H, S, D), float("nan"), device=DEV, dtype=torch.bfloat16)
+            lse = torch.full((B, H, S), float("nan"), device=DEV, dtype=torch.float32)
+            L.call("toa_attn_fwd", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(lse), B, H, Hk, S, D,
+                   1 | (2 if bshd else 0), scale, L.stream(q))
+            torch.cuda.synchronize()
+            outs[form] = ((o.transpose(1, 2) if bshd else o).float(), lse)
+    finally:
+        L.call("toa_attn_set_fwd_variant", -1)
+    (o1, l1), (o2, l2) = outs[1], outs[2]
+    assert torch.isfinite(o2).all() and torch.isfinite(l2).all()
+    assert rel(o2, o1) < 1e-2, rel(o2, o1)
+    assert float((l2 - l1).abs().max()) < 5e-3 * max(1.0, float(l1.abs().max()))
+    if B * H * S <= 32768:
+        orf, lse_ref = _attn_ref(q.float(), k.float(), v.float(), scale)
+        assert rel(o2, orf) < 2e-2, rel(o2, orf)
+        assert float((l2 - lse_ref).abs().max()) < 2e-2
+
+
 @pytest.mark.parametrize("B,H,Hk,S,D", [(2, 8, 2, 512, 128), (1, 4, 1, 1024, 64), (1, 4, 2, 300, 128)])
 def test_rope_attention_matches_two_nodes(B, H, Hk, S, D):
     """rope_attention (one autograd node; the backward writes d(qkv) from

@@ -63,6 +63,7 @@ _SIGS = {
     "toa_dropout_fwd": [c_int, c_p, c_p, c_p, c_i64, c_f, ctypes.c_uint64, ctypes.c_uint64, c_p],
     "toa_accuracy": [c_int, c_p, c_p, c_p, c_int, c_int, c_p],
     "toa_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_p],
+    "toa_attn_fwd_asm": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_p],
     "toa_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_f, c_p],
     "toa_wgrad": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
