@@ -71,9 +71,9 @@ TILE = TK * ROWB         # 16 KiB: one K or V tile in LDS
 VBUF0 = 2 * TILE         # K tiles at 0 / TILE, V tiles at VBUF0 + n TILE (n = 0..2)
 LDS_BYTES = 5 * TILE
 THR = 8.0                # deferred-rescale threshold (log2 units)
-KARG_BYTES = 80
+KARG_BYTES = 88
 KARG = {"Q": 0, "K": 8, "V": 16, "O": 24, "LSE": 32, "B": 40, "H": 44, "Hk": 48, "S": 52, "c": 56,
-        "flags": 60, "nqb": 64, "rep": 68, "g8": 72}
+        "flags": 60, "nqb": 64, "rep": 68, "g8": 72, "dbg": 80}
 
 # ---------------------------------------------------------------- SGPRs
 S_Q, S_K, S_V, S_O, S_L = 4, 6, 8, 10, 12
@@ -86,7 +86,8 @@ S_T0 = 60                 # s60..s67 scratch
 S_DQ, S_DR = 68, 69
 S_FA, S_FB, S_F = 70, 72, 74   # rescale flags (pairs)
 S_OSTR, S_OQB, S_SOFF, S_Q0 = 76, 77, 78, 79
-N_SGPR = 80
+S_TM = 80                 # timing arm: s80..s87 four s_memtime stamps, s88 rescale count, s[90:91] dbg pointer
+N_SGPR = 96
 
 # ---------------------------------------------------------------- VGPRs
 V_KOFF = 1                # v1..v8: K fragment read offsets per 16-d k-step (+ buffer)
@@ -104,6 +105,21 @@ V_P = 80                  # P (bf16 pairs): [block][k-step] x 4
 V_SB = (112, 176)         # score buffers (64 each): [block][key half] x 16
 V_X = 240                 # v240..v255 scratch (row max, rescale, epilogue)
 RING = 6
+
+# Schedule knobs; the DIAGNOSTIC arms (VARIANTS) switch one mechanism off to
+# price it in-process (scripts/attn_fwd_ab.py --variants): their outputs are
+# wrong by construction and only their time is read.
+KNOBS = {"bar": True, "vmwait": True, "lgkm": True, "exp": True, "dma": True, "timing": False, "fine": True}
+VARIANTS = (
+    ("d1", {"bar": False, "vmwait": False}),   # no per-tile barrier nor DMA wait
+    ("d2", {"vmwait": False}),                 # barrier, but not for the DMA to land
+    ("d3", {"lgkm": False}),                   # MFMAs do not wait for their LDS fragments
+    ("d4", {"exp": False}),                    # v_exp_f32 -> v_mov_b32 (transcendental issue cost)
+    ("d5", {"dma": False, "vmwait": False}),   # no K / V staging in the loop
+    ("t1", {"timing": True}),                  # the product kernel + s_memtime stamps (bit-identical outputs)
+    ("c1", {"fine": False}),                   # fillers placed as whole groups (the first schedule)
+    ("t2", {"timing": True, "fine": False}),   # its timing arm
+)
 
 # AGPRs: O^T a[0:127] ([block][d tile] x 16), Q^T fragments a[128:191]
 # ([block][k-step] x 4), row sums a[192:223] ([block] x 16)
@@ -170,14 +186,34 @@ def srd64(a: Asm, dst: int, base: int, row: int, row_bytes: int, nrec):
 
 # ---------------------------------------------------------------- scheduler
 class Item:
-    """A group of filler instructions placed as a unit in one MFMA gap.
-    Gap g = after MFMA g (-1: before the first).  rel / dl: earliest / latest
-    gap.  Items of one stream keep their order."""
+    """A group of filler instructions.  Gap g = after MFMA g (-1: before the
+    first).  rel / dl: earliest / latest gap of every instruction of the
+    group.  Items of one stream keep their order; schedule() places their
+    instructions one by one (split=False: as one unit)."""
 
-    __slots__ = ("ins", "cost", "rel", "dl", "stream")
+    __slots__ = ("ins", "cost", "rel", "dl", "stream", "split")
 
-    def __init__(self, ins, cost, rel, dl, stream):
-        self.ins, self.cost, self.rel, self.dl, self.stream = ins, cost, rel, dl, stream
+    def __init__(self, ins, cost, rel, dl, stream, split=True):
+        self.ins, self.cost, self.rel, self.dl, self.stream, self.split = ins, cost, rel, dl, stream, split
+
+
+def issue_cost(ins: str) -> int:
+    """Vector-issue cycles of one filler beside MFMAs, one wave per SIMD
+    (MI355X_MICROARCH.md constants: transcendental 8, other VALU 4, an
+    MFMA holds the port 8 of its 32; an LDS-DMA piece ~40-60)."""
+    op = ins.split()[0]
+    if op.startswith("buffer_load") and ins.rstrip().endswith("lds"):
+        return 40
+    if op in ("v_exp_f32", "v_log_f32", "v_rcp_f32"):
+        return 8
+    if op.startswith(("v_", "ds_", "buffer_")):
+        return 4
+    if op == "s_nop":
+        return 4 * (int(ins.split()[1]) + 1)
+    return 1
+
+
+GAP_BUDGET = 24     # filler issue cycles one 32x32x16 MFMA gap hides
 
 
 def schedule(a: Asm, mfmas: list, items: list, tail: list | None = None, pre=()):
@@ -192,8 +228,12 @@ def schedule(a: Asm, mfmas: list, items: list, tail: list | None = None, pre=())
     streams: dict = {}
     for it in items:
         assert -1 <= it.rel <= n - 1 and it.dl >= it.rel, (it.ins[:1], it.rel, it.dl)
-        streams.setdefault(it.stream, []).append(it)
-    total = sum(it.cost for it in items)
+        if it.split and KNOBS["fine"]:
+            for ins in it.ins:
+                streams.setdefault(it.stream, []).append(Item([ins], issue_cost(ins), it.rel, it.dl, it.stream))
+        else:
+            streams.setdefault(it.stream, []).append(it)
+    total = sum(it.cost for lst in streams.values() for it in lst)
     place = {g: [] for g in range(-1, n)}
     heads = {s: 0 for s in streams}
     cum = 0.0
@@ -226,6 +266,8 @@ def schedule(a: Asm, mfmas: list, items: list, tail: list | None = None, pre=())
             lds.append(txt.split(";")[1].strip() if ";" in txt else None)
 
     def wait_for(tags):
+        if not KNOBS["lgkm"]:
+            return
         need = 0
         for t in tags:
             idx = max((i for i, x in enumerate(lds) if x == t), default=-1)
@@ -310,7 +352,7 @@ def exp_items(buf: int, base: int, stream="exp") -> list[Item]:
                 regs = [sreg(buf, qb2, kh, r0 + e) for e in range(4)]
                 p = preg(qb2, ks) + 2 * part
                 ins = [f"v_fma_f32 {vr(x)}, {vr(x)}, {sr(S_C)}, -{vr(V_M + qb2)}" for x in regs]
-                ins += [f"v_exp_f32 {vr(x)}, {vr(x)}" for x in regs]
+                ins += [f"v_exp_f32 {vr(x)}, {vr(x)}" if KNOBS["exp"] else f"v_mov_b32 {vr(x)}, {vr(x)}" for x in regs]
                 ins += [f"v_cvt_pk_bf16_f32 {vr(p)}, {vr(regs[0])}, {vr(regs[1])}",
                         f"v_cvt_pk_bf16_f32 {vr(p + 1)}, {vr(regs[2])}, {vr(regs[3])}"]
                 items.append(Item(ins, 58, -1, dl, stream))
@@ -414,7 +456,7 @@ def body(a: Asm, kind: str, p: int, resc_label: str, back_label: str):
              f"s_add_u32 {sr(S_T0)}, {sr(S_I)}, 1",
              f"s_lshl_b32 {sr(S_VT)}, {sr(S_T0)}, 14"]
     items.append(Item(setup, 10, -1, DL_DMA, "dma"))
-    for j in range(4):
+    for j in range(4 if KNOBS["dma"] else 0):
         items.append(Item(dma_piece("K", j, p), 40, -1, DL_DMA, "dma"))
         items.append(Item(dma_piece("V", j, p), 40, -1, DL_DMA, "dma"))
     items.append(Item([f"s_add_u32 {sr(S_M0V)}, {sr(S_M0V)}, {TILE}",
@@ -423,7 +465,8 @@ def body(a: Asm, kind: str, p: int, resc_label: str, back_label: str):
                        f"s_sub_u32 {sr(S_M0V)}, {sr(S_M0V)}, {sr(S_T0 + 1)}"], 8, -1, n - 1, "dma"))
     # --- the barrier: everyone's K_{i+2} / V_{i+1} landed; then the next
     # tile's K offsets and its first fragments
-    items.append(Item(["s_waitcnt vmcnt(0)", "s_barrier"], 8, G_BAR, G_BAR, "bar"))
+    items.append(Item((["s_waitcnt vmcnt(0)"] if KNOBS["vmwait"] else []) + (["s_barrier"] if KNOBS["bar"] else []),
+                      8, G_BAR, G_BAR, "bar", split=False))
     items.append(Item(koff_toggle(), 32, G_BAR, n - 1, "bar"))
     for f in range(3):
         items.append(Item([kread(f)], 6, G_BAR, n - 1, "bar"))
@@ -477,6 +520,8 @@ def rescale_block(a: Asm, label: str, back: str):
     """Out of line: m_new = max(m, mc), alpha = 2^(m - m_new); O, l *= alpha.
     Runs after every P V MFMA of the tile was issued: drain them first."""
     a.label(label)
+    if KNOBS["timing"]:
+        a(f"s_add_u32 {sr(S_TM + 8)}, {sr(S_TM + 8)}, 1")
     a("s_nop 7")
     a("s_nop 7")
     a("s_nop 7")
@@ -501,7 +546,19 @@ def rescale_block(a: Asm, label: str, back: str):
 
 
 # ---------------------------------------------------------------- prologue
+def stamp(a: Asm, k: int):
+    """Timing arm: shader-clock stamp k (0 start, 1 loop, 2 epilogue, 3 end).
+    s_memtime returns through lgkmcnt: the wait also drains LDS reads."""
+    if KNOBS["timing"]:
+        a(f"s_memtime {sr(S_TM + 2 * k, 2)}")
+        a("s_waitcnt lgkmcnt(0)")
+
+
 def prologue(a: Asm):
+    stamp(a, 0)
+    if KNOBS["timing"]:
+        a(f"s_mov_b32 {sr(S_TM + 8)}, 0")
+        a(f"s_load_dwordx2 {sr(S_TM + 10, 2)}, s[0:1], 0x50")
     a(f"s_load_dwordx16 {sr(4, 16)}, s[0:1], 0x0")
     a(f"s_load_dwordx4 {sr(20, 4)}, s[0:1], 0x40")
     a(f"v_lshrrev_b32 {vr(V_X + 15)}, 6, v0")          # wave id (v255: untouched until the epilogue)
@@ -708,10 +765,37 @@ def prologue(a: Asm):
     a(f"s_mov_b32 {sr(S_I)}, 0")
     a(f"s_mov_b32 {sr(S_VR)}, 0")
     a(f"s_add_u32 {sr(S_M0V)}, {sr(S_W1K)}, {VBUF0 + TILE}")
+    stamp(a, 1)
 
 
 # ---------------------------------------------------------------- epilogue
+def timing_store(a: Asm):
+    """Timing arm: 8 dwords per (workgroup, wave) at dbg + 32 (4 wg + wave):
+    prologue, loop and epilogue cycles, tiles, query block, rescales, 0, 0."""
+    if not KNOBS["timing"]:
+        return
+    stamp(a, 3)
+    t = S_T0
+    a(f"s_lshl_b32 {sr(t)}, s2, 2")
+    a(f"s_add_u32 {sr(t)}, {sr(t)}, {sr(S_W)}")
+    a(f"s_lshl_b32 {sr(t)}, {sr(t)}, 5")
+    a(f"s_add_u32 {sr(SRD_Q)}, {sr(S_TM + 10)}, {sr(t)}")
+    a(f"s_addc_u32 {sr(SRD_Q + 1)}, {sr(S_TM + 11)}, 0")
+    a(f"s_mov_b32 {sr(SRD_Q + 2)}, 32")
+    a(f"s_mov_b32 {sr(SRD_Q + 3)}, 0x20000")
+    vals = [f"s_sub_u32 {sr(t)}, {sr(S_TM + 2)}, {sr(S_TM)}", f"s_sub_u32 {sr(t)}, {sr(S_TM + 4)}, {sr(S_TM + 2)}",
+            f"s_sub_u32 {sr(t)}, {sr(S_TM + 6)}, {sr(S_TM + 4)}", f"s_mov_b32 {sr(t)}, {sr(S_T)}",
+            f"s_mov_b32 {sr(t)}, {sr(S_QB)}", f"s_mov_b32 {sr(t)}, {sr(S_TM + 8)}"]
+    a(f"v_mov_b32 {vr(V_T + 1)}, 0")
+    for k, ins in enumerate(vals):
+        a(ins)
+        a(f"v_mov_b32 {vr(V_T)}, {sr(t)}")
+        a(f"buffer_store_dword {vr(V_T)}, {vr(V_T + 1)}, {sr(SRD_Q, 4)}, 0 offen offset:{4 * k}")
+    a("s_waitcnt vmcnt(0)")
+
+
 def epilogue(a: Asm):
+    stamp(a, 2)
     a("s_nop 7")
     a("s_nop 7")
     a("s_nop 7")
@@ -751,15 +835,17 @@ def epilogue(a: Asm):
         a(f"v_add_f32 {vr(x)}, {vr(V_M + qb2)}, {vr(x)}")
         a(f"v_mul_f32 {vr(x)}, 0x3f317218, {vr(x)}")
         a(f"buffer_store_dword {vr(x)}, {vr(lv)}, {sr(SRD_L, 4)}, 0 offen offset:{128 * qb2}")
+    timing_store(a)
 
 
 # ---------------------------------------------------------------- kernel
-def kernel() -> tuple[str, str]:
-    a = Asm(prefix="attn_")
-    a.raw(f".globl {NAME}")
+def kernel(variant: str = "") -> tuple[str, str]:
+    name = NAME + (f"_{variant}" if variant else "")
+    a = Asm(prefix=f"attn{variant}_")
+    a.raw(f".globl {name}")
     a.raw(".p2align 8")
-    a.raw(f".type {NAME},@function")
-    a.raw(f"{NAME}:")
+    a.raw(f".type {name},@function")
+    a.raw(f"{name}:")
     prologue(a)
     lab = {k: a.fresh(k) for k in ("u0", "m0", "m1", "t0", "t1", "epi")}
     resc = {}
@@ -793,18 +879,38 @@ def kernel() -> tuple[str, str]:
     a("s_endpgm")
     for lbl, back in resc.values():
         rescale_block(a, lbl, back)
-    a.raw(f".size {NAME}, .-{NAME}")
-    desc, meta = G._descriptor(NAME, lds_bytes=LDS_BYTES, n_sgpr=N_SGPR, karg_bytes=KARG_BYTES)
+    a.raw(f".size {name}, .-{name}")
+    desc, meta = G._descriptor(name, lds_bytes=LDS_BYTES, n_sgpr=N_SGPR, karg_bytes=KARG_BYTES)
     return "\n".join(a.out) + "\n" + desc, meta
 
 
-def generate() -> str:
+def variant_kernel(vname: str, knobs: dict) -> tuple[str, str]:
+    saved = dict(KNOBS)
+    KNOBS.update(knobs)
+    try:
+        return kernel(vname)
+    finally:
+        KNOBS.clear()
+        KNOBS.update(saved)
+
+
+def all_kernels() -> list[tuple[str, str]]:
+    """The product kernel, then the diagnostic arms (host table order)."""
+    return [kernel()] + [variant_kernel(v, k) for v, k in VARIANTS]
+
+
+def generate(kernels=None) -> str:
     """This kernel alone in a code object (tests; the build embeds it through
     gemm_gen.generate())."""
-    body_, meta = kernel()
-    return "\n".join(['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".amdhsa_code_object_version 5", ".text", body_,
+    kernels = kernels or [kernel()]
+    return "\n".join(['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".amdhsa_code_object_version 5", ".text",
+                      *(b for b, _ in kernels),
                       ".amdgpu_metadata\n---\namdhsa.version:\n  - 1\n  - 2\namdhsa.target: amdgcn-amd-amdhsa--gfx950\n"
-                      "amdhsa.kernels:\n" + meta + "...\n.end_amdgpu_metadata"]) + "\n"
+                      "amdhsa.kernels:\n" + "".join(m for _, m in kernels) + "...\n.end_amdgpu_metadata"]) + "\n"
+
+
+def generate_all() -> str:
+    return generate(all_kernels())
 
 
 if __name__ == "__main__":

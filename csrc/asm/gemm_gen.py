@@ -1304,7 +1304,7 @@ def generate() -> str:
             wgrad_gen.KNOBS.clear()
             wgrad_gen.KNOBS.update(saved)
 
-    for body, meta in (wgrad_gen.kernel(), wgrad_round4(), attn_gen.kernel(), probe_kernel(), kernel("plain", trace=True),
+    for body, meta in (wgrad_gen.kernel(), wgrad_round4(), *attn_gen.all_kernels(), probe_kernel(), kernel("plain", trace=True),
                        _with_knobs({"timing": 1}, lambda: kernel("plain", variant="timing")),
                        _with_knobs({"timing": 2}, lambda: kernel("plain", variant="timing2"))):
         parts.append(body)

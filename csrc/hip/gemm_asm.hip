@@ -33,14 +33,18 @@ namespace {
 
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
-       K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_N = 18 };
+       K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23, K_N = 26 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
                            "toa_gemm_tn_asm_timing2",  "toa_wgrad_nt_asm",           "toa_gemm_tn_asm_plain_v1",
                            "toa_gemm_tn_asm_plain_v2", "toa_gemm_tn_asm_plain_v3", "toa_gemm_tn_asm_plain_v4",
                            "toa_gemm_tn_asm_plain_v5", "toa_gemm_tn_asm_plain_v6", "toa_gemm_tn_asm_plain_v7",
-                           "toa_gemm_tn_asm_plain_v8", "toa_wgrad_nt_asm_v1",       "toa_attn_fwd_asm"};
+                           "toa_gemm_tn_asm_plain_v8", "toa_wgrad_nt_asm_v1",       "toa_attn_fwd_asm",
+                           // K_ATTN_D1 ..: attn_gen.py VARIANTS (diagnostic arms, wrong outputs by design)
+                           "toa_attn_fwd_asm_d1",      "toa_attn_fwd_asm_d2",        "toa_attn_fwd_asm_d3",
+                           "toa_attn_fwd_asm_d4",      "toa_attn_fwd_asm_d5",        "toa_attn_fwd_asm_t1",
+                           "toa_attn_fwd_asm_c1",      "toa_attn_fwd_asm_t2"};
 
 struct DevModule {
   std::once_flag once;
@@ -342,11 +346,45 @@ struct __attribute__((packed)) AttnArgs {
   uint32_t B, H, Hk, S;
   float c;  // scale * log2(e)
   uint32_t flags, nqb, rep, g8, pad;
+  uint64_t dbg;  // the timing arm's records (attn_gen.py timing_store)
 };
-static_assert(sizeof(AttnArgs) == 80, "kernarg block must match csrc/asm/attn_gen.py KARG_BYTES");
+static_assert(sizeof(AttnArgs) == 88, "kernarg block must match csrc/asm/attn_gen.py KARG_BYTES");
+
+static int attn_fwd_asm_launch(int which, const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse,
+                               int B, int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream,
+                               void* dbg = nullptr);
 
 extern "C" int toa_attn_fwd_asm(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B,
                                 int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
+  return attn_fwd_asm_launch(K_ATTN_FWD, q, k, v, o, lse, B, H, Hk, S, D, flags, scale, stream);
+}
+
+// Diagnostic: arm v (1.. = attn_gen.py VARIANTS, 0 = the product kernel),
+// same contract; the arms' outputs are wrong by design (timing only).
+extern "C" int toa_attn_fwd_asm_variant(int v, const bf16_t* q, const bf16_t* k, const bf16_t* v_, bf16_t* o,
+                                        float* lse, int B, int H, int Hk, int S, int D, int flags, float scale,
+                                        hipStream_t stream) {
+  if (v < 0 || v > K_N - K_ATTN_D1 || K_ATTN_D1 + v - 1 == K_ATTN_T1 || K_ATTN_D1 + v - 1 == K_N - 1)
+    return (int)hipErrorInvalidValue;  // the timing arms take toa_attn_fwd_asm_timing
+  return attn_fwd_asm_launch(v ? K_ATTN_D1 + v - 1 : K_ATTN_FWD, q, k, v_, o, lse, B, H, Hk, S, D, flags, scale,
+                             stream);
+}
+
+// Diagnostic: the product kernel with s_memtime stamps (attn_gen.py
+// timing_store): 8 dwords per (workgroup, wave) at dbg + 32 (4 wg + wave) --
+// prologue / loop / epilogue shader cycles, tiles, query block, rescales.
+// which = 1: the product schedule's timing arm, 2: the group-placed one's.
+extern "C" int toa_attn_fwd_asm_timing(int which, void* dbg, const bf16_t* q, const bf16_t* k, const bf16_t* v,
+                                       bf16_t* o, float* lse, int B, int H, int Hk, int S, int D, int flags,
+                                       float scale, hipStream_t stream) {
+  if (!dbg || !al16(dbg) || (which != 1 && which != 2)) return (int)hipErrorInvalidValue;
+  return attn_fwd_asm_launch(which == 1 ? K_ATTN_T1 : K_N - 1, q, k, v, o, lse, B, H, Hk, S, D, flags, scale, stream,
+                             dbg);
+}
+
+static int attn_fwd_asm_launch(int which, const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse,
+                               int B, int H, int Hk, int S, int D, int flags, float scale, hipStream_t stream,
+                               void* dbg) {
   if (D != 128 || !(flags & 1) || B <= 0 || H <= 0 || Hk <= 0 || H % Hk || S <= 0 || S % 256 || !al16(q) ||
       !al16(k) || !al16(v) || !al16(o) || ((uintptr_t)lse & 3))
     return (int)hipErrorInvalidValue;
@@ -356,7 +394,7 @@ extern "C" int toa_attn_fwd_asm(const bf16_t* q, const bf16_t* k, const bf16_t* 
   if (nwg >= (1 << 24) || (int64_t)B * H * S >= (1ll << 32) || (int64_t)S * 256 >= (1ll << 31))
     return (int)hipErrorInvalidValue;
   hipError_t err;
-  hipFunction_t fn = get_fn(K_ATTN_FWD, &err);
+  hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
   AttnArgs a;
   memset(&a, 0, sizeof(a));
@@ -374,6 +412,7 @@ extern "C" int toa_attn_fwd_asm(const bf16_t* q, const bf16_t* k, const bf16_t* 
   a.nqb = (uint32_t)(S / 256);
   a.rep = (uint32_t)(H / Hk);
   a.g8 = ((int64_t)B * Hk) % 8 == 0 ? 1u : 0u;
+  a.dbg = (uint64_t)dbg;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   return (int)hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);

@@ -6,6 +6,8 @@ on random data (guide §5.4 rules 24/25):
     gl   K/V tiles by LDS-DMA into two distinct LDS objects (attn_fwd_gl_kernel)
     asm  the generated gfx950 assembly kernel (csrc/asm/attn_gen.py; default
          since round 5)
+    d1.. its DIAGNOSTIC arms (attn_gen.py VARIANTS: one mechanism switched
+         off each; wrong outputs, timing only -- excluded from the diffs)
 (Round 4 measured more arms of the LDS-DMA kernel and removed them, all
 slower than gl and bit-identical to it, profiles/r4_attn/: buffer-path DMA
 with fragments read one MFMA pair ahead 0.860 vs 0.798 ms, buffer-path DMA
@@ -49,13 +51,19 @@ def main():
     k = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     v = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16)
     P = _lib.ptr
-    forms = {k: v for k, v in {"reg": 0, "gl": 1, "asm": 2}.items() if k in a.forms.split(",")}
+    arms = ("d1", "d2", "d3", "d4", "d5", "t1", "c1")   # attn_gen.py VARIANTS order
+    forms = {k: v for k, v in {"reg": 0, "gl": 1, "asm": 2, **{x: -(i + 1) for i, x in enumerate(arms)}}.items()
+             if k in a.forms.split(",")}
     outs = {}
 
     def run(form):
-        _lib.call("toa_attn_set_fwd_variant", forms[form])
         o = torch.empty(B, S, H, D, device="cuda", dtype=torch.bfloat16)
         lse = torch.empty(B, H, S, device="cuda", dtype=torch.float32)
+        if forms[form] < 0:   # diagnostic arm of the assembly kernel
+            _lib.call("toa_attn_fwd_asm_variant", -forms[form], P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D,
+                      1 | 2, 1.0 / math.sqrt(D), _lib.stream(q))
+            return o, lse
+        _lib.call("toa_attn_set_fwd_variant", forms[form])
         _lib.call("toa_attn_fwd", P(q), P(k), P(v), P(o), P(lse), B, H, Hk, S, D, 1 | 2, 1.0 / math.sqrt(D),
                   _lib.stream(q))
         return o, lse
@@ -67,7 +75,8 @@ def main():
     diff = {f"{f}_vs_{base}": {"o": float((outs[f][0].float() - outs[base][0].float()).abs().max()),
                                "o_rel": float((outs[f][0].float() - outs[base][0].float()).norm()
                                               / outs[base][0].float().norm()),
-                               "lse": float((outs[f][1] - outs[base][1]).abs().max())} for f in list(forms)[1:]}
+                               "lse": float((outs[f][1] - outs[base][1]).abs().max())}
+            for f in list(forms)[1:] if forms[f] >= 0}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = {f: [] for f in forms}
     for _ in range(a.rounds):

@@ -1,7 +1,7 @@
 """Counter subject for the attention kernels at the Llama-3-8B bench shape
-(B=6, H=32, Hkv=8, S=4096, D=128, causal, packed GQA): 2 warm-up and 3
-counted forward + backward passes of the HIP flash attention (dS-form
-backward).  Used with scripts/gpu_attn_pmc.sh."""
+(B=6, H=32, Hkv=8, S=4096, D=128, causal, packed GQA): 5 forward + backward
+passes (dS-form backward) with the HIP LDS-DMA forward, then 5 with the
+assembly forward (forward variants 1 and 2).  Used with scripts/gpu_attn_pmc.sh."""
 import math
 import os
 import sys
@@ -9,7 +9,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-from tf_operator_amd.ops import llm  # noqa: E402
+from tf_operator_amd.ops import _lib, llm  # noqa: E402
 
 
 def main():
@@ -19,11 +19,14 @@ def main():
     k = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16).requires_grad_()
     v = torch.randn(B, Hk, S, D, device="cuda").to(torch.bfloat16).requires_grad_()
     do = torch.randn(B, H, S, D, device="cuda").to(torch.bfloat16)
-    for _ in range(5):
-        o = llm._FlashAttn.apply(q, k, v, 1 / math.sqrt(D))
-        o.backward(do)
-        q.grad = k.grad = v.grad = None
-    torch.cuda.synchronize()
+    for form in (1, 2):
+        _lib.call("toa_attn_set_fwd_variant", form)
+        for _ in range(5):
+            o = llm._FlashAttn.apply(q, k, v, 1 / math.sqrt(D))
+            o.backward(do)
+            q.grad = k.grad = v.grad = None
+        torch.cuda.synchronize()
+    _lib.call("toa_attn_set_fwd_variant", -1)
     print("ok", flush=True)
 
 

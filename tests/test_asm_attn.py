@@ -58,7 +58,7 @@ def run(q, k, v, scale, bshd, g8=None, hits=None):
     lse = np.zeros((B, H, S), np.float32)
     oa, la = mem.add(o), mem.add(lse)
     c = float(np.float32(scale * LOG2E))
-    karg = struct.pack("<5Q4If5I", qa, ka, va, oa, la, B, H, Hk, S, c, 3 if bshd else 1, nqb, H // Hk, int(g8), 0)
+    karg = struct.pack("<5Q4If5IQ", qa, ka, va, oa, la, B, H, Hk, S, c, 3 if bshd else 1, nqb, H // Hk, int(g8), 0, 0)
     assert len(karg) == attn_gen.KARG_BYTES
     e = emu.Emu(TEXT, attn_gen.NAME)
     if hits is not None:      # count entries into the out-of-line rescale blocks
@@ -139,3 +139,33 @@ def test_attn_fwd_rescale_path():
     # wave w of query block qb rescales for tiles 1 .. 4 qb + w (later tiles
     # are past its diagonal, fully masked): block 1 sum(4 + w), block 0 sum(w)
     assert hits[0] == sum(4 + w for w in range(4)) + sum(range(4))
+
+
+def test_timing_arm_is_bit_identical_and_records():
+    """The s_memtime arm (attn_gen.py VARIANTS "t1"): same O / LSE bits as
+    the product kernel, one record per (workgroup, wave) with its tile count
+    and query block."""
+    B, H, Hk, S = 1, 1, 1, 512
+    q, k, v = rnd((B, H, S, 128), 12), rnd((B, Hk, S, 128), 13), rnd((B, Hk, S, 128), 14)
+    text = attn_gen.generate_all()
+    outs = []
+    for name in (attn_gen.NAME, attn_gen.NAME + "_t1"):
+        mem = emu.Memory()
+        qa, ka, va = (mem.add(bf16(x)) for x in (q, k, v))
+        oa = mem.add(np.zeros((B, H, S, 128), np.uint16))
+        la = mem.add(np.zeros((B, H, S), np.float32))
+        dbg = np.zeros((2 * 4, 8), np.uint32)
+        da = mem.add(dbg)
+        c = float(np.float32(LOG2E / math.sqrt(128)))
+        karg = struct.pack("<5Q4If5IQ", qa, ka, va, oa, la, B, H, Hk, S, c, 1, 2, 1, 0, 0, da)
+        e = emu.Emu(text, name)
+        for wg in range(2):
+            e.run(karg, wg, mem)
+        bufs = {base: b for base, b in mem.bufs}
+        outs.append((bufs[oa].copy(), bufs[la].copy(), bufs[da].view(np.uint32).reshape(8, 8).copy()))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    rec = outs[1][2]
+    # generic order: workgroup 0 = query block 1 (8 tiles), workgroup 1 = block 0 (4 tiles)
+    assert list(rec[:4, 3]) == [8] * 4 and list(rec[4:, 3]) == [4] * 4
+    assert list(rec[:4, 4]) == [1] * 4 and list(rec[4:, 4]) == [0] * 4
+    assert (rec[:, :3] > 0).all()

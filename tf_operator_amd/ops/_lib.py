@@ -64,6 +64,9 @@ _SIGS = {
     "toa_accuracy": [c_int, c_p, c_p, c_p, c_int, c_int, c_p],
     "toa_attn_fwd": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_p],
     "toa_attn_fwd_asm": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_p],
+    "toa_attn_fwd_asm_variant": [c_int, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_p],
+    "toa_attn_fwd_asm_timing": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_f,
+                                c_p],
     "toa_attn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_f, c_p],
     "toa_wgrad": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
