@@ -209,6 +209,9 @@ class Emu:
     def op_s_load_dwordx16(self, w, a, m):
         self._sload(w, a, 16)
 
+    def op_s_load_dwordx8(self, w, a, m):
+        self._sload(w, a, 8)
+
     def op_s_load_dwordx4(self, w, a, m):
         self._sload(w, a, 4)
 
@@ -625,7 +628,16 @@ class Emu:
         hardware (kept for prefetch-style loads whose result is discarded;
         the product kernels do not issue this form).  Every other buffer
         access past num_records raises."""
-        assert "lds" not in mods
+        if "lds" in mods:        # LDS-DMA, 4 B per lane to M0 + 4 lane
+            assert "offen" in mods
+            addr = self._buffer_addr(w, a, mods, 4)
+            data = self._gread(addr, 4)
+            dst = w.m0 + 4 * np.arange(64)
+            if dst.max() + 4 > self.lds.size:
+                raise IndexError("LDS-DMA past the LDS")
+            for l in range(64):
+                self.lds[dst[l]:dst[l] + 4] = data[l]
+            return
         voff = self.vget(w, a[1]).astype(np.uint64)
         kind, lo_, hi_ = self._reg(w, a[2])
         srd = [int(w.s[lo_ + i]) & M32 for i in range(4)]
@@ -651,12 +663,26 @@ class Emu:
         lo, hi = self.vrange(w, a[0])
         w.v[lo:hi] = data.T
 
+    def _dropped(self, w, a) -> bool:
+        """A store through a resource of num_records 0 writes nothing (the
+        hardware's range check; attn_bwd_gen.py drops the dS stores of
+        blocks above the diagonal this way).  Counted in self.dropped."""
+        kind, lo, hi = self._reg(w, a[2])
+        if int(w.s[lo + 2]) & M32 == 0:
+            self.dropped = getattr(self, "dropped", 0) + 1
+            return True
+        return False
+
     def op_buffer_store_dword(self, w, a, mods):
+        if self._dropped(w, a):
+            return
         addr = self._buffer_addr(w, a[1:], mods, 4)
         lo, hi = self.vrange(w, a[0])
         self._gwrite(addr, np.ascontiguousarray(w.v[lo]).view(np.uint8).reshape(64, 4))
 
     def op_buffer_store_dwordx4(self, w, a, mods):
+        if self._dropped(w, a):
+            return
         addr = self._buffer_addr(w, a[1:], mods, 16)
         lo, hi = self.vrange(w, a[0])
         self._gwrite(addr, np.ascontiguousarray(w.v[lo:hi].T).view(np.uint8).reshape(64, 16))

@@ -1304,9 +1304,12 @@ def generate() -> str:
             wgrad_gen.KNOBS.clear()
             wgrad_gen.KNOBS.update(saved)
 
+    import attn_bwd_gen  # the attention dK / dV backward, same code object
+
     for body, meta in (wgrad_gen.kernel(), wgrad_round4(), *attn_gen.all_kernels(), probe_kernel(), kernel("plain", trace=True),
                        _with_knobs({"timing": 1}, lambda: kernel("plain", variant="timing")),
-                       _with_knobs({"timing": 2}, lambda: kernel("plain", variant="timing2"))):
+                       _with_knobs({"timing": 2}, lambda: kernel("plain", variant="timing2")),
+                       *attn_bwd_gen.all_kernels()):
         parts.append(body)
         metas.append(meta)
     # what hipcc emits after the last kernel: s_nop padding, so the

@@ -1706,10 +1706,38 @@ extern "C" int toa_attn_set_bwd_timing(void* tstat) {
   g_attn_tstat = (unsigned long long*)tstat;
   return 0;
 }
+// dK / dV of the dS form on the assembly kernel (csrc/asm/attn_bwd_gen.py, host
+// side csrc/hip/gemm_asm.hip): D = 128, the default there.  TOA_ATTN_DKDV=hip,
+// or toa_attn_set_dkdv_variant(0), keeps attn_bwd_dkdv_ds_kernel (A/B, tests);
+// 1 forces the assembly kernel, -1 returns to the environment's choice.
+extern "C" int toa_attn_dkdv_asm(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
+                                 const float* nlse2, const float* ndelta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
+                                 int H, int Hk, int S, int D, float scale, int flags, const float* cosv,
+                                 const float* sinv, int H3, hipStream_t stream);
+static int g_dkdv_variant = -1;
+extern "C" int toa_attn_set_dkdv_variant(int v) {
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
+  g_dkdv_variant = v;
+  return 0;
+}
+static bool attn_dkdv_asm_on() {
+  static const bool env_on = [] {
+    const char* e = getenv("TOA_ATTN_DKDV");
+    return !(e && strcmp(e, "hip") == 0);
+  }();
+  return g_dkdv_variant == 1 || (g_dkdv_variant < 0 && env_on);
+}
+
 template <int D, bool ROPE>
 static void dkdv_ds_launch(hipStream_t stream, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                            const float* nlse2, const float* delta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B, int H,
                            int Hk, int S, float scale, int o_bshd, const float* cosv, const float* sinv, int H3) {
+  if (D == 128 && !g_attn_tstat && attn_dkdv_asm_on()) {
+    // a refused shape (never one the dS form takes) falls through to the HIP kernel
+    if (toa_attn_dkdv_asm(q, k, v, dout, nlse2, delta, dk, dv, ds, B, H, Hk, S, D, scale, o_bshd | (ROPE ? 2 : 0),
+                          cosv, sinv, H3, stream) == 0)
+      return;
+  }
   const dim3 grid((S / 128) * B * Hk), block(512);
   if (g_attn_tstat)
     hipLaunchKernelGGL((attn_bwd_dkdv_ds_kernel<D, ROPE, true>), grid, block, 0, stream, q, k, v, dout, nlse2, delta,

@@ -33,7 +33,8 @@ namespace {
 
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
-       K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23, K_N = 26 };
+       K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
+       K_ATTN_DKDV = 26, K_N = 27 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -44,7 +45,7 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // K_ATTN_D1 ..: attn_gen.py VARIANTS (diagnostic arms, wrong outputs by design)
                            "toa_attn_fwd_asm_d1",      "toa_attn_fwd_asm_d2",        "toa_attn_fwd_asm_d3",
                            "toa_attn_fwd_asm_d4",      "toa_attn_fwd_asm_d5",        "toa_attn_fwd_asm_t1",
-                           "toa_attn_fwd_asm_c1",      "toa_attn_fwd_asm_t2"};
+                           "toa_attn_fwd_asm_c1",      "toa_attn_fwd_asm_t2",        "toa_attn_dkdv_asm"};
 
 struct DevModule {
   std::once_flag once;
@@ -364,7 +365,7 @@ extern "C" int toa_attn_fwd_asm(const bf16_t* q, const bf16_t* k, const bf16_t* 
 extern "C" int toa_attn_fwd_asm_variant(int v, const bf16_t* q, const bf16_t* k, const bf16_t* v_, bf16_t* o,
                                         float* lse, int B, int H, int Hk, int S, int D, int flags, float scale,
                                         hipStream_t stream) {
-  if (v < 0 || v > K_N - K_ATTN_D1 || K_ATTN_D1 + v - 1 == K_ATTN_T1 || K_ATTN_D1 + v - 1 == K_N - 1)
+  if (v < 0 || v > K_ATTN_DKDV - K_ATTN_D1 || K_ATTN_D1 + v - 1 == K_ATTN_T1 || K_ATTN_D1 + v - 1 == K_ATTN_DKDV - 1)
     return (int)hipErrorInvalidValue;  // the timing arms take toa_attn_fwd_asm_timing
   return attn_fwd_asm_launch(v ? K_ATTN_D1 + v - 1 : K_ATTN_FWD, q, k, v_, o, lse, B, H, Hk, S, D, flags, scale,
                              stream);
@@ -378,7 +379,7 @@ extern "C" int toa_attn_fwd_asm_timing(int which, void* dbg, const bf16_t* q, co
                                        bf16_t* o, float* lse, int B, int H, int Hk, int S, int D, int flags,
                                        float scale, hipStream_t stream) {
   if (!dbg || !al16(dbg) || (which != 1 && which != 2)) return (int)hipErrorInvalidValue;
-  return attn_fwd_asm_launch(which == 1 ? K_ATTN_T1 : K_N - 1, q, k, v, o, lse, B, H, Hk, S, D, flags, scale, stream,
+  return attn_fwd_asm_launch(which == 1 ? K_ATTN_T1 : K_ATTN_DKDV - 1, q, k, v, o, lse, B, H, Hk, S, D, flags, scale, stream,
                              dbg);
 }
 
@@ -442,4 +443,67 @@ extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16
   a.lds = (uint32_t)(ldgu * 2);
   a.fc = (uint32_t)(F * 2);
   return launch(K_SWIGLU_BWD, a, stream);
+}
+
+// Causal flash-attention dK / dV backward of the dS form (csrc/asm/attn_bwd_gen.py),
+// the contract of attention.hip's attn_bwd_dkdv_ds_kernel for the shapes this
+// kernel takes: head dim 128, S % 256 == 0; nlse2 / ndelta the delta pass's
+// -lse log2(e) / -delta rows; ds the dQ GEMM's packed dS blocks.  flags bit 0:
+// dO as [B, S, H, D]; bit 1: RoPE -- dK rotated back with cos / sin [S, 64]
+// and dK / dV written into the k / v parts of d(qkv) rows [B S, H3 D] (dk ==
+// dv == dqkv).  One workgroup of 4 waves per (128-key block, kv head, batch),
+// heaviest key blocks first; the 144-byte argument block matches KARG there.
+struct __attribute__((packed)) DkdvArgs {
+  uint64_t q, k, v, dout, nlse2, ndelta, dk, dv, ds, cosv, sinv, dbg;
+  uint32_t B, H, Hk, S;
+  float scale, c;  // scale, scale * log2(e)
+  uint32_t flags, rep, nkb, H3, pad[2];
+};
+static_assert(sizeof(DkdvArgs) == 144, "kernarg block must match csrc/asm/attn_bwd_gen.py KARG_BYTES");
+
+extern "C" int toa_attn_dkdv_asm(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
+                                 const float* nlse2, const float* ndelta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
+                                 int H, int Hk, int S, int D, float scale, int flags, const float* cosv,
+                                 const float* sinv, int H3, hipStream_t stream) {
+  const bool rope = (flags & 2) != 0;
+  if (D != 128 || B <= 0 || H <= 0 || Hk <= 0 || H % Hk || S <= 0 || S % 256 || !al16(q) || !al16(k) || !al16(v) ||
+      !al16(dout) || !al16(dk) || !al16(dv) || !al16(ds) || ((uintptr_t)nlse2 & 3) || ((uintptr_t)ndelta & 3) ||
+      (flags & ~3) || (rope && (!cosv || !sinv || !al16(cosv) || !al16(sinv) || H3 != H + 2 * Hk)))
+    return (int)hipErrorInvalidValue;
+  const int64_t nb = S / 32, nblk = nb * (nb + 1) / 2;
+  const int64_t nwg = (int64_t)(S / 128) * B * Hk;
+  // 32-bit offsets inside the kernel: dS blocks of one batch, dO / Q rows of
+  // one batch, d(qkv) rows; block-coordinate division below 2^24
+  if (nwg >= (1 << 24) || (int64_t)H * nblk * 2048 >= (1ll << 32) || (int64_t)S * H * 256 >= (1ll << 31) ||
+      (int64_t)B * S * (rope ? H3 : Hk) * 256 >= (1ll << 40))
+    return (int)hipErrorInvalidValue;
+  hipError_t err;
+  hipFunction_t fn = get_fn(K_ATTN_DKDV, &err);
+  if (!fn) return (int)err;
+  DkdvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.q = (uint64_t)q;
+  a.k = (uint64_t)k;
+  a.v = (uint64_t)v;
+  a.dout = (uint64_t)dout;
+  a.nlse2 = (uint64_t)nlse2;
+  a.ndelta = (uint64_t)ndelta;
+  a.dk = (uint64_t)dk;
+  a.dv = (uint64_t)dv;
+  a.ds = (uint64_t)ds;
+  a.cosv = (uint64_t)cosv;
+  a.sinv = (uint64_t)sinv;
+  a.B = (uint32_t)B;
+  a.H = (uint32_t)H;
+  a.Hk = (uint32_t)Hk;
+  a.S = (uint32_t)S;
+  a.scale = scale;
+  a.c = scale * 1.4426950408889634f;
+  a.flags = (uint32_t)flags;
+  a.rep = (uint32_t)(H / Hk);
+  a.nkb = (uint32_t)(S / 128);
+  a.H3 = (uint32_t)(rope ? H3 : 0);
+  size_t sz = sizeof(a);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  return (int)hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
 }

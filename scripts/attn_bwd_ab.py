@@ -4,6 +4,8 @@ rounds on random data (guide §5.4 rules 24/25):
 
     split   dQ kernel (recomputes S, dP) + 8-wave dK/dV (K/V re-read from LDS)
     ds      delta pass + dK/dV storing dS + dQ as a GEMM over the stored dS
+            (dK/dV on the assembly kernel, csrc/asm/attn_bwd_gen.py)
+    dship   the same with the HIP dK/dV kernel (attn_bwd_dkdv_ds_kernel)
 
 (Round-4 arms measured with this script, profiles/r4_attn/: kept -- the
 pipelined sub-tile, the store-aware step-end wait, P / dS overlapped with the
@@ -54,11 +56,13 @@ def main():
     outs = {}
 
     # backward form: 0 = split (dQ recomputes S / dP), 1 = dS through HBM + dQ GEMM
-    forms = {"split": 0, "ds": 1}
-    variants = a.variants.split(",")
+    forms = {"split": 0, "ds": 1, "dship": 1}
+    dkdv = {"split": -1, "ds": 1, "dship": 0}
+    variants = a.variants.replace("+", ",").split(",")
 
     def run(variant):
         _lib.call("toa_attn_set_bwd_variant", forms[variant])
+        _lib.call("toa_attn_set_dkdv_variant", dkdv[variant])
         nws = _lib.call_ret("toa_attn_bwd_ws_bytes", B, H, S, D)
         ws = torch.empty(nws, device=dev, dtype=torch.uint8) if nws > 0 else None
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
@@ -109,6 +113,7 @@ def main():
                                 "wait_cyc_per_step": round(float((t[:, w, 1] / steps[:, w]).mean()), 1)}
             res[var]["timing"] = per
     _lib.call("toa_attn_set_bwd_variant", -1)
+    _lib.call("toa_attn_set_dkdv_variant", -1)
     print(json.dumps(res))
 
 

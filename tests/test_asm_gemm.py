@@ -237,12 +237,12 @@ def test_host_kernel_table_matches_generator():
 
     src = open(os.path.join(os.path.dirname(HERE), "csrc", "hip", "gemm_asm.hip")).read()
     generated = set(re.findall(r"^(toa_\w+):", TEXT, re.M))
-    wanted = re.findall(r'"(toa_(?:gemm_tn_asm|wgrad_nt_asm|attn_fwd_asm)\w*)"', src)
+    wanted = re.findall(r'"(toa_(?:gemm_tn_asm|wgrad_nt_asm|attn_fwd_asm|attn_dkdv_asm)\w*)"', src)
     assert wanted and set(wanted) <= generated, set(wanted) - generated
     n = int(re.search(r"K_N = (\d+)", src).group(1))
-    # + the weight gradient's round-4 arm + the attention forward and its arms
+    # + the weight gradient's round-4 arm + the attention forward and its arms + the dK/dV backward
     import attn_gen
-    assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS)
+    assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1
     flags = re.search(r"kVariantPersist\[K_WGRAD_V1 - K_V1\] = \{([^}]*)\}", src).group(1)
     assert [f.strip() == "true" for f in flags.split(",")] == [bool(k.get("persist")) for _, k in gemm_gen.PLAIN_VARIANTS]
 
