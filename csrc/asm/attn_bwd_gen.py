@@ -90,36 +90,58 @@ KARG = {"Q": 0, "K": 8, "V": 16, "dO": 24, "NLSE": 32, "NDELTA": 40, "dK": 48, "
 S_Q, S_K, S_V, S_DO, S_NL, S_ND, S_DK, S_DV, S_DS, S_COS, S_SIN, S_DBG = range(4, 28, 2)
 S_B, S_H, S_HK, S_S, S_SC, S_C, S_FL, S_REP, S_NKB, S_H3 = range(28, 38)
 S_W, S_KB, S_BB, S_HKV, S_NQT, S_TOT, S_IT, S_MOD = range(38, 46)
-S_HEAD, S_NMOD, S_NHEAD, S_DIT, S_DMOD, S_DHEAD, S_HS, S_QS = range(46, 54)
-S_DSTR, S_M0B, S_SOFF, S_NBLK, S_TSOFF, S_LSOFF, S_BUFK, S_BUFS = range(54, 62)
-S_BUFD, S_DELK, S_DELS, S_HQ0, S_NREC, S_DSO0, S_DSO1, S_DD0 = range(62, 70)
+S_HEAD, S_NMOD, S_NHEAD, S_DIT, S_DMOD, S_DHEAD, S_HS256, S_QS64 = range(46, 54)
+S_DSTR, S_TB, S_SOFF, S_NBLK, S_TSOFF, S_LSOFF, S_LB, S_S4 = range(54, 62)
+S_4KB, S_KI, S_32W, S_HQ0, S_NREC, S_DSO0, S_DSO1, S_DD0 = range(62, 70)
 S_DD1, S_TOTM1 = 70, 71
 SRD_DMA, SRD_LD, SRD_DS0, SRD_DS1, SRD_X = 72, 76, 80, 84, 88
+S_LM0 = SRD_X + 2         # the -lse / -delta row's LDS base in a buffer (SRD_X is prologue-only)
 S_T0 = 92                 # s92..s95 scratch
 S_U = 96                  # s96, s97: srd64's own scratch
-N_SGPR = 98
+S_TM = 98                 # s98, s99: the timing arm's loop-start stamp (loop end: s[SRD_X:+1])
+N_SGPR = 100
 
 # ---------------------------------------------------------------- VGPRs
-V_RRO = 1                 # v1..v8: Q / dO row-read offsets per k-step (SD tile buffer)
-V_LO = 9                  # -lse / -delta read offset (SD tile buffer)
-V_TRO, V_TRO8 = 10, 14    # v10..v13, v14..v17: transposed-read offsets per d tile (KV tile buffer)
-V_DMA = 18                # v18..v21: DMA source offsets per piece & 3
+# Tile-buffer read offsets: set A (base 0) serves buffers 0 and 1 through the
+# instructions' 16-bit offsets, set B (base 2 BUFB) buffer 2.
+V_RRO = 1                 # v1..v8: Q / dO row-read offsets per k-step
+V_LO = 9                  # -lse / -delta read offset
+V_TRO, V_TRO8 = 10, 14    # v10..v13, v14..v17: transposed-read offsets per d tile
+V_RRO_B, V_LO_B, V_TRO_B = 82, 90, 91
+V_TRO8_B = (95, 96, 97, 20)
+V_C2 = 18                 # v18, v19: c = scale log2 e twice (packed-math operand)
 V_L4 = 22                 # lane * 4 (the -lse / -delta row DMA)
-V_DSO = 23                # dS store lane offset
+V_DSO = 23                # dS store lane offset: key 16 + query half 8
 V_MD0, V_MD = 24, 25      # mask: r - 4 hh, and + (first key - first query) of the block
 V_T = 26                  # v26..v33 scratch
 V_SF = 34                 # Q / dO fragment ring: 6 x 4
 V_KF = 58                 # dO^T / Q^T fragment ring: 6 x 4
-V_ST = 82                 # dS store staging: 2 x 8
 V_L = 98                  # -lse log2 e per block parity: 2 x 16
 V_PW = 130                # P packs per parity: 2 x 8
 V_SW = 146                # dS packs per parity: 2 x 8
 V_SB = 162                # S (16) + dP (16) per parity: 2 x 32
-V_X = 226                 # v226..v255 scratch (prologue / epilogue)
+V_DMA = 226               # v226..v233: DMA source offsets of the wave's 8 pieces
+V_X = 234                 # v234..v255 scratch (prologue / epilogue)
 
 # AGPRs: dV^T a[0:63], dK^T a[64:127] ([d tile] x 16), K / V B-operand
 # fragments a[128:159] / a[160:191] ([k-step] x 4)
 A_DV, A_DK, A_K, A_V = 0, 64, 128, 160
+
+# Schedule knobs; the DIAGNOSTIC arms (VARIANTS) switch one mechanism off to
+# price it in-process (scripts/attn_dkdv_arms.py): their outputs are wrong by
+# construction and only their time is read.
+KNOBS = {"bar": True, "vmwait": True, "lgkm": True, "exp": True, "dma": True, "valu": True, "lds": True,
+         "timing": False, "merge": True}
+VARIANTS = (
+    ("d1", {"lgkm": False}),                     # MFMAs do not wait for their LDS fragments
+    ("d2", {"bar": False, "vmwait": False}),     # no per-iteration barrier nor DMA wait
+    ("d3", {"exp": False}),                      # v_exp_f32 -> v_mov_b32
+    ("d4", {"dma": False, "vmwait": False}),     # no Q / dO staging in the loop
+    ("d5", {"valu": False}),                     # no softmax / dS VALU (stores kept)
+    ("d6", {"lds": False, "lgkm": False}),       # no LDS fragment reads
+    ("d7", {"lds": False, "lgkm": False, "valu": False, "dma": False, "vmwait": False, "bar": False}),  # MFMAs + SALU
+    ("t1", {"timing": True}),                    # the product kernel + s_memtime stamps (same outputs)
+)
 
 MASK_C = AG.MASK_C        # register r's row offset in a 32x32 accumulator: (r & 3) + 8 (r >> 2)
 
@@ -163,11 +185,27 @@ def kf(i):
     return V_KF + 4 * (i % RING)
 
 
+def rro(buf: int, s: int) -> tuple[int, int]:
+    """(offset register, immediate base) of row reads in tile buffer `buf`."""
+    return (V_RRO + s, buf * BUFB) if buf < 2 else (V_RRO_B + s, 0)
+
+
+def lo(buf: int) -> tuple[int, int]:
+    return (V_LO, buf * BUFB) if buf < 2 else (V_LO_B, 0)
+
+
+def tro(buf: int, dt: int, eight: bool) -> tuple[int, int]:
+    if buf < 2:
+        return (V_TRO8 if eight else V_TRO) + dt, buf * BUFB
+    return (V_TRO8_B[dt] if eight else V_TRO_B + dt), 0
+
+
 # ---------------------------------------------------------------- pieces
-def sd_frag(i: int, m: int) -> str:
+def sd_frag(i: int, m: int, buf: int) -> str:
     """SD fragment i (S / dP interleaved: i = 2 s + (0 Q | 1 dO)) of block half m."""
     s, od = divmod(i, 2)
-    return f"ds_read_b128 {vr(sf(i), 4)}, {vr(V_RRO + s)} offset:{od * OFF_DO + 8192 * m} ; SF{i}"
+    reg, b0 = rro(buf, s)
+    return f"ds_read_b128 {vr(sf(i), 4)}, {vr(reg)} offset:{b0 + od * OFF_DO + 8192 * m} ; SF{i}"
 
 
 def sd_mfmas(p: int) -> list:
@@ -187,25 +225,28 @@ def sd_mfmas(p: int) -> list:
     return out
 
 
-def lse_delta_reads(p: int, m: int) -> list[str]:
+def lse_delta_reads(p: int, m: int, buf: int) -> list[str]:
     """-lse log2 e rows into V_L[p], -delta into dP's accumulator (its
     initial value, so the MFMAs leave dP - delta)."""
+    reg, b0 = lo(buf)
     out = []
     for g in range(4):
-        out.append(f"ds_read_b128 {vr(V_L + 16 * p + 4 * g, 4)}, {vr(V_LO)} offset:{128 * m + 32 * g} ; LL")
+        out.append(f"ds_read_b128 {vr(V_L + 16 * p + 4 * g, 4)}, {vr(reg)} offset:{b0 + 128 * m + 32 * g} ; LL")
     for g in range(4):
-        out.append(f"ds_read_b128 {vr(dpbuf(p) + 4 * g, 4)}, {vr(V_LO)} offset:{256 + 128 * m + 32 * g} ; DL")
+        out.append(f"ds_read_b128 {vr(dpbuf(p) + 4 * g, 4)}, {vr(reg)} offset:{b0 + 256 + 128 * m + 32 * g} ; DL")
     return out
 
 
-def kv_frag(i: int, m: int) -> list[str]:
+def kv_frag(i: int, m: int, buf: int) -> list[str]:
     """KV fragment i (i = 2 (4 s2 + dt) + (0 dO^T | 1 Q^T)) of block half m:
     two transposed reads, 4 queries each (the P / dS pack's query order)."""
     j, q = divmod(i, 2)
     s2, dt = divmod(j, 4)
     base = (0 if q else OFF_DO) + (32 * m + 16 * s2) * ROWB
-    return [f"ds_read_b64_tr_b16 {vr(kf(i), 2)}, {vr(V_TRO + dt)} offset:{base} ; KF{i}",
-            f"ds_read_b64_tr_b16 {vr(kf(i) + 2, 2)}, {vr(V_TRO8 + dt)} offset:{base} ; KF{i}"]
+    r0, b0 = tro(buf, dt, False)
+    r8, b8 = tro(buf, dt, True)
+    return [f"ds_read_b64_tr_b16 {vr(kf(i), 2)}, {vr(r0)} offset:{b0 + base} ; KF{i}",
+            f"ds_read_b64_tr_b16 {vr(kf(i) + 2, 2)}, {vr(r8)} offset:{b8 + base} ; KF{i}"]
 
 
 def kv_mfmas(p: int) -> list:
@@ -230,232 +271,264 @@ def e_items(p: int, masked: bool, rel: int, dl: int, stream: str, st_rel: int | 
     if masked:
         items.append(Item([f"v_add_u32 {vr(V_MD)}, {sr(S_DD0 if p == 0 else S_DD1)}, {vr(V_MD0)}"], 4, rel, dl, stream))
     for j0 in range(0, 16, 4):
-        ins = [f"v_fma_f32 {vr(S0 + j)}, {vr(S0 + j)}, {sr(S_C)}, {vr(L0 + j)}" for j in range(j0, j0 + 4)]
-        ins += [f"v_exp_f32 {vr(S0 + j)}, {vr(S0 + j)}" for j in range(j0, j0 + 4)]
+        ins = [f"v_pk_fma_f32 {vr(S0 + j, 2)}, {vr(S0 + j, 2)}, {vr(V_C2, 2)}, {vr(L0 + j, 2)}" for j in range(j0, j0 + 4, 2)]
+        ins += [f"v_exp_f32 {vr(S0 + j)}, {vr(S0 + j)}" if KNOBS["exp"] else f"v_mov_b32 {vr(S0 + j)}, {vr(S0 + j)}"
+                for j in range(j0, j0 + 4)]
         items.append(Item(ins, 0, rel, dl, stream))
         if masked:   # key > query -> 0; each vcc pair kept together
             for j in range(j0, j0 + 4):
                 items.append(Item([f"v_cmp_lt_i32 vcc, {MASK_C[j]}, {vr(V_MD)}",
                                    f"v_cndmask_b32 {vr(S0 + j)}, {vr(S0 + j)}, 0, vcc"], 8, rel, dl, stream, split=False))
         ins = [f"v_cvt_pk_bf16_f32 {vr(V_PW + 8 * p + j // 2)}, {vr(S0 + j)}, {vr(S0 + j + 1)}" for j in range(j0, j0 + 4, 2)]
-        ins += [f"v_mul_f32 {vr(P0 + j)}, {vr(S0 + j)}, {vr(P0 + j)}" for j in range(j0, j0 + 4)]
+        ins += [f"v_pk_mul_f32 {vr(P0 + j, 2)}, {vr(S0 + j, 2)}, {vr(P0 + j, 2)}" for j in range(j0, j0 + 4, 2)]
         ins += [f"v_cvt_pk_bf16_f32 {vr(V_SW + 8 * p + j // 2)}, {vr(P0 + j)}, {vr(P0 + j + 1)}" for j in range(j0, j0 + 4, 2)]
         items.append(Item(ins, 0, rel, dl, stream))
-    # dS block store: chunk k = the lanes' (key, 8-query group 2 k + hh) -- a
-    # permlane32 swap of copies (the packs stay the MFMA operands)
-    st = V_ST + 8 * p
+    # dS block store: the lane's 4 queries 8 g + 4 hh .. + 3 of key r are the
+    # packs 2 g, 2 g + 1 -> 8 B at (g, key r, query half hh) of the block's
+    # [8-query group][key][8 queries] layout (512 contiguous bytes per store)
     srd = SRD_DS0 if p == 0 else SRD_DS1
     dso = S_DSO0 if p == 0 else S_DSO1
     srel = rel if st_rel is None else max(rel, st_rel)
-    for k in range(2):
-        ins = [f"v_mov_b32 {vr(st + 4 * k + e)}, {vr(V_SW + 8 * p + 4 * k + e)}" for e in range(4)]
-        ins += ["s_nop 1",
-                f"v_permlane32_swap_b32 {vr(st + 4 * k)}, {vr(st + 4 * k + 2)}",
-                f"v_permlane32_swap_b32 {vr(st + 4 * k + 1)}, {vr(st + 4 * k + 3)}",
-                f"buffer_store_dwordx4 {vr(st + 4 * k, 4)}, {vr(V_DSO)}, {sr(srd, 4)}, {sr(dso)} offen offset:{1024 * k} nt"]
-        items.append(Item(ins, 40, srel, max(srel, dl), stream, split=False))
+    for g in range(4):
+        items.append(Item([f"buffer_store_dwordx2 {vr(V_SW + 8 * p + 2 * g, 2)}, {vr(V_DSO)}, {sr(srd, 4)}, {sr(dso)} "
+                           f"offen offset:{512 * g} nt"], 8, max(srel, rel + 1), max(srel, dl), stream))
+    if not KNOBS["valu"]:
+        items = items[-4:]
     for it in items:
         if it.cost == 0:
             it.cost = sum(AG.issue_cost(x) for x in it.ins)
     return items
 
 
-def dso_setup(p: int, mod: int, head: int, m: int) -> list[str]:
-    """Block (step (mod, head), half m) of this wave: dS block byte offset
-    ((hq0 + head) NBLK + qi (qi + 1) / 2 + ki) 2048 into S_DSO<p>, the store
-    resource's size (0 = dropped: block wholly above the diagonal, qi < ki),
-    and the mask shift kw - qs = 32 w - 64 mod - 32 m into S_DD<p>."""
-    t0, t1, t2 = S_T0, S_T0 + 1, S_T0 + 2
-    dso, srd, dd = (S_DSO0, SRD_DS0, S_DD0) if p == 0 else (S_DSO1, SRD_DS1, S_DD1)
-    return [f"s_lshl_b32 {sr(t0)}, {sr(mod)}, 1",
-            f"s_add_u32 {sr(t0)}, {sr(t0)}, {m}",                   # 2 mod + m
+def dso_step(mod: int, head: int) -> list[str]:
+    """Both blocks of step (mod, head) for this wave: dS block byte offsets
+    ((hq0 + head) NBLK + qi (qi + 1) / 2 + ki) 2048 (qi = 4 kb + 2 mod + m,
+    ki = 4 kb + w) into S_DSO0 / S_DSO1, the store resources' sizes (0 =
+    dropped: block wholly above the diagonal, qi < ki), and the mask shifts
+    kw - qs = 32 w - 64 mod - 32 m into S_DD0 / S_DD1."""
+    t0, t1, t2, t3 = S_T0, S_T0 + 1, S_T0 + 2, S_T0 + 3
+    return [f"s_lshl_b32 {sr(t0)}, {sr(mod)}, 1",                   # 2 mod
+            f"s_add_u32 {sr(t1)}, {sr(t0)}, {sr(S_4KB)}",           # qi0
+            f"s_add_u32 {sr(t2)}, {sr(t1)}, 1",
+            f"s_mul_i32 {sr(t1)}, {sr(t1)}, {sr(t2)}",
+            f"s_lshr_b32 {sr(t1)}, {sr(t1)}, 1",                    # qi0 (qi0 + 1) / 2
+            f"s_add_u32 {sr(t3)}, {sr(S_HQ0)}, {sr(head)}",
+            f"s_mul_i32 {sr(t3)}, {sr(t3)}, {sr(S_NBLK)}",
+            f"s_add_u32 {sr(t3)}, {sr(t3)}, {sr(S_KI)}",
+            f"s_add_u32 {sr(t1)}, {sr(t1)}, {sr(t3)}",
+            f"s_lshl_b32 {sr(S_DSO0)}, {sr(t1)}, 11",
+            f"s_add_u32 {sr(t1)}, {sr(t1)}, {sr(t2)}",              # + qi0 + 1: block (qi0 + 1, ki)
+            f"s_lshl_b32 {sr(S_DSO1)}, {sr(t1)}, 11",
             f"s_cmp_ge_u32 {sr(t0)}, {sr(S_W)}",
-            f"s_cselect_b32 {sr(srd + 2)}, {sr(S_NREC)}, 0",
-            f"s_lshl_b32 {sr(t1)}, {sr(S_KB)}, 2",
-            f"s_add_u32 {sr(t0)}, {sr(t0)}, {sr(t1)}",              # qi = 4 kb + 2 mod + m
-            f"s_add_u32 {sr(t2)}, {sr(t0)}, 1",
-            f"s_mul_i32 {sr(t0)}, {sr(t0)}, {sr(t2)}",
-            f"s_lshr_b32 {sr(t0)}, {sr(t0)}, 1",                    # qi (qi + 1) / 2
-            f"s_add_u32 {sr(t1)}, {sr(t1)}, {sr(S_W)}",             # ki = 4 kb + w
-            f"s_add_u32 {sr(t0)}, {sr(t0)}, {sr(t1)}",
-            f"s_add_u32 {sr(t1)}, {sr(S_HQ0)}, {sr(head)}",
-            f"s_mul_i32 {sr(t1)}, {sr(t1)}, {sr(S_NBLK)}",
-            f"s_add_u32 {sr(t0)}, {sr(t0)}, {sr(t1)}",
-            f"s_lshl_b32 {sr(dso)}, {sr(t0)}, 11",
-            f"s_lshl_b32 {sr(t0)}, {sr(S_W)}, 5",
-            f"s_lshl_b32 {sr(t1)}, {sr(mod)}, 6",
-            f"s_sub_u32 {sr(dd)}, {sr(t0)}, {sr(t1)}",
-            f"s_sub_u32 {sr(dd)}, {sr(dd)}, {32 * m}"]
+            f"s_cselect_b32 {sr(SRD_DS0 + 2)}, {sr(S_NREC)}, 0",
+            f"s_add_u32 {sr(t0)}, {sr(t0)}, 1",
+            f"s_cmp_ge_u32 {sr(t0)}, {sr(S_W)}",
+            f"s_cselect_b32 {sr(SRD_DS1 + 2)}, {sr(S_NREC)}, 0",
+            f"s_lshl_b32 {sr(t0)}, {sr(mod)}, 6",
+            f"s_sub_u32 {sr(S_DD0)}, {sr(S_32W)}, {sr(t0)}",
+            f"s_sub_u32 {sr(S_DD1)}, {sr(S_DD0)}, 32"]
 
 
-def advance(mod: int, head: int, inc: str = "1") -> list[str]:
-    """(mod, head) -> the next step's (mod + inc, wrapping to the next head);
-    inc is 1 or an SGPR holding 0 / 1."""
-    return [f"s_add_u32 {sr(mod)}, {sr(mod)}, {inc}",
+def advance(mod: int, head: int) -> list[str]:
+    """(mod, head) -> the next step's: mod + 1, wrapping to the next head
+    (the compare's SCC is the head's carry)."""
+    return [f"s_add_u32 {sr(mod)}, {sr(mod)}, 1",
             f"s_cmp_eq_u32 {sr(mod)}, {sr(S_NQT)}",
-            f"s_cselect_b32 {sr(S_T0 + 3)}, 1, 0",
-            f"s_add_u32 {sr(head)}, {sr(head)}, {sr(S_T0 + 3)}",
-            f"s_cmp_eq_u32 {sr(mod)}, {sr(S_NQT)}",
-            f"s_cselect_b32 {sr(mod)}, 0, {sr(mod)}"]
+            f"s_cselect_b32 {sr(mod)}, 0, {sr(mod)}",
+            f"s_addc_u32 {sr(head)}, {sr(head)}, 0"]
 
 
 def dma_advance() -> list[str]:
     """The DMA step (S_DIT; coordinates S_DMOD / S_DHEAD) moves on unless it
     is the last step already (past the end the last tile is re-fetched into
     a buffer nobody reads: a constant DMA count per iteration)."""
-    return [f"s_add_u32 {sr(S_T0 + 2)}, {sr(S_DIT)}, 1",
-            f"s_cmp_lt_u32 {sr(S_T0 + 2)}, {sr(S_TOT)}",
-            f"s_cselect_b32 {sr(S_DIT)}, {sr(S_T0 + 2)}, {sr(S_DIT)}",
-            f"s_cselect_b32 {sr(S_T0 + 2)}, 1, 0"] + advance(S_DMOD, S_DHEAD, sr(S_T0 + 2))
+    t = S_T0 + 2
+    return [f"s_add_u32 {sr(t)}, {sr(S_DIT)}, 1",
+            f"s_cmp_lt_u32 {sr(t)}, {sr(S_TOT)}",
+            f"s_cselect_b32 {sr(S_DIT)}, {sr(t)}, {sr(S_DIT)}",
+            f"s_cselect_b32 {sr(t)}, 1, 0",
+            f"s_add_u32 {sr(S_DMOD)}, {sr(S_DMOD)}, {sr(t)}",
+            f"s_cmp_eq_u32 {sr(S_DMOD)}, {sr(S_NQT)}",
+            f"s_cselect_b32 {sr(S_DMOD)}, 0, {sr(S_DMOD)}",
+            f"s_addc_u32 {sr(S_DHEAD)}, {sr(S_DHEAD)}, 0"]
 
 
 def dma_setup() -> list[str]:
-    """Tile (S_DMOD, S_DHEAD) into buffer S_BUFD: source offset of this
-    wave's first piece (S_TSOFF) and of the -lse / -delta row (S_LSOFF), LDS
-    base (S_M0B)."""
+    """Tile (S_DMOD, S_DHEAD): source offset of this wave's pieces (S_TSOFF;
+    the row part of each piece is in its VGPR offset) and of the -lse /
+    -delta row (S_LSOFF)."""
     t0, t1 = S_T0, S_T0 + 1
-    return [f"s_lshl_b32 {sr(t0)}, {sr(S_KB)}, 1",
-            f"s_add_u32 {sr(t0)}, {sr(t0)}, {sr(S_DMOD)}",          # qt = 2 kb + mod
-            f"s_lshl_b32 {sr(t0)}, {sr(t0)}, 6",                    # first query row
-            f"s_mul_i32 {sr(t1)}, {sr(S_DHEAD)}, {sr(S_S)}",
-            f"s_add_u32 {sr(t1)}, {sr(t1)}, {sr(t0)}",
-            f"s_lshl_b32 {sr(S_LSOFF)}, {sr(t1)}, 2",               # (head S + q0) 4
-            f"s_mul_i32 {sr(t0)}, {sr(t0)}, {sr(S_QS)}",
-            f"s_mul_i32 {sr(t1)}, {sr(S_DHEAD)}, {sr(S_HS)}",
+    return [f"s_mul_i32 {sr(t0)}, {sr(S_DMOD)}, {sr(S_QS64)}",
+            f"s_mul_i32 {sr(t1)}, {sr(S_DHEAD)}, {sr(S_HS256)}",
             f"s_add_u32 {sr(t0)}, {sr(t0)}, {sr(t1)}",
-            f"s_lshl_b32 {sr(t0)}, {sr(t0)}, 8",
-            f"s_and_b32 {sr(t1)}, {sr(S_W)}, 1",
-            f"s_mul_i32 {sr(t1)}, {sr(t1)}, {sr(S_DSTR)}",
-            f"s_lshl_b32 {sr(t1)}, {sr(t1)}, 5",                    # 32 (w & 1) rows
-            f"s_add_u32 {sr(S_TSOFF)}, {sr(t0)}, {sr(t1)}",
-            f"s_mul_i32 {sr(S_M0B)}, {sr(S_BUFD)}, {BUFB}",
-            f"s_add_u32 {sr(S_M0B)}, {sr(S_M0B)}, {sr(S_SOFF)}"]    # + the wave's region / piece base
+            f"s_add_u32 {sr(S_TSOFF)}, {sr(t0)}, {sr(S_TB)}",
+            f"s_lshl_b32 {sr(t0)}, {sr(S_DMOD)}, 8",
+            f"s_mul_i32 {sr(t1)}, {sr(S_DHEAD)}, {sr(S_S4)}",
+            f"s_add_u32 {sr(t0)}, {sr(t0)}, {sr(t1)}",
+            f"s_add_u32 {sr(S_LSOFF)}, {sr(t0)}, {sr(S_LB)}"]
 
 
-def dma_pieces() -> list[list[str]]:
-    """This wave's 8 pieces of the Q (waves 0, 1) or dO (2, 3) tile, then
-    its -lse (even waves) / -delta (odd) row."""
+def dma_pieces(buf: int) -> list[list[str]]:
+    """This wave's 8 pieces of the Q (waves 0, 1) or dO (2, 3) tile into tile
+    buffer `buf`, then its -lse (even waves) / -delta (odd) row."""
     out = []
     for u in range(8):
-        out.append([f"s_mul_i32 {sr(S_T0 + 2)}, {sr(S_DSTR)}, {4 * u}",
-                    f"s_add_u32 {sr(S_T0 + 2)}, {sr(S_T0 + 2)}, {sr(S_TSOFF)}",
-                    f"s_add_u32 m0, {sr(S_M0B)}, {1024 * u}",
+        out.append([f"s_add_u32 m0, {sr(S_SOFF)}, {buf * BUFB + 1024 * u}",
                     "s_nop 0",
-                    f"buffer_load_dwordx4 {vr(V_DMA + (u & 3))}, {sr(SRD_DMA, 4)}, {sr(S_T0 + 2)} offen lds"])
-    out.append([f"s_mul_i32 {sr(S_T0 + 2)}, {sr(S_BUFD)}, {BUFB}",
-                f"s_and_b32 {sr(S_T0 + 3)}, {sr(S_W)}, 1",
-                f"s_lshl_b32 {sr(S_T0 + 3)}, {sr(S_T0 + 3)}, 8",
-                f"s_add_u32 {sr(S_T0 + 2)}, {sr(S_T0 + 2)}, {sr(S_T0 + 3)}",
-                f"s_add_u32 m0, {sr(S_T0 + 2)}, {OFF_L}",
+                    f"buffer_load_dwordx4 {vr(V_DMA + u)}, {sr(SRD_DMA, 4)}, {sr(S_TSOFF)} offen lds"])
+    out.append([f"s_add_u32 m0, {sr(S_LM0)}, {buf * BUFB}",
                 "s_nop 0",
                 f"buffer_load_dword {vr(V_L4)}, {sr(SRD_LD, 4)}, {sr(S_LSOFF)} offen lds"])
     return out
 
 
-def rot3(buf: int, dl: int) -> list[str]:
-    """buf <- (buf + 1) % 3, and s[dl] = the byte delta of that move."""
-    return [f"s_mov_b32 {sr(dl)}, {BUFB}",
-            f"s_cmp_eq_u32 {sr(buf)}, 2",
-            f"s_cselect_b32 {sr(dl)}, {-2 * BUFB & 0xFFFFFFFF:#x}, {sr(dl)}",
-            f"s_add_u32 {sr(buf)}, {sr(buf)}, 1",
-            f"s_cmp_eq_u32 {sr(buf)}, 3",
-            f"s_cselect_b32 {sr(buf)}, 0, {sr(buf)}"]
-
-
-def rot_sd() -> list[str]:
-    return [f"v_add_u32 {vr(V_RRO + s)}, {sr(S_DELS)}, {vr(V_RRO + s)}" for s in range(8)] + \
-           [f"v_add_u32 {vr(V_LO)}, {sr(S_DELS)}, {vr(V_LO)}"]
-
-
-def rot_kv() -> list[str]:
-    return [f"v_add_u32 {vr(V_TRO + dt)}, {sr(S_DELK)}, {vr(V_TRO + dt)}" for dt in range(4)] + \
-           [f"v_add_u32 {vr(V_TRO8 + dt)}, {sr(S_DELK)}, {vr(V_TRO8 + dt)}" for dt in range(4)]
-
-
 NPRE = 2                  # KV fragments of the next body read at the end of this one
 
 
-def kv_read_items(base: int, m: int, base_prev: int | None, pre: bool, stream: str) -> list[Item]:
+def kv_read_items(base: int, m: int, buf: int, base_prev: int | None, pre: bool, stream: str) -> list[Item]:
     """KV fragment reads for MFMAs base .. base + 15 (fragments 0 .. NPRE - 1
     already read when pre)."""
     items = []
     for i in range(NPRE if pre else 0, 16):
         rel = slot_rel(i, base, base_prev)
-        items.append(Item(kv_frag(i, m), 8, rel, max(rel, base + i - 3), stream))
+        items.append(Item(kv_frag(i, m, buf), 8, rel, max(rel, base + i - 3), stream))
     return items
 
 
-def kv_prefetch_items(rel: int, dl: int, m: int) -> list[Item]:
+def kv_prefetch_items(rel: int, dl: int, m: int, buf: int) -> list[Item]:
     """Fragments 0 .. NPRE - 1 of the next body's KV, read in this body's
     last gaps (rel: after the MFMAs that last used their ring slots)."""
-    return [Item(kv_frag(i, m), 8, rel, dl, "kvpre") for i in range(NPRE)]
+    return [Item(kv_frag(i, m, buf), 8, rel, dl, "kvpre") for i in range(NPRE)]
 
 
-def sd_read_items(base: int, m: int, p: int, rel0: int, base_prev: int | None, ld_rel: int, stream: str) -> list[Item]:
+def sd_read_items(base: int, m: int, p: int, buf: int, rel0: int, base_prev: int | None, ld_rel: int,
+                  stream: str) -> list[Item]:
     """SD(n) reads for MFMAs base .. base + 15: the -lse rows (by the last S
     MFMA) and -delta rows (into dP, by the first dP MFMA) no earlier than gap
     ld_rel, the Q / dO fragments no earlier than rel0."""
-    lr = lse_delta_reads(p, m)
+    lr = lse_delta_reads(p, m, buf)
     items = [Item(lr[4:], 16, ld_rel, max(ld_rel, base - 1), stream + "d"),
              Item(lr[:4], 16, ld_rel, max(ld_rel, base + 11), stream + "l")]
     for i in range(16):
         rel = max(rel0, slot_rel(i, base, base_prev))
-        items.append(Item([sd_frag(i, m)], 4, rel, max(rel, base + i - 3), stream))
+        items.append(Item([sd_frag(i, m, buf)], 4, rel, max(rel, base + i - 3), stream))
     return items
 
 
+def schedule_merged(a: Asm, mfmas: list, items: list, tail=None, pre=()):
+    """attn_gen.schedule, with each lgkmcnt wait also covering the next
+    MFMA's fragments when they are already in flight (one wait per two
+    MFMAs: each wait costs an issue slot, and one wave per SIMD issues at
+    most one instruction per 4 cycles)."""
+    if not KNOBS["merge"]:
+        return schedule(a, mfmas, items, tail, pre=pre)
+    out = []
+
+    class Cap:          # collect schedule()'s output, then rewrite its waits
+        def __call__(self, txt):
+            out.append(txt)
+    saved = dict(AG.KNOBS)
+    AG.KNOBS["lgkm"] = False
+    try:
+        schedule(Cap(), mfmas, items, tail, pre=())
+    finally:
+        AG.KNOBS.clear()
+        AG.KNOBS.update(saved)
+    if not KNOBS["lgkm"]:
+        for t in out:
+            a(t)
+        return
+    # replay: lds = tags of issued reads in order; before MFMA g wait for
+    # the tags of g (and of g + 1 when all of them were read already)
+    lds: list = list(pre)
+    done = 0
+    mf_idx = [i for i, t in enumerate(out) if t.startswith("v_mfma")]
+    need_tags = {i: mfmas[k][1] for k, i in enumerate(mf_idx)}
+    nxt = {mf_idx[k]: mf_idx[k + 1] for k in range(len(mf_idx) - 1)}
+
+    def idx_of(t):
+        return max((i for i, x in enumerate(lds) if x == t), default=-1)
+
+    for i, t in enumerate(out):
+        if i in need_tags:
+            need = 0
+            for tag in need_tags[i]:
+                j = idx_of(tag)
+                assert j >= 0, f"MFMA needs {tag} before any read of it"
+                need = max(need, j + 1)
+            if need > done:
+                j2 = nxt.get(i)
+                if j2 is not None:
+                    idx2 = [idx_of(tag) for tag in need_tags[j2]]
+                    if idx2 and min(idx2) >= 0:
+                        need = max(need, max(idx2) + 1)
+                cnt = min(15, len(lds) - need)
+                a(f"s_waitcnt lgkmcnt({cnt})")
+                done = len(lds) - cnt
+        a(t)
+        if t.startswith("ds_read"):
+            lds.append(t.split(";")[1].strip() if ";" in t else None)
+
+
+def sched(a: Asm, mf: list, items: list, tail=None, pre=()):
+    """The list schedule with this kernel's knobs (lgkm waits, LDS reads)."""
+    items = [it for it in items if it.ins]
+    if not KNOBS["lds"]:
+        items = [it for it in items if not it.ins[0].startswith("ds_read")]
+        mf = [(t, []) for t, _ in mf]
+        pre = ()
+    schedule_merged(a, mf, items, tail, pre=pre)
+
+
 # ---------------------------------------------------------------- loop bodies
-def iteration(a: Asm, m1: bool, m2: bool, top: str):
-    """One step it (not the last): MFMAs KV(2 it) [0..15], SD(2 it + 2)
-    [16..31], KV(2 it + 1) [32..47], SD(2 it + 3) [48..63]."""
+def iteration(a: Asm, m1: bool, m2: bool, ph: int, nxt: str):
+    """One step it (not the last), it % 3 == ph: MFMAs KV(2 it) [0..15],
+    SD(2 it + 2) [16..31], KV(2 it + 1) [32..47], SD(2 it + 3) [48..63].
+    Tile it sits in buffer ph, tile it + 1 in ph + 1, tile it + 2 goes to ph + 2."""
+    kbuf, sbuf_, dbuf = ph, (ph + 1) % 3, (ph + 2) % 3
     mf = kv_mfmas(0) + sd_mfmas(0) + kv_mfmas(1) + sd_mfmas(1)
     n = len(mf)
     items: list[Item] = []
     # KV reads (tile it); KV(2 it)'s first NPRE fragments came with the previous body
-    items += kv_read_items(0, 0, None, True, "kr")
-    items += kv_read_items(32, 1, 0, False, "kr2")
+    items += kv_read_items(0, 0, kbuf, None, True, "kr")
+    items += kv_read_items(32, 1, kbuf, 0, False, "kr2")
     # the barrier: every wave's pieces of tile it + 1 landed (vmcnt: only the
-    # two dS stores of E(2 it) -- issued after every DMA piece -- and any
+    # four dS stores of E(2 it) -- issued after every DMA piece -- and any
     # since may be outstanding), every wave done with tile it - 1
-    items.append(Item(["s_waitcnt vmcnt(2)", "s_barrier"], 8, G_BAR, G_BAR, "bar", split=False))
+    items.append(Item((["s_waitcnt vmcnt(4)"] if KNOBS["vmwait"] else []) + (["s_barrier"] if KNOBS["bar"] else []),
+                      8, G_BAR, G_BAR, "bar", split=False))
     # SD reads (tile it + 1): SD(2 it + 2) after the barrier; SD(2 it + 3)'s
     # -lse / -delta rows after E(2 it + 1) let go of the parity-1 registers
-    items += sd_read_items(16, 0, 0, G_BAR, None, G_BAR, "sr")
-    items += sd_read_items(48, 1, 1, -1, 16, 30, "sr2")
-    # E(2 it + 1) (parity 1: step it, half 1), E(2 it + 2) (parity 0: step it + 1, half 0)
-    items.append(Item(dso_setup(1, S_MOD, S_HEAD, 1), 40, -1, 1, "e1", split=False))
+    items += sd_read_items(16, 0, 0, sbuf_, G_BAR, None, G_BAR, "sr")
+    items += sd_read_items(48, 1, 1, sbuf_, -1, 16, 30, "sr2")
+    # E(2 it + 1) (parity 1: step it, half 1) uses S_DSO1 / S_DD1 / SRD_DS1 of
+    # step it; then both halves' of step it + 1 for E(2 it + 2) (now) and E(2 it + 3)
     items += e_items(1, m1, 1, 29, "e1")
-    items.append(Item(dso_setup(0, S_NMOD, S_NHEAD, 0), 40, 20, 33, "e2", split=False))
+    items.append(Item(dso_step(S_NMOD, S_NHEAD), 40, 30, 33, "e2", split=False))
     items += e_items(0, m2, 33, 61, "e2", st_rel=DL_DMA + 1)
-    # DMA of tile min(it + 2, last) into buffer S_BUFD, after the barrier
-    items.append(Item(dma_setup(), 40, -1, G_BAR, "dma", split=False))
-    for ins in dma_pieces():
+    # DMA of tile min(it + 2, last) into buffer ph + 2, after the barrier
+    items.append(Item(dma_setup(), 16, -1, G_BAR, "dma", split=False))
+    for ins in dma_pieces(dbuf) if KNOBS["dma"] else []:
         items.append(Item(ins, 48, G_BAR, DL_DMA, "dma", split=False))
-    # bookkeeping for the next iteration; the offset rotations (KV after the
-    # last KV(2 it + 1) read, SD after the last SD(2 it + 3) read) and KV(2 it + 2)'s
-    # first fragments (their ring slots last used by MFMAs 44, 45)
+    # bookkeeping for the next iteration, and KV(2 it + 2)'s first fragments
+    # (tile it + 1; their ring slots last used by MFMAs 44, 45)
     book = [[f"s_add_u32 {sr(S_IT)}, {sr(S_IT)}, 1",
              f"s_mov_b32 {sr(S_MOD)}, {sr(S_NMOD)}",
-             f"s_mov_b32 {sr(S_HEAD)}, {sr(S_NHEAD)}"], advance(S_NMOD, S_NHEAD), dma_advance(),
-            rot3(S_BUFD, S_T0 + 3), rot3(S_BUFK, S_DELK), rot3(S_BUFS, S_DELS)]
+             f"s_mov_b32 {sr(S_HEAD)}, {sr(S_NHEAD)}"], advance(S_NMOD, S_NHEAD), dma_advance()]
     for ins in book:   # each group SCC-self-contained
         items.append(Item(ins, 2 * len(ins), DL_DMA + 1, 44, "book", split=False))
-    items.append(Item(rot_kv(), 32, 45, 61, "book"))
-    items += [Item(x.ins, x.cost, 46, n - 1, "book") for x in kv_prefetch_items(0, 0, 0)]
-    items.append(Item(rot_sd(), 36, 61, n - 1, "rot2"))
-    schedule(a, mf, items, [f"s_branch {top}"], pre=("KF0", "KF0", "KF1", "KF1"))
+    items += kv_prefetch_items(46, n - 1, 0, sbuf_)
+    sched(a, mf, items, [f"s_branch {nxt}"], pre=("KF0", "KF0", "KF1", "KF1"))
 
 
-def tail(a: Asm, m1: bool):
+def tail(a: Asm, m1: bool, ph: int):
     """The last step: KV(N - 2) [0..15] with E(N - 1), then KV(N - 1)."""
     mf = kv_mfmas(0) + kv_mfmas(1)
     items: list[Item] = []
-    items += kv_read_items(0, 0, None, True, "kr")
-    items += kv_read_items(16, 1, 0, False, "kr2")
-    items.append(Item(dso_setup(1, S_MOD, S_HEAD, 1), 40, -1, 1, "e1", split=False))
+    items += kv_read_items(0, 0, ph, None, True, "kr")
+    items += kv_read_items(16, 1, ph, 0, False, "kr2")
     items += e_items(1, m1, 1, 13, "e1")
-    schedule(a, mf, items, pre=("KF0", "KF0", "KF1", "KF1"))
-
+    sched(a, mf, items, pre=("KF0", "KF0", "KF1", "KF1"))
 
 
 # ---------------------------------------------------------------- prologue
@@ -464,7 +537,7 @@ def prologue(a: Asm):
     a(f"s_load_dwordx8 {sr(20, 8)}, s[0:1], 0x40")
     a(f"s_load_dwordx8 {sr(28, 8)}, s[0:1], 0x60")
     a(f"s_load_dwordx2 {sr(36, 2)}, s[0:1], 0x80")
-    a(f"v_lshrrev_b32 {vr(V_X + 29)}, 6, v0")            # wave id
+    a(f"v_lshrrev_b32 {vr(V_X + 20)}, 6, v0")            # wave id
     a("s_waitcnt lgkmcnt(0)")
     t0, t1, t2, t3 = S_T0, S_T0 + 1, S_T0 + 2, S_T0 + 3
     # defensive checks (the host launcher validates the same): S = 128 nkb,
@@ -485,7 +558,7 @@ def prologue(a: Asm):
     AG.udiv(a, S_KB, t2, 2, t1)
     AG.udiv(a, S_BB, S_HKV, t2, S_HK)
     a("s_nop 4")
-    a(f"v_readfirstlane_b32 {sr(S_W)}, {vr(V_X + 29)}")
+    a(f"v_readfirstlane_b32 {sr(S_W)}, {vr(V_X + 20)}")
     a("s_nop 4")
     # steps per head pass nqt = S / 64 - 2 kb, total = nqt rep
     a(f"s_lshr_b32 {sr(S_NQT)}, {sr(S_S)}, 6")
@@ -506,8 +579,8 @@ def prologue(a: Asm):
     a(f"s_mul_i32 {sr(t0)}, {sr(t0)}, {sr(S_S)}")                 # (b H + hq0) S
     a(f"s_mul_i32 {sr(t1)}, {sr(S_REP)}, {sr(S_S)}")
     a(f"s_lshl_b32 {sr(t1)}, {sr(t1)}, 8")                       # rep S rows
-    a(f"s_mov_b32 {sr(S_HS)}, {sr(S_S)}")
-    a(f"s_mov_b32 {sr(S_QS)}, 1")
+    a(f"s_mov_b32 {sr(S_HS256)}, {sr(S_S)}")          # head stride in rows (scaled below)
+    a(f"s_mov_b32 {sr(S_QS64)}, 1")                   # query stride in rows
     a(f"s_mov_b32 {sr(S_DSTR)}, {ROWB}")
     a(f"s_cmp_lt_u32 {sr(S_W)}, 2")
     a(f"s_cbranch_scc1 {lq}")
@@ -520,8 +593,8 @@ def prologue(a: Asm):
     a(f"s_mul_i32 {sr(t1)}, {sr(S_S)}, {sr(S_H)}")
     a(f"s_sub_u32 {sr(t1)}, {sr(t1)}, {sr(S_HQ0)}")
     a(f"s_lshl_b32 {sr(t1)}, {sr(t1)}, 8")
-    a(f"s_mov_b32 {sr(S_HS)}, 1")
-    a(f"s_mov_b32 {sr(S_QS)}, {sr(S_H)}")
+    a(f"s_mov_b32 {sr(S_HS256)}, 1")
+    a(f"s_mov_b32 {sr(S_QS64)}, {sr(S_H)}")
     a(f"s_lshl_b32 {sr(S_DSTR)}, {sr(S_H)}, 8")
     a.label(ld + "_do")
     srd64(a, SRD_DMA, S_DO, t0, ROWB, sr(t1))
@@ -529,12 +602,30 @@ def prologue(a: Asm):
     a.label(lq)
     srd64(a, SRD_DMA, S_Q, t0, ROWB, sr(t1))
     a.label(ld)
+    # tile offsets: TSOFF = mod QS64 + head HS256 + TB, with QS64 = 64 QS 256,
+    # HS256 = HS 256, TB = 2 kb 64 QS 256 + 32 (w & 1) DSTR (the wave's rows)
+    t0_, t1_ = S_T0, S_T0 + 1
+    a(f"s_lshl_b32 {sr(S_QS64)}, {sr(S_QS64)}, 14")
+    a(f"s_lshl_b32 {sr(S_HS256)}, {sr(S_HS256)}, 8")
+    a(f"s_mul_i32 {sr(S_TB)}, {sr(S_KB)}, {sr(S_QS64)}")
+    a(f"s_lshl_b32 {sr(S_TB)}, {sr(S_TB)}, 1")
+    a(f"s_and_b32 {sr(t0_)}, {sr(S_W)}, 1")
+    a(f"s_mul_i32 {sr(t0_)}, {sr(t0_)}, {sr(S_DSTR)}")
+    a(f"s_lshl_b32 {sr(t0_)}, {sr(t0_)}, 5")
+    a(f"s_add_u32 {sr(S_TB)}, {sr(S_TB)}, {sr(t0_)}")
+    # -lse / -delta row offsets: LSOFF = mod 256 + head S4 + LB (LB = 2 kb 64 4)
+    a(f"s_lshl_b32 {sr(S_S4)}, {sr(S_S)}, 2")
+    a(f"s_lshl_b32 {sr(S_LB)}, {sr(S_KB)}, 9")
     # piece region / base inside a tile buffer: Q or dO region + 8 (w & 1) pieces
     a(f"s_and_b32 {sr(t0)}, {sr(S_W)}, 1")
     a(f"s_lshl_b32 {sr(S_SOFF)}, {sr(t0)}, 13")
     a(f"s_cmp_ge_u32 {sr(S_W)}, 2")
     a(f"s_cselect_b32 {sr(t0)}, {OFF_DO}, 0")
     a(f"s_add_u32 {sr(S_SOFF)}, {sr(S_SOFF)}, {sr(t0)}")
+    # dS block coordinates: 4 kb, ki = 4 kb + w, 32 w
+    a(f"s_lshl_b32 {sr(S_4KB)}, {sr(S_KB)}, 2")
+    a(f"s_add_u32 {sr(S_KI)}, {sr(S_4KB)}, {sr(S_W)}")
+    a(f"s_lshl_b32 {sr(S_32W)}, {sr(S_W)}, 5")
     # -lse (even waves) / -delta (odd) rows: (b H + hq0) S + .., rep S floats
     a(f"s_mul_i32 {sr(t0)}, {sr(S_BB)}, {sr(S_H)}")
     a(f"s_add_u32 {sr(t0)}, {sr(t0)}, {sr(S_HQ0)}")
@@ -570,10 +661,10 @@ def prologue(a: Asm):
     a(f"v_bfe_u32 {vr(t + 1)}, {vr(r)}, 2, 2")
     a(f"v_or_b32 {vr(t)}, {vr(t)}, {vr(t + 1)}")               # swz(r)
     a(f"v_lshlrev_b32 {vr(t + 2)}, 8, {vr(r)}")                # r 256
-    for s in range(8):
-        a(f"v_add_u32 {vr(t + 1)}, {2 * s}, {vr(hh)}")
+    for s_ in range(8):
+        a(f"v_add_u32 {vr(t + 1)}, {2 * s_}, {vr(hh)}")
         a(f"v_xor_b32 {vr(t + 1)}, {vr(t + 1)}, {vr(t)}")
-        a(f"v_lshl_add_u32 {vr(V_RRO + s)}, {vr(t + 1)}, 4, {vr(t + 2)}")
+        a(f"v_lshl_add_u32 {vr(V_RRO + s_)}, {vr(t + 1)}, 4, {vr(t + 2)}")
     # -lse / -delta rows: OFF_L + 16 hh
     a(f"v_lshlrev_b32 {vr(V_LO)}, 4, {vr(hh)}")
     a(f"v_add_u32 {vr(V_LO)}, {OFF_L}, {vr(V_LO)}")
@@ -597,18 +688,30 @@ def prologue(a: Asm):
         a(f"v_xor_b32 {vr(t + 5)}, {vr(t + 4)}, {vr(t + 2)}")
         a(f"v_lshl_add_u32 {vr(V_TRO8 + dt)}, {vr(t + 5)}, 4, {vr(t + 3)}")
         a(f"v_add_u32 {vr(V_TRO8 + dt)}, {8 * ROWB}, {vr(V_TRO8 + dt)}")
-    # DMA sources: (l >> 4) row + chunk (l & 15) ^ ((l >> 4) << 2) ^ k
+    # set B: the same offsets into buffer 2
+    for x in range(8):
+        a(f"v_add_u32 {vr(V_RRO_B + x)}, {2 * BUFB}, {vr(V_RRO + x)}")
+    a(f"v_add_u32 {vr(V_LO_B)}, {2 * BUFB}, {vr(V_LO)}")
+    for dt in range(4):
+        a(f"v_add_u32 {vr(V_TRO_B + dt)}, {2 * BUFB}, {vr(V_TRO + dt)}")
+        a(f"v_add_u32 {vr(V_TRO8_B[dt])}, {2 * BUFB}, {vr(V_TRO8 + dt)}")
+    # DMA sources: piece u = rows 4 u + (l >> 4) of the wave's 32, chunk
+    # (l & 15) ^ ((l >> 4) << 2) ^ (u & 3) of the swizzled image
     a(f"v_lshlrev_b32 {vr(t)}, 2, {vr(g)}")
     a(f"v_and_b32 {vr(t + 1)}, 15, {vr(l)}")
     a(f"v_xor_b32 {vr(t)}, {vr(t)}, {vr(t + 1)}")
     a(f"v_mul_u32_u24 {vr(t + 2)}, {sr(S_DSTR)}, {vr(g)}")
-    for k in range(4):
-        a(f"v_xor_b32 {vr(t + 1)}, {k}, {vr(t)}")
-        a(f"v_lshl_add_u32 {vr(V_DMA + k)}, {vr(t + 1)}, 4, {vr(t + 2)}")
+    for u in range(8):
+        a(f"s_mul_i32 {sr(t0)}, {sr(S_DSTR)}, {4 * u}")
+        a(f"v_xor_b32 {vr(t + 1)}, {u & 3}, {vr(t)}")
+        a(f"v_lshl_add_u32 {vr(V_DMA + u)}, {vr(t + 1)}, 4, {vr(t + 2)}")
+        a(f"v_add_u32 {vr(V_DMA + u)}, {sr(t0)}, {vr(V_DMA + u)}")
     a(f"v_lshlrev_b32 {vr(V_L4)}, 2, {vr(l)}")
-    # dS store: (2 k + hh) 512 + r 16; mask base r - 4 hh
+    a(f"v_mov_b32 {vr(V_C2)}, {sr(S_C)}")
+    a(f"v_mov_b32 {vr(V_C2 + 1)}, {sr(S_C)}")
+    # dS store: key 16 + hh 8; mask base r - 4 hh
     a(f"v_lshlrev_b32 {vr(V_DSO)}, 4, {vr(r)}")
-    a(f"v_lshl_add_u32 {vr(V_DSO)}, {vr(hh)}, 9, {vr(V_DSO)}")
+    a(f"v_lshl_add_u32 {vr(V_DSO)}, {vr(hh)}, 3, {vr(V_DSO)}")
     a(f"v_lshlrev_b32 {vr(t)}, 2, {vr(hh)}")
     a(f"v_sub_u32 {vr(V_MD0)}, {vr(r)}, {vr(t)}")
     # --- K / V rows of this wave's keys -> B-operand fragments (AGPRs)
@@ -622,26 +725,28 @@ def prologue(a: Asm):
     srd64(a, SRD_X, S_K, t1, ROWB, 32 * ROWB)
     a(f"v_lshlrev_b32 {vr(t)}, 8, {vr(r)}")
     a(f"v_lshl_add_u32 {vr(t)}, {vr(hh)}, 4, {vr(t)}")           # r 256 + 16 hh
-    for s in range(8):
-        a(f"buffer_load_dwordx4 {vr(V_SB + 4 * s, 4)}, {vr(t)}, {sr(SRD_X, 4)}, 0 offen offset:{32 * s}")
+    for s_ in range(8):
+        a(f"buffer_load_dwordx4 {vr(V_SB + 4 * s_, 4)}, {vr(t)}, {sr(SRD_X, 4)}, 0 offen offset:{32 * s_}")
     srd64(a, SRD_X, S_V, t1, ROWB, 32 * ROWB)
-    for s in range(8):
-        a(f"buffer_load_dwordx4 {vr(V_SB + 32 + 4 * s, 4)}, {vr(t)}, {sr(SRD_X, 4)}, 0 offen offset:{32 * s}")
+    for s_ in range(8):
+        a(f"buffer_load_dwordx4 {vr(V_SB + 32 + 4 * s_, 4)}, {vr(t)}, {sr(SRD_X, 4)}, 0 offen offset:{32 * s_}")
+    # the -lse / -delta row's LDS base (SRD_X is free from here on)
+    a(f"s_and_b32 {sr(t0)}, {sr(S_W)}, 1")
+    a(f"s_lshl_b32 {sr(t0)}, {sr(t0)}, 8")
+    a(f"s_add_u32 {sr(S_LM0)}, {sr(t0)}, {OFF_L}")
     # --- tiles 0 and 1 -> buffers 0 and 1
     a(f"s_mov_b32 {sr(S_DMOD)}, 0")
     a(f"s_mov_b32 {sr(S_DHEAD)}, 0")
-    a(f"s_mov_b32 {sr(S_BUFD)}, 0")
     for tile in range(2):
         for x in dma_setup():
             a(x)
-        for ins in dma_pieces():
+        for ins in dma_pieces(tile):
             for x in ins:
                 a(x)
-        a(f"s_add_u32 {sr(S_BUFD)}, {sr(S_BUFD)}, 1")
         if tile == 0:
             for x in advance(S_DMOD, S_DHEAD):
                 a(x)
-    # the next DMA: step 2 clamped to the last (total >= 2), into buffer 2
+    # the next DMA: step 2 clamped to the last (total >= 2)
     a(f"s_mov_b32 {sr(S_DIT)}, 1")
     for x in dma_advance():
         a(x)
@@ -651,32 +756,60 @@ def prologue(a: Asm):
     for x in range(64):
         a(f"v_accvgpr_write_b32 {ar(A_K + x)}, {vr(V_SB + x)}")
     a("s_barrier")
-    # counters: step 0 = (mod 0, head 0), the next (1 % nqt, ..)
+    # counters: step 0 = (mod 0, head 0), the next (1 % nqt, ..); step 0's dS
+    # offsets / masks for E(0) and E(1)
     a(f"s_mov_b32 {sr(S_IT)}, 0")
     a(f"s_mov_b32 {sr(S_MOD)}, 0")
     a(f"s_mov_b32 {sr(S_HEAD)}, 0")
     a(f"s_mov_b32 {sr(S_NMOD)}, 0")
     a(f"s_mov_b32 {sr(S_NHEAD)}, 0")
+    for x in dso_step(S_MOD, S_HEAD):
+        a(x)
     for x in advance(S_NMOD, S_NHEAD):
         a(x)
-    a(f"s_mov_b32 {sr(S_BUFK)}, 0")
-    a(f"s_mov_b32 {sr(S_BUFS)}, 0")
     a("s_nop 1")
+    if KNOBS["timing"]:
+        a(f"s_memtime {sr(S_TM, 2)}")
+        a("s_waitcnt lgkmcnt(0)")
     # --- fill: SD(0), then SD(1) with E(0) (step 0: masked) and KV(0)'s first
-    # fragments; then the SD offsets move to tile 1
+    # fragments (all of tile 0, buffer 0)
     mf = sd_mfmas(0) + sd_mfmas(1)
-    items = sd_read_items(0, 0, 0, -1, None, -1, "sr")
-    items += sd_read_items(16, 1, 1, -1, 0, -1, "sr2")
-    items.append(Item(dso_setup(0, S_MOD, S_HEAD, 0), 40, -1, 17, "e0", split=False))
+    items = sd_read_items(0, 0, 0, 0, -1, None, -1, "sr")
+    items += sd_read_items(16, 1, 1, 0, -1, 0, -1, "sr2")
     items += e_items(0, True, 17, 29, "e0")
-    items += kv_prefetch_items(20, 31, 0)
-    items.append(Item(rot3(S_BUFS, S_DELS), 10, -1, 25, "rot", split=False))
-    items.append(Item(rot_sd(), 36, 29, 31, "rot"))
-    schedule(a, mf, items)
+    items += kv_prefetch_items(20, 31, 0, 0)
+    sched(a, mf, items)
 
 
 # ---------------------------------------------------------------- epilogue
+def timing_store(a: Asm):
+    """Timing arm: 8 dwords per (workgroup, wave) at dbg + 32 (4 wg + wave):
+    cycles from the end of the fill to the end of the loop (lo, hi), steps,
+    key block, 0..."""
+    if not KNOBS["timing"]:
+        return
+    a(f"s_memtime {sr(SRD_X, 2)}")
+    a("s_waitcnt lgkmcnt(0)")
+    t = S_T0
+    a(f"s_sub_u32 {sr(SRD_X)}, {sr(SRD_X)}, {sr(S_TM)}")
+    a(f"s_subb_u32 {sr(SRD_X + 1)}, {sr(SRD_X + 1)}, {sr(S_TM + 1)}")
+    a(f"s_lshl_b32 {sr(t)}, s2, 2")
+    a(f"s_add_u32 {sr(t)}, {sr(t)}, {sr(S_W)}")
+    a(f"s_lshl_b32 {sr(t)}, {sr(t)}, 5")
+    a(f"s_add_u32 {sr(SRD_LD)}, {sr(S_DBG)}, {sr(t)}")
+    a(f"s_addc_u32 {sr(SRD_LD + 1)}, {sr(S_DBG + 1)}, 0")
+    a(f"s_mov_b32 {sr(SRD_LD + 2)}, 32")
+    a(f"s_mov_b32 {sr(SRD_LD + 3)}, 0x20000")
+    a(f"v_mov_b32 {vr(V_T + 1)}, 0")
+    for k, x in enumerate((SRD_X, SRD_X + 1, S_TOT, S_KB)):
+        a(f"v_mov_b32 {vr(V_T)}, {sr(x)}")
+        a(f"buffer_store_dword {vr(V_T)}, {vr(V_T + 1)}, {sr(SRD_LD, 4)}, 0 offen offset:{4 * k}")
+        a("s_nop 1")
+    a("s_waitcnt vmcnt(0)")
+
+
 def epilogue(a: Asm):
+    timing_store(a)
     a("s_waitcnt vmcnt(0)")
     a("s_nop 7")
     a("s_nop 7")
@@ -767,40 +900,45 @@ def epilogue(a: Asm):
 
 
 # ---------------------------------------------------------------- kernel
-def kernel() -> tuple[str, str]:
-    name = NAME
-    a = Asm(prefix="dkdv_")
+def kernel(variant: str = "") -> tuple[str, str]:
+    name = NAME + (f"_{variant}" if variant else "")
+    a = Asm(prefix=f"dkdv{variant}_")
     a.raw(f".globl {name}")
     a.raw(".p2align 8")
     a.raw(f".type {name},@function")
     a.raw(f"{name}:")
     prologue(a)
-    lab = {k: a.fresh(k) for k in ("top", "uu", "um", "mu", "mm", "t", "tu", "tm", "epi")}
-    # iteration dispatch: the last step -> the tail; else by whether E(2 it + 1)
-    # (step it) and E(2 it + 2) (step it + 1) touch the diagonal (mod < 2)
-    a.label(lab["top"])
-    a(f"s_cmp_eq_u32 {sr(S_IT)}, {sr(S_TOTM1)}")
-    a(f"s_cbranch_scc1 {lab['t']}")
-    a(f"s_cmp_lt_u32 {sr(S_MOD)}, 2")
-    a(f"s_cbranch_scc1 {lab['top']}_m")
-    a(f"s_cmp_lt_u32 {sr(S_NMOD)}, 2")
-    a(f"s_cbranch_scc1 {lab['um']}")
-    a(f"s_branch {lab['uu']}")
-    a.label(f"{lab['top']}_m")
-    a(f"s_cmp_lt_u32 {sr(S_NMOD)}, 2")
-    a(f"s_cbranch_scc1 {lab['mm']}")
-    a(f"s_branch {lab['mu']}")
-    for key, m1, m2 in (("uu", False, False), ("um", False, True), ("mu", True, False), ("mm", True, True)):
-        a.label(lab[key])
-        iteration(a, m1, m2, lab["top"])
-    a.label(lab["t"])
-    a(f"s_cmp_lt_u32 {sr(S_MOD)}, 2")
-    a(f"s_cbranch_scc1 {lab['tm']}")
-    a.label(lab["tu"])
-    tail(a, False)
-    a(f"s_branch {lab['epi']}")
-    a.label(lab["tm"])
-    tail(a, True)
+    epi = a.fresh("epi")
+    top = [a.fresh(f"top{ph}") for ph in range(3)]
+    # iteration dispatch per phase it % 3 (the tile buffers): the last step ->
+    # the tail; else by whether E(2 it + 1) (step it) and E(2 it + 2) (step
+    # it + 1) touch the diagonal (mod < 2)
+    for ph in range(3):
+        lab = {k: a.fresh(f"{k}{ph}") for k in ("uu", "um", "mu", "mm", "m", "t", "tm")}
+        a.label(top[ph])
+        a(f"s_cmp_eq_u32 {sr(S_IT)}, {sr(S_TOTM1)}")
+        a(f"s_cbranch_scc1 {lab['t']}")
+        a(f"s_cmp_lt_u32 {sr(S_MOD)}, 2")
+        a(f"s_cbranch_scc1 {lab['m']}")
+        a(f"s_cmp_lt_u32 {sr(S_NMOD)}, 2")
+        a(f"s_cbranch_scc1 {lab['um']}")
+        a(f"s_branch {lab['uu']}")
+        a.label(lab["m"])
+        a(f"s_cmp_lt_u32 {sr(S_NMOD)}, 2")
+        a(f"s_cbranch_scc1 {lab['mm']}")
+        a(f"s_branch {lab['mu']}")
+        for key, m1, m2 in (("uu", False, False), ("um", False, True), ("mu", True, False), ("mm", True, True)):
+            a.label(lab[key])
+            iteration(a, m1, m2, ph, top[(ph + 1) % 3])
+        a.label(lab["t"])
+        a(f"s_cmp_lt_u32 {sr(S_MOD)}, 2")
+        a(f"s_cbranch_scc1 {lab['tm']}")
+        tail(a, False, ph)
+        a(f"s_branch {epi}")
+        a.label(lab["tm"])
+        tail(a, True, ph)
+        a(f"s_branch {epi}")
+    lab = {"epi": epi}
     a.label(lab["epi"])
     epilogue(a)
     a.label(a.abort)
@@ -811,8 +949,19 @@ def kernel() -> tuple[str, str]:
     return "\n".join(a.out) + "\n" + desc, meta
 
 
+def variant_kernel(vname: str, knobs: dict) -> tuple[str, str]:
+    saved = dict(KNOBS)
+    KNOBS.update(knobs)
+    try:
+        return kernel(vname)
+    finally:
+        KNOBS.clear()
+        KNOBS.update(saved)
+
+
 def all_kernels() -> list[tuple[str, str]]:
-    return [kernel()]
+    """The product kernel, then the diagnostic arms (host table order)."""
+    return [kernel()] + [variant_kernel(v, k) for v, k in VARIANTS]
 
 
 def generate(kernels=None) -> str:

@@ -251,6 +251,11 @@ class Emu:
         w.scc = int(y > x)
         self.sset(w, a[0], x - y)
 
+    def op_s_subb_u32(self, w, a, m):
+        x, y = self.sget(w, a[1]), self.sget(w, a[2]) + w.scc
+        w.scc = int(y > x)
+        self.sset(w, a[0], x - y)
+
     def op_s_sub_i32(self, w, a, m):
         self.sset(w, a[0], self.sget(w, a[1]) - self.sget(w, a[2]))
 
@@ -433,6 +438,22 @@ class Emu:
     def op_v_fma_f32(self, w, a, m):
         x, y, z = (self._fop(w, t).astype(np.float64) for t in a[1:4])
         self.vset(w, a[0], f2u((x * y + z).astype(np.float32)))
+
+    def _pair(self, w, tok) -> np.ndarray:
+        lo, hi = self.vrange(w, tok)
+        assert hi == lo + 2 and lo % 2 == 0, tok   # 64-bit operands: even-aligned pairs
+        return u2f(w.v[lo:hi]).astype(np.float64)
+
+    def op_v_pk_fma_f32(self, w, a, m):
+        """Two fp32 FMAs on register pairs (op_sel defaults: low with low)."""
+        x, y, z = (self._pair(w, t) for t in a[1:4])
+        lo, hi = self.vrange(w, a[0])
+        w.v[lo:hi] = f2u((x * y + z).astype(np.float32))
+
+    def op_v_pk_mul_f32(self, w, a, m):
+        x, y = (self._pair(w, t) for t in a[1:3])
+        lo, hi = self.vrange(w, a[0])
+        w.v[lo:hi] = f2u((x * y).astype(np.float32))
 
     def op_v_sub_u32(self, w, a, m):
         self._vbin(w, a, lambda x, y: (x.astype(np.int64) - y.astype(np.int64)) & M32)
@@ -688,6 +709,8 @@ class Emu:
         self._gwrite(addr, np.ascontiguousarray(w.v[lo:hi].T).view(np.uint8).reshape(64, 16))
 
     def op_buffer_store_dwordx2(self, w, a, mods):
+        if self._dropped(w, a):
+            return
         addr = self._buffer_addr(w, a[1:], mods, 8)
         lo, hi = self.vrange(w, a[0])
         data = np.ascontiguousarray(w.v[lo:hi].T).view(np.uint8).reshape(64, 8)

@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_N = 27 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_N = 35 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -45,7 +45,11 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // K_ATTN_D1 ..: attn_gen.py VARIANTS (diagnostic arms, wrong outputs by design)
                            "toa_attn_fwd_asm_d1",      "toa_attn_fwd_asm_d2",        "toa_attn_fwd_asm_d3",
                            "toa_attn_fwd_asm_d4",      "toa_attn_fwd_asm_d5",        "toa_attn_fwd_asm_t1",
-                           "toa_attn_fwd_asm_c1",      "toa_attn_fwd_asm_t2",        "toa_attn_dkdv_asm"};
+                           "toa_attn_fwd_asm_c1",      "toa_attn_fwd_asm_t2",        "toa_attn_dkdv_asm",
+                           // K_DKDV_D1 ..: attn_bwd_gen.py VARIANTS (diagnostic arms, wrong outputs by design)
+                           "toa_attn_dkdv_asm_d1",     "toa_attn_dkdv_asm_d2",       "toa_attn_dkdv_asm_d3",
+                           "toa_attn_dkdv_asm_d4",     "toa_attn_dkdv_asm_d5",       "toa_attn_dkdv_asm_d6",
+                           "toa_attn_dkdv_asm_d7",     "toa_attn_dkdv_asm_t1"};
 
 struct DevModule {
   std::once_flag once;
@@ -461,10 +465,46 @@ struct __attribute__((packed)) DkdvArgs {
 };
 static_assert(sizeof(DkdvArgs) == 144, "kernarg block must match csrc/asm/attn_bwd_gen.py KARG_BYTES");
 
+static int attn_dkdv_launch(int which, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
+                            const float* nlse2, const float* ndelta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B, int H,
+                            int Hk, int S, int D, float scale, int flags, const float* cosv, const float* sinv, int H3,
+                            hipStream_t stream, void* dbg = nullptr);
+
 extern "C" int toa_attn_dkdv_asm(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                                  const float* nlse2, const float* ndelta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
                                  int H, int Hk, int S, int D, float scale, int flags, const float* cosv,
                                  const float* sinv, int H3, hipStream_t stream) {
+  return attn_dkdv_launch(K_ATTN_DKDV, q, k, v, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S, D, scale, flags, cosv,
+                          sinv, H3, stream);
+}
+
+// Diagnostic: arm v (1.. = attn_bwd_gen.py VARIANTS, 0 = the product kernel),
+// same contract; the arms' outputs are wrong by design (timing only).
+extern "C" int toa_attn_dkdv_asm_variant(int v, const bf16_t* q, const bf16_t* k, const bf16_t* v_,
+                                         const bf16_t* dout, const float* nlse2, const float* ndelta, bf16_t* dk,
+                                         bf16_t* dv, bf16_t* ds, int B, int H, int Hk, int S, int D, float scale,
+                                         int flags, const float* cosv, const float* sinv, int H3, hipStream_t stream) {
+  if (v < 0 || v > K_DKDV_T1 - K_DKDV_D1) return (int)hipErrorInvalidValue;  // the timing arm takes its own entry
+  return attn_dkdv_launch(v ? K_DKDV_D1 + v - 1 : K_ATTN_DKDV, q, k, v_, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S,
+                          D, scale, flags, cosv, sinv, H3, stream);
+}
+
+// Diagnostic: the product kernel with s_memtime stamps (attn_bwd_gen.py
+// timing_store): 8 dwords per (workgroup, wave) at dbg + 32 (4 wg + wave) --
+// loop cycles (lo, hi), steps, key block.
+extern "C" int toa_attn_dkdv_asm_timing(void* dbg, const bf16_t* q, const bf16_t* k, const bf16_t* v,
+                                        const bf16_t* dout, const float* nlse2, const float* ndelta, bf16_t* dk,
+                                        bf16_t* dv, bf16_t* ds, int B, int H, int Hk, int S, int D, float scale,
+                                        int flags, const float* cosv, const float* sinv, int H3, hipStream_t stream) {
+  if (!dbg || !al16(dbg)) return (int)hipErrorInvalidValue;
+  return attn_dkdv_launch(K_DKDV_T1, q, k, v, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S, D, scale, flags, cosv,
+                          sinv, H3, stream, dbg);
+}
+
+static int attn_dkdv_launch(int which, const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
+                            const float* nlse2, const float* ndelta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B, int H,
+                            int Hk, int S, int D, float scale, int flags, const float* cosv, const float* sinv, int H3,
+                            hipStream_t stream, void* dbg) {
   const bool rope = (flags & 2) != 0;
   if (D != 128 || B <= 0 || H <= 0 || Hk <= 0 || H % Hk || S <= 0 || S % 256 || !al16(q) || !al16(k) || !al16(v) ||
       !al16(dout) || !al16(dk) || !al16(dv) || !al16(ds) || ((uintptr_t)nlse2 & 3) || ((uintptr_t)ndelta & 3) ||
@@ -478,7 +518,7 @@ extern "C" int toa_attn_dkdv_asm(const bf16_t* q, const bf16_t* k, const bf16_t*
       (int64_t)B * S * (rope ? H3 : Hk) * 256 >= (1ll << 40))
     return (int)hipErrorInvalidValue;
   hipError_t err;
-  hipFunction_t fn = get_fn(K_ATTN_DKDV, &err);
+  hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
   DkdvArgs a;
   memset(&a, 0, sizeof(a));
@@ -503,6 +543,7 @@ extern "C" int toa_attn_dkdv_asm(const bf16_t* q, const bf16_t* k, const bf16_t*
   a.rep = (uint32_t)(H / Hk);
   a.nkb = (uint32_t)(S / 128);
   a.H3 = (uint32_t)(rope ? H3 : 0);
+  a.dbg = (uint64_t)dbg;
   size_t sz = sizeof(a);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   return (int)hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);

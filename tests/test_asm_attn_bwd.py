@@ -144,17 +144,17 @@ def check(r, S):
 
 def expected_drops(B, H, Hk, S):
     """Stores of blocks wholly above the diagonal: per (kv head, query head,
-    key block kb) step mod < 2, half m, wave w with 2 mod + m < w -- two
+    key block kb) step mod < 2, half m, wave w with 2 mod + m < w -- four
     stores each."""
     rep = H // Hk
     per = sum(1 for mod in range(2) for m in range(2) for w in range(4) if 2 * mod + m < w)
-    return 2 * per * B * Hk * rep * (S // 128)
+    return 4 * per * B * Hk * rep * (S // 128)
 
 
 def test_kernel_mfma_count():
     lines = [ln for ln in TEXT.splitlines() if ln.startswith("  v_mfma")]
-    # fill (32) + 4 iteration variants x 64 + 2 tails x 32
-    assert len(lines) == 32 + 4 * 64 + 2 * 32
+    # fill (32) + 3 buffer phases x (4 iteration variants x 64 + 2 tails x 32)
+    assert len(lines) == 32 + 3 * (4 * 64 + 2 * 32)
 
 
 def test_dkdv_single_head_s256():

@@ -104,6 +104,10 @@ _SIGS = {
     "toa_attn_set_dkdv_variant": [c_int],
     "toa_attn_dkdv_asm": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_f, c_int,
                           c_p, c_p, c_int, c_p],
+    "toa_attn_dkdv_asm_variant": [c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
+                                  c_f, c_int, c_p, c_p, c_int, c_p],
+    "toa_attn_dkdv_asm_timing": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
+                                 c_f, c_int, c_p, c_p, c_int, c_p],
     "toa_attn_bwd_rope": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int,
                           c_int, c_f, c_p],
     "toa_emulate_xfer": [c_p, c_p, c_i64, c_int, ctypes.c_double, c_p],
