@@ -210,3 +210,63 @@ extern "C" int toa_emulate_copy_nocu(const void* src, void* dst, int64_t nbytes,
   if (nbytes <= 0) return 0;
   return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDeviceNoCU, stream);
 }
+
+// ---------------------------------------------------------------------------
+// Copy-engine all-gather of the ZeRO-1 weights (parallel/pull_gather.py):
+// after a rank's AdamW has written its shard of a bucket it publishes the
+// step's epoch in its own IPC-exported flag word for that bucket (system-
+// scope release: the update's writes are visible to the peers' copy
+// engines first); each rank's copy stream waits until every peer published
+// the epoch (bounded spin: a missing peer sets its error bit, never hangs),
+// then pulls the peers' shards with hipMemcpyDeviceToDeviceNoCU (SDMA, no
+// workgroup on any CU -- the GEMMs of the forward keep every CU).
+// ---------------------------------------------------------------------------
+struct PeerFlags {
+  unsigned* f[TOA_MAX_RANKS];  // each rank's flag array, mapped (own one at [rank])
+};
+
+__global__ void flag_publish_kernel(unsigned* flag, unsigned epoch) {
+  __threadfence_system();
+  __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void flags_wait_kernel(PeerFlags peers, int idx, int rank, int world, unsigned epoch, unsigned* err,
+                                  long long timeout_cycles) {
+  const int r = threadIdx.x;
+  if (r < world && r != rank) {
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load(peers.f[r] + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (wall_clock64() - t0 > timeout_cycles) {
+        atomicOr(err, 1u << r);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+  }
+  __threadfence_system();
+}
+
+extern "C" int toa_flag_publish(void* flag, unsigned epoch, hipStream_t stream) {
+  if (!flag) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(flag_publish_kernel, dim3(1), dim3(1), 0, stream, (unsigned*)flag, epoch);
+  return (int)hipGetLastError();
+}
+
+// flags: `world` device pointers (each rank's flag array); waits for entry
+// idx of every peer's array to reach epoch.  err: bit r set on a timeout.
+extern "C" int toa_flags_wait(void* const* flags, int idx, int rank, int world, unsigned epoch, unsigned* err,
+                              int timeout_ms, hipStream_t stream) {
+  if (world < 1 || world > TOA_MAX_RANKS || rank < 0 || rank >= world || idx < 0 || !err)
+    return (int)hipErrorInvalidValue;
+  PeerFlags p;
+  for (int r = 0; r < TOA_MAX_RANKS; ++r) p.f[r] = r < world ? (unsigned*)flags[r] : nullptr;
+  hipLaunchKernelGGL(flags_wait_kernel, dim3(1), dim3(64), 0, stream, p, idx, rank, world, epoch, err,
+                     (long long)timeout_ms * 100000ll);  // wall_clock64: 100 MHz
+  return (int)hipGetLastError();
+}
+
+// A copy on a copy engine (SDMA): peer-mapped source, local destination.
+extern "C" int toa_copy_nocu(const void* src, void* dst, int64_t nbytes, hipStream_t stream) {
+  if (nbytes <= 0) return 0;
+  return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDeviceNoCU, stream);
+}

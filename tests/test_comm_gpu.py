@@ -263,3 +263,70 @@ def test_emulate_xfer_moves_bytes_at_the_paced_rate():
     want_ms = src.numel() / 100e9 * 1e3  # 0.67 ms at 100 GB/s
     assert 0.9 * want_ms <= times[100.0] <= 1.6 * want_ms, times
     assert times[0.0] < 0.5 * want_ms, times
+
+
+def _pull_worker(rank, world, port, q):
+    """Copy-engine weight all-gather (parallel/pull_gather.py) between two
+    processes on the one GPU: IPC-mapped flat buffers, flag publish / wait
+    kernels, SDMA copies; each step's result vs the exact concatenation."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tf_operator_amd.parallel import zero
+        from tf_operator_amd.parallel.pull_gather import GpuIpcTransport, PullGather
+
+        sizes = [64 * world * k for k in (4096, 1, 333, 2048)]   # 1 MiB .. bf16 buckets
+        ranges, lo = [], 0
+        for n in sizes:
+            ranges.append((lo, lo + n))
+            lo += n
+        buf = torch.zeros(lo, device="cuda", dtype=torch.bfloat16)
+        t = GpuIpcTransport(buf, rank, world, len(ranges), timeout_ms=20000)
+        pg = PullGather(t, ranges, rank, world)
+        ok = True
+        for step in range(6):
+            want = torch.empty(lo, dtype=torch.bfloat16)
+            for r in range(world):
+                g = torch.Generator().manual_seed(100 * step + r)
+                vals = torch.randn(lo, generator=g).to(torch.bfloat16)
+                for (s, e) in zero.owned_ranges(ranges, world, r):
+                    want[s:e] = vals[s:e]
+                if r == rank:
+                    mine = vals.cuda()
+            buf.fill_(-7)
+            for (s, e) in zero.owned_ranges(ranges, world, rank):   # "AdamW" on the compute stream
+                buf[s:e].copy_(mine[s:e])
+            pg.new_step()
+            works = [pg.launch_one(b) for b in reversed(range(len(ranges)))]
+            for w in works:
+                w.wait()
+            got = buf.cpu()
+            ok = ok and torch.equal(got.view(torch.int16), want.view(torch.int16))
+            dist.barrier()   # the test's own stand-in for the next step's reduce-scatter ordering
+        torch.cuda.synchronize()
+        t.check()
+        pg.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, ok, None))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.timeout(240)
+def test_pull_gather_copy_engine_two_processes():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _port()
+    procs = [ctx.Process(target=_pull_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, ok, err in res:
+        assert err is None, (rank, err)
+        assert ok, rank

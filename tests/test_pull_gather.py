@@ -1,0 +1,98 @@
+"""The copy-engine ZeRO-1 weight all-gather's pull protocol
+(parallel/pull_gather.py) on the CPU: gloo ranks pull their peers' shards
+through file-backed shared memory (ShmTransport, the GPU transport's
+protocol: publish epoch -> wait for every peer's epoch -> copy the peers'
+shards) and the result is compared bit for bit with
+dist.all_gather_into_tensor of the same shards, over several steps, at
+world 2 and 4, bf16 and fp32, with buckets of different sizes."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, tag, dtype, q):
+    import torch.distributed as dist
+
+    from tf_operator_amd.parallel import zero
+    from tf_operator_amd.parallel.pull_gather import PullGather, ShmTransport
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    t = None
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        sizes = [64 * world * k for k in (3, 1, 7, 2)]          # bucket lengths (multiples of 8 world)
+        ranges, lo = [], 0
+        for n in sizes:
+            ranges.append((lo, lo + n))
+            lo += n
+        numel = lo
+        t = ShmTransport(tag, rank, world, numel, dtype, len(ranges))
+        pg = PullGather(t, ranges, rank, world)
+        ok = True
+        for step in range(4):
+            g = torch.Generator().manual_seed(1000 * step + rank)
+            # this rank's "updated" shards (owned ranges), other ranges stale
+            t.buf.copy_(torch.full((numel,), -1.0).to(dtype))
+            for (s, e) in zero.owned_ranges([(a, b) for a, b in ranges], world, rank):
+                t.buf[s:e].copy_(torch.randn(e - s, generator=g).to(dtype))
+            ref = t.buf.clone()
+            pg.new_step()
+            for b in reversed(range(len(ranges))):    # ParamGather.order(): forward-need order
+                pg.launch_one(b).wait()
+            # reference: RCCL's (here gloo's) all-gather of the same shards
+            for (s, e) in ranges:
+                n = (e - s) // world
+                out = torch.empty(e - s, dtype=dtype)
+                dist.all_gather_into_tensor(out, ref[s + rank * n:s + (rank + 1) * n].clone())
+                ok = ok and torch.equal(out.view(torch.int16 if dtype == torch.bfloat16 else torch.int32),
+                                        t.buf[s:e].clone().view(torch.int16 if dtype == torch.bfloat16 else torch.int32))
+        q.put((rank, ok, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        if t is not None:
+            t.close()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world,dtype", [(2, torch.bfloat16), (4, torch.float32)])
+def test_pull_gather_matches_all_gather(world, dtype):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port, tag = _port(), f"t{os.getpid()}_{world}"
+    procs = [ctx.Process(target=_worker, args=(r, world, port, tag, dtype, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=150) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, ok, err in res:
+        assert err is None, (rank, err)
+        assert ok, rank
+    leftovers = [f for f in os.listdir("/dev/shm") if f.startswith(f"toa_pull_{tag}")]
+    assert not leftovers, leftovers
+
+
+def test_zero_ag_mode_env(monkeypatch):
+    from tf_operator_amd.parallel import pull_gather
+
+    monkeypatch.delenv("TOA_ZERO_AG", raising=False)
+    assert pull_gather.mode_from_env() == "rccl"
+    monkeypatch.setenv("TOA_ZERO_AG", "sdma")
+    assert pull_gather.mode_from_env() == "sdma"
+    monkeypatch.setenv("TOA_ZERO_AG", "bogus")
+    with pytest.raises(ValueError):
+        pull_gather.mode_from_env()

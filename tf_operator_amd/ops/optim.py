@@ -166,13 +166,15 @@ class FlatAdamW:
             self.done = None
 
     @torch.no_grad()
-    def step(self, grad_scale=1.0, lr=None, bucket_order=None, after_bucket=None):
+    def step(self, grad_scale=1.0, lr=None, bucket_order=None, after_bucket=None, before_bucket=None):
         """One update.  With a sharded update (``owned``: one range per
         gradient bucket) and ``bucket_order`` / ``after_bucket``, the owned
         shards are updated bucket by bucket in that order and
         ``after_bucket(b)`` runs right after bucket b's update is enqueued --
         the ZeRO-1 all-gather of b then starts as soon as ITS shard is done
-        instead of after the whole update (parallel/zero.ParamGather.launch_one).
+        instead of after the whole update (parallel/zero.ParamGather.launch_one);
+        ``before_bucket(b)`` runs right before it (the traffic emulator's
+        fused-reduce cost, parallel/emulate.py).
         Every element is updated exactly once either way: bit-identical."""
         f = self.flat
         self.step_count += 1
@@ -181,7 +183,7 @@ class FlatAdamW:
         if clip:
             self._norm_sq()
         if bucket_order is not None and self.owned is not None and not self.overlap:
-            self._step_pipelined(lr, grad_scale, clip, bucket_order, after_bucket)
+            self._step_pipelined(lr, grad_scale, clip, bucket_order, after_bucket, before_bucket)
             return
         if self.overlap and f.param.dtype == torch.bfloat16:
             main = torch.cuda.current_stream(f.device)
@@ -233,7 +235,7 @@ class FlatAdamW:
             if self.post_update is not None:
                 self.post_update(0, f.numel)
 
-    def _step_pipelined(self, lr, grad_scale, clip, order, after):
+    def _step_pipelined(self, lr, grad_scale, clip, order, after, before=None):
         f = self.flat
         self.grads_zeroed = False
         hip = _lib.use_hip(f.grad)
@@ -241,6 +243,8 @@ class FlatAdamW:
             _lib.call("toa_step_inc", _lib.ptr(self._dstep), _lib.stream(f.grad))
         for b in order:
             lo, hi = self.owned[b]
+            if before is not None:
+                before(b)
             for a, e, decay in self.runs:
                 a2, b2 = max(a, lo), min(e, hi)
                 if a2 >= b2:

@@ -21,7 +21,13 @@ priority too): (N-1)/N x bucket bytes, paced to ``TOA_EMULATE_GBPS`` GB/s
 on ``TOA_EMULATE_CHANNELS`` workgroups (default 32).  ``TOA_EMULATE_AG=sdma``
 moves the all-gathers' bytes with a copy engine instead
 (``toa_emulate_copy_nocu``: no workgroup on any CU, unpaced), the stand-in
-for pulling the peers' weight shards over xGMI by SDMA.
+for pulling the peers' weight shards over xGMI by SDMA.  ``TOA_EMULATE_RS=sdma``
+does the same for the reduce-scatters -- each rank pulls the peers' slices of
+its own shard into a staging area by SDMA -- and moves the reduction into
+the optimizer: before each bucket's AdamW the compute stream reads the N-1
+staged slices once (:meth:`CommEmulator.fused_reduce`, the extra HBM read
+an AdamW that sums N gradient slices would do).  Then no collective holds a
+CU during backward; the reduce costs one read of (N-1)/N of the gradients.
 
 The other ranks' shards are never updated (their "gathered" weights stay
 as they were), so the loss is meaningless; the TIME is rank 0's.  Compare
@@ -73,6 +79,10 @@ class CommEmulator:
         self.ag_mode = os.environ.get("TOA_EMULATE_AG", "ring")
         if self.ag_mode not in ("ring", "sdma"):
             raise ValueError(f"TOA_EMULATE_AG={self.ag_mode!r}: expected ring or sdma")
+        self.rs_mode = os.environ.get("TOA_EMULATE_RS", "ring")
+        if self.rs_mode not in ("ring", "sdma"):
+            raise ValueError(f"TOA_EMULATE_RS={self.rs_mode!r}: expected ring or sdma")
+        self.sum_out = None
         self.stream = torch.cuda.Stream(device=self.device, priority=-1) if self.device.type == "cuda" else None
         self.scratch = None
         self.calls = 0
@@ -97,7 +107,7 @@ class CommEmulator:
             if self.move and nbytes > 0:
                 dst = self._scratch(nbytes)
                 buf.record_stream(self.stream)
-                if kind == "all_gather" and self.ag_mode == "sdma":
+                if (self.ag_mode if kind == "all_gather" else self.rs_mode) == "sdma":
                     _lib.call("toa_emulate_copy_nocu", _lib.ptr(buf), _lib.ptr(dst), int(nbytes), _lib.stream(dst))
                 else:
                     _lib.call("toa_emulate_xfer", _lib.ptr(buf), _lib.ptr(dst), int(nbytes), self.channels,
@@ -106,6 +116,22 @@ class CommEmulator:
             ev = torch.cuda.Event()
             ev.record(self.stream)
         return _Done(ev)
+
+
+    def fused_reduce(self, bucket: torch.Tensor):
+        """TOA_EMULATE_RS=sdma: the optimizer's extra read of the N-1 staged
+        gradient slices of this rank's shard of `bucket` (bf16), on the
+        current (compute) stream, before the shard's AdamW."""
+        if self.rs_mode != "sdma" or not self.move or self.stream is None:
+            return
+        n = bucket.numel() // self.world
+        k = self.world - 1
+        if n == 0 or k == 0:
+            return
+        staged = self._scratch(k * n * 2)[:k * n * 2].view(torch.bfloat16).view(k, n)
+        if self.sum_out is None or self.sum_out.numel() < n:
+            self.sum_out = torch.empty(n, dtype=torch.float32, device=self.device)
+        torch.sum(staged, dim=0, dtype=torch.float32, out=self.sum_out[:n])
 
 
 class _NullWork:

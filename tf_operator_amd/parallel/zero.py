@@ -80,9 +80,10 @@ class ParamGather:
     """In-place all-gather of the updated bf16 weights after a sharded
     optimizer step, waited for per bucket by the next forward."""
 
-    def __init__(self, flat, buckets, rank, world, group=None, on_gathered=None, emulator=None):
+    def __init__(self, flat, buckets, rank, world, group=None, on_gathered=None, emulator=None, pull=None):
         self.flat = flat
         self.emu = emulator  # parallel/emulate.CommEmulator: paced traffic instead of RCCL (world 1)
+        self.pull = pull     # parallel/pull_gather.PullGather: copy-engine pulls instead of RCCL (TOA_ZERO_AG=sdma)
         self.ranges = [(b[0], b[1]) for b in buckets]
         self.rank, self.world, self.group = rank, world, group
         self.on_gathered = on_gathered  # fn(lo, hi) on the waiting stream (W^T refresh)
@@ -97,7 +98,11 @@ class ParamGather:
         """All-gather bucket b (its owned shard must be updated on the
         current stream already: the collective waits for that stream)."""
         lo, hi = self.ranges[b]
-        if self.emu is not None:
+        if self.pull is not None:
+            if b == self.order()[0]:
+                self.pull.new_step()   # one epoch per optimizer step, the same on every rank
+            self.works[b] = self.pull.launch_one(b)
+        elif self.emu is not None:
             self.works[b] = self.emu.collective(self.flat.param[lo:hi], kind="all_gather")
         else:
             self.works[b] = all_gather_(self.flat.param[lo:hi], self.rank, self.world, self.group)

@@ -78,7 +78,8 @@ class LlamaTrainer:
             self.flat.shard_state(self.bucketer.owned)
             self.opt = FlatAdamW(self.flat, lr=lr, owned=self.bucketer.owned)
             self.gather = ParamGather(self.flat, self.bucketer.buckets, self.bucketer.rank, self.bucketer.world,
-                                      on_gathered=self.wt.refresh if self.wt else None, emulator=self.bucketer.emu)
+                                      on_gathered=self.wt.refresh if self.wt else None, emulator=self.bucketer.emu,
+                                      pull=self._pull_gather())
         else:
             if overlap_optimizer is None:
                 overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
@@ -166,14 +167,38 @@ class LlamaTrainer:
             # ZeRO-1 tail, bucket by bucket in forward-need order: each
             # bucket's all-gather starts as soon as its shard is updated
             self.opt.step(grad_scale=self.bucketer.grad_scale, bucket_order=self.gather.order(),
-                          after_bucket=self.gather.launch_one)
+                          after_bucket=self.gather.launch_one, before_bucket=self._emulated_fused_reduce)
         else:
             self.opt.step(grad_scale=self.bucketer.grad_scale)
             if self.gather is not None:
                 self.gather.launch()
         self._phase("first_update_issued")
+        if self.gather is not None and self.gather.pull is not None:
+            self.gather.pull.poll()   # a peer that never published surfaces one step later
         self.step_idx += 1
         return loss_sum / len(batches)
+
+    def _pull_gather(self):
+        """TOA_ZERO_AG=sdma on a one-node GPU job (every rank on this node):
+        the weight all-gather as copy-engine pulls (parallel/pull_gather.py)."""
+        from ..parallel import pull_gather
+
+        bk = self.bucketer
+        if pull_gather.mode_from_env() != "sdma" or bk.world < 2 or bk.emu is not None:
+            return None
+        if self.flat.param.device.type != "cuda" or int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != bk.world:
+            raise RuntimeError("TOA_ZERO_AG=sdma needs a GPU job whose ranks share one node "
+                               "(LOCAL_WORLD_SIZE == world: the operator's node-local layout)")
+        t = pull_gather.GpuIpcTransport(self.flat.param, bk.rank, bk.world, len(bk.buckets), group=bk.group)
+        return pull_gather.PullGather(t, [(b[0], b[1]) for b in bk.buckets], bk.rank, bk.world)
+
+    def _emulated_fused_reduce(self, b):
+        """TOA_EMULATE_RS=sdma (parallel/emulate.py): price the reduction an
+        AdamW summing the copy-engine-pulled gradient slices would do."""
+        emu = self.bucketer.emu
+        if emu is not None:
+            lo, hi = self.gather.ranges[b]
+            emu.fused_reduce(self.flat.grad[lo:hi])
 
     def tokens_per_step(self, world=1):
         return self.micro_batch * self.seq_len * self.grad_accum * world
