@@ -131,7 +131,8 @@ A_DV, A_DK, A_K, A_V = 0, 64, 128, 160
 # price it in-process (scripts/attn_dkdv_arms.py): their outputs are wrong by
 # construction and only their time is read.
 KNOBS = {"bar": True, "vmwait": True, "lgkm": True, "exp": True, "dma": True, "valu": True, "lds": True,
-         "timing": False, "merge": True}
+         "timing": False, "merge": True,
+         "gbar": G_BAR, "dldma": DL_DMA, "lead": 3}   # schedule parameters (the s* arms sweep them)
 VARIANTS = (
     ("d1", {"lgkm": False}),                     # MFMAs do not wait for their LDS fragments
     ("d2", {"bar": False, "vmwait": False}),     # no per-iteration barrier nor DMA wait
@@ -141,6 +142,13 @@ VARIANTS = (
     ("d6", {"lds": False, "lgkm": False}),       # no LDS fragment reads
     ("d7", {"lds": False, "lgkm": False, "valu": False, "dma": False, "vmwait": False, "bar": False}),  # MFMAs + SALU
     ("t1", {"timing": True}),                    # the product kernel + s_memtime stamps (same outputs)
+    # schedule-parameter arms (correct outputs; A/B by time)
+    ("s1", {"gbar": 6}),
+    ("s2", {"gbar": 14}),
+    ("s3", {"dldma": 28}),
+    ("s4", {"lead": 2}),
+    ("s5", {"lead": 5}),
+    ("s6", {"merge": False}),
 )
 
 MASK_C = AG.MASK_C        # register r's row offset in a 32x32 accumulator: (r & 3) + 8 (r >> 2)
@@ -391,7 +399,7 @@ def kv_read_items(base: int, m: int, buf: int, base_prev: int | None, pre: bool,
     items = []
     for i in range(NPRE if pre else 0, 16):
         rel = slot_rel(i, base, base_prev)
-        items.append(Item(kv_frag(i, m, buf), 8, rel, max(rel, base + i - 3), stream))
+        items.append(Item(kv_frag(i, m, buf), 8, rel, max(rel, base + i - KNOBS["lead"]), stream))
     return items
 
 
@@ -411,7 +419,7 @@ def sd_read_items(base: int, m: int, p: int, buf: int, rel0: int, base_prev: int
              Item(lr[:4], 16, ld_rel, max(ld_rel, base + 11), stream + "l")]
     for i in range(16):
         rel = max(rel0, slot_rel(i, base, base_prev))
-        items.append(Item([sd_frag(i, m, buf)], 4, rel, max(rel, base + i - 3), stream))
+        items.append(Item([sd_frag(i, m, buf)], 4, rel, max(rel, base + i - KNOBS["lead"]), stream))
     return items
 
 
@@ -486,6 +494,7 @@ def iteration(a: Asm, m1: bool, m2: bool, ph: int, nxt: str):
     SD(2 it + 2) [16..31], KV(2 it + 1) [32..47], SD(2 it + 3) [48..63].
     Tile it sits in buffer ph, tile it + 1 in ph + 1, tile it + 2 goes to ph + 2."""
     kbuf, sbuf_, dbuf = ph, (ph + 1) % 3, (ph + 2) % 3
+    G_BAR, DL_DMA = KNOBS["gbar"], KNOBS["dldma"]   # noqa: N806 -- the sweep arms' values
     mf = kv_mfmas(0) + sd_mfmas(0) + kv_mfmas(1) + sd_mfmas(1)
     n = len(mf)
     items: list[Item] = []

@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_N = 35 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_N = 41 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -49,7 +49,10 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // K_DKDV_D1 ..: attn_bwd_gen.py VARIANTS (diagnostic arms, wrong outputs by design)
                            "toa_attn_dkdv_asm_d1",     "toa_attn_dkdv_asm_d2",       "toa_attn_dkdv_asm_d3",
                            "toa_attn_dkdv_asm_d4",     "toa_attn_dkdv_asm_d5",       "toa_attn_dkdv_asm_d6",
-                           "toa_attn_dkdv_asm_d7",     "toa_attn_dkdv_asm_t1"};
+                           "toa_attn_dkdv_asm_d7",     "toa_attn_dkdv_asm_t1",
+                           // schedule-parameter arms (correct outputs)
+                           "toa_attn_dkdv_asm_s1",     "toa_attn_dkdv_asm_s2",       "toa_attn_dkdv_asm_s3",
+                           "toa_attn_dkdv_asm_s4",     "toa_attn_dkdv_asm_s5",       "toa_attn_dkdv_asm_s6"};
 
 struct DevModule {
   std::once_flag once;
@@ -484,7 +487,8 @@ extern "C" int toa_attn_dkdv_asm_variant(int v, const bf16_t* q, const bf16_t* k
                                          const bf16_t* dout, const float* nlse2, const float* ndelta, bf16_t* dk,
                                          bf16_t* dv, bf16_t* ds, int B, int H, int Hk, int S, int D, float scale,
                                          int flags, const float* cosv, const float* sinv, int H3, hipStream_t stream) {
-  if (v < 0 || v > K_DKDV_T1 - K_DKDV_D1) return (int)hipErrorInvalidValue;  // the timing arm takes its own entry
+  if (v < 0 || v > K_N - K_DKDV_D1 || K_DKDV_D1 + v - 1 == K_DKDV_T1)
+    return (int)hipErrorInvalidValue;  // the timing arm takes its own entry
   return attn_dkdv_launch(v ? K_DKDV_D1 + v - 1 : K_ATTN_DKDV, q, k, v_, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S,
                           D, scale, flags, cosv, sinv, H3, stream);
 }
