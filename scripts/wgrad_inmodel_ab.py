@@ -4,10 +4,15 @@ process (one model, one set of buffers): alternating timed windows of
 
     python scripts/wgrad_inmodel_ab.py [--rounds 3] [--steps 4] [--arms wgrad=asm+gemm=nosk,wgrad=hip+gemm=nosk]
 
-An arm is settings joined by '+': wgrad=asm|hip (ops.gemm.set_wgrad_kernel),
+An arm is settings joined by '+': wgrad=asm|hip|asm_v1 (ops.gemm.set_wgrad_kernel),
 gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy), attnf=N /
-attnb=N (toa_attn_set_fwd_variant / toa_attn_set_bwd_variant forms).  Same-process windows
-remove the box-to-box spread (about +-2.5 %) from the comparison.
+attnb=N / attnd=N (toa_attn_set_fwd_variant / _bwd_variant / _dkdv_variant forms),
+or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
+weight-gradient schedule, the HIP attention forward and dK/dV) and head
+(this tree's defaults).  Same-process windows remove the box-to-box spread
+(about +-2.5 %) from the comparison:
+
+    python scripts/wgrad_inmodel_ab.py --arms r4,head --rounds 8
 """
 import argparse
 import json
@@ -24,6 +29,8 @@ from tf_operator_amd.train.llm import LlamaTrainer  # noqa: E402
 
 def apply(arm: str):
     """arm: settings joined by '+', e.g. wgrad=hip+gemm=nosk."""
+    presets = {"r4": "gemm=nosk+wgrad=asm_v1+attnf=1+attnd=0", "head": "gemm=asm+wgrad=asm+attnf=-1+attnd=-1"}
+    arm = presets.get(arm, arm)
     for part in arm.split("+"):
         key, val = part.split("=")
         if key == "wgrad":
@@ -34,6 +41,8 @@ def apply(arm: str):
             _lib.call("toa_attn_set_fwd_variant", int(val))
         elif key == "attnb":
             _lib.call("toa_attn_set_bwd_variant", int(val))
+        elif key == "attnd":
+            _lib.call("toa_attn_set_dkdv_variant", int(val))
         else:
             raise SystemExit(f"unknown arm {arm}")
 

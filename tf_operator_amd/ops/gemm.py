@@ -326,8 +326,10 @@ def wgrad_kernel() -> str:
 
 
 def set_wgrad_kernel(name: str):
+    """asm | hip | asm_v1 (the round-4 assembly schedule, bit-identical: the
+    round-to-round A/B of scripts/wgrad_inmodel_ab.py)."""
     global _WGRAD_KERNEL
-    if name not in ("asm", "hip"):
+    if name not in ("asm", "hip", "asm_v1"):
         raise ValueError(f"unknown weight-gradient kernel {name!r}")
     _WGRAD_KERNEL = name
 
@@ -368,8 +370,9 @@ def wgrad_hip_(g, dy2, x2, beta=1.0, split=None):
     ws = _workspace(dy2.device, nbytes) if nbytes > 0 else None
     args = (_lib.ptr(dy2), dy2.stride(0), _lib.ptr(x2), x2.stride(0), _lib.ptr(g), K, _lib.ptr(ws),
             N, K, T, int(split), int(beta != 0.0), _lib.stream(dy2))
-    if wgrad_kernel() == "asm":
-        rc = _lib.call_ret("toa_wgrad_asm", *args)
+    kern = wgrad_kernel()
+    if kern in ("asm", "asm_v1"):
+        rc = _lib.call_ret("toa_wgrad_asm", *args) if kern == "asm" else _lib.call_ret("toa_wgrad_asm_variant", 1, *args)
         if rc == 0:
             return g
         if rc != HIP_ERROR_INVALID_VALUE:
