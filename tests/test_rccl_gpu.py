@@ -82,3 +82,48 @@ def test_rccl_world1_zero_and_allreduce_match_no_collectives():
     assert losses[-1] < losses[0]
     for name, same_loss, same_param, same_master in ok:
         assert same_loss and same_param and same_master, (name, same_loss, same_param, same_master)
+
+
+def _pipe_worker(pipe, q):
+    """One process per arm (the trainer reads TOA_ZERO_PIPE at init): rank 0
+    of an emulated world-2 ZeRO-1 step on the GPU (TOA_EMULATE_WORLD=2, no
+    traffic) -- the HIP AdamW over rank 0's shards, bucket by bucket
+    (pipelined) or all at once."""
+    os.environ.update(TOA_ZERO="1", TOA_EMULATE_WORLD="2", TOA_EMULATE_BYTES="0", TOA_ZERO_PIPE=str(pipe))
+    try:
+        from tf_operator_amd.train.llm import LlamaTrainer
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        torch.manual_seed(0)
+        tr = LlamaTrainer("llama-tiny128", dev, micro_batch=2, seq_len=256)
+        assert tr.gather is not None and tr.pipeline_tail == bool(pipe)
+        batch = [tr.synthetic_batch()]
+        losses = [float(tr.step(batch)) for _ in range(3)]
+        tr.gather.wait_all()
+        torch.cuda.synchronize()
+        q.put((pipe, losses, tr.flat.param.detach().cpu(), tr.flat.master.detach().cpu(), None))
+    except Exception as e:  # pragma: no cover
+        q.put((pipe, None, None, None, repr(e)))
+
+
+@pytest.mark.timeout(300)
+def test_zero_pipelined_tail_bit_identical_on_gpu():
+    """the pipelined ZeRO-1 tail on the GPU path (HIP AdamW writing
+    the bf16 weights of each owned shard, the all-gather launched per bucket)
+    gives the same losses, weights and fp32 master shards bit for bit as the
+    whole-update-first tail."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    res = {}
+    for pipe in (0, 1):
+        p = ctx.Process(target=_pipe_worker, args=(pipe, q))
+        p.start()
+        r = q.get(timeout=250)
+        p.join(timeout=30)
+        assert r[4] is None, r[4]
+        res[r[0]] = r
+    (_, l0, p0, m0, _), (_, l1, p1, m1, _) = res[0], res[1]
+    assert l0 == l1
+    assert torch.equal(p0.view(torch.int16), p1.view(torch.int16))
+    assert torch.equal(m0, m1)
