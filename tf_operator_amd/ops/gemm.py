@@ -75,7 +75,7 @@ def resolve_auto(world: int = 1) -> str:
     in force.  The assembly kernel with the library-form slot map, the
     per-shape tile order and the fused SwiGLU epilogues wins in-model: the
     Llama-3-8B step is 5.5 +- 1.6 ms faster than on ``nosk`` (12 ABBA rounds
-    in one process, profiles/r5_ab2/inmodel.log; 9.4 ms less kernel time
+    in one process, profiles/r5_asm_gemm/inmodel_abba12.log; 9.4 ms less kernel time
     under rocprofv3, profiles/r5_prof1).  Like ``nosk`` it never holds the
     whole chip (one workgroup per tile, no stream-K), so the data-parallel
     collectives overlap it.  Round 4 measured the other way (946.3 vs 930.1
