@@ -446,7 +446,7 @@ def mfma(i: int, j: int, sub: int) -> str:
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
          "align": True, "drain_end": False, "map": "lib0", "persist": False, "dual": "", "zero_late": True,
-         "nostore": False, "store_nt": True, "store_same": False}
+         "nostore": False, "store_nt": True, "store_same": False, "epi_pipe": True}
 
 
 def _stamp(k: int) -> str:
@@ -847,10 +847,107 @@ def epilogue_swiglu_fwd(a: Asm):
             store16(a, ps + 4 * p, V_E + 1, SRD_S, S_T0, p)
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
         a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T1)}")
-        a("s_waitcnt vmcnt(0)")             # scratch reused by the next row block
+        if not SCHED["epi_pipe"]:
+            a("s_waitcnt vmcnt(0)")         # (round 4) scratch reused by the next row block
+        # epi_pipe: no drain -- a store reads its data registers within two
+        # wait states of issue (cdna_hip_programming.md, asm stores), and the
+        # next row block rewrites them dozens of instructions later
+
+
+EPI_DEPTH = 6    # SwiGLU backward: gu row blocks loaded this many rounds ahead (staging in the free fragment VGPRs)
 
 
 def epilogue_swiglu_bwd(a: Asm):
+    if SCHED["epi_pipe"]:
+        return epilogue_swiglu_bwd_pipe(a)
+    return epilogue_swiglu_bwd_r4(a)
+
+
+def epilogue_swiglu_bwd_pipe(a: Asm):
+    """The SwiGLU backward epilogue with its gu loads software-pipelined:
+    16 rounds (8 row blocks x 2 column halves), round r's 4 loads issued
+    EPI_DEPTH rounds ahead into staging slots in the main loop's fragment
+    VGPRs (free here), each round waiting only for its own loads (counted
+    vmcnt: VMEM completes in issue order) instead of draining every load
+    and store per round -- the round-4 form exposed a full memory latency 32
+    times per tile (59 % MFMA busy in the model, profiles/r5_pmc)."""
+    a(f"s_mov_b32 {sr(S_E0)}, 0")                             # dgu row block
+    a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")
+    a(f"s_mov_b32 {sr(S_T2)}, 0")                             # gu row block of the next prefetch
+    a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 4")
+    a(f"v_mov_b32 {vr(V_E + 4)}, {-LOG2E!r}")
+    rounds = [(j, half) for j in range(8) for half in range(2)]
+    D = EPI_DEPTH
+    seq: list = []     # VMEM ops in issue order: ("L" | "S", round)
+
+    def slot(r):
+        return V_FX0 + 16 * (r % D)                           # lg = slot, lu = slot + 8
+
+    def issue_loads(r):
+        j, half = rounds[r]
+        lg, lu = slot(r), slot(r) + 8
+        for q, p in enumerate((2 * half, 2 * half + 1)):
+            a(f"buffer_load_dwordx4 {vr(lg + 4 * q, 4)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T2)} offen offset:{64 * p}")
+            a(f"buffer_load_dwordx4 {vr(lu + 4 * q, 4)}, {vr(V_E + 3)}, {sr(SRD_S, 4)}, {sr(S_T2)} offen offset:{64 * p}")
+            seq.extend([("L", r), ("L", r)])
+        if half == 1:
+            a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_T1)}")   # the next prefetch reads the next row block
+
+    for r in range(min(D, len(rounds))):
+        issue_loads(r)
+    for r, (j, half) in enumerate(rounds):
+        ps_ = (2 * half, 2 * half + 1)
+        d = V_E + 24                        # 16 f32: ds (no memory dependency: first)
+        for q, p in enumerate(ps_):
+            read_pair(a, d + 8 * q, p, j)
+        pd = V_E + 40                       # bf16-rounded ds, then unpacked
+        for q in range(2):
+            cvt_pack8(a, pd + 4 * q, d + 8 * q)
+        for q in range(2):
+            unpack8(a, d + 8 * q, pd + 4 * q)
+        last = max(i for i, x in enumerate(seq) if x == ("L", r))
+        a(f"s_waitcnt vmcnt({min(63, len(seq) - last - 1)})")   # this round's loads only
+        lg, lu = slot(r), slot(r) + 8
+        gf, uf = V_E + 48, V_E + 64
+        for q in range(2):
+            unpack8(a, gf + 8 * q, lg + 4 * q)
+            unpack8(a, uf + 8 * q, lu + 4 * q)
+        if r + D < len(rounds):
+            issue_loads(r + D)              # into the slot just unpacked
+        sg, tmp, tt = V_E + 80, V_E + 96, V_E + 8
+        for e in range(16):                 # sg = 1 / (1 + exp(-g))
+            a(f"v_mul_f32 {vr(sg + e)}, {vr(V_E + 4)}, {vr(gf + e)}")
+        for e in range(16):
+            a(f"v_exp_f32 {vr(sg + e)}, {vr(sg + e)}")
+        for e in range(16):
+            a(f"v_add_f32 {vr(sg + e)}, 1.0, {vr(sg + e)}")
+        for e in range(16):
+            a(f"v_rcp_f32 {vr(sg + e)}, {vr(sg + e)}")
+        for e in range(16):                 # du = d * g * sg  -> tmp
+            a(f"v_mul_f32 {vr(tmp + e)}, {vr(d + e)}, {vr(gf + e)}")
+            a(f"v_mul_f32 {vr(tmp + e)}, {vr(tmp + e)}, {vr(sg + e)}")
+        for e in range(16):                 # dg = d * u * sg * (1 + g (1 - sg)) -> uf
+            a(f"v_sub_f32 {vr(tt)}, 1.0, {vr(sg + e)}")
+            a(f"v_fma_f32 {vr(tt)}, {vr(gf + e)}, {vr(tt)}, 1.0")
+            a(f"v_mul_f32 {vr(uf + e)}, {vr(d + e)}, {vr(uf + e)}")
+            a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(sg + e)}")
+            a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(tt)}")
+        pdg, pdu = V_E + 40, V_E + 112      # 8 + 4 regs: reuse gf for the last du pair
+        for q in range(2):
+            cvt_pack8(a, pdg + 4 * q, uf + 8 * q)
+        cvt_pack8(a, pdu, tmp)
+        cvt_pack8(a, gf, tmp + 8)
+        for q, p in enumerate(ps_):
+            store16(a, pdg + 4 * q, V_E, SRD_C, S_E0, p)
+        store16(a, pdu, V_E + 2, SRD_C, S_E0, ps_[0])
+        store16(a, gf, V_E + 2, SRD_C, S_E0, ps_[1])
+        seq.extend([("S", r)] * 4)
+        a("s_nop 1")                        # store data read before the next round rewrites it
+        if half == 1:
+            a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+
+
+def epilogue_swiglu_bwd_r4(a: Asm):
     """acc = ds (never stored).  gu rows: gate at n, up at F + n; pairs p of
     fragments give 8 consecutive n per lane: 16-byte loads and stores."""
     a(f"s_mov_b32 {sr(S_E0)}, 0")                             # dgu row block
@@ -1286,6 +1383,10 @@ def generate() -> str:
     metas = []
     for epi in EPIS:
         body, meta = kernel(epi)
+        parts.append(body)
+        metas.append(meta)
+    for epi in ("swiglu_fwd", "swiglu_bwd"):   # round-4 epilogues (per-round drains): in-model A/B arms
+        body, meta = _with_knobs({"epi_pipe": False}, lambda: kernel(epi, variant="r4"))
         parts.append(body)
         metas.append(meta)
     for vname, knobs in PLAIN_VARIANTS:

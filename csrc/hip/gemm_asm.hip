@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_N = 41 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_N = 43 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -52,7 +52,9 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            "toa_attn_dkdv_asm_d7",     "toa_attn_dkdv_asm_t1",
                            // schedule-parameter arms (correct outputs)
                            "toa_attn_dkdv_asm_s1",     "toa_attn_dkdv_asm_s2",       "toa_attn_dkdv_asm_s3",
-                           "toa_attn_dkdv_asm_s4",     "toa_attn_dkdv_asm_s5",       "toa_attn_dkdv_asm_s6"};
+                           "toa_attn_dkdv_asm_s4",     "toa_attn_dkdv_asm_s5",       "toa_attn_dkdv_asm_s6",
+                           // the round-4 SwiGLU epilogues (drain per row block): in-model A/B arms
+                           "toa_gemm_tn_asm_swiglu_fwd_r4", "toa_gemm_tn_asm_swiglu_bwd_r4"};
 
 struct DevModule {
   std::once_flag once;
@@ -426,6 +428,16 @@ static int attn_fwd_asm_launch(int which, const bf16_t* q, const bf16_t* k, cons
   return (int)hipModuleLaunchKernel(fn, (unsigned)nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
 }
 
+// In-model A/B (scripts/wgrad_inmodel_ab.py epi=r4): 1 = the fused SwiGLU
+// GEMMs run the round-4 epilogues (every row block drained); 0 = the
+// software-pipelined ones (csrc/asm/gemm_gen.py epilogue_swiglu_bwd_pipe).
+static int g_epi_r4 = 0;
+extern "C" int toa_gemm_asm_set_epi_variant(int v) {
+  if (v < 0 || v > 1) return (int)hipErrorInvalidValue;
+  g_epi_r4 = v;
+  return 0;
+}
+
 extern "C" int toa_gemm_asm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* Wgu, int64_t ldw, bf16_t* GU,
                                    int64_t ldgu, bf16_t* S, int64_t lds_, int M, int F, int K, hipStream_t stream) {
   if (!common_ok(M, K, ldx, ldw, X, Wgu) || F <= 0 || F % 128 || !ld_ok(ldgu, 2 * F) || !ld_ok(lds_, F) || !al16(GU) ||
@@ -436,7 +448,7 @@ extern "C" int toa_gemm_asm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W
   a.lds = (uint32_t)(lds_ * 2);
   a.fw = (uint32_t)((int64_t)F * ldw * 2);
   a.fc = (uint32_t)(F * 2);
-  return launch(K_SWIGLU_FWD, a, stream);
+  return launch(g_epi_r4 ? K_SWIGLU_FWD_R4 : K_SWIGLU_FWD, a, stream);
 }
 
 extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16_t* WdT, int64_t ldw,
@@ -449,7 +461,7 @@ extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16
   a.S = (uint64_t)GU;
   a.lds = (uint32_t)(ldgu * 2);
   a.fc = (uint32_t)(F * 2);
-  return launch(K_SWIGLU_BWD, a, stream);
+  return launch(g_epi_r4 ? K_SWIGLU_BWD_R4 : K_SWIGLU_BWD, a, stream);
 }
 
 // Causal flash-attention dK / dV backward of the dS form (csrc/asm/attn_bwd_gen.py),

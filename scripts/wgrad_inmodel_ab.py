@@ -7,6 +7,7 @@ process (one model, one set of buffers): alternating timed windows of
 An arm is settings joined by '+': wgrad=asm|hip|asm_v1 (ops.gemm.set_wgrad_kernel),
 gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy), attnf=N /
 attnb=N / attnd=N (toa_attn_set_fwd_variant / _bwd_variant / _dkdv_variant forms),
+epi=r4|pipe (the fused SwiGLU GEMMs' epilogues, toa_gemm_asm_set_epi_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
 (this tree's defaults).  Same-process windows remove the box-to-box spread
@@ -29,7 +30,8 @@ from tf_operator_amd.train.llm import LlamaTrainer  # noqa: E402
 
 def apply(arm: str):
     """arm: settings joined by '+', e.g. wgrad=hip+gemm=nosk."""
-    presets = {"r4": "gemm=nosk+wgrad=asm_v1+attnf=1+attnd=0", "head": "gemm=asm+wgrad=asm+attnf=-1+attnd=-1"}
+    presets = {"r4": "gemm=nosk+wgrad=asm_v1+attnf=1+attnd=0+epi=r4",
+               "head": "gemm=asm+wgrad=asm+attnf=-1+attnd=-1+epi=pipe"}
     arm = presets.get(arm, arm)
     for part in arm.split("+"):
         key, val = part.split("=")
@@ -43,6 +45,8 @@ def apply(arm: str):
             _lib.call("toa_attn_set_bwd_variant", int(val))
         elif key == "attnd":
             _lib.call("toa_attn_set_dkdv_variant", int(val))
+        elif key == "epi":   # the fused SwiGLU GEMMs' epilogues: r4 (drained per row block) or pipe
+            _lib.call("toa_gemm_asm_set_epi_variant", 1 if val == "r4" else 0)
         else:
             raise SystemExit(f"unknown arm {arm}")
 

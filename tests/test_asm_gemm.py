@@ -243,7 +243,9 @@ def test_host_kernel_table_matches_generator():
     # + the weight gradient's round-4 arm + the attention forward and its arms + the dK/dV backward
     import attn_bwd_gen
     import attn_gen
-    assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + len(attn_bwd_gen.VARIANTS)
+    # + the round-4 SwiGLU epilogue arms (2)
+    assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
+        len(attn_bwd_gen.VARIANTS) + 2
     flags = re.search(r"kVariantPersist\[K_WGRAD_V1 - K_V1\] = \{([^}]*)\}", src).group(1)
     assert [f.strip() == "true" for f in flags.split(",")] == [bool(k.get("persist")) for _, k in gemm_gen.PLAIN_VARIANTS]
 
