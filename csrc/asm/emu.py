@@ -369,7 +369,8 @@ class Emu:
         self.vset(w, a[0], np.clip(np.trunc(f), 0, M32).astype(np.uint64).astype(np.uint32))
 
     def op_v_rcp_iflag_f32(self, w, a, m):
-        self.vset(w, a[0], f2u(np.float32(1.0) / u2f(self.vget(w, a[1]))))
+        with np.errstate(divide="ignore"):
+            self.vset(w, a[0], f2u(np.float32(1.0) / u2f(self.vget(w, a[1]))))
 
     op_v_rcp_f32 = op_v_rcp_iflag_f32
 
@@ -449,6 +450,11 @@ class Emu:
         x, y, z = (self._pair(w, t) for t in a[1:4])
         lo, hi = self.vrange(w, a[0])
         w.v[lo:hi] = f2u((x * y + z).astype(np.float32))
+
+    def op_v_pk_add_f32(self, w, a, m):
+        x, y = (self._pair(w, t) for t in a[1:3])
+        lo, hi = self.vrange(w, a[0])
+        w.v[lo:hi] = f2u((x + y).astype(np.float32))
 
     def op_v_pk_mul_f32(self, w, a, m):
         x, y = (self._pair(w, t) for t in a[1:3])

@@ -446,7 +446,8 @@ def mfma(i: int, j: int, sub: int) -> str:
 SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4, "sub1_gap": 1, "xbar": 23,
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
          "align": True, "drain_end": False, "map": "lib0", "persist": False, "dual": "", "zero_late": True,
-         "nostore": False, "store_nt": True, "store_same": False, "epi_pipe": True}
+         "nostore": False, "store_nt": True, "store_same": False, "epi_pipe": True,
+         "epi_pk": True}
 
 
 def _stamp(k: int) -> str:
@@ -799,7 +800,23 @@ def epilogue_plain(a: Asm):
 def silu_times(a: Asm, out: int, g: int, u: int, t: int, n: int):
     """out[e] = silu(g[e]) * u[e] = g / (1 + 2^(-g log2 e)) * u, e < n
     (batched per op: a transcendental's result is consumed n instructions
-    later, past the forwarding hazard)."""
+    later, past the forwarding hazard).  epi_pk: the non-transcendental ops
+    on register pairs (v_pk_*_f32; constants -log2 e and 1.0 as pairs at
+    V_E + 4 / V_E + 6)."""
+    if SCHED["epi_pk"]:
+        for e in range(0, n, 2):
+            a(f"v_pk_mul_f32 {vr(t + e, 2)}, {vr(V_E + 4, 2)}, {vr(g + e, 2)}")
+        for e in range(n):
+            a(f"v_exp_f32 {vr(t + e)}, {vr(t + e)}")
+        for e in range(0, n, 2):
+            a(f"v_pk_add_f32 {vr(t + e, 2)}, {vr(V_E + 6, 2)}, {vr(t + e, 2)}")
+        for e in range(n):
+            a(f"v_rcp_f32 {vr(t + e)}, {vr(t + e)}")
+        for e in range(0, n, 2):
+            a(f"v_pk_mul_f32 {vr(t + e, 2)}, {vr(g + e, 2)}, {vr(t + e, 2)}")
+        for e in range(0, n, 2):
+            a(f"v_pk_mul_f32 {vr(out + e, 2)}, {vr(t + e, 2)}, {vr(u + e, 2)}")
+        return
     for e in range(n):
         a(f"v_mul_f32 {vr(t + e)}, {vr(V_E + 3)}, {vr(g + e)}")
     for e in range(n):
@@ -822,6 +839,10 @@ def epilogue_swiglu_fwd(a: Asm):
     a(f"s_mov_b32 {sr(S_T0)}, 0")
     a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 4")
     a(f"v_mov_b32 {vr(V_E + 3)}, {-LOG2E!r}")
+    for x in (4, 5):
+        a(f"v_mov_b32 {vr(V_E + x)}, {-LOG2E!r}")
+    for x in (6, 7):
+        a(f"v_mov_b32 {vr(V_E + x)}, 1.0")
     for j in range(8):
         g, u = V_E + 8, V_E + 24            # 16 f32 each (2 pairs)
         for p in range(2):
@@ -876,6 +897,12 @@ def epilogue_swiglu_bwd_pipe(a: Asm):
     a(f"s_mov_b32 {sr(S_T2)}, 0")                             # gu row block of the next prefetch
     a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDS)}, 4")
     a(f"v_mov_b32 {vr(V_E + 4)}, {-LOG2E!r}")
+    if SCHED["epi_pk"]:   # pairs: -log2 e (V_E + 4), 1.0 (V_E + 6), -1.0 (V_E + 10)
+        a(f"v_mov_b32 {vr(V_E + 5)}, {-LOG2E!r}")
+        for x in (6, 7):
+            a(f"v_mov_b32 {vr(V_E + x)}, 1.0")
+        for x in (10, 11):
+            a(f"v_mov_b32 {vr(V_E + x)}, -1.0")
     rounds = [(j, half) for j in range(8) for half in range(2)]
     D = EPI_DEPTH
     seq: list = []     # VMEM ops in issue order: ("L" | "S", round)
@@ -915,23 +942,42 @@ def epilogue_swiglu_bwd_pipe(a: Asm):
         if r + D < len(rounds):
             issue_loads(r + D)              # into the slot just unpacked
         sg, tmp, tt = V_E + 80, V_E + 96, V_E + 8
-        for e in range(16):                 # sg = 1 / (1 + exp(-g))
-            a(f"v_mul_f32 {vr(sg + e)}, {vr(V_E + 4)}, {vr(gf + e)}")
-        for e in range(16):
-            a(f"v_exp_f32 {vr(sg + e)}, {vr(sg + e)}")
-        for e in range(16):
-            a(f"v_add_f32 {vr(sg + e)}, 1.0, {vr(sg + e)}")
-        for e in range(16):
-            a(f"v_rcp_f32 {vr(sg + e)}, {vr(sg + e)}")
-        for e in range(16):                 # du = d * g * sg  -> tmp
-            a(f"v_mul_f32 {vr(tmp + e)}, {vr(d + e)}, {vr(gf + e)}")
-            a(f"v_mul_f32 {vr(tmp + e)}, {vr(tmp + e)}, {vr(sg + e)}")
-        for e in range(16):                 # dg = d * u * sg * (1 + g (1 - sg)) -> uf
-            a(f"v_sub_f32 {vr(tt)}, 1.0, {vr(sg + e)}")
-            a(f"v_fma_f32 {vr(tt)}, {vr(gf + e)}, {vr(tt)}, 1.0")
-            a(f"v_mul_f32 {vr(uf + e)}, {vr(d + e)}, {vr(uf + e)}")
-            a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(sg + e)}")
-            a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(tt)}")
+        if SCHED["epi_pk"]:                 # the same math on register pairs
+            for e in range(0, 16, 2):       # sg = 1 / (1 + exp(-g))
+                a(f"v_pk_mul_f32 {vr(sg + e, 2)}, {vr(V_E + 4, 2)}, {vr(gf + e, 2)}")
+            for e in range(16):
+                a(f"v_exp_f32 {vr(sg + e)}, {vr(sg + e)}")
+            for e in range(0, 16, 2):
+                a(f"v_pk_add_f32 {vr(sg + e, 2)}, {vr(V_E + 6, 2)}, {vr(sg + e, 2)}")
+            for e in range(16):
+                a(f"v_rcp_f32 {vr(sg + e)}, {vr(sg + e)}")
+            for e in range(0, 16, 2):       # du = d * g * sg  -> tmp
+                a(f"v_pk_mul_f32 {vr(tmp + e, 2)}, {vr(d + e, 2)}, {vr(gf + e, 2)}")
+                a(f"v_pk_mul_f32 {vr(tmp + e, 2)}, {vr(tmp + e, 2)}, {vr(sg + e, 2)}")
+            for e in range(0, 16, 2):       # dg = d * u * sg * (1 + g (1 - sg)) -> uf
+                a(f"v_pk_fma_f32 {vr(tt, 2)}, {vr(sg + e, 2)}, {vr(V_E + 10, 2)}, {vr(V_E + 6, 2)}")
+                a(f"v_pk_fma_f32 {vr(tt, 2)}, {vr(gf + e, 2)}, {vr(tt, 2)}, {vr(V_E + 6, 2)}")
+                a(f"v_pk_mul_f32 {vr(uf + e, 2)}, {vr(d + e, 2)}, {vr(uf + e, 2)}")
+                a(f"v_pk_mul_f32 {vr(uf + e, 2)}, {vr(uf + e, 2)}, {vr(sg + e, 2)}")
+                a(f"v_pk_mul_f32 {vr(uf + e, 2)}, {vr(uf + e, 2)}, {vr(tt, 2)}")
+        else:
+            for e in range(16):             # sg = 1 / (1 + exp(-g))
+                a(f"v_mul_f32 {vr(sg + e)}, {vr(V_E + 4)}, {vr(gf + e)}")
+            for e in range(16):
+                a(f"v_exp_f32 {vr(sg + e)}, {vr(sg + e)}")
+            for e in range(16):
+                a(f"v_add_f32 {vr(sg + e)}, 1.0, {vr(sg + e)}")
+            for e in range(16):
+                a(f"v_rcp_f32 {vr(sg + e)}, {vr(sg + e)}")
+            for e in range(16):             # du = d * g * sg  -> tmp
+                a(f"v_mul_f32 {vr(tmp + e)}, {vr(d + e)}, {vr(gf + e)}")
+                a(f"v_mul_f32 {vr(tmp + e)}, {vr(tmp + e)}, {vr(sg + e)}")
+            for e in range(16):             # dg = d * u * sg * (1 + g (1 - sg)) -> uf
+                a(f"v_sub_f32 {vr(tt)}, 1.0, {vr(sg + e)}")
+                a(f"v_fma_f32 {vr(tt)}, {vr(gf + e)}, {vr(tt)}, 1.0")
+                a(f"v_mul_f32 {vr(uf + e)}, {vr(d + e)}, {vr(uf + e)}")
+                a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(sg + e)}")
+                a(f"v_mul_f32 {vr(uf + e)}, {vr(uf + e)}, {vr(tt)}")
         pdg, pdu = V_E + 40, V_E + 112      # 8 + 4 regs: reuse gf for the last du pair
         for q in range(2):
             cvt_pack8(a, pdg + 4 * q, uf + 8 * q)
@@ -1386,7 +1432,7 @@ def generate() -> str:
         parts.append(body)
         metas.append(meta)
     for epi in ("swiglu_fwd", "swiglu_bwd"):   # round-4 epilogues (per-round drains): in-model A/B arms
-        body, meta = _with_knobs({"epi_pipe": False}, lambda: kernel(epi, variant="r4"))
+        body, meta = _with_knobs({"epi_pipe": False, "epi_pk": False}, lambda: kernel(epi, variant="r4"))
         parts.append(body)
         metas.append(meta)
     for vname, knobs in PLAIN_VARIANTS:
