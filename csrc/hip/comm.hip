@@ -265,6 +265,34 @@ extern "C" int toa_flags_wait(void* const* flags, int idx, int rank, int world, 
   return (int)hipGetLastError();
 }
 
+// The owner's half of the copy-engine reduce-scatter
+// (parallel/pull_gather.PullReduceScatter): dst[i] <- bf16(dst[i] + src[0][i]
+// + ... + src[nsl - 1][i]), summed in fp32 in that order and rounded once;
+// src slices `stride` elements apart (the peers' pulled slices, staged).
+// n a multiple of 8, 16-byte aligned.  HBM-bound: 8 elements per thread.
+__global__ __launch_bounds__(256) void sum_slices_bf16_kernel(bf16_t* __restrict__ dst, const bf16_t* __restrict__ src,
+                                                              int nsl, int64_t stride, int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc[8], f[8];
+    unpack8(ld16(dst + i * 8), acc);
+    for (int k = 0; k < nsl; ++k) {
+      unpack8(__builtin_nontemporal_load((const u32x4*)(src + k * stride) + i), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    st16(dst + i * 8, pack8(acc));
+  }
+}
+
+extern "C" int toa_sum_slices_bf16(bf16_t* dst, const bf16_t* src, int nsl, int64_t stride, int64_t n,
+                                   hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (n % 8 || stride % 8 || nsl < 0 || (((uintptr_t)dst | (uintptr_t)src) & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sum_slices_bf16_kernel, dim3(toa_stream_grid(n / 8, 256)), dim3(256), 0, stream, dst, src, nsl,
+                     stride, n / 8);
+  return (int)hipGetLastError();
+}
+
 // A copy on a copy engine (SDMA): peer-mapped source, local destination.
 extern "C" int toa_copy_nocu(const void* src, void* dst, int64_t nbytes, hipStream_t stream) {
   if (nbytes <= 0) return 0;

@@ -330,3 +330,132 @@ def test_pull_gather_copy_engine_two_processes():
     for rank, ok, err in res:
         assert err is None, (rank, err)
         assert ok, rank
+
+
+def _rs_pull_worker(rank, world, port, q):
+    """Copy-engine reduce-scatter (PullReduceScatter over GpuIpcTransport)
+    between two processes on the one GPU: each shard must equal the fp32 sum
+    (own slice first, peers in rank order, one rounding) of both ranks'
+    gradients, the rest of the buffer untouched."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tf_operator_amd.parallel import zero
+        from tf_operator_amd.parallel.pull_gather import GpuIpcTransport, PullReduceScatter
+
+        sizes = [64 * world * k for k in (4096, 1, 333, 2048)]
+        ranges, lo = [], 0
+        for n in sizes:
+            ranges.append((lo, lo + n))
+            lo += n
+        buf = torch.zeros(lo, device="cuda", dtype=torch.bfloat16)
+        t = GpuIpcTransport(buf, rank, world, len(ranges), timeout_ms=20000, what="reduce-scatter")
+        rs = PullReduceScatter(t, ranges, rank, world)
+        ok = True
+        for step in range(5):
+            grads = [torch.randn(lo, generator=torch.Generator().manual_seed(31 * step + r)).to(torch.bfloat16)
+                     for r in range(world)]
+            buf.copy_(grads[rank].cuda())            # "backward" on the compute stream
+            works = [(b, rs.launch_one(b)) for b in reversed(range(len(ranges)))]
+            for b, w in works:
+                w.wait()
+                rs.reduce(b)
+            rs.new_step()
+            want = grads[rank].clone()
+            for s_, e in zero.owned_ranges(ranges, world, rank):
+                acc = grads[rank][s_:e].float()
+                for r in range(world):
+                    if r != rank:
+                        acc += grads[r][s_:e].float()
+                want[s_:e] = acc.to(torch.bfloat16)
+            ok = ok and torch.equal(buf.cpu().view(torch.int16), want.view(torch.int16))
+            dist.barrier()   # the test's stand-in for the all-gather that orders the next backward
+        torch.cuda.synchronize()
+        t.check()
+        rs.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, ok, None))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, None, repr(e)))
+
+
+def test_pull_reduce_scatter_copy_engine_two_processes():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _port()
+    procs = [ctx.Process(target=_rs_pull_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, ok, err in res:
+        assert err is None, (rank, err)
+        assert ok, rank
+
+
+def _zero_sdma_trainer_worker(rank, world, port, out, sdma):
+    """llama-tiny ZeRO-1 steps, both ranks on the one GPU and the same batch.
+    sdma: the weight all-gather AND the gradient reduce-scatter by copy-engine
+    pulls (no collective on either path; the process group is gloo and
+    carries only the norm); world 1 (rank 0 only): the unsharded reference."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    if sdma:
+        os.environ.update(TOA_ZERO_AG="sdma", TOA_ZERO_RS="sdma")
+    try:
+        torch.cuda.set_device(0)
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        from tf_operator_amd.models.llama import PRESETS
+        from tf_operator_amd.train.llm import LlamaTrainer
+
+        tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device("cuda", 0), micro_batch=2, seq_len=128, lr=1e-3,
+                          bucket_mb=0.25, shard_optimizer=world > 1)
+        if world > 1:
+            assert tr.bucketer.pull_rs is not None and tr.gather.pull is not None
+            assert len(tr.bucketer.buckets) > 2
+        b = tr.synthetic_batch()
+        losses = [float(tr.step([b])) for _ in range(5)]
+        if tr.gather is not None:
+            tr.gather.wait_all()
+        torch.cuda.synchronize()
+        if world > 1:
+            tr.bucketer.pull_rs.check()
+            tr.gather.pull.check()
+        torch.save({"losses": losses, "param": tr.flat.param.float().cpu()}, f"{out}.{world}.{rank}")
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        torch.save({"err": repr(e)}, f"{out}.{world}.{rank}")
+
+
+def test_zero_trainer_both_collectives_by_copy_engine(tmp_path):
+    """TOA_ZERO_AG=sdma + TOA_ZERO_RS=sdma end to end: two ranks on the same
+    batch must train like one unsharded rank (the sum of two equal bf16
+    gradients halves back exactly; only the norm's summation order differs)."""
+    ctx = mp.get_context("spawn")
+    out = str(tmp_path / "res")
+    ref = ctx.Process(target=_zero_sdma_trainer_worker, args=(0, 1, _port(), out, False))
+    ref.start()
+    ref.join(timeout=300)
+    port = _port()
+    procs = [ctx.Process(target=_zero_sdma_trainer_worker, args=(r, 2, port, out, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    r1 = torch.load(f"{out}.1.0", weights_only=True)
+    assert "err" not in r1, r1
+    for r in range(2):
+        r2 = torch.load(f"{out}.2.{r}", weights_only=True)
+        assert "err" not in r2, (r, r2)
+        assert max(abs(a - b) for a, b in zip(r1["losses"], r2["losses"])) < 2e-3, (r1["losses"], r2["losses"])
+        d = (r1["param"] - r2["param"]).abs().max()
+        assert float(d) <= 2e-2 * float(r1["param"].abs().max()), float(d)

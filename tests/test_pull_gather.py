@@ -96,3 +96,85 @@ def test_zero_ag_mode_env(monkeypatch):
     monkeypatch.setenv("TOA_ZERO_AG", "bogus")
     with pytest.raises(ValueError):
         pull_gather.mode_from_env()
+
+
+def _rs_worker(rank, world, port, tag, q):
+    """The copy-engine reduce-scatter protocol (PullReduceScatter) over
+    ShmTransport: each rank's shard of every bucket must equal the fp32 sum
+    (own slice first, then the peers in rank order, rounded once) of every
+    rank's gradients; the rest of the buffer keeps this rank's own values."""
+    import torch.distributed as dist
+
+    from tf_operator_amd.parallel import zero
+    from tf_operator_amd.parallel.pull_gather import PullReduceScatter, ShmTransport
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    t = None
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        sizes = [64 * world * k for k in (5, 1, 3, 2)]
+        ranges, lo = [], 0
+        for n in sizes:
+            ranges.append((lo, lo + n))
+            lo += n
+        t = ShmTransport(tag, rank, world, lo, torch.bfloat16, len(ranges))
+        rs = PullReduceScatter(t, ranges, rank, world)
+        ok = True
+        for step in range(3):
+            grads = [torch.randn(lo, generator=torch.Generator().manual_seed(77 * step + r)).to(torch.bfloat16)
+                     for r in range(world)]
+            t.buf.copy_(grads[rank])
+            dist.barrier()   # stand-in for the previous step's all-gather ordering
+            works = [(b, rs.launch_one(b)) for b in reversed(range(len(ranges)))]   # backward order
+            for b, w in works:
+                w.wait()
+                rs.reduce(b)
+            rs.new_step()
+            want = grads[rank].clone()
+            for s, e in zero.owned_ranges(ranges, world, rank):
+                acc = grads[rank][s:e].float()
+                for r in range(world):
+                    if r != rank:
+                        acc += grads[r][s:e].float()
+                want[s:e] = acc.to(torch.bfloat16)
+            ok = ok and torch.equal(t.buf.clone().view(torch.int16), want.view(torch.int16))
+            dist.barrier()
+        q.put((rank, ok, None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        if t is not None:
+            t.close()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 4])
+def test_pull_reduce_scatter_matches_sum(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port, tag = _port(), f"rs{os.getpid()}_{world}"
+    procs = [ctx.Process(target=_rs_worker, args=(r, world, port, tag, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=150) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, ok, err in res:
+        assert err is None, (rank, err)
+        assert ok, rank
+    leftovers = [f for f in os.listdir("/dev/shm") if f.startswith(f"toa_pull_{tag}")]
+    assert not leftovers, leftovers
+
+
+def test_zero_rs_mode_env(monkeypatch):
+    from tf_operator_amd.parallel import pull_gather
+
+    monkeypatch.delenv("TOA_ZERO_RS", raising=False)
+    assert pull_gather.rs_mode_from_env() == "rccl"
+    monkeypatch.setenv("TOA_ZERO_RS", "sdma")
+    assert pull_gather.rs_mode_from_env() == "sdma"
+    monkeypatch.setenv("TOA_ZERO_RS", "ring")
+    with pytest.raises(ValueError):
+        pull_gather.rs_mode_from_env()

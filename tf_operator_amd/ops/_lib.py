@@ -118,6 +118,7 @@ _SIGS = {
     "toa_flag_publish": [c_p, ctypes.c_uint, c_p],
     "toa_flags_wait": [c_p, c_int, c_int, c_int, ctypes.c_uint, c_p, c_int, c_p],
     "toa_copy_nocu": [c_p, c_p, c_i64, c_p],
+    "toa_sum_slices_bf16": [c_p, c_p, c_int, c_i64, c_i64, c_p],
     "toa_gemm_tune": [c_int, c_int, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_f, c_int, c_p, c_p, c_p,
                       c_p, c_p, c_int],
     "toa_gemm_kernel_name": [c_int, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_p, c_int],

@@ -108,6 +108,9 @@ class GradBucketer:
         # launch collectives (the trainer disarms the others); armed by default
         self.armed = True
         self.launched = [False] * len(self.buckets)
+        # parallel/pull_gather.PullReduceScatter: the sharded reduce-scatter
+        # by copy-engine pulls instead of RCCL (TOA_ZERO_RS=sdma; set by the trainer)
+        self.pull_rs = None
         self.shard = bool(shard) and self.enabled and zero.feasible(self.buckets, self.world)
         self.owned = (zero.owned_ranges(self.buckets, self.world, self.rank) if self.shard
                       else [(0, flat.numel)])
@@ -182,6 +185,10 @@ class GradBucketer:
                 self.works.append(self.emu.collective(view))
             self.path_counts["collective"] += 1
             return
+        if self.shard and self.pull_rs is not None:
+            self.works.append(self.pull_rs.launch_one(b))
+            self.finishers.append(lambda b=b: self.pull_rs.reduce(b))
+            return
         if self.shard:
             w, fin = zero.reduce_scatter_(view, self.rank, self.world, self.group)
             self.works.append(w)
@@ -208,6 +215,9 @@ class GradBucketer:
             fin()
         if self.ipc is not None:
             self.ipc.poll()  # a peer timeout in the one-shot kernel must not pass silently
+        if self.pull_rs is not None:
+            self.pull_rs.new_step()
+            self.pull_rs.poll()  # a peer that never published surfaces one step later
         self.works = []
         self.finishers = []
         self.pending = [b[2] for b in self.buckets]

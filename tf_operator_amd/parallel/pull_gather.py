@@ -56,6 +56,13 @@ def mode_from_env() -> str:
     return m
 
 
+def rs_mode_from_env() -> str:
+    m = os.environ.get("TOA_ZERO_RS", "rccl")
+    if m not in ("rccl", "sdma"):
+        raise ValueError(f"TOA_ZERO_RS={m!r}: expected rccl or sdma")
+    return m
+
+
 class _Event:
     """Work-like handle: ``wait()`` makes the current stream wait (GPU) or
     is a no-op (CPU: the pull already ran synchronously)."""
@@ -100,8 +107,10 @@ class ShmTransport:
         self.my_flags[idx] = epoch
         self.my_flags.flush()
 
-    def pull(self, idx: int, epoch: int, pieces):
-        """pieces: [(peer, lo, hi)] element ranges of the flat buffer."""
+    def pull(self, idx: int, epoch: int, pieces, dst=None):
+        """pieces: [(peer, lo, hi)] element ranges of the flat buffer, copied
+        to the same range of this rank's buffer -- or [(peer, lo, hi, off)]
+        copied to dst[off:off + hi - lo] (the reduce-scatter's staging)."""
         t0 = time.monotonic()
         for r in range(self.world):
             if r == self.rank:
@@ -110,8 +119,9 @@ class ShmTransport:
                 if time.monotonic() - t0 > self.timeout:
                     raise RuntimeError(f"pull all-gather: rank {r} never published bucket {idx} epoch {epoch}")
                 time.sleep(0.0005)
-        for r, lo, hi in pieces:
-            self.buf[lo:hi].copy_(self.peer_bufs[r][lo:hi])
+        for r, lo, hi, *off in pieces:
+            o = off[0] if off else lo
+            (self.buf if dst is None else dst)[o:o + hi - lo].copy_(self.peer_bufs[r][lo:hi])
         return _Event()
 
     def close(self):
@@ -128,13 +138,15 @@ class GpuIpcTransport:
     arrays through toa_ipc_alloc handles, waits / publishes / copies by the
     HIP entry points of csrc/hip/comm.hip on a high-priority copy stream."""
 
-    def __init__(self, buf: torch.Tensor, rank: int, world: int, nflags: int, group=None, timeout_ms: int = 60000):
+    def __init__(self, buf: torch.Tensor, rank: int, world: int, nflags: int, group=None, timeout_ms: int = 60000,
+                 what: str = "all-gather"):
         from torch.multiprocessing.reductions import reduce_tensor
 
         from ..ops import _lib
 
         if world > 8:
-            raise ValueError("the copy-engine all-gather is for one node (<= 8 ranks)")
+            raise ValueError(f"the copy-engine {what} is for one node (<= 8 ranks)")
+        self.what = what
         self._lib = _lib
         self.rank, self.world, self.group = rank, world, group
         self.buf, self.nflags, self.timeout_ms = buf, nflags, int(timeout_ms)
@@ -187,8 +199,8 @@ class GpuIpcTransport:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
         if int(ok.item()) != 1:
             self.close()
-            raise RuntimeError("copy-engine all-gather setup failed: " + "; ".join(errs + ([err] if err else [])
-                                                                              or ["on a peer rank"]))
+            raise RuntimeError(f"copy-engine {what} setup failed: " + "; ".join(errs + ([err] if err else [])
+                                                                            or ["on a peer rank"]))
         self.err = torch.zeros(1, device=buf.device, dtype=torch.int32)
         self.stream = torch.cuda.Stream(device=buf.device, priority=-1)
 
@@ -196,16 +208,19 @@ class GpuIpcTransport:
         L = self._lib
         L.call("toa_flag_publish", ctypes.c_void_p(self._own.value + 4 * idx), epoch, L.stream(self.buf))
 
-    def pull(self, idx: int, epoch: int, pieces):
+    def pull(self, idx: int, epoch: int, pieces, dst=None):
+        """As ShmTransport.pull, on the copy stream (SDMA copies)."""
         L = self._lib
         cur = torch.cuda.current_stream(self.buf.device)
         self.stream.wait_stream(cur)   # this rank's readers of the old weights are done
         st = ctypes.c_void_p(self.stream.cuda_stream)
         L.call("toa_flags_wait", self.flags, idx, self.rank, self.world, epoch, L.ptr(self.err), self.timeout_ms, st)
         es = self.buf.element_size()
-        for r, lo, hi in pieces:
+        out = self.buf if dst is None else dst
+        for r, lo, hi, *off in pieces:
             src = self.peer_bufs[r].data_ptr() + es * lo
-            L.call("toa_copy_nocu", ctypes.c_void_p(src), ctypes.c_void_p(self.buf.data_ptr() + es * lo),
+            o = off[0] if off else lo
+            L.call("toa_copy_nocu", ctypes.c_void_p(src), ctypes.c_void_p(out.data_ptr() + es * o),
                    es * (hi - lo), st)
         ev = torch.cuda.Event()
         ev.record(self.stream)
@@ -230,14 +245,13 @@ class GpuIpcTransport:
                 self._err_ev.record(self.stream)
 
     def _raise(self, e: int):
-        raise RuntimeError(f"copy-engine all-gather: ranks {[r for r in range(8) if e >> r & 1]} never "
-                           "published their shards (peer lost or stalled); the weights are stale")
+        raise RuntimeError(f"copy-engine {self.what}: ranks {[r for r in range(8) if e >> r & 1]} never "
+                           "published their shards (peer lost or stalled); the result is stale")
 
     def check(self):
         e = int(self.err.item())
         if e:
-            raise RuntimeError(f"copy-engine all-gather: ranks {[r for r in range(8) if e >> r & 1]} never "
-                               "published their shards (peer lost or stalled); the weights are stale")
+            self._raise(e)
 
     def close(self):
         torch.cuda.synchronize()
@@ -278,6 +292,103 @@ class PullGather:
         it and pull the peers'.  Returns a Work-like handle."""
         self.t.publish(b, self.epoch)
         return self.t.pull(b, self.epoch, self.pieces(b))
+
+    def check(self):
+        if hasattr(self.t, "check"):
+            self.t.check()
+
+    def poll(self):
+        if hasattr(self.t, "poll"):
+            self.t.poll()
+
+    def close(self):
+        self.t.close()
+
+
+class PullReduceScatter:
+    """The ZeRO-1 gradient reduce-scatter by peer pulls (``TOA_ZERO_RS=sdma``;
+    the traffic was priced on one GPU first, ``TOA_EMULATE_RS=sdma``,
+    ``profiles/r5_overlap2/``).  Per bucket, in backward order:
+
+      every rank (compute stream):  bucket b's gradients are final ->
+                                    publish the epoch in its flag word
+      owner of shard r (copy stream): wait for every peer's epoch -> N-1
+                                    SDMA copies of the peers' slices of
+                                    shard r into a staging area -> event
+      owner (compute stream, before the update):  wait the event ->
+                                    shard r += the staged slices, summed in
+                                    fp32 and rounded once (``reduce``)
+
+    No reduction workgroup holds CUs while the backward runs; the sum is one
+    HBM-bound pass over 1/N of the bucket per peer.  A peer cannot overwrite
+    its bucket-b gradients (step t+1's backward) before the owner pulled
+    them: the owner publishes its updated shard of b only after this pull,
+    and the peer's next backward of b follows its forward's wait for that
+    shard (the weight all-gather, by RCCL or by pulls).
+
+    ``transport``: ShmTransport / GpuIpcTransport over the flat GRADIENT
+    buffer (its own flag words); ``ranges``: the buckets' flat [lo, hi)."""
+
+    def __init__(self, transport, ranges, rank: int, world: int):
+        self.t = transport
+        self.ranges = [tuple(r) for r in ranges]
+        self.rank, self.world = rank, world
+        self.epoch = 1
+        self.stage_off, off = [], 0
+        for lo, hi in self.ranges:
+            if (hi - lo) % world:
+                raise ValueError("bucket not divisible into world shards")
+            self.stage_off.append(off)
+            off += (world - 1) * ((hi - lo) // world)
+        buf = transport.buf
+        self.staging = torch.empty(max(off, 1), dtype=buf.dtype, device=buf.device)
+
+    def new_step(self):
+        """Every rank calls this once per optimizer step (same count on all),
+        after the step's last bucket was launched."""
+        self.epoch += 1
+
+    def shard(self, b):
+        lo, hi = self.ranges[b]
+        n = (hi - lo) // self.world
+        return lo + self.rank * n, lo + (self.rank + 1) * n
+
+    def pieces(self, b):
+        """The peers' slices of this rank's shard -> consecutive staging slots
+        (peers in rank order)."""
+        lo, hi = self.ranges[b]
+        n = (hi - lo) // self.world
+        s = lo + self.rank * n
+        peers = [r for r in range(self.world) if r != self.rank]
+        return [(r, s, s + n, self.stage_off[b] + k * n) for k, r in enumerate(peers)]
+
+    def launch_one(self, b):
+        """Bucket b's gradients are final on the current stream: publish
+        them and pull the peers' slices of this rank's shard.  Returns a
+        Work-like handle (the current stream waits the pulls)."""
+        self.t.publish(b, self.epoch)
+        return self.t.pull(b, self.epoch, self.pieces(b), dst=self.staging)
+
+    def reduce(self, b):
+        """Shard b += the staged slices (after the handle's wait)."""
+        s, e = self.shard(b)
+        n, k = e - s, self.world - 1
+        if n == 0 or k == 0:
+            return
+        buf = self.t.buf
+        st = self.staging[self.stage_off[b]:self.stage_off[b] + k * n]
+        if buf.is_cuda:
+            from ..ops import _lib
+
+            if buf.dtype != torch.bfloat16:
+                raise ValueError("the copy-engine reduce-scatter sums bf16 gradients")
+            _lib.call("toa_sum_slices_bf16", ctypes.c_void_p(buf.data_ptr() + 2 * s), _lib.ptr(st), k, n, n,
+                      _lib.stream(buf))
+            return
+        acc = buf[s:e].float()
+        for j in range(k):
+            acc += st[j * n:(j + 1) * n].float()
+        buf[s:e].copy_(acc.to(buf.dtype))
 
     def check(self):
         if hasattr(self.t, "check"):

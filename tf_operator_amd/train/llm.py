@@ -76,6 +76,7 @@ class LlamaTrainer:
         if self.bucketer.shard:  # ZeRO-1: reduce-scatter, owned-shard AdamW, in-place all-gather
             # fp32 master / m / v only for the owned shards: 12 B/param x (1 - 1/world) of HBM freed
             self.flat.shard_state(self.bucketer.owned)
+            self.bucketer.pull_rs = self._pull_reduce()
             self.opt = FlatAdamW(self.flat, lr=lr, owned=self.bucketer.owned)
             self.gather = ParamGather(self.flat, self.bucketer.buckets, self.bucketer.rank, self.bucketer.world,
                                       on_gathered=self.wt.refresh if self.wt else None, emulator=self.bucketer.emu,
@@ -191,6 +192,23 @@ class LlamaTrainer:
                                "(LOCAL_WORLD_SIZE == world: the operator's node-local layout)")
         t = pull_gather.GpuIpcTransport(self.flat.param, bk.rank, bk.world, len(bk.buckets), group=bk.group)
         return pull_gather.PullGather(t, [(b[0], b[1]) for b in bk.buckets], bk.rank, bk.world)
+
+    def _pull_reduce(self):
+        """TOA_ZERO_RS=sdma on a one-node GPU job: the gradient
+        reduce-scatter as copy-engine pulls plus an owner-side sum
+        (parallel/pull_gather.PullReduceScatter)."""
+        from ..parallel import pull_gather
+
+        bk = self.bucketer
+        if pull_gather.rs_mode_from_env() != "sdma" or bk.world < 2 or bk.emu is not None:
+            return None
+        if (self.flat.grad.device.type != "cuda" or self.flat.grad.dtype != torch.bfloat16
+                or int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != bk.world):
+            raise RuntimeError("TOA_ZERO_RS=sdma needs bf16 gradients on a GPU job whose ranks share one node "
+                               "(LOCAL_WORLD_SIZE == world: the operator's node-local layout)")
+        t = pull_gather.GpuIpcTransport(self.flat.grad, bk.rank, bk.world, len(bk.buckets), group=bk.group,
+                                        what="reduce-scatter")
+        return pull_gather.PullReduceScatter(t, [(b[0], b[1]) for b in bk.buckets], bk.rank, bk.world)
 
     def _emulated_fused_reduce(self, b):
         """TOA_EMULATE_RS=sdma (parallel/emulate.py): price the reduction an
