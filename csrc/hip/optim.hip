@@ -95,7 +95,7 @@ __device__ __forceinline__ void st_s(T* p, T v, bool nt) {
 }
 
 // The clipped gradient scale and (graph-replayable form) the bias
-// corrections, shared by the flat and the W^T-writing kernels.
+// corrections.
 __device__ __forceinline__ float adam_prologue(float b1, float b2, float grad_scale, const float* norm_sq,
                                                float max_norm, const int* step_dev, float& inv_bc1,
                                                float& inv_sqrt_bc2) {
@@ -113,8 +113,7 @@ __device__ __forceinline__ float adam_prologue(float b1, float b2, float grad_sc
   return scale;
 }
 
-// One parameter's update (both kernels run exactly this expression, so their
-// results are bit-identical).
+// One parameter's update.
 __device__ __forceinline__ void adam_elem(float g, float& p, float& m, float& v, float scale, float b1, float b2,
                                           float omb1, float omb2, float lr, float lrwd, float eps, float inv_bc1,
                                           float inv_sqrt_bc2) {
@@ -177,134 +176,16 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
   }
 }
 
-// AdamW over 2-D weights [R][C] that ALSO writes their transposed bf16 copies
-// wt[C][R] (ops/wt.py: the data-gradient GEMM's operand).  The separate
-// refresh re-read every bf16 weight after the update (transpose_bf16_kernel,
-// 6.1 ms per Llama-3-8B step); here the updated values are transposed in
-// registers and stored straight away: 28 -> 30 B per weight instead of
-// 28 + 4.  Geometry of the transpose kernel: one wave per 64 x 64 tile, lane
-// (rb, cb) = (lane >> 3, lane & 7) owns the 8 x 8 block at rows 8 rb..,
-// cols 8 cb..; a tile row is read by 8 lanes as 256 contiguous bytes (fp32
-// streams) or 128 (bf16).  Rows are processed four at a time (the loads of
-// four rows in flight, 112 VGPRs), and the packed bf16 rows are kept for the
-// final in-register transpose.  Same per-element expression as
-// adamw_flat_kernel (adam_elem): master / m / v / param bit-identical.
-// Up to 8 weights per launch (one decay run of a layer holds 4): a launch
-// per weight left a tail per weight (qkv / o ran at 4.8-5.0 TB/s).
-struct WtSegs {
-  int64_t off[8];    // flat element offset (param / grad)
-  int64_t soff[8];   // fp32 state offset (== off unless the state is sharded)
-  bf16_t* wt[8];     // W^T [C][R]
-  int R[8], C[8];
-  int64_t tile0[9];  // first 64 x 64 tile of each weight; tile0[n] = total
-  int n;
-};
-
-template <bool GRAD_BF16>
-__global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ master0, bf16_t* __restrict__ param0,
-                                                       void* __restrict__ grad0, int zero_grad, float* __restrict__ m0_,
-                                                       float* __restrict__ v0_, const WtSegs segs, float lr, float b1,
-                                                       float b2, float eps, float wd, float inv_bc1,
-                                                       float inv_sqrt_bc2, float grad_scale,
-                                                       const float* __restrict__ norm_sq, float max_norm,
-                                                       const int* __restrict__ step_dev) {
-  const float scale = adam_prologue(b1, b2, grad_scale, norm_sq, max_norm, step_dev, inv_bc1, inv_sqrt_bc2);
-  const float omb1 = 1.f - b1, omb2 = 1.f - b2, lrwd = lr * wd;
-  const int lane = threadIdx.x & 63;
-  const int rb = lane >> 3, cb = lane & 7;
-  const int64_t ntiles = segs.tile0[segs.n];
-  const int64_t wstride = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const size_t gsz = GRAD_BF16 ? 2 : 4;
-  for (int64_t tt = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tt < ntiles; tt += wstride) {
-    int sg = 0;  // wave-uniform
-    while (sg + 1 < segs.n && tt >= segs.tile0[sg + 1]) ++sg;
-    const int R = segs.R[sg], C = segs.C[sg];
-    const int tiles_c = C >> 6;
-    const int64_t t = tt - segs.tile0[sg];
-    float* master = master0 + segs.soff[sg];
-    float* m = m0_ + segs.soff[sg];
-    float* v = v0_ + segs.soff[sg];
-    bf16_t* param = param0 + segs.off[sg];
-    void* grad = (char*)grad0 + segs.off[sg] * gsz;
-    bf16_t* wt = segs.wt[sg];
-    const int tr = (int)(t / tiles_c), tc = (int)(t - (int64_t)tr * tiles_c);
-    const int r0 = tr * 64 + 8 * rb, c0 = tc * 64 + 8 * cb;
-    u32x4 pk[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      float g[4][8];
-      f32x4 p0[4], p1[4], m0[4], m1[4], v0[4], v1[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t e = (int64_t)(r0 + 4 * h + i) * C + c0;  // 8 contiguous elements
-        if (GRAD_BF16) {
-          unpack8(__builtin_nontemporal_load((const u32x4*)((const bf16_t*)grad + e)), g[i]);
-        } else {
-          const f32x4 a = __builtin_nontemporal_load((const f32x4*)((const float*)grad + e));
-          const f32x4 b = __builtin_nontemporal_load((const f32x4*)((const float*)grad + e) + 1);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { g[i][j] = a[j]; g[i][j + 4] = b[j]; }
-        }
-        p0[i] = __builtin_nontemporal_load((const f32x4*)(master + e));
-        p1[i] = __builtin_nontemporal_load((const f32x4*)(master + e) + 1);
-        m0[i] = __builtin_nontemporal_load((const f32x4*)(m + e));
-        m1[i] = __builtin_nontemporal_load((const f32x4*)(m + e) + 1);
-        v0[i] = __builtin_nontemporal_load((const f32x4*)(v + e));
-        v1[i] = __builtin_nontemporal_load((const f32x4*)(v + e) + 1);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t e = (int64_t)(r0 + 4 * h + i) * C + c0;
-        float p[8], mm[8], vv[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          p[j] = p0[i][j]; p[j + 4] = p1[i][j];
-          mm[j] = m0[i][j]; mm[j + 4] = m1[i][j];
-          vv[j] = v0[i][j]; vv[j + 4] = v1[i][j];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          adam_elem(g[i][j], p[j], mm[j], vv[j], scale, b1, b2, omb1, omb2, lr, lrwd, eps, inv_bc1, inv_sqrt_bc2);
-        f32x4 q0, q1, n0, n1, w0, w1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          q0[j] = p[j]; q1[j] = p[j + 4];
-          n0[j] = mm[j]; n1[j] = mm[j + 4];
-          w0[j] = vv[j]; w1[j] = vv[j + 4];
-        }
-        __builtin_nontemporal_store(q0, (f32x4*)(master + e));
-        __builtin_nontemporal_store(q1, (f32x4*)(master + e) + 1);
-        __builtin_nontemporal_store(n0, (f32x4*)(m + e));
-        __builtin_nontemporal_store(n1, (f32x4*)(m + e) + 1);
-        __builtin_nontemporal_store(w0, (f32x4*)(v + e));
-        __builtin_nontemporal_store(w1, (f32x4*)(v + e) + 1);
-        pk[4 * h + i] = pack8(p);
-        __builtin_nontemporal_store(pk[4 * h + i], (u32x4*)(param + e));
-        if (zero_grad) {
-          if (GRAD_BF16) {
-            st16((bf16_t*)grad + e, u32x4{0, 0, 0, 0});
-          } else {
-            *((f32x4*)((float*)grad + e)) = f32x4{0.f, 0.f, 0.f, 0.f};
-            *((f32x4*)((float*)grad + e) + 1) = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
-      }
-    }
-    u32x4 out[8];
-    tr8x8(pk, out);
-    bf16_t* d = wt + (int64_t)c0 * R + r0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) *(u32x4*)(d + (int64_t)j * R) = out[j];
-  }
-}
-
-// Variant switch for in-process A/B (scripts/stream_ab.py): bit 0 = the
-// non-temporal AdamW, bit 1 = the row-structured non-temporal SwiGLU,
-// bits 8.. = AdamW grid cap / 1024 (0: toa_stream_grid's 2048).  Default
-// from the A/B on MI355X (profiles/r2_stream_ab/): AdamW NT with a 16K-block
-// grid 5.43 -> 5.52 TB/s, SwiGLU rows+NT fwd 0.404 -> 0.373 ms and bwd
-// 0.723 -> 0.653 ms at T = 24576, F = 14336; all arms bit-identical.
-static int g_stream_variant = 1 | 2 | (16 << 8);
+// Variant switch for in-process A/B (scripts/stream_ab.py,
+// scripts/adamw_grid_bench.py): bit 0 = the non-temporal AdamW, bit 1 = the
+// row-structured non-temporal SwiGLU, bits 8.. = AdamW grid cap / 1024 (0:
+// toa_stream_grid's 2048).  Defaults from A/Bs on MI355X: AdamW NT
+// (profiles/r2_stream_ab/), SwiGLU rows+NT fwd 0.404 -> 0.373 ms and bwd
+// 0.723 -> 0.653 ms at T = 24576, F = 14336; and the AdamW grid at one
+// 8-element chunk per thread (cap 255K blocks, above any Llama-3-8B launch):
+// 1.247 -> 1.174 ms for one layer's 218M parameters against the round-2 16K
+// cap (profiles/r5_adamw/).  All arms bit-identical.
+static int g_stream_variant = 1 | 2 | (255 << 8);
 int toa_stream_variant() { return g_stream_variant; }
 extern "C" int toa_set_stream_variant(int v) {
   const int old = g_stream_variant;
@@ -354,47 +235,6 @@ extern "C" int toa_adamw_flat_dstep(float* master, bf16_t* param, void* grad, in
   if (step_dev == nullptr) return (int)hipErrorInvalidValue;
   return adamw_launch(master, param, grad, grad_flags, m, v, n, lr, beta1, beta2, eps, weight_decay, 1, grad_scale,
                       norm_sq, max_norm, step_dev, stream);
-}
-
-// AdamW of up to 8 2-D weights plus their transposed copies.  desc: n rows
-// of 4 int64 {flat offset, fp32 state offset, W^T address, R << 32 | C}
-// (host memory, passed by value in the kernel arguments); bases are the
-// flat master / param / grad / m / v buffers.  R, C multiples of 64;
-// every address 16-byte aligned.  step_dev as in toa_adamw_flat_dstep
-// (nullptr: the host step count `step`).
-extern "C" int toa_adamw_wt(float* master, bf16_t* param, void* grad, int grad_flags, float* m, float* v,
-                            const int64_t* desc, int n, float lr, float beta1, float beta2, float eps,
-                            float weight_decay, int step, const int* step_dev, float grad_scale, const float* norm_sq,
-                            float max_norm, hipStream_t stream) {
-  if (n <= 0 || n > 8 || desc == nullptr || param == nullptr) return (int)hipErrorInvalidValue;
-  WtSegs sg{};
-  sg.n = n;
-  int64_t tiles = 0;
-  const size_t gsz = (grad_flags & 1) ? 2 : 4;
-  for (int i = 0; i < n; ++i) {
-    const int64_t* d = desc + 4 * i;
-    sg.off[i] = d[0];
-    sg.soff[i] = d[1];
-    sg.wt[i] = (bf16_t*)(uintptr_t)d[2];
-    sg.R[i] = (int)(d[3] >> 32);
-    sg.C[i] = (int)(d[3] & 0xffffffff);
-    if (sg.R[i] <= 0 || sg.C[i] <= 0 || sg.R[i] % 64 || sg.C[i] % 64 || d[0] % 8 || d[1] % 8) return (int)hipErrorInvalidValue;
-    if (((uintptr_t)(master + d[1]) | (uintptr_t)(param + d[0]) | (uintptr_t)((char*)grad + d[0] * gsz) |
-         (uintptr_t)(m + d[1]) | (uintptr_t)(v + d[1]) | (uintptr_t)sg.wt[i]) & 15)
-      return (int)hipErrorInvalidValue;
-    sg.tile0[i] = tiles;
-    tiles += (int64_t)(sg.R[i] / 64) * (sg.C[i] / 64);
-  }
-  sg.tile0[n] = tiles;
-  const float bc1 = 1.f - powf(beta1, (float)step);
-  const float bc2 = 1.f - powf(beta2, (float)step);
-  const float inv_bc1 = 1.f / bc1, inv_sqrt_bc2 = 1.f / sqrtf(bc2);
-  const unsigned grid = (unsigned)std::min<int64_t>((tiles + 3) / 4, 16384);
-  const int zero_grad = (grad_flags >> 1) & 1;
-  auto k = (grad_flags & 1) ? adamw_wt_kernel<true> : adamw_wt_kernel<false>;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, sg, lr, beta1, beta2,
-                     eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq, max_norm, step_dev);
-  return (int)hipGetLastError();
 }
 
 __global__ void step_inc_kernel(int* step) { step[0] += 1; }

@@ -8,7 +8,7 @@ An arm is settings joined by '+': wgrad=asm|hip|asm_v1 (ops.gemm.set_wgrad_kerne
 gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy), attnf=N /
 attnb=N / attnd=N (toa_attn_set_fwd_variant / _bwd_variant / _dkdv_variant forms),
 epi=r4|pipe (the fused SwiGLU GEMMs' epilogues, toa_gemm_asm_set_epi_variant),
-adamwt=0|1 (TOA_ADAMW_WT: the AdamW writing the W^T copies itself, or the separate refresh),
+adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
 (this tree's defaults).  Same-process windows remove the box-to-box spread
@@ -18,7 +18,6 @@ weight-gradient schedule, the HIP attention forward and dK/dV) and head
 """
 import argparse
 import json
-import os
 import statistics
 import sys
 import time
@@ -49,8 +48,8 @@ def apply(arm: str):
             _lib.call("toa_attn_set_dkdv_variant", int(val))
         elif key == "epi":   # the fused SwiGLU GEMMs' epilogues: r4 (drained per row block) or pipe
             _lib.call("toa_gemm_asm_set_epi_variant", 1 if val == "r4" else 0)
-        elif key == "adamwt":  # read at every optimizer step (ops/wt.py fusable)
-            os.environ["TOA_ADAMW_WT"] = val
+        elif key == "adamcap":
+            _lib.call_ret("toa_set_stream_variant", 1 | 2 | (int(val) << 8))
         else:
             raise SystemExit(f"unknown arm {arm}")
 

@@ -1005,41 +1005,6 @@ def test_adamw_device_step_matches_host_step():
     assert float((out[0] - out[1]).abs().max()) < 1e-6
 
 
-@pytest.mark.parametrize("gdt,dstep,clip", [(torch.bfloat16, False, 1.0), (torch.float32, True, 0.0),
-                                             (torch.bfloat16, True, 0.5)])
-def test_adamw_wt_fused_bit_identical(monkeypatch, gdt, dstep, clip):
-    """The AdamW that also writes the W^T copies (toa_adamw_wt) against the
-    flat AdamW plus the separate transpose refresh: master, moments and bf16
-    weights bit-identical, every W^T equal to the updated weight's transpose;
-    a 64 x 96 weight (not fusable) and 1-D weights take the flat path."""
-    _lib()
-    from tf_operator_amd.ops.optim import FlatAdamW
-    from tf_operator_amd.ops.wt import TransposedWeights
-    from tf_operator_amd.parallel.flat import FlatParams
-
-    shapes = [(256, 512), (64,), (192, 128), (64, 96), (128,), (512, 64)]
-    out = []
-    for fuse in ("0", "1"):
-        monkeypatch.setenv("TOA_ADAMW_WT", fuse)
-        torch.manual_seed(7)
-        ps = [torch.nn.Parameter(torch.randn(*sh, device=DEV).to(torch.bfloat16)) for sh in shapes]
-        flat = FlatParams(ps, grad_dtype=gdt)
-        wt = TransposedWeights(flat, [p for p in ps if p.dim() == 2])
-        assert len(wt.fusable()) == (3 if fuse == "1" else 0)
-        opt = FlatAdamW(flat, lr=1e-2, weight_decay=0.1, max_grad_norm=clip, transposed=wt, device_step=dstep)
-        g = torch.Generator(device=DEV)
-        g.manual_seed(11)
-        for _ in range(3):
-            flat.grad.copy_(torch.randn(flat.grad.numel(), device=DEV, generator=g).to(gdt))
-            opt.step()
-        torch.cuda.synchronize()
-        for _, _, p, view in wt.items:
-            assert torch.equal(view, p.data.t()), f"stale W^T (fuse={fuse})"
-        out.append([t.clone() for t in (flat.master, flat.exp_avg, flat.exp_avg_sq, flat.param)])
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("N,K,T", [(100, 784, 100), (10, 100, 100), (64, 576, 64)])
 def test_wgrad_fp32_accumulate(N, K, T):
     """bf16 dY^T X accumulated straight into an fp32 master gradient (one

@@ -238,26 +238,3 @@ def test_first_step_asm_scope(monkeypatch):
     tr.step_idx = 1
     tr.step([])
     assert seen == [True, False]
-
-
-def test_adamw_split_covers_run_exactly():
-    """FlatAdamW._launch_split: the fusable weights inside a run go to the
-    W^T-writing kernel, the gaps to the flat kernel, and together they cover
-    the run exactly once; a weight straddling the run stays flat."""
-    from tf_operator_amd.ops.optim import FlatAdamW
-
-    calls = []
-    stub = type("S", (), {})()
-    stub._launch = lambda a, b, *args: calls.append(("flat", a, b))
-    stub._launch_wt = lambda items, *args: calls.append(("wt", [(it[0], it[1]) for it in items]))
-    fused = [(64, 64 + 4096, 64, 64, None), (8192, 8192 + 8192, 64, 128, None), (20000, 30000, 100, 100, None)]
-    done = set()
-    FlatAdamW._launch_split(stub, 0, 24576, True, 1e-3, 1.0, False, False, None, fused, done)
-    assert calls == [("flat", 0, 64), ("flat", 4160, 8192), ("wt", [(64, 4160), (8192, 16384)]),
-                     ("flat", 16384, 24576)]
-    assert done == {64, 8192}
-    # more than 8 weights in a run: batches of 8
-    calls.clear()
-    fused = [(4096 * i, 4096 * (i + 1), 64, 64, None) for i in range(10)]
-    FlatAdamW._launch_split(stub, 0, 40960, True, 1e-3, 1.0, False, False, None, fused, set())
-    assert [len(c[1]) for c in calls] == [8, 2] and all(c[0] == "wt" for c in calls)

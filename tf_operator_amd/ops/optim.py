@@ -68,13 +68,7 @@ class FlatAdamW:
 
     def __init__(self, flat, lr=3e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, max_grad_norm=1.0,
                  overlap=False, buckets=None, fuse_zero_grad=False, post_update=None, owned=None, group=None,
-                 device_step=False, transposed=None):
-        # transposed: ops.wt.TransposedWeights -- the unsharded serial step
-        # writes those W^T copies from its own kernel (toa_adamw_wt) and
-        # refreshes only the rest; post_update defaults to its refresh
-        self.transposed = transposed
-        if post_update is None and transposed is not None:
-            post_update = transposed.refresh
+                 device_step=False):
         self.post_update = post_update
         # device_step: the step count lives in device memory and is advanced
         # by a kernel, so a captured HIP graph of the whole training step
@@ -129,41 +123,6 @@ class FlatAdamW:
                   float(self.beta1), float(self.beta2), float(self.eps),
                   float(self.weight_decay if decay else 0.0), step, float(grad_scale),
                   _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), stream)
-
-    def _launch_wt(self, items, decay, lr, grad_scale, clip, zero, stream):
-        """AdamW of up to 8 2-D weights (flat offset, end, R, C, W^T view)
-        plus their W^T copies, one launch."""
-        f = self.flat
-        desc = (ctypes.c_int64 * (4 * len(items)))()
-        for i, (off, _, R, C, view) in enumerate(items):
-            desc[4 * i:4 * i + 4] = [off, f.state_index(off), view.data_ptr(), (R << 32) | C]
-        gflags = int(f.grad.dtype == torch.bfloat16) | (2 if zero else 0)
-        step, sdev = (1, _lib.ptr(self._dstep)) if self.device_step else (self.step_count, None)
-        _lib.call("toa_adamw_wt", f.master.data_ptr(), f.param.data_ptr(), f.grad.data_ptr(), gflags,
-                  f.exp_avg.data_ptr(), f.exp_avg_sq.data_ptr(), desc, len(items), float(lr), float(self.beta1),
-                  float(self.beta2), float(self.eps), float(self.weight_decay if decay else 0.0), step, sdev,
-                  float(grad_scale), _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), stream)
-
-    def _launch_split(self, a, b, decay, lr, grad_scale, clip, zero, stream, fused, done):
-        """Update run [a, b): the fusable weights inside it through
-        toa_adamw_wt (8 per launch; their offsets added to `done`), the gaps
-        flat."""
-        cur, batch = a, []
-        for item in fused:
-            off, end = item[0], item[1]
-            if off >= cur and end <= b:
-                if off > cur:
-                    self._launch(cur, off, decay, lr, grad_scale, clip, zero, stream)
-                batch.append(item)
-                if len(batch) == 8:
-                    self._launch_wt(batch, decay, lr, grad_scale, clip, zero, stream)
-                    batch = []
-                done.add(off)
-                cur = end
-        if batch:
-            self._launch_wt(batch, decay, lr, grad_scale, clip, zero, stream)
-        if cur < b:
-            self._launch(cur, b, decay, lr, grad_scale, clip, zero, stream)
 
     def _work_runs(self):
         """(a, b, decay) runs this rank updates."""
@@ -256,19 +215,13 @@ class FlatAdamW:
             pbf = f.param.dtype == torch.bfloat16
             if self.device_step:
                 _lib.call("toa_step_inc", _lib.ptr(self._dstep), s)
-            fused = (self.transposed.fusable() if self.transposed is not None and pbf and self.owned is None
-                     and self.post_update == self.transposed.refresh else [])
-            done = set()
             for (a, b, decay) in self._work_runs():
-                self._launch_split(a, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s, fused, done)
+                self._launch(a, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
             self.grads_zeroed = self.fuse_zero_grad and self.owned is None
             if not pbf:
                 f.param_from_master()
             if self.post_update is not None:
-                if done:
-                    self.post_update(0, f.numel, skip=done)
-                else:
-                    self.post_update(0, f.numel)
+                self.post_update(0, f.numel)
         else:
             for (a, b, decay) in self._work_runs():
                 adamw_reference(f.state_view(f.master, a, b), f.grad[a:b], f.state_view(f.exp_avg, a, b),

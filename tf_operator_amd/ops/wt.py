@@ -8,12 +8,10 @@ forward's ``x W^T`` form (profiles/r1_gemm_tuning_coldcache.log).  Keeping
 ``dX = dY (W^T)^T``.
 
 The copies live in ONE flat bf16 buffer (15 GB at Llama-3-8B: 288 GB of
-HBM leaves room for it).  The unsharded optimizer step writes them itself
-(``toa_adamw_wt``, csrc/hip/optim.hip: the updated bf16 values transposed in
-registers, 2 B per weight instead of the refresh's 4); otherwise -- the
-overlapped per-bucket update, the ZeRO-1 all-gather, a checkpoint load --
-they are refreshed after the weights change by the HBM-bound
-``toa_transpose_bf16`` kernel (csrc/hip/transpose.hip, ~6 ms per step at 8B).  ``param._toa_wt`` is the [in, out] view that
+HBM leaves room for it) and are refreshed right after the optimizer writes
+the bf16 weights -- per gradient bucket, on the optimizer's stream -- by the
+HBM-bound ``toa_transpose_bf16`` kernel (csrc/hip/transpose.hip, ~7 ms per
+step at 8B).  ``param._toa_wt`` is the [in, out] view that
 :func:`tf_operator_amd.ops.gemm.linear_dgrad` picks up.
 
 Anything that rewrites the weights outside the optimizer (checkpoint load,
@@ -75,29 +73,13 @@ class TransposedWeights:
         return self.buf.numel() * self.buf.element_size()
 
     @torch.no_grad()
-    def refresh(self, lo: int = 0, hi: int | None = None, skip=()):
+    def refresh(self, lo: int = 0, hi: int | None = None):
         """Re-transpose every weight overlapping flat range [lo, hi) on the
-        current stream, except the flat offsets in `skip` (weights whose
-        copy the optimizer's fused kernel already wrote, ops/optim.py)."""
+        current stream."""
         hi = self.flat.numel if hi is None else hi
         for a, b, p, view in self.items:
-            if a < hi and b > lo and a not in skip:
+            if a < hi and b > lo:
                 transpose_into(view, p.data)
-
-    def fusable(self):
-        """(flat offset, end, rows, cols, W^T view) of the weights whose
-        AdamW can write the transposed copy itself (``toa_adamw_wt``: rows and
-        columns multiples of 64, 16-byte aligned; TOA_ADAMW_WT=0 turns the
-        fusion off)."""
-        if os.environ.get("TOA_ADAMW_WT", "1") == "0":
-            return []
-        out = []
-        for a, b, p, view in self.items:
-            R, C = p.shape
-            if (view.is_cuda and p.dtype == torch.bfloat16 and R % 64 == 0 and C % 64 == 0 and a % 8 == 0
-                    and view.data_ptr() % 16 == 0):
-                out.append((a, b, R, C, view))
-        return out
 
     def detach(self):
         for _, _, p, _ in self.items:

@@ -86,7 +86,7 @@ class LlamaTrainer:
                 overlap_optimizer = os.environ.get("TOA_OPT_OVERLAP", "0") == "1"
             self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
                                  fuse_zero_grad=not self.fresh_grads,
-                                 transposed=self.wt)
+                                 post_update=self.wt.refresh if self.wt else None)
         if self.opt.overlap or self.gather is not None:
             self._hooks = self._install_param_waits()
         self.step_idx = 0
