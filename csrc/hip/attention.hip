@@ -1064,10 +1064,21 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
                                                          float* __restrict__ NLSE2, int rows, int H, int S,
                                                          int o_bshd) {
   constexpr int LPR = D / 8;  // lanes per row, 16 B each
-  const int row = blockIdx.x * (256 / LPR) + (int)threadIdx.x / LPR;
+  const int lin = blockIdx.x * (256 / LPR) + (int)threadIdx.x / LPR;
   const int c = threadIdx.x % LPR;
-  if (row >= rows) return;  // whole LPR-lane groups leave together
-  const int s = row % S, bh = row / S;
+  if (lin >= rows) return;  // whole LPR-lane groups leave together
+  // O / dO in [B, S, H, D]: walk the rows in (b, s, h) order, so a wave's
+  // loads are contiguous (in (b, h, s) order they sit H * D apart)
+  int s, bh;
+  if (o_bshd) {
+    const int h = lin % H, bs = lin / H;
+    s = bs % S;
+    bh = (bs / S) * H + h;
+  } else {
+    s = lin % S;
+    bh = lin / S;
+  }
+  const int row = bh * S + s;
   const int64_t off = o_off<D>(bh / H, bh % H, s, H, S, o_bshd) + c * 8;
   float a[8], g[8];
   unpack8(ld16(O + off), a);
