@@ -138,7 +138,9 @@ extern "C" int toa_rope_fwd(const bf16_t* qkv, const float* cosv, const float* s
                             int B, int S, int Hq, int Hkv, int D, int rep, hipStream_t stream) {
   if (D % 16 != 0 || Hq % Hkv != 0) return (int)hipErrorInvalidValue;
   int64_t units = (int64_t)B * S * (Hq + 2 * Hkv) * (D / 16);
-  hipLaunchKernelGGL(rope_fwd_kernel, dim3(toa_stream_grid(units, 256)), dim3(256), 0, stream, qkv, cosv, sinv, q, k,
+  // one unit per thread (a 2048-block cap left each thread 18 units at the bench shape)
+  const unsigned grid = (unsigned)std::max<int64_t>((units + 255) / 256, 1);
+  hipLaunchKernelGGL(rope_fwd_kernel, dim3(grid), dim3(256), 0, stream, qkv, cosv, sinv, q, k,
                      v, B, S, Hq, Hkv, D, rep);
   return (int)hipGetLastError();
 }

@@ -14,11 +14,14 @@ import torch
 from . import _lib
 
 
+SUMSQ_WS = 32768  # floats of toa_sumsq's partials workspace (its grid cap)
+
+
 def grad_norm_sq(flat_grad: torch.Tensor, workspace=None, out=None):
     """Squared L2 norm of a flat gradient (fp32 0-d device tensor)."""
     out = torch.zeros(1, device=flat_grad.device, dtype=torch.float32) if out is None else out
     if _lib.use_hip(flat_grad):
-        ws = torch.empty(2048, device=flat_grad.device, dtype=torch.float32) if workspace is None else workspace
+        ws = torch.empty(SUMSQ_WS, device=flat_grad.device, dtype=torch.float32) if workspace is None else workspace
         _lib.call("toa_sumsq", _lib.ptr(flat_grad), flat_grad.numel(), int(flat_grad.dtype == torch.bfloat16),
                   _lib.ptr(ws), _lib.ptr(out), 0, _lib.stream(flat_grad))
     else:
@@ -93,7 +96,7 @@ class FlatAdamW:
         # without weight decay the decay split is moot: one launch over the whole buffer
         self.runs = flat.decay_runs() if weight_decay else [[0, flat.numel, False]]
         self._norm = torch.zeros(1, device=flat.device, dtype=torch.float32)
-        self._ws = torch.empty(2048, device=flat.device, dtype=torch.float32)
+        self._ws = torch.empty(SUMSQ_WS, device=flat.device, dtype=torch.float32)
         self.last_norm_sq = self._norm
         self.overlap = bool(overlap) and flat.device.type == "cuda" and _lib.available()
         # zero each gradient slice as the update reads it (the caller then skips zero_grad)
