@@ -225,11 +225,13 @@ class GradBucketer:
 
     def verify(self):
         """Synchronous health check of the collectives behind the CURRENT
-        weights (the one-shot kernel's peer-timeout word; ``finish()`` polls
-        it one step late).  Checkpoint paths call this before staging
+        weights (the one-shot kernel's and the copy-engine reduce-scatter's
+        peer-timeout words; ``finish()`` polls them one step late).  Checkpoint paths call this before staging
         anything, so an update built from stale peer slots is never saved."""
         if self.ipc is not None:
             self.ipc.check()
+        if self.pull_rs is not None:
+            self.pull_rs.check()
 
     @property
     def grad_scale(self):

@@ -260,7 +260,9 @@ def trainer_state(tr: LlamaTrainer, data=None):
     tr.opt.wait_all()
     if tr.gather is not None:
         tr.gather.wait_all()
-    tr.bucketer.verify()  # never persist an update built from a failed one-shot all-reduce
+    tr.bucketer.verify()  # never persist an update built from a failed one-shot all-reduce / pulled reduce-scatter
+    if tr.gather is not None and tr.gather.pull is not None:
+        tr.gather.pull.check()  # ... or from weights a copy-engine all-gather never completed
     return {"flat": tr.flat.state_dict(), "opt": tr.opt.state_dict(), "step": tr.step_idx,
             "rank": tr.bucketer.rank, "world": tr.bucketer.world, "rng": rng_state(tr.device),
             "data": data.state_dict() if data is not None else None}
