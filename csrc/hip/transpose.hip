@@ -12,7 +12,8 @@
 // of one rb read 128 contiguous bytes of a row), transposes the block in
 // registers (v_perm byte selects), and stores 8 rows of 16 B of dst (the 8
 // lanes of one cb write 128 contiguous bytes).  All 8 loads are issued
-// before the first store.
+// before the first store; loads and stores non-temporal (W^T is read next
+// in the backward, long after any cache would have kept it).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16_t* __res
     tr8x8(in, out);
     bf16_t* d = dst + (int64_t)c0 * ldd + r0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) *(u32x4*)(d + j * ldd) = out[j];
+    for (int j = 0; j < 8; ++j) __builtin_nontemporal_store(out[j], (u32x4*)(d + j * ldd));
   }
 }
 
