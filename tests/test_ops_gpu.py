@@ -979,6 +979,43 @@ def test_dp_trainer_hip_graph_matches_eager():
     assert float((m0 - m1).abs().max()) <= 1e-4 * float(m0.abs().max()) + 1e-6
 
 
+@pytest.mark.parametrize("n", [1000, 8 * 256 * 2048 + 24, 40_000_000])
+def test_grad_norm_sq_matches_fp64(n):
+    """toa_sumsq at one 8-element chunk per thread (up to 32768 partials,
+    then a grid-stride loop) against an fp64 sum of squares; bf16 and fp32,
+    with a tail that is not a multiple of 8."""
+    _lib()
+    from tf_operator_amd.ops.optim import grad_norm_sq
+
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    x = torch.randn(n, device=DEV, generator=g)
+    for t in (x.to(torch.bfloat16), x):
+        ref = float(t.double().pow(2).sum())
+        got = float(grad_norm_sq(t))
+        assert abs(got - ref) <= 1e-5 * ref, (t.dtype, got, ref)
+
+
+def test_sum_slices_bf16_matches_fp32():
+    """The copy-engine reduce-scatter's owner-side sum (toa_sum_slices_bf16):
+    dst + slices summed in fp32 in order and rounded once, bit for bit."""
+    _lib()
+    from tf_operator_amd.ops import _lib as L
+
+    n, k = 3 * 1024 * 1024 + 8, 7
+    g = torch.Generator(device=DEV)
+    g.manual_seed(9)
+    dst = torch.randn(n, device=DEV, generator=g).to(torch.bfloat16)
+    src = torch.randn(k * n, device=DEV, generator=g).to(torch.bfloat16)
+    acc = dst.float()
+    for j in range(k):
+        acc += src[j * n:(j + 1) * n].float()
+    want = acc.to(torch.bfloat16)
+    L.call("toa_sum_slices_bf16", L.ptr(dst), L.ptr(src), k, n, n, L.stream(dst))
+    torch.cuda.synchronize()
+    assert torch.equal(dst.view(torch.int16), want.view(torch.int16))
+
+
 def test_adamw_device_step_matches_host_step():
     _lib()
     from tf_operator_amd.ops import _lib as L
