@@ -447,7 +447,7 @@ SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
          "align": True, "drain_end": False, "map": "lib0", "persist": False, "dual": "", "zero_late": True,
          "nostore": False, "store_nt": True, "store_same": False, "epi_pipe": True,
-         "epi_pk": True}
+         "epi_pk": True, "epi_f32s": True}
 
 
 def _stamp(k: int) -> str:
@@ -855,13 +855,21 @@ def epilogue_swiglu_fwd(a: Asm):
         for p in range(2):
             store16(a, pg + 4 * p, V_E, SRD_C, S_E0, p)
             store16(a, pu + 4 * p, V_E + 2, SRD_C, S_E0, p)
-        # s = silu(g) * u on the bf16-rounded values (what backward re-reads)
-        gf, uf, sv, ps, t = V_E + 56, V_E + 72, V_E + 88, V_E + 104, V_E + 8   # t: g/u regs, consumed
-        for p in range(2):
-            unpack8(a, gf + 8 * p, pg + 4 * p)
-            unpack8(a, uf + 8 * p, pu + 4 * p)
-        for h in range(2):                  # 8 elements at a time (scratch t: 8 regs)
-            silu_times(a, sv + 8 * h, gf + 8 * h, uf + 8 * h, t, 8)
+        sv, ps = V_E + 88, V_E + 104
+        if SCHED["epi_f32s"]:
+            # s = silu(g) * u straight from the fp32 accumulators (no bf16 round
+            # trip: 32 VALU per row block fewer; the unfused path and round 4
+            # used the stored bf16 values, a difference below bf16 rounding)
+            for h in range(2):              # scratch: the free V_E + 56 .. 63
+                silu_times(a, sv + 8 * h, g + 8 * h, u + 8 * h, V_E + 56, 8)
+        else:
+            # s = silu(g) * u on the bf16-rounded values (what backward re-reads)
+            gf, uf, t = V_E + 56, V_E + 72, V_E + 8   # t: g/u regs, consumed
+            for p in range(2):
+                unpack8(a, gf + 8 * p, pg + 4 * p)
+                unpack8(a, uf + 8 * p, pu + 4 * p)
+            for h in range(2):              # 8 elements at a time (scratch t: 8 regs)
+                silu_times(a, sv + 8 * h, gf + 8 * h, uf + 8 * h, t, 8)
         for p in range(2):
             cvt_pack8(a, ps + 4 * p, sv + 8 * p)
         for p in range(2):
@@ -1432,7 +1440,8 @@ def generate() -> str:
         parts.append(body)
         metas.append(meta)
     for epi in ("swiglu_fwd", "swiglu_bwd"):   # round-4 epilogues (per-round drains): in-model A/B arms
-        body, meta = _with_knobs({"epi_pipe": False, "epi_pk": False}, lambda: kernel(epi, variant="r4"))
+        body, meta = _with_knobs({"epi_pipe": False, "epi_pk": False, "epi_f32s": False},
+                                 lambda: kernel(epi, variant="r4"))
         parts.append(body)
         metas.append(meta)
     for vname, knobs in PLAIN_VARIANTS:
