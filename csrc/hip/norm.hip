@@ -312,6 +312,16 @@ static inline int pick_ch(int cols) {
 // one row per wave (norm_fwd_kernel / norm_bwd_kernel, every other shape).
 // toa_norm_set_row pins a form for in-process tests (-1 = the default).
 static int g_norm_row = 1;
+// Forward row kernel's grid cap in workgroups (toa_norm_set_fwd_cap for A/B).
+// One row per workgroup, no cap: 0.1488 -> 0.1381 ms at 24576 x 4096 against
+// the old 2048-workgroup grid-stride (scripts/rms_fwd_grid_ab.py,
+// profiles/r5_grid/rms_fwd.log); outputs identical.
+static const int kNormFwdCapDefault = 1 << 30;
+static int g_norm_fwd_cap = kNormFwdCapDefault;
+extern "C" int toa_norm_set_fwd_cap(int c) {
+  g_norm_fwd_cap = c > 0 ? c : kNormFwdCapDefault;
+  return 0;
+}
 static int norm_row_form() { return g_norm_row; }
 extern "C" int toa_norm_set_row(int v) {
   g_norm_row = v < 0 ? 1 : (v ? 1 : 0);
@@ -378,7 +388,7 @@ static int norm_fwd_launch(const void* x, const void* res, void* h_out, const vo
   if (cols % 8 != 0) return (int)hipErrorInvalidValue;
   int chv = pick_ch(cols);
   if (RMS && sizeof(T) == 2 && cols % 2048 == 0 && cols <= 8192 && norm_row_form()) {
-    const int nb = rows < 256 * 8 ? rows : 256 * 8;  // 8 workgroups per CU, grid-stride over rows
+    const int nb = rows < g_norm_fwd_cap ? rows : g_norm_fwd_cap;  // grid-stride over rows beyond the cap
     const bf16_t *x16 = (const bf16_t*)x, *r16 = (const bf16_t*)res, *w16 = (const bf16_t*)w;
     bf16_t *h16 = (bf16_t*)h_out, *y16 = (bf16_t*)y;
     switch (cols / 2048) {
