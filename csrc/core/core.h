@@ -122,7 +122,11 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
 extern const char* kAnnNodeLocal;      // amd.com/node-local: "true" | "false" (default: auto)
 extern const char* kAnnGpuVisibility;  // amd.com/gpu-visibility=node on node-local pods
 extern const char* kLabelNodeLocal;    // training.amd.com/node-local
-int64_t rank_world(const Json& job);   // Chief+Master+Worker (TFJob) / Master+Worker (PyTorchJob)
+// a TFJob PS replica that requests a GPU is an RCCL rank (rank W + p, after
+// Chief+Master+Worker): the parameter server on the GPU, parallel/ps_collective.py
+bool gpu_ps(const Json& job, const Options& opt);
+// Chief+Master+Worker (+ GPU PS) for a TFJob / Master+Worker for a PyTorchJob
+int64_t rank_world(const Json& job, const Options& opt);
 bool node_local(const Json& job, const Options& opt);
 void apply_node_local(const Json& job, const std::string& rtype, Json& pod_template, const Options& opt);
 // apply gen_env to a pod template (in place)

@@ -6,8 +6,10 @@
 //   `tensorflow` container and only for distributed jobs (pod.go:261-319);
 //   PLUS the ROCm/RCCL block consumed by the PyTorch-ROCm trainer:
 //   MASTER_ADDR/MASTER_PORT (rank-0 = Chief, else Master, else Worker-0),
-//   WORLD_SIZE (= Chief+Master+Worker; PS/Evaluator are outside the RCCL
-//   world), RANK, LOCAL_RANK/LOCAL_WORLD_SIZE (one GPU per pod; in the
+//   WORLD_SIZE (= Chief+Master+Worker, plus the PS replicas when they request
+//   a GPU -- nodelocal.cc gpu_ps -- as ranks W..W+P-1; a CPU PS and the
+//   Evaluator stay outside the RCCL world), RANK, LOCAL_RANK/LOCAL_WORLD_SIZE
+//   (one GPU per pod; in the
 //   node-local layout -- nodelocal.cc -- the rank's index on the one node
 //   and the node's rank count),
 //   TOA_ROLE / TOA_PS_HOSTS for parameter-server mode, NCCL_* knobs.
@@ -173,9 +175,11 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
     if (!opt.inject_rocm_env) return out;
     // --- ROCm / RCCL rendezvous block ---
     int64_t n_chief = spec_replicas(job, "Chief"), n_master = spec_replicas(job, "Master");
-    int64_t n_worker = spec_replicas(job, "Worker");
+    int64_t n_worker = spec_replicas(job, "Worker"), n_ps = spec_replicas(job, "PS");
     std::string r0 = n_chief > 0 ? "Chief" : (n_master > 0 ? "Master" : "Worker");
-    int64_t world = n_chief + n_master + n_worker;
+    const int64_t trainers = n_chief + n_master + n_worker;
+    const bool ps_ranks = gpu_ps(job, opt);
+    int64_t world = trainers + (ps_ranks ? n_ps : 0);
     std::string role = rt;
     rocm_block(job, rtype, index, opt, c, out);
     if (world > 0) {
@@ -189,6 +193,7 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
     if (rtype == "Chief") rank = index;
     else if (rtype == "Master") rank = n_chief + index;
     else if (rtype == "Worker") rank = n_chief + n_master + index;
+    else if (rtype == "PS" && ps_ranks) rank = trainers + index;
     if (rank >= 0) {
       const bool nl = node_local(job, opt);
       add_env(out, c, "RANK", std::to_string(rank));
@@ -200,8 +205,10 @@ Json gen_env(const Json& job, const std::string& rtype, int index, const Options
       }
     }
     add_env(out, c, "TOA_ROLE", role);
-    int64_t n_ps = spec_replicas(job, "PS");
     if (n_ps > 0) {
+      // the trainer checks the world against these (ps_collective.ps_world_env)
+      add_env(out, c, "TOA_PS_IN_WORLD", ps_ranks ? "1" : "0");
+      add_env(out, c, "TOA_NUM_TRAINERS", std::to_string(trainers));
       std::string hosts;
       int port = port_from_job(job, "PS");
       for (int64_t i = 0; i < n_ps; ++i) {

@@ -88,17 +88,35 @@ const char* kAnnGpuVisibility = "amd.com/gpu-visibility";
 const char* kLabelNodeLocal = "training.amd.com/node-local";
 const char* kPodResourcesDir = "/var/lib/kubelet/pod-resources";
 
-static bool is_rank_type(const std::string& kind, const std::string& rtype) {
-  if (kind == "TFJob") return rtype == "Chief" || rtype == "Master" || rtype == "Worker";
+// Parameter servers on the GPU.  The reference makes the PS a first-class
+// member of the cluster spec (pkg/controller.v1/tensorflow/tensorflow.go:142-173)
+// whose variables every worker pushes to and pulls from each step
+// (examples/v1/dist-mnist/dist_mnist.py:149-165).  Here a PS replica that
+// requests a GPU runs in the SAME RCCL world as the trainers
+// (parallel/ps_collective.py: reduce onto the PS during backward, broadcast of
+// its shard back), so the operator -- not the payload -- owns that world:
+// WORLD_SIZE counts it, its RANK is W + p, and in the node-local layout it is
+// co-located and gets the same privileged / hostPID / NCCL_HOSTID treatment,
+// so its pushes and pulls take xGMI instead of the socket transport.  A CPU
+// PS (no GPU request) stays outside, as before.
+bool gpu_ps(const Json& job, const Options& opt) {
+  if (job_kind(job) != "TFJob") return false;
+  const Json* s = replica_specs(job).find("PS");
+  return s && !s->is_null() && replicas_of(*s) > 0 && pod_resource_request(*s, opt.gpu_resource) > 0.0;
+}
+
+static bool is_rank_type(const Json& job, const std::string& kind, const std::string& rtype, const Options& opt) {
+  if (kind == "TFJob")
+    return rtype == "Chief" || rtype == "Master" || rtype == "Worker" || (rtype == "PS" && gpu_ps(job, opt));
   if (kind == "PyTorchJob") return rtype == "Master" || rtype == "Worker";
   return false;
 }
 
-int64_t rank_world(const Json& job) {
+int64_t rank_world(const Json& job, const Options& opt) {
   const std::string kind = job_kind(job);
   int64_t world = 0;
   for (const auto& kv : replica_specs(job).fields())
-    if (is_rank_type(kind, kv.first) && !kv.second.is_null()) world += replicas_of(kv.second);
+    if (is_rank_type(job, kind, kv.first, opt) && !kv.second.is_null()) world += replicas_of(kv.second);
   return world;
 }
 
@@ -107,10 +125,10 @@ bool node_local(const Json& job, const Options& opt) {
   if (kind != "TFJob" && kind != "PyTorchJob") return false;
   const std::string mode = lower(job.path({"metadata", "annotations"}).get(kAnnNodeLocal).str());
   if (mode != "privileged" && mode != "true") return false;
-  const int64_t world = rank_world(job);
+  const int64_t world = rank_world(job, opt);
   if (world < 2 || world > opt.gpus_per_node) return false;
   for (const auto& kv : replica_specs(job).fields()) {
-    if (!is_rank_type(kind, kv.first) || kv.second.is_null()) continue;
+    if (!is_rank_type(job, kind, kv.first, opt) || kv.second.is_null()) continue;
     if (pod_resource_request(kv.second, opt.gpu_resource) != 1.0) return false;
   }
   return true;
@@ -127,7 +145,7 @@ static Json host_path_volume(const std::string& name, const std::string& path) {
 
 void apply_node_local(const Json& job, const std::string& rtype, Json& tpl, const Options& opt) {
   const std::string kind = job_kind(job);
-  if (!is_rank_type(kind, rtype) || !node_local(job, opt)) return;
+  if (!is_rank_type(job, kind, rtype, opt) || !node_local(job, opt)) return;
   const std::string name = job.get("metadata").get("name").str();
   const KindInfo& ki = kind_info(kind);
   Json& tmd = tpl["metadata"];

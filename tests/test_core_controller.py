@@ -5,6 +5,7 @@ pure C++ reconcile engine observed pods/services and assert on the returned
 actions and status.
 """
 import json
+import os
 
 import pytest
 
@@ -572,6 +573,77 @@ def test_node_local_pod_spec_and_env():
     assert "securityContext" not in ps["spec"]["containers"][0]
     assert "NCCL_HOSTID" not in {e["name"] for e in ps["spec"]["containers"][0]["env"]}
     assert "LOCAL_RANK" not in {e["name"] for e in ps["spec"]["containers"][0]["env"]}
+
+
+def _gpu_ps_job(workers=2, ps=1, annotation=None):
+    job = _gpu_job(workers, ps=ps, annotation=annotation)
+    job["spec"]["tfReplicaSpecs"]["PS"]["template"]["spec"]["containers"][0]["resources"] = {
+        "limits": {"amd.com/gpu": 1}}
+    return job
+
+
+def test_gpu_ps_is_in_the_rccl_world():
+    """BASELINE config #2 (PS=1 Worker=2, one MI355X each): a PS replica that
+    requests a GPU is an RCCL rank the operator owns -- WORLD_SIZE counts it
+    and PS p is rank W + p (reference: the PS is a first-class member of the
+    cluster spec, tensorflow.go:142-173).  A CPU PS stays outside."""
+    job = _gpu_ps_job(2, ps=2)
+    envs = {(rt, i): {e["name"]: e["value"] for e in core.gen_env(job, rt, i)}
+            for rt, i in (("Worker", 0), ("Worker", 1), ("PS", 0), ("PS", 1))}
+    assert {e["WORLD_SIZE"] for e in envs.values()} == {"4"}
+    assert [envs[k]["RANK"] for k in sorted(envs)] == ["2", "3", "0", "1"]  # PS 0/1, Worker 0/1
+    assert {e["TOA_PS_IN_WORLD"] for e in envs.values()} == {"1"}
+    assert {e["TOA_NUM_TRAINERS"] for e in envs.values()} == {"2"}
+    assert {e["MASTER_ADDR"] for e in envs.values()} == {"test-tfjob-worker-0.default.svc"}
+    cpu = _gpu_job(2, ps=1)  # PS without a GPU request
+    w = {e["name"]: e["value"] for e in core.gen_env(cpu, "Worker", 1)}
+    p = {e["name"]: e["value"] for e in core.gen_env(cpu, "PS", 0)}
+    assert w["WORLD_SIZE"] == "2" and w["TOA_PS_IN_WORLD"] == "0" and "RANK" not in p
+
+
+def test_gpu_ps_node_local_layout():
+    """PS=1 Worker=2 GPU TFJob with amd.com/node-local: all three pods are
+    co-located rank pods with identical WORLD_SIZE / LOCAL_WORLD_SIZE, the same
+    affinity term, privileged + hostIPC + hostPID and NCCL_HOSTID from the
+    node's name, so the PS's pushes and pulls take xGMI, not the socket
+    transport; and the trainer's join_ps_world accepts that env as is."""
+    from tf_operator_amd.parallel import ps_collective
+
+    job = _gpu_ps_job(2, ps=1, annotation="privileged")
+    assert core.node_local(job, {})
+    pods = {p["pod"]["metadata"]["name"]: p["pod"] for p in ops(run(job), "create_pod")}
+    assert sorted(pods) == ["test-tfjob-ps-0", "test-tfjob-worker-0", "test-tfjob-worker-1"]
+    terms, ranks = [], {}
+    for name, pod in pods.items():
+        spec, c = pod["spec"], pod["spec"]["containers"][0]
+        env = {e["name"]: e.get("value") for e in c["env"]}
+        downward = {e["name"]: e["valueFrom"]["fieldRef"]["fieldPath"] for e in c["env"] if "valueFrom" in e}
+        assert spec["hostIPC"] is True and spec["hostPID"] is True, name
+        assert c["securityContext"]["privileged"] is True, name
+        assert downward["NCCL_HOSTID"] == "spec.nodeName", name
+        assert env["WORLD_SIZE"] == "3" and env["LOCAL_WORLD_SIZE"] == "3", name
+        assert env["LOCAL_RANK"] == env["RANK"] and env["TOA_NODE_LOCAL"] == "1", name
+        terms.append(spec["affinity"]["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"])
+        ranks[name] = int(env["RANK"])
+        assert pod["metadata"]["labels"]["training.amd.com/node-local"] == "true"
+        # the trainer's check passes on exactly this env, and fails on a tampered one
+        saved = dict(os.environ)
+        try:
+            os.environ.update({k: v for k, v in env.items() if v is not None})
+            w, s_, role, idx = ps_collective.ps_world_env()
+            assert (w, s_) == (2, 1)
+            ps_collective.join_ps_world(w, s_, role, idx)
+            os.environ["WORLD_SIZE"] = "2"
+            with pytest.raises(RuntimeError, match="inconsistent"):
+                ps_collective.join_ps_world(w, s_, role, idx)
+        finally:
+            os.environ.clear()
+            os.environ.update(saved)
+    assert all(t == terms[0] for t in terms)
+    assert ranks == {"test-tfjob-worker-0": 0, "test-tfjob-worker-1": 1, "test-tfjob-ps-0": 2}
+    # 8 GPU ranks fit one node; 7 workers + 2 GPU servers do not
+    assert core.node_local(_gpu_ps_job(7, ps=1, annotation="privileged"), {})
+    assert not core.node_local(_gpu_ps_job(7, ps=2, annotation="privileged"), {})
 
 
 def test_node_local_keeps_user_security_context_and_env():

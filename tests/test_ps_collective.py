@@ -141,8 +141,12 @@ def test_async_ps_applies_every_push(tmp_path):
     assert any(torch.equal(res[w]["param"], ps["param"]) for w in range(workers))
 
 
-@pytest.mark.parametrize("mode", ["sync", "async"])
-def test_tfjob_ps1_worker2_resnet_e2e(mode):
+@pytest.mark.parametrize("mode,gpu_ps", [("sync", False), ("async", False), ("sync", True)])
+def test_tfjob_ps1_worker2_resnet_e2e(mode, gpu_ps):
+    """PS=1 Worker=2 through the operator and the local kubelet.  gpu_ps: every
+    replica requests one amd.com/gpu (BASELINE config #2), so the operator puts
+    the PS into the world itself (WORLD_SIZE 3, PS rank 2) and the payload only
+    checks it; otherwise the CPU PS joins the trainers' gloo world."""
     from tf_operator_amd.sdk import container, pod_template
     from tf_operator_amd.testing.cluster import LocalCluster
 
@@ -150,12 +154,13 @@ def test_tfjob_ps1_worker2_resnet_e2e(mode):
            "--batch", "4", "--classes", "10", "--steps", "3", "--warmup", "1", "--ps-mode", mode]
     env = {"OMP_NUM_THREADS": "1", "TOA_NO_GPU": "1", "CUDA_VISIBLE_DEVICES": ""}
     spec = {rt: {"replicas": n, "restartPolicy": "Never",
-                 "template": pod_template(container(image="toa/trainer", command=cmd, env=env))}
+                 "template": pod_template(container(image="toa/trainer", command=cmd, env=env,
+                                                    gpus=1 if gpu_ps else 0))}
             for rt, n in (("PS", 1), ("Worker", 2))}
-    name = f"rn-ps-{mode}"
+    name = f"rn-ps-{mode}" + ("-gpu" if gpu_ps else "")
     job = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob", "metadata": {"name": name, "namespace": "default"},
            "spec": {"runPolicy": {"cleanPodPolicy": "None"}, "tfReplicaSpecs": spec}}
-    with LocalCluster(gpus=0) as c:
+    with LocalCluster(gpus=3 if gpu_ps else 0) as c:
         c.client.create(job)
         done = c.client.wait_for_job(name, polling_interval=0.2, timeout_seconds=240)
         conds = [x["type"] for x in done["status"]["conditions"]]
@@ -165,3 +170,5 @@ def test_tfjob_ps1_worker2_resnet_e2e(mode):
         # the PS applied the optimizer: sync = one update per step, async = one per push
         want = 4 if mode == "sync" else 8
         assert f"ps 0: {want} {mode} updates" in logs[f"{name}-ps-0"], logs
+        owner = "operator" if gpu_ps else "payload"
+        assert f"ps world ({owner}): 2 trainers + 1 servers, rank 2 of 3" in logs[f"{name}-ps-0"], logs

@@ -14,6 +14,7 @@ all-reduce among themselves.  Reports samples/sec to the operator."""
 from __future__ import annotations
 
 import argparse
+import os
 import time
 
 import torch
@@ -65,6 +66,9 @@ def main(argv=None):
     if mode != "none":
         ps_collective.join_ps_world(workers, servers, role, idx)
     info = rt.init_dist()
+    if mode != "none":
+        owner = "operator" if os.environ.get("TOA_PS_IN_WORLD") == "1" else "payload"
+        rt.log(f"ps world ({owner}): {workers} trainers + {servers} servers, rank {info.rank} of {info.world}")
     dev = pick_device() if info.backend != "gloo" else torch.device("cpu")
     dt_ = model_dtype(dev)
     torch.manual_seed(0)

@@ -46,22 +46,51 @@ from .flat import ALIGN, FlatParams
 
 
 def ps_world_env():
-    """(workers, servers, role, index) from the operator's TFJob env block
-    (``WORLD_SIZE`` counts chief/master/workers, ``TOA_PS_HOSTS`` lists the
-    servers, ``TOA_ROLE`` / ``TOA_REPLICA_INDEX`` name this replica)."""
+    """(workers, servers, role, index) from the operator's TFJob env block.
+
+    ``TOA_PS_HOSTS`` lists the servers and ``TOA_ROLE`` / ``TOA_REPLICA_INDEX``
+    name this replica.  When the PS replicas request a GPU the operator puts
+    them into the RCCL world itself (csrc/core/nodelocal.cc ``gpu_ps``):
+    ``TOA_PS_IN_WORLD=1``, ``WORLD_SIZE`` = trainers + servers, PS p has
+    ``RANK`` = trainers + p, and ``TOA_NUM_TRAINERS`` counts the trainers.
+    Otherwise (a CPU PS: the gloo parity path) ``WORLD_SIZE`` counts only the
+    trainers."""
     hosts = [h for h in os.environ.get("TOA_PS_HOSTS", "").split(",") if h]
     w = int(os.environ.get("WORLD_SIZE", "1"))
+    if os.environ.get("TOA_PS_IN_WORLD") == "1":
+        w = int(os.environ.get("TOA_NUM_TRAINERS", w - len(hosts)))
     role = os.environ.get("TOA_ROLE", "worker")
     idx = int(os.environ.get("TOA_REPLICA_INDEX", os.environ.get("RANK", "0")))
     return w, len(hosts), role, idx
 
 
 def join_ps_world(workers: int, servers: int, role: str, index: int):
-    """Rewrite RANK / WORLD_SIZE so the process group spans workers AND
-    servers (PS p = rank workers + p); call before ``Runtime.init_dist``."""
+    """Make sure the process group about to be created spans workers AND
+    servers (PS p = rank workers + p); call before ``Runtime.init_dist``.
+
+    Operator-owned world (``TOA_PS_IN_WORLD=1``, GPU parameter servers): a
+    consistency check only -- ``WORLD_SIZE`` / ``RANK`` must already be what
+    the protocol needs, and a mismatch (an operator and a payload that
+    disagree about the world) fails loudly instead of forming a wrong group.
+    CPU PS replicas (``TOA_PS_IN_WORLD`` unset or 0) are outside the
+    operator's world, so the payload extends it here for its gloo group."""
+    want_world = workers + servers
+    if os.environ.get("TOA_PS_IN_WORLD") == "1":
+        world = int(os.environ.get("WORLD_SIZE", "-1"))
+        rank = int(os.environ.get("RANK", "-1"))
+        problems = []
+        if world != want_world:
+            problems.append(f"WORLD_SIZE={world}, expected {workers} trainers + {servers} servers = {want_world}")
+        if role == "ps" and rank != workers + index:
+            problems.append(f"PS {index} has RANK={rank}, expected {workers + index}")
+        if role != "ps" and not 0 <= rank < workers:
+            problems.append(f"{role} {index} has RANK={rank}, outside the trainers' ranks [0, {workers})")
+        if problems:
+            raise RuntimeError("parameter-server world from the operator is inconsistent: " + "; ".join(problems))
+        return
     if role == "ps":
         os.environ["RANK"] = str(workers + index)
-    os.environ["WORLD_SIZE"] = str(workers + servers)
+    os.environ["WORLD_SIZE"] = str(want_world)
 
 
 def shard_ranges(numel: int, servers: int) -> list[tuple[int, int]]:
