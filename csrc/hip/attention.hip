@@ -1865,8 +1865,14 @@ static bool attn_fwd_asm_on() {
 extern "C" int toa_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int H,
                             int Hk, int S, int D, int flags, float scale, hipStream_t stream) {
   if (!attn_shape_ok(B, H, Hk, S, D, flags)) return (int)hipErrorInvalidValue;
-  if (D == 128 && S % 256 == 0 && attn_fwd_asm_on())
-    return toa_attn_fwd_asm(q, k, v, o, lse, B, H, Hk, S, D, flags, scale, stream);
+  if (D == 128 && S % 256 == 0 && attn_fwd_asm_on()) {
+    // the assembly launcher refuses (hipErrorInvalidValue) what it cannot
+    // run -- unaligned q/k/v/o, 32-bit size limits, a module that did not
+    // load -- before touching the stream: those inputs take the HIP kernel,
+    // as the dK/dV path does (dkdv_ds_launch)
+    const int rc = toa_attn_fwd_asm(q, k, v, o, lse, B, H, Hk, S, D, flags, scale, stream);
+    if (rc != (int)hipErrorInvalidValue) return rc;
+  }
   const int o_bshd = (flags >> 1) & 1;
   // S % 256 == 0: every 256-row block and 64-key tile is full, no clamping
   const bool tail = S % FWD_QB != 0;

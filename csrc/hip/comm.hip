@@ -233,7 +233,9 @@ __global__ void flag_publish_kernel(unsigned* flag, unsigned epoch) {
 __global__ void flags_wait_kernel(PeerFlags peers, int idx, int rank, int world, unsigned epoch, unsigned* err,
                                   long long timeout_cycles) {
   const int r = threadIdx.x;
-  if (r < world && r != rank) {
+  // a peer already marked lost (an earlier bucket's wait timed out) is not
+  // waited for again: a lost peer costs one timeout per run, not one per bucket
+  if (r < world && r != rank && !(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (1u << r))) {
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(peers.f[r] + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
       if (wall_clock64() - t0 > timeout_cycles) {

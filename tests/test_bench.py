@@ -52,6 +52,25 @@ def _check(r, n):
     lat = r["submit_to_first_step"]
     assert "error" not in lat and r.get("submit_to_first_step_p50_s", 0) > 0, lat
     assert lat["breakdown_p50_s"]["submit_to_pods_created"] < r["submit_to_first_step_p50_s"]
+    _check_schema(r, n)
+
+
+def _check_schema(r, n):
+    """Fields the driver's runs are read by (pinned): the GEMM fallback count
+    and the ZeRO-1 collectives A/B record.  On a GPU node at N > 1 the A/B
+    carries rccl_ms / sdma_ms / windows; here (gloo, no GPU) it says why it
+    was skipped."""
+    fb = r["gemm_fallbacks"]
+    assert set(fb) == {"calls", "by_shape"} and fb["calls"] == sum(fb["by_shape"].values())
+    ab = r["collectives_ab"]
+    assert "rccl_transport_ok" in ab
+    if "rccl_ms" in ab:
+        assert ab["sdma_ms"] > 0 and ab["rccl_ms"] > 0 and len(ab["windows"]) == 4
+        assert {w["transport"] for w in ab["windows"]} == {"rccl", "sdma"}
+    else:
+        assert set(ab) & {"skipped", "error"}, ab
+        if n > 1:
+            assert "GPU" in ab.get("skipped", ""), ab
 
 
 @pytest.mark.timeout(600)
@@ -131,3 +150,37 @@ def test_bench_under_torchrun_four_ranks():
     assert r["replicas_identical"] is True and "ZeRO-1" in r["config"]["optimizer"]
     assert r["config"]["gemm_policy"] in ("asm", "nosk")  # asm when libtoa_hip carries the kernels
     assert r["submit_to_first_step_p50_s"] > 0
+
+
+@pytest.mark.timeout(1200)
+def test_bench_under_torchrun_eight_ranks():
+    """The driver's N = 8 command shape, rehearsed on gloo: torchrun with 8
+    ranks, ZeRO-1 over 8 shards, latency probes as a TFJob Worker=8 in the
+    node-local layout (verdict r5: the headline job at its real world size)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "8", *TINY, "--zero", "1",
+           "--latency-probes", "1", "--cold-probes", "0"]
+    env = _env()
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=1180)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json_line(p.stdout)
+    _check(r, 8)
+    assert r["config"]["launched_by"] == "torchrun" and "ZeRO-1" in r["config"]["optimizer"]
+    assert r["gemm_fallbacks"]["calls"] == 0
+
+
+@pytest.mark.timeout(1200)
+def test_bench_launcher_eight_workers():
+    """`python bench.py --gpus 8`: the benchmark submitted as a TFJob Worker=8
+    through the local operator stack (the launcher form of the driver's N = 8
+    run), eight gloo ranks on the CPU."""
+    env = _env()
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "8", *TINY, "--latency-probes", "0", "--cold-probes",
+                        "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=1180)
+    assert p.returncode == 0, p.stderr[-4000:]
+    r = _json_line(p.stdout)
+    _check(r, 8)
+    assert r["config"]["launched_by"] == "operator"
+    assert len(r["submit_to_first_step"]["samples_s"]) == 1   # the benchmark job itself

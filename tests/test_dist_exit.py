@@ -68,3 +68,25 @@ def test_clean_run_exits_zero():
     procs = _launch(script, 2, _port())
     codes = [p.wait(timeout=90) for p in procs]
     assert codes == [0, 0], [p.stdout.read() for p in procs]
+
+
+def test_sys_exit_status_survives_a_hung_teardown():
+    """sys.exit(3) does not reach sys.excepthook: the status is
+    recorded, the teardown takes the failure path, and if even that hangs
+    the replica leaves with 3 -- never 0, which would hide the failure from
+    the operator.  The hang is forced by a process-group abort that blocks."""
+    script = textwrap.dedent("""
+        import sys, time
+        sys.path.insert(0, {root!r})
+        import torch.distributed as dist
+        from tf_operator_amd.train import dist as tdist
+        tdist.init(backend="gloo")
+        tdist.EXIT_TEARDOWN_S = 1.0
+        dist.distributed_c10d._abort_process_group = lambda *a, **k: time.sleep(60)
+        sys.exit(3)
+    """).format(root=ROOT)
+    procs = _launch(script, 2, _port())
+    t0 = time.time()
+    codes = [p.wait(timeout=60) for p in procs]
+    assert codes == [3, 3], [p.stdout.read() for p in procs]
+    assert time.time() - t0 < 45

@@ -4,7 +4,7 @@ through file-backed shared memory (ShmTransport, the GPU transport's
 protocol: publish epoch -> wait for every peer's epoch -> copy the peers'
 shards) and the result is compared bit for bit with
 dist.all_gather_into_tensor of the same shards, over several steps, at
-world 2 and 4, bf16 and fp32, with buckets of different sizes."""
+world 2, 4 and 8 (the headline job's size), bf16 and fp32, with buckets of different sizes."""
 import os
 import socket
 
@@ -68,7 +68,7 @@ def _worker(rank, world, port, tag, dtype, q):
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("world,dtype", [(2, torch.bfloat16), (4, torch.float32)])
+@pytest.mark.parametrize("world,dtype", [(2, torch.bfloat16), (4, torch.float32), (8, torch.bfloat16)])
 def test_pull_gather_matches_all_gather(world, dtype):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -150,7 +150,7 @@ def _rs_worker(rank, world, port, tag, q):
 
 
 @pytest.mark.timeout(180)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_pull_reduce_scatter_matches_sum(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -178,3 +178,63 @@ def test_zero_rs_mode_env(monkeypatch):
     monkeypatch.setenv("TOA_ZERO_RS", "ring")
     with pytest.raises(ValueError):
         pull_gather.rs_mode_from_env()
+
+
+def _lost_peer_worker(rank, world, port, tag, lost, q):
+    """World-8 protocol with one peer (`lost`) that never publishes: every
+    other rank's pull must fail within the transport's timeout, naming the
+    lost rank, instead of hanging the step."""
+    import time
+
+    import torch.distributed as dist
+
+    from tf_operator_amd.parallel.pull_gather import PullGather, ShmTransport
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    t = None
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ranges = [(0, 64 * world), (64 * world, 192 * world)]
+        t = ShmTransport(tag, rank, world, 192 * world, torch.bfloat16, len(ranges), timeout_s=2.0)
+        pg = PullGather(t, ranges, rank, world)
+        pg.new_step()
+        if rank == lost:
+            t.publish = lambda idx, epoch: None      # stalled: never publishes its shards
+        t0 = time.monotonic()
+        try:
+            for b in reversed(range(len(ranges))):
+                pg.launch_one(b).wait()
+            q.put((rank, "ok", time.monotonic() - t0))
+        except RuntimeError as e:
+            q.put((rank, str(e), time.monotonic() - t0))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "setup: " + repr(e), 0.0))
+    finally:
+        for p in (getattr(t, "paths", [None])[rank:rank + 1] + getattr(t, "fpaths", [None])[rank:rank + 1]):
+            if p:
+                try:
+                    os.unlink(p)
+                except FileNotFoundError:
+                    pass
+
+
+@pytest.mark.timeout(180)
+def test_pull_gather_world8_lost_peer_fails_every_rank_in_time():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, lost = 8, 5
+    port, tag = _port(), f"lost{os.getpid()}"
+    procs = [ctx.Process(target=_lost_peer_worker, args=(r, world, port, tag, lost, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (msg, dt) for r, msg, dt in (q.get(timeout=150) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    for r in range(world):
+        msg, dt = res[r]
+        if r == lost:
+            continue   # it pulls from live peers; its own failure shows up as theirs
+        assert f"rank {lost} never published" in msg, (r, msg)
+        assert dt < 10.0, (r, dt)

@@ -76,6 +76,11 @@ def parser() -> argparse.ArgumentParser:
                     help="capture RCCL's transport selection (NCCL_DEBUG=INFO to a file) into the JSON line")
     ap.add_argument("--calibrate", choices=("0", "1"), default="1",
                     help="box-speed record: fixed-shape GEMM rates around the timed region, clock during it")
+    ap.add_argument("--collectives-ab", choices=("auto", "0", "1"), default="auto",
+                    help="after the timed region, time the ZeRO-1 collectives on RCCL and on the copy engines "
+                         "(copy-engine pulls) in alternating windows of the same process group; auto = on for "
+                         "a sharded one-node GPU job with N > 1")
+    ap.add_argument("--ab-steps", type=int, default=3, help="timed steps per collectives A/B window")
     return ap
 
 
@@ -428,6 +433,84 @@ def transport_ok(summary: dict | None, n_ranks: int):
     return all(t.upper().startswith("P2P") for t in trans)
 
 
+def collectives_ab(tr, batches, args, info, rccl_ok) -> dict:
+    """Time the two ZeRO-1 collective transports in the same process group,
+    after the headline measurement (which stays on the configured default):
+    windows in ABBA order -- the default, the other, the other, the default
+    -- each one untimed step after the switch and ``--ab-steps`` timed steps
+    bracketed by a barrier + synchronize, MAX over ranks.  The switch
+    (``LlamaTrainer.set_collective_transport``) drains and barriers, so no
+    pull crosses a window.  Returns {rccl_ms, sdma_ms, windows, ...} or
+    {skipped: reason} / {error: ...}; never raises."""
+    import torch
+
+    from ..train import dist as tdist
+
+    world = info.world
+    want = args.collectives_ab == "1" or (args.collectives_ab == "auto" and world > 1)
+    if not want:
+        return {"skipped": "off (--collectives-ab 0, or N = 1)"}
+    if tr.gather is None:
+        return {"skipped": "ZeRO-1 off: no sharded collectives"}
+    if info.device.type != "cuda":
+        return {"skipped": "copy-engine pulls need GPUs (this run has none)"}
+    if int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != world:
+        return {"skipped": "ranks span nodes (LOCAL_WORLD_SIZE != world): no IPC pulls"}
+    if rccl_ok is False:
+        return {"skipped": "RCCL channels are not all P2P: the ranks cannot reach each other's GPUs"}
+    default = tr.collective_transport()
+    other = "sdma" if default == "rccl" else "rccl"
+    k = max(1, args.ab_steps)
+    times = {"rccl": [], "sdma": []}
+    windows = []
+    try:
+        for arm in (default, other, other, default):
+            tr.set_collective_transport(arm)
+            tr.step(batches)                      # the first step after a switch is not timed
+            tdist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(k):
+                tr.step(batches)
+            torch.cuda.synchronize()
+            tdist.barrier()
+            torch.cuda.synchronize()
+            dt = tdist.all_max(time.perf_counter() - t0, info.device)
+            times[arm].append(dt / k * 1e3)
+            windows.append({"transport": arm, "ms_per_step": round(dt / k * 1e3, 2)})
+        tr.set_collective_transport(default)
+        if tr.gather is not None:
+            tr.gather.wait_all()
+        for x in tr._pull_transports():
+            x.check()                             # a timed-out peer wait would have poisoned the sdma windows
+    except Exception as e:  # noqa: BLE001 - the headline measurement stands; the A/B reports its failure
+        return {"error": f"{type(e).__name__}: {str(e)[:500]}", "windows": windows}
+    out = {"default": default, "steps_per_window": k, "windows": windows,
+           "rccl_ms": round(statistics.median(times["rccl"]), 2), "sdma_ms": round(statistics.median(times["sdma"]), 2)}
+    out["faster"] = "sdma" if out["sdma_ms"] < out["rccl_ms"] else "rccl"
+    return out
+
+
+def _ab_watchdog(budget_s: float, emit):
+    """A hung A/B window (a stalled copy-engine pull, a collective that never
+    completes) must not cost the headline line: after `budget_s` rank 0
+    emits what it has and every rank leaves."""
+    import threading
+
+    def fire():
+        try:
+            emit()
+        finally:
+            sys.stdout.flush()
+            os._exit(0)
+
+    t = threading.Timer(budget_s, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+
 def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_by: str = "replica",
                 t_probes_done: float | None = None) -> int:
     """t_probes_done: under torchrun rank 0 ran the latency probes before
@@ -530,6 +613,10 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
     startup = {f"{a}->{b}": round(phases[b] - phases[a], 3) for a, b in zip(order, order[1:])}
     on_gpu = dev.type == "cuda"
     rc = 0
+    rl = summarize_rccl_log(rccl_log)
+    ok = transport_ok(rl, n_gpus)
+    any_bad = tdist.all_max(1.0 if ok is False else 0.0, dev) > 0   # any rank's channels off P2P
+    out = None
     if info.rank == 0:
         out = {
             "metric": METRIC.format(n=n_gpus),
@@ -570,14 +657,14 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
             "loss_max_over_ranks": round(loss_max, 4),
             "replicas_identical": bool(in_sync),
             "peak_mem_gib": round(peak_mem, 1),
+            # GEMMs that left the hand-written kernels for the library (ops/gemm.py): 0 at the bench shape
+            "gemm_fallbacks": {"calls": sum(_gemm.fallbacks().values()), "by_shape": _gemm.fallbacks()},
         }
         cr = cal.record()
         if cr is not None:
             out["calibration"] = cr
-        rl = summarize_rccl_log(rccl_log)
         if rl:
             out["rccl"] = rl
-        ok = transport_ok(rl, n_gpus)
         if ok is not None:
             # one node: every channel must ride P2P (xGMI); SHM / NET means the
             # ranks could not see each other's GPUs and this run measured the
@@ -588,6 +675,11 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
                       f"{rl['channel_connections_by_transport']}", file=sys.stderr, flush=True)
         if probe is not None:
             _attach_probe(out, probe)
+
+    def emit(ab):
+        if out is None:
+            return
+        out["collectives_ab"] = dict(ab, rccl_transport_ok=None if ok is None else bool(ok and not any_bad))
         if args.result_file:
             tmp = args.result_file + ".tmp"
             with open(tmp, "w") as f:
@@ -595,6 +687,14 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
             os.replace(tmp, args.result_file)
         else:
             print(json.dumps(out), flush=True)
+
+    # the two ZeRO-1 collective transports, timed after the headline (which
+    # stays on the configured default); a hung window still emits the line
+    budget = 120.0 + 3.0 * 4 * (max(1, args.ab_steps) + 1) * max(ms, 1.0) / 1e3
+    wd = _ab_watchdog(budget, lambda: emit({"error": f"A/B did not finish within {budget:.0f} s"}))
+    ab = collectives_ab(tr, batches, args, info, False if any_bad else ok)
+    wd.cancel()
+    emit(ab)
     tdist.shutdown()
     return rc
 
@@ -634,7 +734,7 @@ def run_launcher(args) -> int:
                str(args.micro_batch), "--grad-accum", str(args.grad_accum), "--zero", args.zero,
                "--warm-start", args.warm_start,
                "--rccl-log", args.rccl_log, "--latency-probes", "0", "--result-file", res_file,
-               "--calibrate", args.calibrate]
+               "--calibrate", args.calibrate, "--collectives-ab", args.collectives_ab, "--ab-steps", str(args.ab_steps)]
         if args.bucket_mb is not None:
             cmd += ["--bucket-mb", str(args.bucket_mb)]
         timeout = args.probe_timeout + 60 + 30 * (args.steps + args.warmup)

@@ -202,6 +202,49 @@ def _gemm(ta, tb, m, n, k, a, lda, b, ldb, c, ldc, beta):
 
 _asm_first = False
 
+# GEMMs of a GPU training step that left the hand-written kernels for the
+# library (hipBLASLt / torch.matmul) under the ``asm`` policy, per (op, shape):
+# a user's TFJob at, say, seq 4000 would otherwise run the library for every
+# GEMM without a trace.  Warned once per shape on stderr; the bench record
+# carries the counts (``gemm_fallbacks``).
+_FALLBACKS: dict = {}
+_fallback_lock = threading.Lock()
+
+
+def _fallback(op: str, shape, target: str, why: str):
+    key = f"{op} {'x'.join(str(int(d)) for d in shape)} -> {target}"
+    with _fallback_lock:
+        n = _FALLBACKS.get(key, 0)
+        _FALLBACKS[key] = n + 1
+    if n == 0:
+        import sys
+
+        print(f"[toa.gemm] WARNING: {key} ({why}); later calls of this shape are counted, not logged",
+              file=sys.stderr, flush=True)
+
+
+def fallbacks() -> dict:
+    """{"op MxNxK -> target": calls} since the process started (or reset)."""
+    with _fallback_lock:
+        return dict(_FALLBACKS)
+
+
+def reset_fallbacks():
+    with _fallback_lock:
+        _FALLBACKS.clear()
+
+
+def _why_not_asm(x2: torch.Tensor, w: torch.Tensor, n_mult: int = 256) -> str:
+    M, K = x2.shape
+    N = w.shape[0]
+    if x2.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return f"dtype {x2.dtype}/{w.dtype}, not bf16"
+    if M % 256 or N % n_mult:
+        return f"M={M} / N={N} not multiples of 256 (tokens per micro-batch x seq, output features)"
+    if K % 64 or K < 128:
+        return f"K={K} not a multiple of 64 >= 128"
+    return "layout: non-unit column stride, unaligned rows or base"
+
 
 class first_step:
     """Context of a trainer's FIRST step under the hipBLASLt policies: every
@@ -253,7 +296,11 @@ def linear_fwd(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         _lib.call("toa_gemm_asm", _lib.ptr(x2), x2.stride(0), _lib.ptr(w), w.stride(0), _lib.ptr(y), N, M, N,
                   x2.shape[1], _lib.stream(x2))
         return y
-    if not _ok(x2, w):
+    lib_ok = _ok(x2, w)
+    if _MODE == "asm" and x2.is_cuda and x2.dim() == 2 and w.dim() == 2:
+        _fallback("fwd", (x2.shape[0], w.shape[0], x2.shape[1]), "hipBLASLt" if lib_ok else "torch.matmul",
+                  _why_not_asm(x2, w))
+    if not lib_ok:
         return torch.matmul(x2, w.t())
     M, K = x2.shape
     N = w.shape[0]
@@ -266,7 +313,11 @@ def linear_dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     wt = getattr(w, "_toa_wt", None)
     if wt is not None:  # W^T kept by ops.wt.TransposedWeights: dx = dy (W^T)^T, the forward's form
         return linear_fwd(dy2, wt)
-    if not _ok(dy2, w):
+    lib_ok = _ok(dy2, w)
+    if _MODE == "asm" and dy2.is_cuda and dy2.dim() == 2 and w.dim() == 2:
+        _fallback("dgrad", (dy2.shape[0], w.shape[1], dy2.shape[1]), "hipBLASLt" if lib_ok else "torch.matmul",
+                  "no transposed weight copy (ops/wt.py) for this weight")
+    if not lib_ok:
         return torch.matmul(dy2, w)
     M, N = dy2.shape
     K = w.shape[1]
@@ -387,6 +438,10 @@ def wgrad_acc_(g: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float
     """g[N,K] = beta*g + dy2[M,N]^T @ x2[M,K]  (in place; g bf16 or fp32)."""
     if beta in (0.0, 1.0) and wgrad_hip_ok(g, dy2, x2):
         return wgrad_hip_(g, dy2, x2, beta)
+    if dy2.is_cuda and g.dtype == torch.bfloat16 and dy2.dim() == 2 and x2.dim() == 2:
+        T, N = dy2.shape
+        _fallback("wgrad", (N, x2.shape[1], T), "hipBLASLt" if _ok(dy2, x2) else "torch.mm",
+                  "output dims not multiples of 256, tokens not a multiple of 128 (>= 1024), or layout")
     if (g.dtype == torch.float32 and dy2.dtype == x2.dtype == torch.bfloat16 and g.is_cuda and g.is_contiguous()
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and _lib.has("toa_gemm")):
         # fp32 master-gradient accumulation (small payloads): one hipBLASLt call

@@ -34,6 +34,20 @@ an 8-GPU run measures it.  Transports:
   memory (/dev/shm), so gloo tests check the pulled bytes against
   ``dist.all_gather_into_tensor`` bit for bit (tests/test_pull_gather.py).
 
+Failure semantics.  A peer that never publishes costs its waiting ranks one
+bounded spin (``timeout_ms``, once per run: a peer already marked lost is
+not waited for again, csrc/hip/comm.hip ``flags_wait_kernel``).  The wait
+only sets the peer's error bit; the copies behind it still run, so from
+that bucket on the pulled weights (or gradient slices) are STALE and the
+model is poisoned until the job restarts.  ``poll()`` surfaces the bit one
+step later as a RuntimeError (the replica exits non-zero, the operator
+restarts it), and ``check()`` -- run by every checkpoint save, train/llm.py
+``trainer_state`` -- refuses to persist a poisoned state, so a restart
+resumes from the last good checkpoint.  Teardown: ``LlamaTrainer.close``
+(registered at exit) drains this rank's pulls, synchronises, barriers the
+group and only then unmaps / frees, so no rank frees exported memory a
+slower peer is still pulling.
+
 Reference parity: the payloads' gradient exchange
 (``examples/v1/distribution_strategy/keras-API/multi_worker_strategy-with-keras.py:76-77``;
 SURVEY P3 / K16) -- the sharded step's weight half, moved without CUs.
@@ -61,6 +75,16 @@ def rs_mode_from_env() -> str:
     if m not in ("rccl", "sdma"):
         raise ValueError(f"TOA_ZERO_RS={m!r}: expected rccl or sdma")
     return m
+
+
+def timeout_ms_from_env() -> int:
+    """How long a puller waits for a peer's epoch before marking it lost
+    (``TOA_PULL_TIMEOUT_MS``, default 60 s: a peer writing a checkpoint or
+    compiling on its first step is slow, not lost)."""
+    v = int(os.environ.get("TOA_PULL_TIMEOUT_MS", "60000"))
+    if v <= 0:
+        raise ValueError(f"TOA_PULL_TIMEOUT_MS={v}: must be > 0")
+    return v
 
 
 class _Event:

@@ -128,6 +128,7 @@ def shutdown():
 
 
 _FAILED = []          # set by the excepthook: the interpreter is exiting on an uncaught exception
+_EXIT_STATUS = []     # non-zero sys.exit() statuses (the excepthook does not see SystemExit)
 EXIT_TEARDOWN_S = 20.0
 
 
@@ -142,6 +143,18 @@ def _install_failure_hook():
 
     hook._toa_failure_hook = True
     sys.excepthook = hook
+    # sys.excepthook never sees SystemExit: a replica leaving by sys.exit(n)
+    # with n != 0 (examples/dist_mnist.py) records n here, so its teardown
+    # takes the failure path and a hung teardown still exits with n, not 0
+    prev_exit = sys.exit
+
+    def exit_(status=None):
+        code = status if isinstance(status, int) else (0 if status is None else 1)
+        if code:
+            _EXIT_STATUS.append(code)
+        prev_exit(status)
+
+    sys.exit = exit_
 
 
 def _bounded(fn, timeout: float) -> bool:
@@ -173,11 +186,12 @@ def _shutdown_quietly():
         except Exception:  # noqa: BLE001 - fall back to the graceful path, still bounded
             graceful()
 
-    if _FAILED:
+    if _FAILED or _EXIT_STATUS:
+        status = _EXIT_STATUS[-1] if _EXIT_STATUS else 1
         if not _bounded(abort, EXIT_TEARDOWN_S):
-            sys.stderr.write("[dist] process group teardown did not finish after a failure; exiting 1\n")
+            sys.stderr.write(f"[dist] process group teardown did not finish after a failure; exiting {status}\n")
             sys.stderr.flush()
-            os._exit(1)
+            os._exit(status)
     elif not _bounded(graceful, 3 * EXIT_TEARDOWN_S):
         sys.stderr.write("[dist] process group teardown hung after a clean run; exiting 0\n")
         sys.stderr.flush()

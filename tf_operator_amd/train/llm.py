@@ -1,6 +1,7 @@
 """Data-parallel Llama trainer step (the flagship MI355X training path).
 
-One process per GPU.  Per step: forward (fused HIP ops + hipBLASLt GEMMs),
+One process per GPU.  Per step: forward (fused HIP ops + the gfx950
+assembly GEMMs and attention, ops/gemm.py, ops/llm.py),
 backward writing weight gradients straight into the flat bf16 gradient
 buffer, bucketed RCCL all-reduce overlapped with backward, one fused AdamW
 over the flat fp32 master/m/v (device-side grad clipping, no host sync).
@@ -89,6 +90,14 @@ class LlamaTrainer:
                                  post_update=self.wt.refresh if self.wt else None)
         if self.opt.overlap or self.gather is not None:
             self._hooks = self._install_param_waits()
+        self._closed = False
+        self._closed_registered = bool(self._pull_transports())
+        if self._closed_registered:
+            import atexit
+
+            # registered after the process group's own atexit teardown
+            # (train/dist.py init), so it runs BEFORE it (LIFO)
+            atexit.register(self.close)
         self.step_idx = 0
         # start-up diagnostics: called with a phase name after the first
         # step's forward / backward / update are issued (host side; the
@@ -187,10 +196,17 @@ class LlamaTrainer:
         bk = self.bucketer
         if pull_gather.mode_from_env() != "sdma" or bk.world < 2 or bk.emu is not None:
             return None
+        return self._build_pull_gather()
+
+    def _build_pull_gather(self):
+        from ..parallel import pull_gather
+
+        bk = self.bucketer
         if self.flat.param.device.type != "cuda" or int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != bk.world:
             raise RuntimeError("TOA_ZERO_AG=sdma needs a GPU job whose ranks share one node "
                                "(LOCAL_WORLD_SIZE == world: the operator's node-local layout)")
-        t = pull_gather.GpuIpcTransport(self.flat.param, bk.rank, bk.world, len(bk.buckets), group=bk.group)
+        t = pull_gather.GpuIpcTransport(self.flat.param, bk.rank, bk.world, len(bk.buckets), group=bk.group,
+                                        timeout_ms=pull_gather.timeout_ms_from_env())
         return pull_gather.PullGather(t, [(b[0], b[1]) for b in bk.buckets], bk.rank, bk.world)
 
     def _pull_reduce(self):
@@ -202,13 +218,114 @@ class LlamaTrainer:
         bk = self.bucketer
         if pull_gather.rs_mode_from_env() != "sdma" or bk.world < 2 or bk.emu is not None:
             return None
+        return self._build_pull_reduce()
+
+    def _build_pull_reduce(self):
+        from ..parallel import pull_gather
+
+        bk = self.bucketer
         if (self.flat.grad.device.type != "cuda" or self.flat.grad.dtype != torch.bfloat16
                 or int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != bk.world):
             raise RuntimeError("TOA_ZERO_RS=sdma needs bf16 gradients on a GPU job whose ranks share one node "
                                "(LOCAL_WORLD_SIZE == world: the operator's node-local layout)")
+        if not self.fresh_grads:
+            # the zeroing pass at the start of step t+1 runs on the compute
+            # stream before any wait, and nothing orders it after the owners'
+            # pulls of this rank's step-t slices: an owner could sum zeroed
+            # gradients.  Fresh gradients (the default) have no such pass --
+            # the next backward's first write to a bucket comes after the
+            # forward waited for that bucket's updated shard, i.e. after the pull.
+            raise RuntimeError("TOA_ZERO_RS=sdma needs fresh gradients (TOA_FRESH_GRADS=1, the default)")
         t = pull_gather.GpuIpcTransport(self.flat.grad, bk.rank, bk.world, len(bk.buckets), group=bk.group,
-                                        what="reduce-scatter")
+                                        what="reduce-scatter", timeout_ms=pull_gather.timeout_ms_from_env())
         return pull_gather.PullReduceScatter(t, [(b[0], b[1]) for b in bk.buckets], bk.rank, bk.world)
+
+    # ---- ZeRO-1 collective transport, switchable between steps (bench A/B)
+    def collective_transport(self) -> str | None:
+        """"rccl" | "sdma" for a sharded trainer (both halves on the same
+        transport), "mixed" when only one half pulls, None unsharded."""
+        if self.gather is None:
+            return None
+        ag, rs = self.gather.pull is not None, self.bucketer.pull_rs is not None
+        return "sdma" if ag and rs else ("rccl" if not (ag or rs) else "mixed")
+
+    def set_collective_transport(self, kind: str):
+        """Switch both ZeRO-1 collectives (the weight all-gather and the
+        gradient reduce-scatter) to RCCL or to the copy-engine pulls between
+        two steps.  Collective: every rank calls it at the same step.  The
+        switch drains first -- every outstanding gather waited (and its W^T
+        refresh run), the device synchronised, a barrier -- so no rank pulls
+        across the boundary.  The pull transports are built once, on the
+        first switch to "sdma", and kept (``close`` frees them)."""
+        if self.gather is None:
+            raise RuntimeError("collective transport: the trainer is not sharded (ZeRO-1 off)")
+        if kind not in ("rccl", "sdma"):
+            raise ValueError(kind)
+        self.opt.wait_all()
+        self.gather.wait_all()
+        torch.cuda.synchronize()
+        self._group_barrier()
+        ag, rs = getattr(self, "_pulls", (None, None))
+        ag, rs = ag or self.gather.pull, rs or self.bucketer.pull_rs
+        if kind == "sdma":
+            # built in the same order on every rank (both constructors are collective)
+            ag = ag or self._build_pull_gather()
+            rs = rs or self._build_pull_reduce()
+            if not self._closed_registered:
+                import atexit
+
+                atexit.register(self.close)
+                self._closed_registered = True
+            self.gather.pull, self.bucketer.pull_rs = ag, rs
+        else:
+            self.gather.pull, self.bucketer.pull_rs = None, None
+        self._pulls = (ag, rs)
+
+    def _pull_transports(self):
+        cur = [(self.gather.pull if self.gather is not None else None), getattr(self.bucketer, "pull_rs", None)]
+        out = []
+        for x in cur + list(getattr(self, "_pulls", ())):
+            if x is not None and all(x is not y for y in out):
+                out.append(x)
+        return out
+
+    def _group_barrier(self):
+        import torch.distributed as dist
+
+        group = self.bucketer.group
+        if not dist.is_initialized():
+            return
+        if dist.get_backend(group) == "nccl":
+            dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier(group=group)
+        torch.cuda.synchronize()
+
+    def close(self, timeout_s: float = 60.0):
+        """Orderly teardown of the copy-engine transports: this rank's pulls
+        are drained and the device synchronised, then a barrier over the
+        group (every peer has finished pulling from this rank's exported
+        parameter / gradient / flag memory), and only then the IPC mappings
+        are closed and the flag memory freed.  Idempotent; registered at
+        exit.  After a failure (a peer may be gone) the barrier is bounded
+        and the memory is left to process exit."""
+        pulls = self._pull_transports()
+        if self._closed or not pulls:
+            return
+        self._closed = True
+        from . import dist as _dist
+
+        try:
+            self.opt.wait_all()
+            if self.gather is not None:
+                self.gather.wait_all()
+            torch.cuda.synchronize()
+        except Exception:  # noqa: BLE001 - a failed run still frees nothing a peer may read
+            return
+        if _dist._FAILED or _dist._EXIT_STATUS or not _dist._bounded(self._group_barrier, timeout_s):
+            return
+        for p in pulls:
+            p.close()
 
     def _emulated_fused_reduce(self, b):
         """TOA_EMULATE_RS=sdma (parallel/emulate.py): price the reduction an
