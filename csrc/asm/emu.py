@@ -218,6 +218,13 @@ class Emu:
     def op_s_load_dwordx2(self, w, a, m):
         self._sload(w, a, 2)
 
+    def op_s_load_dword(self, w, a, m):
+        self._sload(w, a, 1)
+
+    def op_s_sleep(self, w, a, m):
+        """A wait with no architectural effect (the emulator has no clock)."""
+        w.slept = getattr(w, "slept", 0) + 64 * self._lit(a[0])
+
     def op_s_memtime(self, w, a, m):
         """A monotonically increasing stand-in for the shader clock: this
         wave's instruction count (the timing kernel's records stay ordered)."""

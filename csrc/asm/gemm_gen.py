@@ -86,7 +86,7 @@ KARG = {
     "X": 0, "W": 8, "C": 16, "S": 24,
     "ldx": 32, "ldw": 36, "ldc": 40, "lds": 44,
     "ktiles": 48, "tiles_m": 52, "tiles_n": 56, "xq": 60, "xr": 64,
-    "per_group": 68, "fw": 72, "fc": 76, "map": 80, "grid": 84,
+    "per_group": 68, "fw": 72, "fc": 76, "map": 80, "grid": 84, "phase": 88,
 }
 MAP_WALK_COLS = 16
 MAP_DEFAULT = 2          # groups of 4 row tiles walk the column tiles
@@ -102,6 +102,7 @@ S_KT, S_TM_N, S_TN_N, S_XQ = 16, 17, 18, 19
 S_XR, S_PG, S_FW, S_FC = 20, 21, 22, 23
 S_TILE, S_TM, S_TN = 24, 25, 26
 S_T0, S_T1, S_T2, S_T3 = 27, 28, 29, 30
+S_PHASE = 31        # kernarg `phase` word (start offsets of the first wave, phase_delay)
 SRD_X, SRD_W, SRD_C, SRD_S = 32, 36, 40, 44
 S_M0X, S_M0XT, S_M0W, S_M0WT = 48, 49, 50, 51
 S_LOOP = 52
@@ -221,6 +222,7 @@ def prologue_args(a: Asm):
     a(f"s_load_dwordx16 {sr(S_ARGS, 16)}, s[0:1], 0x0")
     a(f"s_load_dwordx4 {sr(S_ARGS + 16, 4)}, s[0:1], 0x40")
     a(f"s_load_dwordx2 {sr(S_MAP, 2)}, s[0:1], 0x50")
+    a(f"s_load_dword {sr(S_PHASE)}, s[0:1], {KARG['phase']:#x}")
     a("s_mov_b32 m0, 0")
     a(f"v_mov_b32 {vr(V_TID)}, v0")
     a("s_waitcnt lgkmcnt(0)")
@@ -244,12 +246,49 @@ def prologue_args(a: Asm):
     a(f"s_cmp_ge_u32 {sr(S_MAP)}, {2 * MAP_WALK_COLS}")
     a(f"s_cbranch_scc1 {a.abort}")
     a(f"s_lshr_b32 {sr(S_WALK)}, {sr(S_MAP)}, 4")
+    phase_delay(a)
     if SCHED["persist"]:
         # persistent: the grid size; 0 would walk one tile forever
         a(f"s_cmp_eq_u32 {sr(S_KGRID)}, 0")
         a(f"s_cbranch_scc1 {a.abort}")
         a(f"s_mov_b32 {sr(S_GRID)}, {sr(S_KGRID)}")
         a(f"s_mov_b32 {sr(S_ITER)}, s2")
+
+
+PHASE_FIRST_WAVE = 256   # workgroups 0..255: the first one on each of the 256 CUs
+
+
+def phase_delay(a: Asm):
+    """Start offsets for the first wave of workgroups (kernarg `phase`:
+    bits [15:0] n, bits [19:16] log2 g; 0 = off).  Every tile of these
+    kernels takes the same time, so the 256 workgroups that start together
+    keep finishing together, and their epilogues -- a burst of HBM traffic
+    with the MFMA pipe idle (the SwiGLU backward loads 256 KiB of gate / up
+    and stores 256 KiB per tile) -- all hit memory at once.  Workgroup b of
+    the first wave sleeps ((b >> 3) mod g) * n * 512 cycles before its
+    prologue: its CU then runs g phase groups apart for the rest of the
+    kernel (the next workgroups are dispatched to whichever CU frees first),
+    so each epilogue burst meets 1/g of the chip's traffic.  (b >> 3: the
+    dispatcher deals workgroups round-robin over the 8 XCDs, so every XCD
+    gets every phase.)"""
+    l_done, l_sleep = a.fresh("phase_done"), a.fresh("phase_sleep")
+    a(f"s_cmp_ge_u32 s2, {PHASE_FIRST_WAVE}")
+    a(f"s_cbranch_scc1 {l_done}")
+    a(f"s_and_b32 {sr(S_T0)}, {sr(S_PHASE)}, 0xffff")            # n
+    a(f"s_lshr_b32 {sr(S_T1)}, {sr(S_PHASE)}, 16")
+    a(f"s_and_b32 {sr(S_T1)}, {sr(S_T1)}, 15")                   # log2 g
+    a(f"s_lshl_b32 {sr(S_T2)}, 1, {sr(S_T1)}")
+    a(f"s_sub_u32 {sr(S_T2)}, {sr(S_T2)}, 1")
+    a(f"s_lshr_b32 {sr(S_T3)}, s2, 3")
+    a(f"s_and_b32 {sr(S_T3)}, {sr(S_T3)}, {sr(S_T2)}")           # phase group
+    a(f"s_mul_i32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T3)}")           # sleeps of 512 cycles
+    a.label(l_sleep)
+    a(f"s_cmp_eq_u32 {sr(S_T0)}, 0")
+    a(f"s_cbranch_scc1 {l_done}")
+    a("s_sleep 8")
+    a(f"s_sub_u32 {sr(S_T0)}, {sr(S_T0)}, 1")
+    a(f"s_branch {l_sleep}")
+    a.label(l_done)
 
 
 def tile_setup(a: Asm, epi: str, bid: str = "s2"):
@@ -447,7 +486,11 @@ SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4
          "xdma_gap": 3, "merge_bar": False, "timing": 0,
          "align": True, "drain_end": False, "map": "lib0", "persist": False, "dual": "", "zero_late": True,
          "nostore": False, "store_nt": True, "store_same": False, "epi_pipe": True,
-         "epi_pk": True, "epi_f32s": True}
+         "epi_pk": True, "epi_f32s": True,
+         # DIAGNOSTIC arms of the SwiGLU backward epilogue (SWIGLU_BWD_VARIANTS;
+         # wrong outputs by design): no gu loads (ds stands in for gate and up),
+         # no SwiGLU math (the loaded gu stored as dgu), no dgu stores, no epilogue
+         "epi_noload": False, "epi_novalu": False, "epi_nostore": False, "epi_none": False}
 
 
 def _stamp(k: int) -> str:
@@ -918,8 +961,12 @@ def epilogue_swiglu_bwd_pipe(a: Asm):
     def slot(r):
         return V_FX0 + 16 * (r % D)                           # lg = slot, lu = slot + 8
 
+    noload, novalu, nostore = SCHED["epi_noload"], SCHED["epi_novalu"], SCHED["epi_nostore"]
+
     def issue_loads(r):
         j, half = rounds[r]
+        if noload:
+            return
         lg, lu = slot(r), slot(r) + 8
         for q, p in enumerate((2 * half, 2 * half + 1)):
             a(f"buffer_load_dwordx4 {vr(lg + 4 * q, 4)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T2)} offen offset:{64 * p}")
@@ -932,6 +979,21 @@ def epilogue_swiglu_bwd_pipe(a: Asm):
         issue_loads(r)
     for r, (j, half) in enumerate(rounds):
         ps_ = (2 * half, 2 * half + 1)
+        if novalu:   # DIAGNOSTIC: the loaded gu goes straight back out as dgu
+            last = max(i for i, x in enumerate(seq) if x == ("L", r))
+            a(f"s_waitcnt vmcnt({min(63, len(seq) - last - 1)})")
+            lg, lu = slot(r), slot(r) + 8
+            if not nostore:
+                for q, p in enumerate(ps_):
+                    store16(a, lg + 4 * q, V_E, SRD_C, S_E0, p)
+                    store16(a, lu + 4 * q, V_E + 2, SRD_C, S_E0, p)
+                seq.extend([("S", r)] * 4)
+            a("s_nop 1")
+            if r + D < len(rounds):
+                issue_loads(r + D)
+            if half == 1:
+                a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+            continue
         d = V_E + 24                        # 16 f32: ds (no memory dependency: first)
         for q, p in enumerate(ps_):
             read_pair(a, d + 8 * q, p, j)
@@ -940,9 +1002,12 @@ def epilogue_swiglu_bwd_pipe(a: Asm):
             cvt_pack8(a, pd + 4 * q, d + 8 * q)
         for q in range(2):
             unpack8(a, d + 8 * q, pd + 4 * q)
-        last = max(i for i, x in enumerate(seq) if x == ("L", r))
-        a(f"s_waitcnt vmcnt({min(63, len(seq) - last - 1)})")   # this round's loads only
-        lg, lu = slot(r), slot(r) + 8
+        if noload:   # DIAGNOSTIC: ds stands in for both gate and up
+            lg = lu = pd
+        else:
+            last = max(i for i, x in enumerate(seq) if x == ("L", r))
+            a(f"s_waitcnt vmcnt({min(63, len(seq) - last - 1)})")   # this round's loads only
+            lg, lu = slot(r), slot(r) + 8
         gf, uf = V_E + 48, V_E + 64
         for q in range(2):
             unpack8(a, gf + 8 * q, lg + 4 * q)
@@ -991,11 +1056,12 @@ def epilogue_swiglu_bwd_pipe(a: Asm):
             cvt_pack8(a, pdg + 4 * q, uf + 8 * q)
         cvt_pack8(a, pdu, tmp)
         cvt_pack8(a, gf, tmp + 8)
-        for q, p in enumerate(ps_):
-            store16(a, pdg + 4 * q, V_E, SRD_C, S_E0, p)
-        store16(a, pdu, V_E + 2, SRD_C, S_E0, ps_[0])
-        store16(a, gf, V_E + 2, SRD_C, S_E0, ps_[1])
-        seq.extend([("S", r)] * 4)
+        if not nostore:
+            for q, p in enumerate(ps_):
+                store16(a, pdg + 4 * q, V_E, SRD_C, S_E0, p)
+            store16(a, pdu, V_E + 2, SRD_C, S_E0, ps_[0])
+            store16(a, gf, V_E + 2, SRD_C, S_E0, ps_[1])
+            seq.extend([("S", r)] * 4)
         a("s_nop 1")                        # store data read before the next round rewrites it
         if half == 1:
             a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
@@ -1155,8 +1221,9 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
             a(ins)
     if persist:
         persistent_next(a, epi, l_tile)
-    epi_offsets(a, epi)
-    {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
+    if not SCHED["epi_none"]:   # (the "none" arm: DIAGNOSTIC, the main loop alone)
+        epi_offsets(a, epi)
+        {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
     if trace or timing or SCHED["drain_end"]:
         a("s_waitcnt vmcnt(0)")
     # else: end with the epilogue's stores still in flight -- the wave's end
@@ -1413,6 +1480,18 @@ PLAIN_VARIANTS = (
 # second loop body for odd SIMDs (with and without MFMA alignment) -1..-3 %.
 
 
+# DIAGNOSTIC arms of the fused SwiGLU backward (wrong outputs by design),
+# launched by index through toa_gemm_asm_swiglu_bwd_variant: where the fused
+# epilogue's time goes (scripts/asm_gemm_bench.py --swiglu-variants).
+SWIGLU_BWD_VARIANTS = (
+    ("b1", {"epi_none": True}),          # the main loop alone
+    ("b2", {"epi_noload": True}),        # math + stores, no gu loads
+    ("b3", {"epi_novalu": True}),        # gu loads + dgu stores, no math
+    ("b4", {"epi_nostore": True}),       # loads + math, no stores
+    ("b5", {"epi_noload": True, "epi_nostore": True}),   # math alone
+)
+
+
 def _with_knobs(knobs: dict, fn):
     """Run fn() with the layout globals / SCHED entries in `knobs` overridden."""
     g = globals()
@@ -1446,6 +1525,10 @@ def generate() -> str:
         metas.append(meta)
     for vname, knobs in PLAIN_VARIANTS:
         body, meta = _with_knobs(knobs, lambda: kernel("plain", variant=vname))
+        parts.append(body)
+        metas.append(meta)
+    for vname, knobs in SWIGLU_BWD_VARIANTS:
+        body, meta = _with_knobs(knobs, lambda: kernel("swiglu_bwd", variant=vname))
         parts.append(body)
         metas.append(meta)
     import attn_gen   # the attention forward and the weight-gradient kernel share this code object

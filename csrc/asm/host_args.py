@@ -14,9 +14,10 @@ def grid_params(tiles_m: int, tiles_n: int):
 
 
 def pack(X, W, C, S, ldx_b, ldw_b, ldc_b, lds_b, K, tiles_m, tiles_n, fw_b=0, fc_b=0, grid=None,
-         tile_map=MAP_DEFAULT) -> bytes:
+         tile_map=MAP_DEFAULT, phase=0) -> bytes:
     """grid: a persistent kernel's workgroup count; tile_map: the tile order
-    (gemm_gen.KARG "map": log2 group | 16 for column groups)."""
+    (gemm_gen.KARG "map": log2 group | 16 for column groups); phase: the
+    first wave's start offsets (gemm_gen.phase_delay)."""
     nwg, xq, xr, pg = grid_params(tiles_m, tiles_n)
     buf = bytearray(KARG_BYTES)
     struct.pack_into("<QQQQ", buf, KARG["X"], X, W, C, S)
@@ -24,6 +25,7 @@ def pack(X, W, C, S, ldx_b, ldw_b, ldc_b, lds_b, K, tiles_m, tiles_n, fw_b=0, fc
     struct.pack_into("<IIIIII", buf, KARG["ktiles"], K // 64, tiles_m, tiles_n, xq, xr, pg)
     struct.pack_into("<II", buf, KARG["fw"], fw_b, fc_b)
     struct.pack_into("<II", buf, KARG["map"], tile_map, grid or 0)
+    struct.pack_into("<I", buf, KARG["phase"], phase)
     return bytes(buf)
 
 

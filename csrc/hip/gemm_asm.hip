@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_N = 43 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_N = 48 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -54,7 +54,11 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            "toa_attn_dkdv_asm_s1",     "toa_attn_dkdv_asm_s2",       "toa_attn_dkdv_asm_s3",
                            "toa_attn_dkdv_asm_s4",     "toa_attn_dkdv_asm_s5",       "toa_attn_dkdv_asm_s6",
                            // the round-4 SwiGLU epilogues (drain per row block): in-model A/B arms
-                           "toa_gemm_tn_asm_swiglu_fwd_r4", "toa_gemm_tn_asm_swiglu_bwd_r4"};
+                           "toa_gemm_tn_asm_swiglu_fwd_r4", "toa_gemm_tn_asm_swiglu_bwd_r4",
+                           // K_SWBWD_V1 ..: gemm_gen.py SWIGLU_BWD_VARIANTS (diagnostic arms, wrong outputs by design)
+                           "toa_gemm_tn_asm_swiglu_bwd_b1", "toa_gemm_tn_asm_swiglu_bwd_b2",
+                           "toa_gemm_tn_asm_swiglu_bwd_b3", "toa_gemm_tn_asm_swiglu_bwd_b4",
+                           "toa_gemm_tn_asm_swiglu_bwd_b5"};
 
 struct DevModule {
   std::once_flag once;
@@ -87,7 +91,8 @@ struct __attribute__((packed)) Args {
   uint32_t fw, fc;  // swiglu: up-half row offset in W (bytes) / column offset in gu (bytes)
   uint32_t map;     // tile order: log2 group | 16 = column groups walk the rows (gemm_gen.py KARG)
   uint32_t grid;    // persistent kernels: the workgroup count
-  uint32_t pad[2];
+  uint32_t phase;   // first-wave start offsets: n | log2 g << 16 (gemm_gen.py phase_delay; 0 = off)
+  uint32_t pad;
 };
 static_assert(sizeof(Args) == 96, "kernarg block must match csrc/asm/gemm_gen.py KARG_BYTES");
 
@@ -102,11 +107,32 @@ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 constexpr bool kVariantPersist[K_WGRAD_V1 - K_V1] = {false, false, true, false, false, false, false, true};
 constexpr unsigned kPersistGrid = 256;
 
+// First-wave start offsets per kernel family (plain / SwiGLU forward /
+// SwiGLU backward): the phase word of gemm_gen.py phase_delay.  Set by
+// toa_gemm_asm_set_phase (in-process A/B) or TOA_ASM_PHASE_{PLAIN,FWD,BWD}.
+uint32_t g_phase[3] = {0, 0, 0};
+std::once_flag g_phase_env;
+
+uint32_t phase_word(int which) {
+  std::call_once(g_phase_env, [] {
+    const char* names[3] = {"TOA_ASM_PHASE_PLAIN", "TOA_ASM_PHASE_FWD", "TOA_ASM_PHASE_BWD"};
+    for (int i = 0; i < 3; ++i) {
+      const char* e = getenv(names[i]);
+      if (e && *e) g_phase[i] = (uint32_t)strtoul(e, nullptr, 0);
+    }
+  });
+  if (which == K_PLAIN) return g_phase[0];
+  if (which == K_SWIGLU_FWD || which == K_SWIGLU_FWD_R4) return g_phase[1];
+  if (which == K_SWIGLU_BWD || which == K_SWIGLU_BWD_R4) return g_phase[2];
+  return 0;
+}
+
 int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
   hipError_t err;
   hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
   Args k = a;
+  k.phase = phase_word(which);
   size_t sz = sizeof(k);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned nwg = grid ? grid : a.tiles_m * a.tiles_n;
@@ -161,6 +187,16 @@ bool common_ok(int M, int K, int64_t ldx, int64_t ldw, const void* X, const void
 }
 
 }  // namespace
+
+// A/B: the first-wave start offsets of one kernel family (0 plain, 1 SwiGLU
+// forward, 2 SwiGLU backward): word = n | log2 g << 16, each first-wave
+// workgroup sleeping ((b >> 3) mod g) * n * 512 cycles (0 = off).
+extern "C" int toa_gemm_asm_set_phase(int kind, unsigned word) {
+  if (kind < 0 || kind > 2 || (word >> 20) != 0) return (int)hipErrorInvalidValue;
+  phase_word(K_PLAIN);  // env defaults read first, so an explicit setting wins
+  g_phase[kind] = word;
+  return 0;
+}
 
 extern "C" int toa_gemm_asm_available() {
   hipError_t err;
@@ -462,6 +498,22 @@ extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16
   a.lds = (uint32_t)(ldgu * 2);
   a.fc = (uint32_t)(F * 2);
   return launch(g_epi_r4 ? K_SWIGLU_BWD_R4 : K_SWIGLU_BWD, a, stream);
+}
+
+// DIAGNOSTIC: arm v (1..) of the fused SwiGLU backward (gemm_gen.py
+// SWIGLU_BWD_VARIANTS: the main loop alone, no loads, no math, no stores),
+// same arguments and checks as toa_gemm_asm_swiglu_bwd; v = 0 the product.
+extern "C" int toa_gemm_asm_swiglu_bwd_variant(int v, const bf16_t* dY, int64_t ldy, const bf16_t* WdT, int64_t ldw,
+                                               const bf16_t* GU, int64_t ldgu, bf16_t* dGU, int64_t lddgu, int M,
+                                               int F, int K, hipStream_t stream) {
+  if (v < 0 || v > K_N - K_SWBWD_V1 || !common_ok(M, K, ldy, ldw, dY, WdT) || F <= 0 || F % 256 ||
+      !ld_ok(ldgu, 2 * F) || !ld_ok(lddgu, 2 * F) || !al16(GU) || !al16(dGU))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(dY, ldy, WdT, ldw, dGU, lddgu, M, F / 256, K);
+  a.S = (uint64_t)GU;
+  a.lds = (uint32_t)(ldgu * 2);
+  a.fc = (uint32_t)(F * 2);
+  return launch(v == 0 ? K_SWIGLU_BWD : K_SWBWD_V1 + v - 1, a, stream);
 }
 
 // Causal flash-attention dK / dV backward of the dS form (csrc/asm/attn_bwd_gen.py),

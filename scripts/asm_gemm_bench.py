@@ -49,6 +49,23 @@ def asm_swiglu_bwd(d2, wdt, gu):
     return dgu
 
 
+def with_phase(kind, word, fn):
+    """Run fn with the first-wave start offsets of kernel family `kind`
+    (0 plain, 1 SwiGLU fwd, 2 SwiGLU bwd) set to `word` (gemm_gen.phase_delay),
+    then back to 0."""
+    _lib.call("toa_gemm_asm_set_phase", kind, word)
+    try:
+        return fn()
+    finally:
+        _lib.call("toa_gemm_asm_set_phase", kind, 0)
+
+
+def asm_swiglu_bwd_variant(v, d2, wdt, gu, dgu):
+    M, F = d2.shape[0], wdt.shape[0]
+    _lib.call("toa_gemm_asm_swiglu_bwd_variant", v, _lib.ptr(d2), d2.stride(0), _lib.ptr(wdt), wdt.stride(0),
+              _lib.ptr(gu), 2 * F, _lib.ptr(dgu), 2 * F, M, F, d2.shape[1], _lib.stream(d2))
+
+
 def asm_variant(v, x, w, y):
     M, K = x.shape
     N = w.shape[0]
@@ -321,6 +338,7 @@ def bench(a):
     out = {"tokens": T, "forms": {}}
     variants = [int(v) for v in a.variants.split(",") if v]
     maps = [int(v) for v in a.maps.split(",") if v]
+    phases = [int(v, 0) for v in a.phases.split(",") if v]
     for name, (K, N) in FORMS.items():
         for kind, (kk, nn) in (("fwd", (K, N)), ("dgrad_wt", (N, K))):
             if a.forms and f"{name}.{kind}" not in a.forms.split(","):
@@ -336,6 +354,8 @@ def bench(a):
                 arms.append((f"asm_v{v}", lambda v=v: asm_variant(v, x, w, yv)))
             for tm_ in maps:
                 arms.append((f"asm_map{tm_}", lambda tm_=tm_: asm_map(tm_, x, w, yv)))
+            for ph in phases:
+                arms.append((f"asm_ph{ph:#x}", lambda ph=ph: with_phase(0, ph, lambda: asm(x, w, yv))))
             ts = {k: [] for k, _ in arms}
             for _ in range(a.rounds):
                 for k, f in arms:
@@ -348,6 +368,9 @@ def bench(a):
             for tm_ in maps:
                 asm_map(tm_, x, w, yv)
                 same[f"asm_map{tm_}"] = bool(torch.equal(y, yv))
+            for ph in phases:
+                with_phase(0, ph, lambda: asm(x, w, yv))
+                same[f"asm_ph{ph:#x}"] = bool(torch.equal(y, yv))
             err = rel(y, x.float() @ w.float().t()) if T * nn <= 24576 * 28672 else -1.0
             fl = 2.0 * T * nn * kk
             rec = {k: {"ms": round(statistics.median(v), 4), "TFps": round(fl / statistics.median(v) / 1e9, 1)}
@@ -370,11 +393,24 @@ def bench(a):
                 ("blt_unfused_fwd", lambda: (gemm.set_mode("nosk"), llm.swiglu(gemm.linear_fwd(x, wgu)))),
                 ("asm_fused_bwd", lambda: asm_swiglu_bwd(d2, wdt, gu)),
                 ("blt_unfused_bwd", lambda: (gemm.set_mode("nosk"), llm.swiglu_bwd(gemm.linear_fwd(d2, wdt), gu)))]
+        dgu_v = torch.empty_like(gu)
+        for v in [int(t) for t in a.swiglu_variants.split(",") if t]:
+            arms.append((f"asm_fused_bwd_b{v}", lambda v=v: asm_swiglu_bwd_variant(v, d2, wdt, gu, dgu_v)))
+        for ph in phases:
+            arms += [(f"asm_fused_fwd_ph{ph:#x}", lambda ph=ph: with_phase(1, ph, lambda: asm_swiglu(x, wgu))),
+                     (f"asm_fused_bwd_ph{ph:#x}", lambda ph=ph: with_phase(2, ph, lambda: asm_swiglu_bwd(d2, wdt, gu)))]
         ts = {k: [] for k, _ in arms}
         for _ in range(a.rounds):
             for k, f in arms:
                 ts[k].append(timer(f, a.reps))
         out["mlp_ms"] = {k: round(statistics.median(v), 4) for k, v in ts.items()}
+        if phases:   # the start offsets change when a tile runs, never what it computes
+            ref_f, ref_b = asm_swiglu(x, wgu), asm_swiglu_bwd(d2, wdt, gu)
+            out["mlp_phase_bit_identical"] = {
+                f"{ph:#x}": bool(all(torch.equal(p_, q_) for p_, q_ in zip(
+                    with_phase(1, ph, lambda: asm_swiglu(x, wgu)), ref_f))
+                    and torch.equal(with_phase(2, ph, lambda: asm_swiglu_bwd(d2, wdt, gu)), ref_b))
+                for ph in phases}
         print(json.dumps({"mlp_ms": out["mlp_ms"]}), flush=True)
     print(json.dumps(out))
 
@@ -392,6 +428,10 @@ def main():
     ap.add_argument("--mlp", type=int, default=1)
     ap.add_argument("--variants", default="", help="plain-kernel A/B arms to add, e.g. 1,2,3")
     ap.add_argument("--maps", default="", help="tile orders to add as arms (kernarg map words, e.g. 2,3,18,20)")
+    ap.add_argument("--swiglu-variants", default="", help="fused SwiGLU backward diagnostic arms (1..5) "
+                                                          "added to the MLP arms (gemm_gen.SWIGLU_BWD_VARIANTS)")
+    ap.add_argument("--phases", default="", help="first-wave start-offset words to add as arms (n | log2 g << 16, "
+                                                 "e.g. 0x10028,0x20014): plain forms and the fused MLP")
     ap.add_argument("--timing", action="store_true", help="wait-cycle breakdown of the product kernel (--forms)")
     ap.add_argument("--wgrad", action="store_true", help="weight-gradient forms: asm NT vs HIP vs hipBLASLt")
     ap.add_argument("--wgrad-splits", default="", help="extra asm arms with every tile cut into S K-pieces, e.g. 1,2,3")

@@ -48,6 +48,10 @@ def apply(arm: str):
             _lib.call("toa_attn_set_dkdv_variant", int(val))
         elif key == "epi":   # the fused SwiGLU GEMMs' epilogues: r4 (drained per row block) or pipe
             _lib.call("toa_gemm_asm_set_epi_variant", 1 if val == "r4" else 0)
+        elif key == "mlpov":   # the MLP backward's down wgrad on a side stream (ops.llm.set_mlp_overlap)
+            from tf_operator_amd.ops import llm
+
+            llm.set_mlp_overlap(val == "1")
         elif key == "adamcap":
             _lib.call_ret("toa_set_stream_variant", 1 | 2 | (int(val) << 8))
         else:

@@ -121,6 +121,28 @@ def test_asm_gemm_timing_kernel_emulated():
     assert (rec[:, :, 3] > 0).all() and (rec[:, :, 4] > 0).all()
 
 
+@pytest.mark.parametrize("phase", [0x10003, 0x20001])
+def test_asm_gemm_phase_offsets_same_output(phase):
+    """The first wave's start offsets (gemm_gen.phase_delay) change only when
+    a workgroup starts: C is the product kernel's bit for bit (the grid spans
+    three phase groups, so the sleep loop runs for some workgroups)."""
+    rng = np.random.default_rng(19)
+    M, N, K = 512, 2560, 128      # 20 workgroups: groups (b >> 3) 0, 1, 2
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)))
+    outs, slept = [], []
+    for ph in (0, phase):
+        mem = emu.Memory()
+        ax, aw, ac = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16))
+        karg = host_args.pack(ax, aw, ac, 0, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256, phase=ph)
+        e = emu.Emu(TEXT, "toa_gemm_tn_asm_plain")
+        for wg in range((M // 256) * (N // 256)):
+            e.run(karg, wg, mem)
+        outs.append(mem.bufs[2][1].view(np.uint16).reshape(M, N).copy())
+    assert np.array_equal(outs[0], outs[1])
+    close(tof(outs[0]), tof(X) @ tof(W).T)
+
+
 def test_asm_gemm_strided_rows_emulated():
     """ld > K on both operands and an output view with ld > N, offset columns."""
     rng = np.random.default_rng(7)
@@ -243,9 +265,9 @@ def test_host_kernel_table_matches_generator():
     # + the weight gradient's round-4 arm + the attention forward and its arms + the dK/dV backward
     import attn_bwd_gen
     import attn_gen
-    # + the round-4 SwiGLU epilogue arms (2)
+    # + the round-4 SwiGLU epilogue arms (2) + the SwiGLU backward's diagnostic arms
     assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
-        len(attn_bwd_gen.VARIANTS) + 2
+        len(attn_bwd_gen.VARIANTS) + 2 + len(gemm_gen.SWIGLU_BWD_VARIANTS)
     flags = re.search(r"kVariantPersist\[K_WGRAD_V1 - K_V1\] = \{([^}]*)\}", src).group(1)
     assert [f.strip() == "true" for f in flags.split(",")] == [bool(k.get("persist")) for _, k in gemm_gen.PLAIN_VARIANTS]
 

@@ -386,10 +386,14 @@ def set_wgrad_kernel(name: str):
 
 
 def _workspace(dev, nbytes):
-    t = _ws.get(dev)
+    """Split-K partials scratch, one per (device, stream): a weight gradient
+    on a side stream (ops.llm set_mlp_overlap) must not share it with one on
+    the main stream."""
+    key = (dev, torch.cuda.current_stream(dev).stream_id if torch.device(dev).type == "cuda" else 0)
+    t = _ws.get(key)
     if t is None or t.numel() * 4 < nbytes:
         t = torch.empty((nbytes + 3) // 4, device=dev, dtype=torch.float32)
-        _ws[dev] = t
+        _ws[key] = t
     return t
 
 
