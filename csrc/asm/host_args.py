@@ -63,13 +63,15 @@ def wgrad_plan(M: int, N: int, K: int) -> tuple[int, int]:
     return (tiles, 1) if best == 1 else (tiles - rem, best)
 
 
-def pack_nt(A, B, C, WS, lda_b, ldb_b, ldc_b, beta, K, tiles_m, tiles_n, full, split) -> bytes:
+def pack_nt(A, B, C, WS, lda_b, ldb_b, ldc_b, beta, K, tiles_m, tiles_n, full, split, tile_map=3) -> bytes:
     """The weight-gradient kernel's block (csrc/asm/wgrad_gen.py KARG): the
-    same 80 bytes, with beta / full / rem / split in the forward kernels'
-    lds / xq / xr / per_group slots."""
+    same bytes, with beta / full / rem / split in the forward kernels'
+    lds / xq / xr / per_group slots and the tile order in the map slot
+    (wgrad_gen.MAP_DEFAULT = 3: groups of 8 row tiles walk the columns)."""
     rem = tiles_m * tiles_n - full
     buf = bytearray(KARG_BYTES)
     struct.pack_into("<QQQQ", buf, 0, A, B, C, WS)
     struct.pack_into("<IIII", buf, 32, lda_b, ldb_b, ldc_b, beta)
     struct.pack_into("<IIIIII", buf, 48, K // 64, tiles_m, tiles_n, full, rem, split)
+    struct.pack_into("<I", buf, KARG["map"], tile_map)
     return bytes(buf)

@@ -69,7 +69,8 @@ def pos(r: int, c: int) -> int:
 
 # kernarg block (byte offsets)
 KARG = {"A": 0, "B": 8, "C": 16, "WS": 24, "lda": 32, "ldb": 36, "ldc": 40, "beta": 44, "ktiles": 48,
-        "tiles_m": 52, "tiles_n": 56, "full": 60, "rem": 64, "split": 68}
+        "tiles_m": 52, "tiles_n": 56, "full": 60, "rem": 64, "split": 68, "map": 80}
+MAP_DEFAULT = 3     # groups of 8 row tiles (dW rows) walk the column tiles: the round-4/5 order
 
 # SGPRs
 S_A, S_B, S_C, S_WS = 4, 6, 8, 10
@@ -86,7 +87,8 @@ S_E0, S_E1 = 67, 68
 S_Q, S_R = 69, 70
 S_S, S_J, S_PIECE = 71, 72, 73   # k-piece index, tail tile index, 1 for a k-piece workgroup
 S_ADVA, S_ADVB, S_KTP = 74, 75, 76   # 64 lda, 64 ldb, k-tiles of this workgroup
-N_SGPR = 78
+S_MAPW, S_LG, S_WALK = 77, 78, 79    # kernarg tile order (gemm_gen.KARG "map"): word, log2 group, walk flag
+N_SGPR = 80
 
 # VGPRs
 V_DA, V_RALO, V_RAHI = 1, 2, 3
@@ -105,6 +107,7 @@ KNOBS = {"map": "lib0", "zero_late": True}
 def prologue(a: Asm):
     a(f"s_load_dwordx16 {sr(4, 16)}, s[0:1], 0x0")
     a(f"s_load_dwordx4 {sr(20, 4)}, s[0:1], 0x40")
+    a(f"s_load_dword {sr(S_MAPW)}, s[0:1], {KARG['map']:#x}")
     a("s_mov_b32 m0, 0")
     a(f"v_mov_b32 {vr(V_TID)}, v0")
     a("s_waitcnt lgkmcnt(0)")
@@ -144,16 +147,32 @@ def prologue(a: Asm):
     a.label(l_done)
     a(f"s_cmp_lt_u32 {sr(S_KTP)}, 2")
     a(f"s_cbranch_scc1 {a.abort}")
-    # --- tile -> (tm, tn): groups of 8 row tiles walk the column tiles
-    a(f"s_lshl_b32 {sr(S_T3)}, {sr(S_TN_N)}, 3")
+    # --- tile -> (tm, tn) by the kernarg map (the TN kernels' encoding,
+    # gemm_gen.tile_setup): groups of 2^lg tiles of the grouped dimension
+    # (rows of dW; columns when the walk bit is set) walk the other one.
+    # A word the host never packs (lg > 6, bits above the walk flag) ends
+    # the workgroup before any memory access.
+    a(f"s_and_b32 {sr(S_LG)}, {sr(S_MAPW)}, 15")
+    a(f"s_cmp_gt_u32 {sr(S_LG)}, 6")
+    a(f"s_cbranch_scc1 {a.abort}")
+    a(f"s_cmp_ge_u32 {sr(S_MAPW)}, 32")
+    a(f"s_cbranch_scc1 {a.abort}")
+    a(f"s_lshr_b32 {sr(S_WALK)}, {sr(S_MAPW)}, 4")
+    a(f"s_cmp_eq_u32 {sr(S_WALK)}, 0")
+    a(f"s_cselect_b32 {sr(S_E0)}, {sr(S_TM_N)}, {sr(S_TN_N)}")   # grouped count
+    a(f"s_cselect_b32 {sr(S_E1)}, {sr(S_TN_N)}, {sr(S_TM_N)}")   # walked count
+    a(f"s_lshl_b32 {sr(S_T3)}, {sr(S_E1)}, {sr(S_LG)}")          # tiles per group
     G.udiv(a, S_Q, S_R, S_TILE, S_T3)
-    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, 3")          # first_m
-    a(f"s_sub_u32 {sr(S_T1)}, {sr(S_TM_N)}, {sr(S_T0)}")
-    a(f"s_min_u32 {sr(S_T1)}, {sr(S_T1)}, 8")
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_Q)}, {sr(S_LG)}")          # first grouped tile
+    a(f"s_sub_u32 {sr(S_T1)}, {sr(S_E0)}, {sr(S_T0)}")
+    a(f"s_lshl_b32 {sr(S_T2)}, 1, {sr(S_LG)}")
+    a(f"s_min_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_T2)}")          # this group's size
     a(f"s_mov_b32 {sr(S_T2)}, {sr(S_R)}")
     G.udiv(a, S_Q, S_R, S_T2, S_T1)
-    a(f"s_add_u32 {sr(S_TM)}, {sr(S_T0)}, {sr(S_R)}")
-    a(f"s_mov_b32 {sr(S_TN)}, {sr(S_Q)}")
+    a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_R)}")           # grouped-dimension tile
+    a(f"s_cmp_eq_u32 {sr(S_WALK)}, 0")
+    a(f"s_cselect_b32 {sr(S_TM)}, {sr(S_T0)}, {sr(S_Q)}")
+    a(f"s_cselect_b32 {sr(S_TN)}, {sr(S_Q)}, {sr(S_T0)}")
 
     # --- buffer resources: 64 rows x 256 columns from row k_begin, column 256 tm / tn
     a(f"s_mul_i32 {sr(S_T3)}, {sr(S_S)}, {sr(S_KTP)}")

@@ -316,11 +316,41 @@ extern "C" int toa_gemm_asm_probe(void* out, const bf16_t* X, int64_t ldx, const
 // pieces' fp32 partials (workspace W, toa_wgrad_workspace bytes) are summed in
 // a fixed order by wgrad.hip's reduce kernel.
 extern "C" int toa_wgrad_split(int M, int N, int K);
-extern "C" int toa_wgrad_reduce(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem, int split,
-                                int beta, hipStream_t stream);
+extern "C" int toa_wgrad_reduce_map(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem,
+                                    int split, int beta, unsigned map, hipStream_t stream);
 
 static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C,
                             int64_t ldc, float* W, int M, int N, int K, int split, int beta, hipStream_t stream);
+
+// Tile order of the weight-gradient kernel (wgrad_gen.py, the TN kernels'
+// map encoding), per shape from the in-process sweep of round 6
+// (profiles/r6_wmap; scripts/asm_gemm_bench.py --wgrad --wgrad-maps):
+//   * 3 = groups of 8 row (dW row) tiles walking the column tiles: the
+//     round-4/5 order, kept where nothing measured faster (qkv, o, down);
+//   * tall outputs (tiles_m >= 4 tiles_n) with at most 8 waves of tiles
+//     (gate|up: 112 x 16): 18 = groups of 4 COLUMN tiles walking all the row
+//     tiles, 3.85 vs 3.97 ms (-3.2 %);
+//   * tall outputs with many waves (lm_head: 501 x 16): 2 = row groups of
+//     4, 17.50 vs 17.86 ms (-2.0 %).
+// toa_wgrad_asm_set_map forces one (in-process A/B; -1 = this rule), as does
+// TOA_WGRAD_TILE_MAP.
+static int g_wgrad_map_forced = -2;  // -2: TOA_WGRAD_TILE_MAP not read yet
+static uint32_t wgrad_tile_map(int tiles_m, int tiles_n) {
+  if (g_wgrad_map_forced == -2) {
+    const char* e = getenv("TOA_WGRAD_TILE_MAP");
+    const int v = (e && *e) ? atoi(e) : -1;
+    g_wgrad_map_forced = (v >= 0 && v < 32 && (v & 15) <= 6) ? v : -1;
+  }
+  if (g_wgrad_map_forced >= 0) return (uint32_t)g_wgrad_map_forced;
+  const int64_t tiles = (int64_t)tiles_m * tiles_n;
+  if (tiles_m >= 4 * tiles_n) return tiles <= 8 * 256 ? 18u : 2u;
+  return 3u;
+}
+extern "C" int toa_wgrad_asm_set_map(int map) {
+  if (map < -1 || map >= 32 || (map >= 0 && (map & 15) > 6)) return (int)hipErrorInvalidValue;
+  g_wgrad_map_forced = map;
+  return 0;
+}
 
 extern "C" int toa_wgrad_asm(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc,
                              float* W, int M, int N, int K, int split, int beta, hipStream_t stream) {
@@ -370,6 +400,7 @@ static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_
   a.xq = (uint32_t)full;
   a.xr = (uint32_t)rem;
   a.per_group = (uint32_t)split;
+  a.map = wgrad_tile_map(M / 256, N / 256);
   hipError_t err;
   hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
@@ -378,7 +409,7 @@ static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_
   const unsigned nwg = (unsigned)(full + (split > 1 ? rem * split : 0));
   err = hipModuleLaunchKernel(fn, nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
   if (err != hipSuccess) return (int)err;
-  if (split > 1 && rem > 0) return toa_wgrad_reduce(W, C, ldc, M, N, full, rem, split, beta, stream);
+  if (split > 1 && rem > 0) return toa_wgrad_reduce_map(W, C, ldc, M, N, full, rem, split, beta, a.map, stream);
   return 0;
 }
 

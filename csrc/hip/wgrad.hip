@@ -105,6 +105,22 @@ __device__ __forceinline__ void wg_tile_coords(int tile, int tiles_m, int tiles_
   *tn = (tile - group * per_group) / gsz;
 }
 
+// The tile order of the assembly NT kernel's `map` word (csrc/asm/wgrad_gen.py,
+// the TN kernels' encoding): groups of 2^lg tiles of the grouped dimension
+// (rows; columns when bit 4 is set) walk the other one.  map 3 is
+// wg_tile_coords' order.
+__device__ __forceinline__ void wg_tile_coords_map(int tile, int tiles_m, int tiles_n, unsigned map, int* tm,
+                                                   int* tn) {
+  const int lg = (int)(map & 15u);
+  const bool walk = (map >> 4) & 1u;
+  const int a_n = walk ? tiles_n : tiles_m, b_n = walk ? tiles_m : tiles_n;
+  const int per = b_n << lg, group = tile / per, within = tile - group * per;
+  const int first = group << lg, gsz = min(a_n - first, 1 << lg);
+  const int ta = first + within % gsz, tb = within / gsz;
+  *tm = walk ? tb : ta;
+  *tn = walk ? ta : tb;
+}
+
 __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restrict__ A, int64_t lda,
                                                           const bf16_t* __restrict__ B, int64_t ldb,
                                                           bf16_t* __restrict__ C, int64_t ldc, float* __restrict__ W,
@@ -244,10 +260,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
 // Tail tile j of `rem`: C = (beta ? C : 0) + sum_s W[s][j], summed in split order.
 __global__ __launch_bounds__(256) void wgrad_tile_reduce_kernel(const float* __restrict__ W, bf16_t* __restrict__ C,
                                                                 int64_t ldc, int M, int N, int full, int rem,
-                                                                int split, int beta) {
+                                                                int split, int beta, unsigned map) {
   const int j = blockIdx.x;
   int tm, tn;
-  wg_tile_coords(full + j, M / WG_BM, N / WG_BN, &tm, &tn);
+  wg_tile_coords_map(full + j, M / WG_BM, N / WG_BN, map, &tm, &tn);
   for (int e = threadIdx.x; e < WG_BM * WG_BN / 8; e += 256) {
     const int row = e / (WG_BN / 8), col = (e % (WG_BN / 8)) * 8;
     bf16_t* p = C + (int64_t)(tm * WG_BM + row) * ldc + tn * WG_BN + col;
@@ -295,11 +311,18 @@ static void wg_plan(int M, int N, int K, int* full, int* split) {
 // The reduce kernel of a split plan, for the assembly NT kernel
 // (csrc/hip/gemm_asm.hip toa_wgrad_asm), which writes the same tile-major
 // fp32 partials.
+// map: the tile order the pieces were computed in (wg_tile_coords_map).
+extern "C" int toa_wgrad_reduce_map(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem,
+                                    int split, int beta, unsigned map, hipStream_t stream) {
+  if (rem <= 0 || split < 2 || W == nullptr || map >= 32u || (map & 15u) > 6u) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split, beta,
+                     map);
+  return (int)hipGetLastError();
+}
+
 extern "C" int toa_wgrad_reduce(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem, int split,
                                 int beta, hipStream_t stream) {
-  if (rem <= 0 || split < 2 || W == nullptr) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split, beta);
-  return (int)hipGetLastError();
+  return toa_wgrad_reduce_map(W, C, ldc, M, N, full, rem, split, beta, 3u, stream);
 }
 
 // Auto plan's split factor (1 = no split-K at all).
@@ -342,6 +365,6 @@ extern "C" int toa_wgrad(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t 
                      beta);
   if (split > 1 && rem > 0)
     hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split,
-                       beta);
+                       beta, 3u);
   return (int)hipGetLastError();
 }

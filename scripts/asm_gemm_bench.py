@@ -288,6 +288,19 @@ def wgrad(a):
                       K, T, 0, 0, _lib.stream(dy))
 
         arms = [("asm", asm_), ("asm_v1", asm_v1), ("hip", hip), ("blt", lambda: torch.mm(dy.t(), x))]
+        g4 = torch.empty_like(g)
+
+        def mapped(tm_):   # the product kernel with another tile order (toa_wgrad_asm_set_map)
+            _lib.call("toa_wgrad_asm_set_map", tm_)
+            try:
+                _lib.call("toa_wgrad_asm", _lib.ptr(dy), N, _lib.ptr(x), K, _lib.ptr(g4), K, _lib.ptr(ws), N, K, T,
+                          0, 0, _lib.stream(dy))
+            finally:
+                _lib.call("toa_wgrad_asm_set_map", -1)
+
+        wmaps = [int(v) for v in a.wgrad_maps.split(",") if v]
+        for tm_ in wmaps:
+            arms.append((f"asm_map{tm_}", lambda tm_=tm_: mapped(tm_)))
         for sp in (int(v) for v in a.wgrad_splits.split(",") if v):
             # every tile cut into `sp` K-pieces (1: none) instead of the auto plan
             if sp * (N // 256) * (K // 256) >= (1 << 14) or T % (64 * sp):
@@ -314,6 +327,10 @@ def wgrad(a):
         asm_v1()
         torch.cuda.synchronize()
         rec["asm_v1_bit_identical"] = bool(torch.equal(g, g3))
+        for tm_ in wmaps:
+            mapped(tm_)
+            torch.cuda.synchronize()
+            rec[f"asm_map{tm_}_bit_identical"] = bool(torch.equal(g, g4))
         res[f"{name}.wgrad"] = rec
         print(json.dumps({f"{name}.wgrad": rec}), flush=True)
         del dy, x, g, g2, ws
@@ -434,6 +451,9 @@ def main():
                                                  "e.g. 0x10028,0x20014): plain forms and the fused MLP")
     ap.add_argument("--timing", action="store_true", help="wait-cycle breakdown of the product kernel (--forms)")
     ap.add_argument("--wgrad", action="store_true", help="weight-gradient forms: asm NT vs HIP vs hipBLASLt")
+    ap.add_argument("--wgrad-maps", default="", help="weight-gradient tile orders as extra arms (map words: "
+                                                     "log2 group | 16 for column groups; the per-shape default "
+                                                     "is gemm_asm.hip wgrad_tile_map)")
     ap.add_argument("--wgrad-splits", default="", help="extra asm arms with every tile cut into S K-pieces, e.g. 1,2,3")
     a = ap.parse_args()
     if a.probe:

@@ -8,6 +8,7 @@ An arm is settings joined by '+': wgrad=asm|hip|asm_v1 (ops.gemm.set_wgrad_kerne
 gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy), attnf=N /
 attnb=N / attnd=N (toa_attn_set_fwd_variant / _bwd_variant / _dkdv_variant forms),
 epi=r4|pipe (the fused SwiGLU GEMMs' epilogues, toa_gemm_asm_set_epi_variant),
+wmap=N (the weight-gradient tile order, toa_wgrad_asm_set_map; -1 = the per-shape rule),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -48,10 +49,8 @@ def apply(arm: str):
             _lib.call("toa_attn_set_dkdv_variant", int(val))
         elif key == "epi":   # the fused SwiGLU GEMMs' epilogues: r4 (drained per row block) or pipe
             _lib.call("toa_gemm_asm_set_epi_variant", 1 if val == "r4" else 0)
-        elif key == "mlpov":   # the MLP backward's down wgrad on a side stream (ops.llm.set_mlp_overlap)
-            from tf_operator_amd.ops import llm
-
-            llm.set_mlp_overlap(val == "1")
+        elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
+            _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":
             _lib.call_ret("toa_set_stream_variant", 1 | 2 | (int(val) << 8))
         else:

@@ -116,3 +116,49 @@ def test_wgrad_round4_arm_matches_product_kernel():
             e.run(karg, wg, mem)
         outs.append(mem.bufs[3][1].copy())
     assert np.array_equal(outs[0], outs[1])
+
+
+def _map_coords(t, tm_n, tn_n, tile_map):
+    """wgrad_gen / wgrad.hip wg_tile_coords_map: tile index -> (tm, tn)."""
+    lg, walk = tile_map & 15, tile_map >> 4
+    a_n, b_n = (tn_n, tm_n) if walk else (tm_n, tn_n)
+    group, within = divmod(t, b_n << lg)
+    first = group << lg
+    gsz = min(a_n - first, 1 << lg)
+    ta, tb = first + within % gsz, within // gsz
+    return (tb, ta) if walk else (ta, tb)
+
+
+@pytest.mark.parametrize("tile_map", [0, 2, 18, 20])
+def test_wgrad_tile_maps_same_output(tile_map):
+    """Other tile orders of the weight-gradient kernel (kernarg map, the TN
+    kernels' encoding) give the default order's result bit for bit: whole-K
+    tiles write the same C, and the k-pieces' fp32 partials -- slot j holding
+    tail tile full + j of the ORDER, which the map-aware reduce kernel places
+    by the same map -- assemble the same sums."""
+    M, N, T = 768, 512, 256
+    tm_n, tn_n = M // 256, N // 256
+    rng = np.random.default_rng(23)
+    A = bf16(rng.standard_normal((T, M)))
+    B = bf16(rng.standard_normal((T, N)))
+    outs = []
+    for tmap, (full, sp) in ((3, (6, 1)), (tile_map, (6, 1)), (3, (0, 2)), (tile_map, (0, 2))):
+        mem = emu.Memory()
+        aa, ab, ac = mem.add(A), mem.add(B), mem.add(np.zeros((M, N), np.uint16))
+        aw = mem.add(np.zeros(6 * 2 * 65536, np.float32))
+        karg = host_args.pack_nt(aa, ab, ac, aw, 2 * M, 2 * N, 2 * N, 0, T, tm_n, tn_n, full, sp,
+                                 tile_map=tmap)
+        e = emu.Emu(TEXT, "toa_wgrad_nt_asm")
+        for wg in range(full + (6 - full) * sp):
+            e.run(karg, wg, mem)
+        if sp == 1:
+            outs.append(mem.bufs[2][1].copy())
+            continue
+        ws = mem.bufs[3][1].view(np.float32).reshape(sp, 6, 256, 256)
+        C = np.zeros((M, N), np.float32)
+        for j in range(6):
+            tm, tn = _map_coords(full + j, tm_n, tn_n, tmap)
+            C[256 * tm:256 * tm + 256, 256 * tn:256 * tn + 256] = ws[0, j] + ws[1, j]
+        outs.append(C)
+    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[2], outs[3])

@@ -159,23 +159,6 @@ def swiglu_down(gu, wd):
     return _SwiGLUDown.apply(gu, wd)
 
 
-# TOA_MLP_OVERLAP=1: the MLP backward's down-projection weight gradient on a
-# side stream, overlapping the fused SwiGLU backward GEMM (set_mlp_overlap)
-_MLP_OVERLAP = [os.environ.get("TOA_MLP_OVERLAP", "0") == "1"]
-_SIDE = {}
-
-
-def set_mlp_overlap(on: bool):
-    _MLP_OVERLAP[0] = bool(on)
-
-
-def _side_stream(dev):
-    st = _SIDE.get(dev)
-    if st is None:
-        st = _SIDE[dev] = torch.cuda.Stream(device=dev)
-    return st
-
-
 class _SwiGLUMLP(torch.autograd.Function):
     """out = swiglu(x Wgu^T) Wd^T with the SwiGLU fused into the GEMMs
     (ops/gemm.py ``swiglu_gate_up`` / ``swiglu_down_dgrad``,
@@ -199,28 +182,7 @@ class _SwiGLUMLP(torch.autograd.Function):
     def backward(ctx, dout):
         x, wgu, wd, gu, s = ctx.saved_tensors
         d2 = dout.reshape(-1, dout.shape[-1])
-        side_done = None
-        if _MLP_OVERLAP[0] and d2.is_cuda and getattr(wd, "main_grad", None) is not None:
-            # the down projection's weight gradient (MFMA-bound, little HBM
-            # traffic) on a side stream, beside the fused SwiGLU backward GEMM
-            # whose epilogue is an HBM burst with the matrix cores idle: the
-            # two kernels' workgroups share the CUs
-            cur = torch.cuda.current_stream(d2.device)
-            side = _side_stream(d2.device)
-            side.wait_stream(cur)
-            hook = wd.__dict__.pop("_toa_ready", None)   # fired once the main stream has waited
-            try:
-                with torch.cuda.stream(side):
-                    dwd = accumulate_mm(wd, d2.t(), s)
-                    side_done = torch.cuda.Event()
-                    side_done.record(side)
-            finally:
-                if hook is not None:
-                    wd._toa_ready = hook
-            s.record_stream(side)
-            dout.record_stream(side)
-        else:
-            dwd = accumulate_mm(wd, d2.t(), s)
+        dwd = accumulate_mm(wd, d2.t(), s)
         del s
         dgu = gemm.swiglu_down_dgrad(d2, wd, gu)
         if dgu is None:
@@ -229,11 +191,6 @@ class _SwiGLUMLP(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         dx = gemm.linear_dgrad(dgu, wgu).view_as(x) if ctx.needs_input_grad[0] else None
         dwgu = accumulate_mm(wgu, dgu.t(), x2)
-        if side_done is not None:
-            torch.cuda.current_stream(d2.device).wait_event(side_done)
-            hook = getattr(wd, "_toa_ready", None)
-            if hook is not None:
-                hook(wd)
         return dx, dwgu, dwd
 
 
