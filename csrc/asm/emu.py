@@ -586,7 +586,8 @@ class Emu:
         d0, d1 = self.vrange(w, a[0])
         a0, a1 = self.vrange(w, a[1])
         b0, b1 = self.vrange(w, a[2])
-        c0, c1 = self.vrange(w, a[3])
+        c_zero = a[3] == "0"          # srcC may be the inline constant 0
+        c0, c1 = (0, 4) if c_zero else self.vrange(w, a[3])
         assert d1 - d0 == 4 and a1 - a0 == 4 and b1 - b0 == 4 and c1 - c0 == 4
 
         def elems(r0):  # [64 lanes, 8] bf16 -> f32
@@ -605,7 +606,7 @@ class Emu:
             A[l & 15, 8 * (l >> 4): 8 * (l >> 4) + 8] = ea[l]
             B[8 * (l >> 4): 8 * (l >> 4) + 8, l & 15] = eb[l]
         D = A.astype(np.float64) @ B.astype(np.float64)
-        C = u2f(w.v[c0:c0 + 4]).astype(np.float64)     # [4, 64]
+        C = np.zeros((4, 64)) if c_zero else u2f(w.v[c0:c0 + 4]).astype(np.float64)     # [4, 64]
         out = np.empty((4, 64), np.float64)
         for l in range(64):
             for r in range(4):

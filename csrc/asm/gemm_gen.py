@@ -115,6 +115,9 @@ S_Q, S_R = 69, 70   # division results
 # barrier, W-free barrier), s88..s89 the kernel's start stamp
 S_TMT, S_ACC, S_T_START = 72, 84, 88
 S_ITER, S_GRID = 90, 91   # persistent arms: this workgroup's tile-order index, the grid size
+# deferred-store arm (SCHED "defer", never with the timing kernel, whose stamps
+# use s72..s89): the previous tile's C resource, its row-block offset and step
+SRD_D, S_DOFF, S_DSTEP = 72, 76, 77
 S_MAP, S_KGRID = 92, 93   # kernarg map / grid words (s94, s95: the map's decoded log2 group, walk flag)
 S_LG, S_WALK = 94, 95
 N_SGPR = 96
@@ -474,11 +477,13 @@ def frag_read(kind: str, f: int, sub: int) -> str:
     return f"ds_read_b128 {vr(dst + 4 * f, 4)}, {vr(base)} offset:{off}"
 
 
-def mfma(i: int, j: int, sub: int) -> str:
+def mfma(i: int, j: int, sub: int, czero: bool = False) -> str:
+    """czero: the accumulator starts at 0 (srcC = inline 0: the tile's first
+    k-step, no zeroing pass)."""
     fw = (V_FW0 if sub == 0 else V_FW1) + 4 * i
     fx = (V_FX0 if sub == 0 else V_FX1) + 4 * j
     acc = 4 * (8 * i + j)
-    return f"v_mfma_f32_16x16x32_bf16 {ar(acc, 4)}, {vr(fw, 4)}, {vr(fx, 4)}, {ar(acc, 4)}"
+    return f"v_mfma_f32_16x16x32_bf16 {ar(acc, 4)}, {vr(fw, 4)}, {vr(fx, 4)}, {'0' if czero else ar(acc, 4)}"
 
 
 # schedule knobs of the main loop (A/B arms: PLAIN_VARIANTS)
@@ -490,7 +495,10 @@ SCHED = {"dma_gap": 4, "prio": False, "wait_slot": 95, "read_gap": 1, "group": 4
          # DIAGNOSTIC arms of the SwiGLU backward epilogue (SWIGLU_BWD_VARIANTS;
          # wrong outputs by design): no gu loads (ds stands in for gate and up),
          # no SwiGLU math (the loaded gu stored as dgu), no dgu stores, no epilogue
-         "epi_noload": False, "epi_novalu": False, "epi_nostore": False, "epi_none": False}
+         "epi_noload": False, "epi_novalu": False, "epi_nostore": False, "epi_none": False,
+         # persistent plain kernel whose C stores are issued in the NEXT tile's
+         # first k-iteration (packed bf16 parked in a[128:255]; deferred_pack)
+         "defer": False}
 
 
 def _stamp(k: int) -> str:
@@ -655,14 +663,17 @@ def span_mfmas(m: dict) -> list[int]:
 
 
 def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, trace_base: int = 0,
-                  mapname: str = ""):
+                  mapname: str = "", first: bool = False, extra: dict | None = None):
     """One 64-k tile placed by an explicit slot map (SLOT_MAPS).  Map keys
     beyond the placements: `split` puts each barrier that many MFMAs after
     its wait (the MFMA issued in between runs while the wave waits at the
     barrier); `m0_lag` advances M0 that many MFMAs after each piece instead
     of right behind it; `adv` gives the slots of the X / W resource advances
     (default: with the last piece of the half); `nt_w` the W pieces loaded
-    non-temporal."""
+    non-temporal.  first: the tile's first k-tile (phase-1 MFMAs start their
+    accumulators at 0); extra: {slot: [instructions]} placed after those
+    MFMAs (the deferred C stores: their VMEM ops before the next-tile wait
+    are counted in its vmcnt)."""
     m = SLOT_MAPS[mapname or SCHED["map"]]
     split, lag = m.get("split", 0), m.get("m0_lag", 0)
     nt_w = set(m.get("nt_w", ()))
@@ -700,6 +711,10 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
         vm = sum(1 for n in m["xdma"] + m["wdma"] if n < m["wait"])
     else:
         vm = 0
+    for n, ins in (extra or {}).items():
+        slots[n] += ins
+        if n < m["wait"] or (n == m["wait"] and not next_reads):
+            vm += sum(1 for x in ins if x.startswith(("buffer_", "global_")))
     def stamp_around(k, n):
         """stamp k before the wait in slot n, stamp k+1 right after its
         barrier (slot n + split; with a split the MFMA between them counts)"""
@@ -742,9 +757,130 @@ def iteration_map(a: Asm, with_dma: bool, next_reads: bool, vm_after_dma: int, t
             a("s_waitcnt lgkmcnt(0)")
         if SCHED["align"]:
             a(".p2alignl 3, 0xbf800000")
-        a(mfma(i, j, sub))
+        a(mfma(i, j, sub, czero=first and sub == 0))
         for ins in slots[n]:
             a(ins)
+
+
+# ---------------------------------------------------------------- deferred C stores
+DEFER_AGPR = 128          # a[128:255]: the previous tile's C, packed bf16 (32 stores x 4 registers)
+
+
+def deferred_pack(a: Asm):
+    """The finished tile's accumulators -> bf16 pairs parked in a[128:255],
+    store k = 4 j + p (row block j, column pair p) in a[128 + 4k : +3]: the
+    data of epilogue_plain's store (j, p).  Staged through V4..V131 (the
+    fragment registers, free between tiles) because the packs overwrite
+    accumulators later row blocks still read."""
+    f = V_E + 8                                       # 32 fp32 of one row block
+    for j in range(8):
+        for p in range(4):
+            read_pair(a, f + 8 * p, p, j)
+        for p in range(4):
+            cvt_pack8(a, V_FX0 + 16 * j + 4 * p, f + 8 * p)
+    for r in range(128):
+        a(f"v_accvgpr_write_b32 {ar(DEFER_AGPR + r)}, {vr(V_FX0 + r)}")
+
+
+def deferred_stores() -> dict:
+    """{slot: instructions} of the previous tile's 32 C stores, store k after
+    MFMA k of the next tile's first k-tile: before MFMA 32 + k, whose
+    accumulator (fresh, srcC = 0) is the store's data register.  Row block j
+    at S_DOFF (advanced by 16 rows after its 4th store); a resource with
+    num_records 0 (the first tile: nothing deferred) drops them all."""
+    nt = " nt" if SCHED["store_nt"] else ""
+    out = {}
+    for k in range(32):
+        p = k % 4
+        ins = [f"buffer_store_dwordx4 {ar(DEFER_AGPR + 4 * k, 4)}, {vr(V_E)}, {sr(SRD_D, 4)}, {sr(S_DOFF)} offen "
+               f"offset:{64 * p}{nt}"]
+        if p == 3:
+            ins.append(f"s_add_u32 {sr(S_DOFF)}, {sr(S_DOFF)}, {sr(S_DSTEP)}")
+        out[k] = ins
+    return out
+
+
+def kernel_defer(name: str) -> tuple[str, str]:
+    """The persistent plain kernel with deferred C stores (SCHED "defer"):
+    a workgroup per CU walks its tiles; tile t's C leaves as 32 stores spread
+    over tile t + 1's first k-iteration (one per MFMA gap, under the matrix
+    core's work) instead of a burst with the MFMA pipe idle at the end of
+    every tile -- the epilogue's HBM traffic costs the plain kernel 1-5 %
+    (the no-store arm, profiles/r6_nostore).  The next tile's first two
+    k-tiles are staged before the pack, so their flight hides under it;
+    its first k-step starts the accumulators at 0 (no zeroing pass)."""
+    a = Asm(prefix="defer_")
+    a.raw(f".globl {name}")
+    a.raw(".p2align 8")
+    a.raw(f".type {name},@function")
+    a.raw(f"{name}:")
+    prologue(a, "plain")
+    a(f"s_cmp_lt_u32 {sr(S_KT)}, 3")                # the first k-iteration is peeled: K >= 192
+    a(f"s_cbranch_scc1 {a.abort}")
+    epi_offsets(a, "plain")                          # V_E: this lane's C offset, the same in every tile
+    a(f"s_lshl_b32 {sr(S_DSTEP)}, {sr(S_LDC)}, 4")  # 16 rows
+    for r in range(4):                               # nothing deferred yet: num_records 0 drops the stores
+        a(f"s_mov_b32 {sr(SRD_D + r)}, {0x20000 if r == 3 else 0}")
+    prologue_dma(a)
+    a("s_waitcnt vmcnt(16)")
+    a("s_barrier")
+    l_tile, l_loop, l_tail, l_last = a.fresh("tile"), a.fresh("loop"), a.fresh("tail"), a.fresh("last")
+    a.label(l_tile)
+    for j in range(8):
+        a(frag_read("x", j, 0))
+    for i in range(8):
+        a(frag_read("w", i, 0))
+    a("s_waitcnt lgkmcnt(0)")
+    a(f"s_mov_b32 {sr(S_DOFF)}, 0")
+    iteration_map(a, with_dma=True, next_reads=True, vm_after_dma=16, first=True, extra=deferred_stores())
+    a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_KT)}, 3")
+    a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
+    a(f"s_cbranch_scc1 {l_tail}")
+    if SCHED["align"]:
+        a(".p2alignl 6, 0xbf800000")
+    a.label(l_loop)
+    iteration_map(a, with_dma=True, next_reads=True, vm_after_dma=16)
+    a(f"s_sub_u32 {sr(S_LOOP)}, {sr(S_LOOP)}, 1")
+    a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
+    a(f"s_cbranch_scc0 {l_loop}")
+    a.label(l_tail)
+    iteration_map(a, with_dma=False, next_reads=True, vm_after_dma=0)
+    iteration_map(a, with_dma=False, next_reads=False, vm_after_dma=0)
+    a("s_nop 15")                                    # MFMA results -> VALU reads
+    a("s_nop 15")
+    # --- next tile: stage parity back to 0 (M0 bases toggled KT times, read bases KT - 1)
+    l_even, l_par = a.fresh("even"), a.fresh("par")
+    a(f"s_bitcmp1_b32 {sr(S_KT)}, 0")
+    a(f"s_cbranch_scc0 {l_even}")
+    a(f"s_xor_b32 {sr(S_M0X)}, {sr(S_M0X)}, {sr(S_M0XT)}")
+    a(f"s_xor_b32 {sr(S_M0W)}, {sr(S_M0W)}, {sr(S_M0WT)}")
+    a(f"s_branch {l_par}")
+    a.label(l_even)
+    a(f"v_xor_b32 {vr(V_RX)}, {vr(V_RX)}, {vr(V_RXT)}")
+    a(f"v_xor_b32 {vr(V_RW)}, {vr(V_RW)}, {vr(V_RWT)}")
+    a.label(l_par)
+    a(f"s_add_u32 {sr(S_ITER)}, {sr(S_ITER)}, {sr(S_GRID)}")
+    a(f"s_mul_i32 {sr(S_T0)}, {sr(S_TM_N)}, {sr(S_TN_N)}")
+    a(f"s_cmp_ge_u32 {sr(S_ITER)}, {sr(S_T0)}")
+    a(f"s_cbranch_scc1 {l_last}")
+    a("s_barrier")                                   # every wave done reading this tile's LDS
+    tile_setup(a, "plain", sr(S_ITER))
+    prologue_dma(a)                                  # the next tile's k-tiles 0 and 1, in flight under the pack
+    deferred_pack(a)
+    for r in range(4):
+        a(f"s_mov_b32 {sr(SRD_D + r)}, {sr(SRD_C + r)}")
+    tile_c(a, "plain")
+    a("s_waitcnt vmcnt(16)")                         # the next tile's k-tile 0 (k-tile 1's 16 pieces are younger)
+    a("s_barrier")
+    a(f"s_branch {l_tile}")
+    a.label(l_last)
+    epilogue_plain(a)                                # the last tile: stored at once
+    a.label(a.abort)
+    a("s_endpgm")
+    a.raw(f".size {name}, .-{name}")
+    body = "\n".join(a.out)
+    desc, meta = _descriptor(name)
+    return body + "\n" + desc, meta
 
 
 # ---------------------------------------------------------------- epilogues
@@ -1133,6 +1269,9 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     into a host-coherent buffer in the S slot; toa_gemm_tn_asm_trace).
     variant: an A/B arm of the plain kernel (PLAIN_VARIANTS)."""
     name = "toa_gemm_tn_asm_trace" if trace else f"toa_gemm_tn_asm_{epi}" + (f"_{variant}" if variant else "")
+    if SCHED["defer"]:
+        assert epi == "plain" and not trace and not SCHED["timing"] and SCHED["persist"] and SCHED["map"]
+        return kernel_defer(name)
     if SCHED["timing"]:
         name = "toa_gemm_tn_asm_timing" + ("" if SCHED["timing"] == 1 else str(SCHED["timing"]))
     a = Asm(prefix=("trace_" if trace else epi + "_" + (variant + "_" if variant else "")))
@@ -1464,6 +1603,7 @@ PLAIN_VARIANTS = (
     ("v6", {"store_same": True, "diag": True}),  # DIAGNOSTIC: every workgroup stores tile (0, 0) (L2-hot writes)
     ("v7", {"store_nt": False}),            # C stores without the non-temporal hint
     ("v8", {"persist": True, "store_nt": False}),
+    ("v9", {"persist": True, "defer": True}),   # persistent, C stores deferred into the next tile's first k-tile
 )
 # measured (profiles/r4_asm_gemm/ab1..diag2): MFMAs on 8-byte boundaries, ending
 # with the epilogue's stores in flight, two barriers per tile and the wait 16

@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_N = 48 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_N = 49 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -58,7 +58,9 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // K_SWBWD_V1 ..: gemm_gen.py SWIGLU_BWD_VARIANTS (diagnostic arms, wrong outputs by design)
                            "toa_gemm_tn_asm_swiglu_bwd_b1", "toa_gemm_tn_asm_swiglu_bwd_b2",
                            "toa_gemm_tn_asm_swiglu_bwd_b3", "toa_gemm_tn_asm_swiglu_bwd_b4",
-                           "toa_gemm_tn_asm_swiglu_bwd_b5"};
+                           "toa_gemm_tn_asm_swiglu_bwd_b5",
+                           // the plain kernel's ninth A/B arm (after the table above was laid out)
+                           "toa_gemm_tn_asm_plain_v9"};
 
 struct DevModule {
   std::once_flag once;
@@ -102,9 +104,13 @@ constexpr uint32_t kMapWalkCols = 16;
 bool ld_ok(int64_t ld, int64_t min_cols) { return ld >= min_cols && ld % 8 == 0 && ld * 2 * 256 < (1ll << 32); }
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// A/B arms that walk several tiles per workgroup (gemm_gen.py SCHED
-// "persist"), by variant number 1..: their grid is one workgroup per CU.
-constexpr bool kVariantPersist[K_WGRAD_V1 - K_V1] = {false, false, true, false, false, false, false, true};
+// The plain kernel's A/B arms by variant number 1.. (gemm_gen.py
+// PLAIN_VARIANTS): kernel id, and whether it walks several tiles per
+// workgroup (SCHED "persist": its grid is one workgroup per CU).
+constexpr int kNumPlainVariants = 9;
+constexpr int kVariantFn[kNumPlainVariants] = {K_V1,     K_V1 + 1, K_V1 + 2, K_V1 + 3,  K_V1 + 4,
+                                               K_V1 + 5, K_V1 + 6, K_V1 + 7, K_PLAIN_V9};
+constexpr bool kVariantPersist[kNumPlainVariants] = {false, false, true, false, false, false, false, true, true};
 constexpr unsigned kPersistGrid = 256;
 
 // First-wave start offsets per kernel family (plain / SwiGLU forward /
@@ -149,12 +155,16 @@ int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
 // of 4 tiles walking the rows (map 18) stream fewer of them: +1.5..3 % at
 // down.fwd / gate_up.dgrad / lm_head.dgrad.  At K = 4096..6144 row groups of
 // 4 (map 2) are as fast or 0.5..1 % faster.  Override: TOA_ASM_TILE_MAP.
+int g_map_forced = -2;  // -2: TOA_ASM_TILE_MAP not read yet; -1: the per-shape rule
+
 uint32_t tile_map(uint32_t tiles_m, uint32_t tiles_n, uint32_t ktiles) {
-  static const int forced = [] {
+  if (g_map_forced == -2) {
     const char* e = getenv("TOA_ASM_TILE_MAP");
-    return (e && *e) ? atoi(e) : -1;
-  }();
-  if (forced >= 0 && forced < 32 && (forced & 15) <= 6) return (uint32_t)forced;
+    const int v = (e && *e) ? atoi(e) : -1;
+    g_map_forced = (v >= 0 && v < 32 && (v & 15) <= 6) ? v : -1;
+  }
+  const int forced = g_map_forced;
+  if (forced >= 0) return (uint32_t)forced;
   (void)tiles_m;
   (void)tiles_n;
   return ktiles >= 128 ? (kMapWalkCols | 2) : kMapDefault;
@@ -198,6 +208,14 @@ extern "C" int toa_gemm_asm_set_phase(int kind, unsigned word) {
   return 0;
 }
 
+// A/B: force the TN kernels' tile order (a map word) for every launch, -1 =
+// the per-shape rule (tile_map).
+extern "C" int toa_gemm_asm_set_map(int map) {
+  if (map < -1 || map >= 32 || (map >= 0 && (map & 15) > 6)) return (int)hipErrorInvalidValue;
+  g_map_forced = map;
+  return 0;
+}
+
 extern "C" int toa_gemm_asm_available() {
   hipError_t err;
   return get_fn(K_PLAIN, &err) != nullptr ? 1 : 0;
@@ -215,14 +233,15 @@ extern "C" int toa_gemm_asm(const bf16_t* X, int64_t ldx, const bf16_t* W, int64
 // gemm_gen.py PLAIN_VARIANTS lists), same arguments and checks as toa_gemm_asm.
 extern "C" int toa_gemm_asm_variant(int v, const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C,
                                     int64_t ldc, int M, int N, int K, hipStream_t stream) {
-  if (v < 0 || v > K_N - K_V1 || !common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C))
+  if (v < 0 || v > kNumPlainVariants || !common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) ||
+      !al16(C) || (v == 9 && K < 192))
     return (int)hipErrorInvalidValue;
   Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
   if (v > 0 && kVariantPersist[v - 1]) {
     const unsigned tiles = a.tiles_m * a.tiles_n;
-    return launch(K_V1 + v - 1, a, stream, tiles < kPersistGrid ? tiles : kPersistGrid);
+    return launch(kVariantFn[v - 1], a, stream, tiles < kPersistGrid ? tiles : kPersistGrid);
   }
-  return launch(v == 0 ? K_PLAIN : K_V1 + v - 1, a, stream);
+  return launch(v == 0 ? K_PLAIN : kVariantFn[v - 1], a, stream);
 }
 
 // A/B: the product kernel with an explicit tile order (kernarg `map`, see

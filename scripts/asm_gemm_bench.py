@@ -411,6 +411,17 @@ def bench(a):
                 ("asm_fused_bwd", lambda: asm_swiglu_bwd(d2, wdt, gu)),
                 ("blt_unfused_bwd", lambda: (gemm.set_mode("nosk"), llm.swiglu_bwd(gemm.linear_fwd(d2, wdt), gu)))]
         dgu_v = torch.empty_like(gu)
+
+        def mapped(tm_, fn):
+            _lib.call("toa_gemm_asm_set_map", tm_)
+            try:
+                return fn()
+            finally:
+                _lib.call("toa_gemm_asm_set_map", -1)
+
+        for tm_ in maps:
+            arms += [(f"asm_fused_fwd_map{tm_}", lambda tm_=tm_: mapped(tm_, lambda: asm_swiglu(x, wgu))),
+                     (f"asm_fused_bwd_map{tm_}", lambda tm_=tm_: mapped(tm_, lambda: asm_swiglu_bwd(d2, wdt, gu)))]
         for v in [int(t) for t in a.swiglu_variants.split(",") if t]:
             arms.append((f"asm_fused_bwd_b{v}", lambda v=v: asm_swiglu_bwd_variant(v, d2, wdt, gu, dgu_v)))
         for ph in phases:

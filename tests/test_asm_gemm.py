@@ -82,14 +82,22 @@ def test_asm_gemm_variants_match_product_kernel(variant):
     close(tof(out[0]), tof(X) @ tof(W).T)
 
 
-@pytest.mark.parametrize("grid", [1, 3, 10])
-def test_asm_gemm_persistent_arm_emulated(grid):
-    """The persistent arm: `grid` workgroups walk the 10 tiles of a 5 x 2
-    grid (S_ITER += grid), staging the next tile under the epilogue; C equals
-    the product kernel's bit for bit."""
-    name = next(f"toa_gemm_tn_asm_plain_{v}" for v, k in gemm_gen.PLAIN_VARIANTS if k.get("persist"))
+PERSIST_ARMS = [v for v, k in gemm_gen.PLAIN_VARIANTS if k.get("persist") and k.get("store_nt", True)]
+
+
+@pytest.mark.parametrize("arm", PERSIST_ARMS)
+@pytest.mark.parametrize("grid,K", [(1, 320), (3, 320), (10, 320), (3, 192), (4, 256)])
+def test_asm_gemm_persistent_arm_emulated(arm, grid, K):
+    """The persistent arms: `grid` workgroups walk the 10 tiles of a 5 x 2
+    grid (S_ITER += grid), staging the next tile under the epilogue (v3) or
+    parking the finished tile's C in AGPRs and storing it during the next
+    tile's first k-iteration (v9, deferred stores: the first tile's stores
+    dropped by a zero-size resource, the last tile's stored at once); C
+    equals the product kernel's bit for bit.  K = 320: odd k-tile count (the
+    stage parity fix-up); 192: v9's peeled first iteration and no loop."""
+    name = f"toa_gemm_tn_asm_plain_{arm}"
     rng = np.random.default_rng(13)
-    M, N, K = 1280, 512, 320   # odd k-tile count: the stage parity fix-up runs
+    M, N = 1280, 512
     X = bf16(rng.standard_normal((M, K)))
     W = bf16(rng.standard_normal((N, K)))
     outs = []
@@ -268,7 +276,8 @@ def test_host_kernel_table_matches_generator():
     # + the round-4 SwiGLU epilogue arms (2) + the SwiGLU backward's diagnostic arms
     assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
         len(attn_bwd_gen.VARIANTS) + 2 + len(gemm_gen.SWIGLU_BWD_VARIANTS)
-    flags = re.search(r"kVariantPersist\[K_WGRAD_V1 - K_V1\] = \{([^}]*)\}", src).group(1)
+    flags = re.search(r"kVariantPersist\[kNumPlainVariants\] = \{([^}]*)\}", src).group(1)
+    assert int(re.search(r"kNumPlainVariants = (\d+)", src).group(1)) == len(gemm_gen.PLAIN_VARIANTS)
     assert [f.strip() == "true" for f in flags.split(",")] == [bool(k.get("persist")) for _, k in gemm_gen.PLAIN_VARIANTS]
 
 
