@@ -221,12 +221,39 @@ extern "C" int toa_gemm_asm_available() {
   return get_fn(K_PLAIN, &err) != nullptr ? 1 : 0;
 }
 
+// Persistent plain kernel (PLAIN_VARIANTS v3: a workgroup per CU walks its
+// tiles, the next tile's first k-tiles staged under the current epilogue).
+// In isolation it is 1.5-2.8 % faster at the qkv / o forward and data-gradient
+// forms (K <= 6144, N <= 6144; profiles/r6_defer), but in the model the step
+// is the same (-0.3 +- 0.8 ms, 8 ABBA rounds, profiles/r6_persist): the chip
+// runs these GEMMs at its power cap, so fewer stalls become a lower clock.  So
+// the rule (-1) keeps one workgroup per tile everywhere; toa_gemm_asm_set_persist
+// / TOA_ASM_PERSIST force the persistent form for the forms above (1) or off (0).
+int g_persist = -2;
+bool use_persist(int N, int K) {
+  if (g_persist == -2) {
+    const char* e = getenv("TOA_ASM_PERSIST");
+    g_persist = (e && *e) ? (atoi(e) ? 1 : 0) : -1;
+  }
+  return g_persist == 1 && K <= 6144 && N <= 6144;
+}
+
 extern "C" int toa_gemm_asm(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C, int64_t ldc, int M,
                             int N, int K, hipStream_t stream) {
   if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C))
     return (int)hipErrorInvalidValue;
   Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  if (use_persist(N, K)) {
+    const unsigned tiles = a.tiles_m * a.tiles_n;
+    return launch(kVariantFn[2], a, stream, tiles < kPersistGrid ? tiles : kPersistGrid);
+  }
   return launch(K_PLAIN, a, stream);
+}
+
+extern "C" int toa_gemm_asm_set_persist(int v) {
+  if (v < -1 || v > 1) return (int)hipErrorInvalidValue;
+  g_persist = v;
+  return 0;
 }
 
 // A/B: variant v of the plain kernel (0 = the product kernel, 1.. = the arms

@@ -9,6 +9,7 @@ gemm=asm|nosk (ops.gemm.set_mode: forward / data-gradient policy), attnf=N /
 attnb=N / attnd=N (toa_attn_set_fwd_variant / _bwd_variant / _dkdv_variant forms),
 epi=r4|pipe (the fused SwiGLU GEMMs' epilogues, toa_gemm_asm_set_epi_variant),
 wmap=N (the weight-gradient tile order, toa_wgrad_asm_set_map; -1 = the per-shape rule),
+persist=N (the plain TN kernel's persistent form, toa_gemm_asm_set_persist; -1 = the per-shape rule),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -49,6 +50,8 @@ def apply(arm: str):
             _lib.call("toa_attn_set_dkdv_variant", int(val))
         elif key == "epi":   # the fused SwiGLU GEMMs' epilogues: r4 (drained per row block) or pipe
             _lib.call("toa_gemm_asm_set_epi_variant", 1 if val == "r4" else 0)
+        elif key == "persist":   # TN plain kernel: -1 = the per-shape rule, 0 = never persistent, 1 = always
+            _lib.call("toa_gemm_asm_set_persist", int(val))
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":
