@@ -131,7 +131,7 @@ A_DV, A_DK, A_K, A_V = 0, 64, 128, 160
 # price it in-process (scripts/attn_dkdv_arms.py): their outputs are wrong by
 # construction and only their time is read.
 KNOBS = {"bar": True, "vmwait": True, "lgkm": True, "exp": True, "dma": True, "valu": True, "lds": True,
-         "timing": False, "merge": True,
+         "timing": False, "merge": True, "pk": False,
          "gbar": G_BAR, "dldma": DL_DMA, "lead": 3}   # schedule parameters (the s* arms sweep them)
 VARIANTS = (
     ("d1", {"lgkm": False}),                     # MFMAs do not wait for their LDS fragments
@@ -149,6 +149,7 @@ VARIANTS = (
     ("s4", {"lead": 2}),
     ("s5", {"lead": 5}),
     ("s6", {"merge": False}),
+    ("s7", {"pk": True}),                        # round 5: P / dS on packed v_pk_fma / v_pk_mul pairs
 )
 
 MASK_C = AG.MASK_C        # register r's row offset in a 32x32 accumulator: (r & 3) + 8 (r >> 2)
@@ -278,8 +279,14 @@ def e_items(p: int, masked: bool, rel: int, dl: int, stream: str, st_rel: int | 
     S0, P0, L0 = sbuf(p), dpbuf(p), V_L + 16 * p
     if masked:
         items.append(Item([f"v_add_u32 {vr(V_MD)}, {sr(S_DD0 if p == 0 else S_DD1)}, {vr(V_MD0)}"], 4, rel, dl, stream))
+    pk = KNOBS["pk"]
     for j0 in range(0, 16, 4):
-        ins = [f"v_pk_fma_f32 {vr(S0 + j, 2)}, {vr(S0 + j, 2)}, {vr(V_C2, 2)}, {vr(L0 + j, 2)}" for j in range(j0, j0 + 4, 2)]
+        if pk:
+            ins = [f"v_pk_fma_f32 {vr(S0 + j, 2)}, {vr(S0 + j, 2)}, {vr(V_C2, 2)}, {vr(L0 + j, 2)}"
+                   for j in range(j0, j0 + 4, 2)]
+        else:   # scalar: beside MFMAs a packed f32 op costs more than two scalar ones (MI355X_MICROARCH.md
+                # 'price of one filler'; -3.5 % per call at the bench shape, profiles/r6_dkdv)
+            ins = [f"v_fma_f32 {vr(S0 + j)}, {vr(S0 + j)}, {vr(V_C2)}, {vr(L0 + j)}" for j in range(j0, j0 + 4)]
         ins += [f"v_exp_f32 {vr(S0 + j)}, {vr(S0 + j)}" if KNOBS["exp"] else f"v_mov_b32 {vr(S0 + j)}, {vr(S0 + j)}"
                 for j in range(j0, j0 + 4)]
         items.append(Item(ins, 0, rel, dl, stream))
@@ -288,7 +295,10 @@ def e_items(p: int, masked: bool, rel: int, dl: int, stream: str, st_rel: int | 
                 items.append(Item([f"v_cmp_lt_i32 vcc, {MASK_C[j]}, {vr(V_MD)}",
                                    f"v_cndmask_b32 {vr(S0 + j)}, {vr(S0 + j)}, 0, vcc"], 8, rel, dl, stream, split=False))
         ins = [f"v_cvt_pk_bf16_f32 {vr(V_PW + 8 * p + j // 2)}, {vr(S0 + j)}, {vr(S0 + j + 1)}" for j in range(j0, j0 + 4, 2)]
-        ins += [f"v_pk_mul_f32 {vr(P0 + j, 2)}, {vr(S0 + j, 2)}, {vr(P0 + j, 2)}" for j in range(j0, j0 + 4, 2)]
+        if pk:
+            ins += [f"v_pk_mul_f32 {vr(P0 + j, 2)}, {vr(S0 + j, 2)}, {vr(P0 + j, 2)}" for j in range(j0, j0 + 4, 2)]
+        else:
+            ins += [f"v_mul_f32 {vr(P0 + j)}, {vr(S0 + j)}, {vr(P0 + j)}" for j in range(j0, j0 + 4)]
         ins += [f"v_cvt_pk_bf16_f32 {vr(V_SW + 8 * p + j // 2)}, {vr(P0 + j)}, {vr(P0 + j + 1)}" for j in range(j0, j0 + 4, 2)]
         items.append(Item(ins, 0, rel, dl, stream))
     # dS block store: the lane's 4 queries 8 g + 4 hh .. + 3 of key r are the

@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_N = 49 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_N = 50 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -60,7 +60,9 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            "toa_gemm_tn_asm_swiglu_bwd_b3", "toa_gemm_tn_asm_swiglu_bwd_b4",
                            "toa_gemm_tn_asm_swiglu_bwd_b5",
                            // the plain kernel's ninth A/B arm (after the table above was laid out)
-                           "toa_gemm_tn_asm_plain_v9"};
+                           "toa_gemm_tn_asm_plain_v9",
+                           // the dK/dV kernel's arm s7 (attn_bwd_gen.py VARIANTS, appended)
+                           "toa_attn_dkdv_asm_s7"};
 
 struct DevModule {
   std::once_flag once;
@@ -614,12 +616,21 @@ static int attn_dkdv_launch(int which, const bf16_t* q, const bf16_t* k, const b
                             int Hk, int S, int D, float scale, int flags, const float* cosv, const float* sinv, int H3,
                             hipStream_t stream, void* dbg = nullptr);
 
+// In-model A/B: toa_attn_dkdv_asm_set_arm(1) runs the packed-VALU arm (s7,
+// the round-5 form) in place of the product kernel; 0 = the product.
+static int g_dkdv_arm = 0;
+extern "C" int toa_attn_dkdv_asm_set_arm(int v) {
+  if (v < 0 || v > 1) return (int)hipErrorInvalidValue;
+  g_dkdv_arm = v;
+  return 0;
+}
+
 extern "C" int toa_attn_dkdv_asm(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout,
                                  const float* nlse2, const float* ndelta, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
                                  int H, int Hk, int S, int D, float scale, int flags, const float* cosv,
                                  const float* sinv, int H3, hipStream_t stream) {
-  return attn_dkdv_launch(K_ATTN_DKDV, q, k, v, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S, D, scale, flags, cosv,
-                          sinv, H3, stream);
+  return attn_dkdv_launch(g_dkdv_arm ? K_DKDV_S7 : K_ATTN_DKDV, q, k, v, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S,
+                          D, scale, flags, cosv, sinv, H3, stream);
 }
 
 // Diagnostic: arm v (1.. = attn_bwd_gen.py VARIANTS, 0 = the product kernel),
@@ -628,10 +639,13 @@ extern "C" int toa_attn_dkdv_asm_variant(int v, const bf16_t* q, const bf16_t* k
                                          const bf16_t* dout, const float* nlse2, const float* ndelta, bf16_t* dk,
                                          bf16_t* dv, bf16_t* ds, int B, int H, int Hk, int S, int D, float scale,
                                          int flags, const float* cosv, const float* sinv, int H3, hipStream_t stream) {
-  if (v < 0 || v > K_N - K_DKDV_D1 || K_DKDV_D1 + v - 1 == K_DKDV_T1)
+  // arms 1..14 sit at K_DKDV_D1.., arm 15 (s7) was appended at K_DKDV_S7
+  constexpr int kDkdvArms = K_SWIGLU_FWD_R4 - K_DKDV_D1 + 1;
+  if (v < 0 || v > kDkdvArms || (v && v < kDkdvArms && K_DKDV_D1 + v - 1 == K_DKDV_T1))
     return (int)hipErrorInvalidValue;  // the timing arm takes its own entry
-  return attn_dkdv_launch(v ? K_DKDV_D1 + v - 1 : K_ATTN_DKDV, q, k, v_, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S,
-                          D, scale, flags, cosv, sinv, H3, stream);
+  const int which = v == 0 ? K_ATTN_DKDV : (v < kDkdvArms ? K_DKDV_D1 + v - 1 : K_DKDV_S7);
+  return attn_dkdv_launch(which, q, k, v_, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S, D, scale, flags, cosv, sinv,
+                          H3, stream);
 }
 
 // Diagnostic: the product kernel with s_memtime stamps (attn_bwd_gen.py

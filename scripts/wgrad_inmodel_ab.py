@@ -50,6 +50,8 @@ def apply(arm: str):
             _lib.call("toa_attn_set_dkdv_variant", int(val))
         elif key == "epi":   # the fused SwiGLU GEMMs' epilogues: r4 (drained per row block) or pipe
             _lib.call("toa_gemm_asm_set_epi_variant", 1 if val == "r4" else 0)
+        elif key == "dkpk":   # the assembly dK/dV with round 5's packed P / dS VALU (1) or the scalar product (0)
+            _lib.call("toa_attn_dkdv_asm_set_arm", int(val))
         elif key == "persist":   # TN plain kernel: -1 = the per-shape rule, 0 = never persistent, 1 = always
             _lib.call("toa_gemm_asm_set_persist", int(val))
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word

@@ -55,7 +55,7 @@ def reference(q, k, v, do, scale):
     return p, o, lse, kk, vv
 
 
-def run(q, k, v, do, bshd=False, rope=False, seed=0):
+def run(q, k, v, do, bshd=False, rope=False, seed=0, text=None, name=None):
     B, H, S, D = q.shape
     Hk = k.shape[1]
     rep = H // Hk
@@ -99,7 +99,7 @@ def run(q, k, v, do, bshd=False, rope=False, seed=0):
     karg = struct.pack("<12Q4I2f4I2I", qa, ka, va, doa, nlse, ndel, dka, dva, dsa, cosa, sina, 0,
                        B, H, Hk, S, scale, c, flags, rep, nkb, H3, 0, 0)
     assert len(karg) == attn_bwd_gen.KARG_BYTES
-    e = emu.Emu(TEXT, attn_bwd_gen.NAME)
+    e = emu.Emu(text or TEXT, name or attn_bwd_gen.NAME)
     e.dropped = 0
     for wg in range(nkb * B * Hk):
         e.run(karg, wg, mem)
@@ -190,3 +190,16 @@ def test_dkdv_s512_two_kv_heads():
     B, H, Hk, S = 1, 4, 2, 512
     r = run(rnd((B, H, S, 128), 13), rnd((B, Hk, S, 128), 14), rnd((B, Hk, S, 128), 15), rnd((B, H, S, 128), 16))
     check(r, S)
+
+
+def test_dkdv_packed_valu_arm_matches():
+    """Arm s7 (round 5's P / dS on packed v_pk_fma_f32 / v_pk_mul_f32 pairs;
+    the product kernel now uses scalar ops): the same dK / dV / dS to fp64
+    tolerance, the diagonal blocks' stores dropped the same way."""
+    knobs = dict(attn_bwd_gen.VARIANTS)["s7"]
+    text = attn_bwd_gen.generate([attn_bwd_gen.variant_kernel("s7", knobs)])
+    B, H, Hk, S = 1, 2, 1, 256
+    r = run(rnd((B, H, S, 128), 5), rnd((B, Hk, S, 128), 6), rnd((B, Hk, S, 128), 7), rnd((B, H, S, 128), 8),
+            bshd=True, text=text, name=attn_bwd_gen.NAME + "_s7")
+    check(r, S)
+    assert r["dropped"] == expected_drops(B, H, Hk, S)

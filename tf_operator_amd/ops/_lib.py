@@ -102,6 +102,7 @@ _SIGS = {
     "toa_wgrad_asm_set_map": [c_int],
     "toa_gemm_asm_set_map": [c_int],
     "toa_gemm_asm_set_persist": [c_int],
+    "toa_attn_dkdv_asm_set_arm": [c_int],
     "toa_gemm_asm_timing": [c_int, c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_probe": [c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int, c_int, c_p],
     "toa_attn_set_bwd_variant": [c_int],
