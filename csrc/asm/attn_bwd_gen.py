@@ -111,7 +111,7 @@ V_RRO_B, V_LO_B, V_TRO_B = 82, 90, 91
 V_TRO8_B = (95, 96, 97, 20)
 V_C2 = 18                 # v18, v19: c = scale log2 e twice (packed-math operand)
 V_L4 = 22                 # lane * 4 (the -lse / -delta row DMA)
-V_DSO = 23                # dS store lane offset: key 16 + query half 8
+V_DSO = 23                # dS store lane offset: key 16 + query half 8 (8-B stores) / + 512 (16-B stores)
 V_MD0, V_MD = 24, 25      # mask: r - 4 hh, and + (first key - first query) of the block
 V_T = 26                  # v26..v33 scratch
 V_SF = 34                 # Q / dO fragment ring: 6 x 4
@@ -121,7 +121,7 @@ V_PW = 130                # P packs per parity: 2 x 8
 V_SW = 146                # dS packs per parity: 2 x 8
 V_SB = 162                # S (16) + dP (16) per parity: 2 x 32
 V_DMA = 226               # v226..v233: DMA source offsets of the wave's 8 pieces
-V_X = 234                 # v234..v255 scratch (prologue / epilogue)
+V_X = 234                 # v234..v255 scratch (prologue / epilogue; in the loop v234..v249 the 16-B dS store staging)
 
 # AGPRs: dV^T a[0:63], dK^T a[64:127] ([d tile] x 16), K / V B-operand
 # fragments a[128:159] / a[160:191] ([k-step] x 4)
@@ -131,7 +131,7 @@ A_DV, A_DK, A_K, A_V = 0, 64, 128, 160
 # price it in-process (scripts/attn_dkdv_arms.py): their outputs are wrong by
 # construction and only their time is read.
 KNOBS = {"bar": True, "vmwait": True, "lgkm": True, "exp": True, "dma": True, "valu": True, "lds": True,
-         "timing": False, "merge": True, "pk": False,
+         "timing": False, "merge": True, "pk": False, "dsst": True, "dswide": False,
          "gbar": G_BAR, "dldma": DL_DMA, "lead": 3}   # schedule parameters (the s* arms sweep them)
 VARIANTS = (
     ("d1", {"lgkm": False}),                     # MFMAs do not wait for their LDS fragments
@@ -150,6 +150,9 @@ VARIANTS = (
     ("s5", {"lead": 5}),
     ("s6", {"merge": False}),
     ("s7", {"pk": True}),                        # round 5: P / dS on packed v_pk_fma / v_pk_mul pairs
+    ("d8", {"dsst": False}),                     # DIAGNOSTIC: no dS block stores (the dQ GEMM's input)
+    ("s8", {"dswide": True}),                    # 16-B dS stores by permlane32 swaps (2 per block): measured
+                                                 # 0.8 % slower than the four 8-B ones (profiles/r6_dkdv/arms3.log)
 )
 
 MASK_C = AG.MASK_C        # register r's row offset in a 32x32 accumulator: (r & 3) + 8 (r >> 2)
@@ -307,11 +310,38 @@ def e_items(p: int, masked: bool, rel: int, dl: int, stream: str, st_rel: int | 
     srd = SRD_DS0 if p == 0 else SRD_DS1
     dso = S_DSO0 if p == 0 else S_DSO1
     srel = rel if st_rel is None else max(rel, st_rel)
-    for g in range(4):
-        items.append(Item([f"buffer_store_dwordx2 {vr(V_SW + 8 * p + 2 * g, 2)}, {vr(V_DSO)}, {sr(srd, 4)}, {sr(dso)} "
-                           f"offen offset:{512 * g} nt"], 8, max(srel, rel + 1), max(srel, dl), stream))
+    nst = 0
+    if KNOBS["dswide"]:
+        # 16-B stores: the packs of groups 2k and 2k + 1 copied to scratch
+        # (the packs themselves are KV(n)'s B operands) and one
+        # v_permlane32_swap per dword, so lanes < 32 hold the 8 queries of
+        # group 2k and lanes >= 32 those of group 2k + 1 for their key (the
+        # lane offset V_DSO then steps 512 B per lane half): 2 stores per
+        # block instead of 4.  The stores cost 14 % of the kernel (arm d8),
+        # but not through their count: this arm (s8) is 0.8 % slower than the
+        # product's four 8-B stores (profiles/r6_dkdv/arms3.log).  The movs of
+        # both pairs go first, so a swap reads scratch written >= 3
+        # instructions earlier.
+        tmp = [V_X + 8 * p + 4 * k for k in range(2)]
+        for k in range(2):
+            items.append(Item([f"v_mov_b32 {vr(tmp[k] + e)}, {vr(V_SW + 8 * p + 4 * k + e)}" for e in range(4)], 0,
+                              max(srel, rel + 1), max(srel, dl), stream))
+        for k in range(2):
+            items.append(Item([f"v_permlane32_swap_b32 {vr(tmp[k])}, {vr(tmp[k] + 2)}",
+                               f"v_permlane32_swap_b32 {vr(tmp[k] + 1)}, {vr(tmp[k] + 3)}",
+                               f"buffer_store_dwordx4 {vr(tmp[k], 4)}, {vr(V_DSO)}, {sr(srd, 4)}, {sr(dso)} "
+                               f"offen offset:{1024 * k} nt"], 16, max(srel, rel + 1), max(srel, dl), stream,
+                              split=False))
+        nst = 4
+    else:
+        for g in range(4):
+            items.append(Item([f"buffer_store_dwordx2 {vr(V_SW + 8 * p + 2 * g, 2)}, {vr(V_DSO)}, {sr(srd, 4)}, "
+                               f"{sr(dso)} offen offset:{512 * g} nt"], 8, max(srel, rel + 1), max(srel, dl), stream))
+        nst = 4
+    if not KNOBS["dsst"]:   # DIAGNOSTIC: no dS block stores
+        items = items[:-nst]
     if not KNOBS["valu"]:
-        items = items[-4:]
+        items = items[-nst:] if KNOBS["dsst"] else []
     for it in items:
         if it.cost == 0:
             it.cost = sum(AG.issue_cost(x) for x in it.ins)
@@ -512,9 +542,10 @@ def iteration(a: Asm, m1: bool, m2: bool, ph: int, nxt: str):
     items += kv_read_items(0, 0, kbuf, None, True, "kr")
     items += kv_read_items(32, 1, kbuf, 0, False, "kr2")
     # the barrier: every wave's pieces of tile it + 1 landed (vmcnt: only the
-    # four dS stores of E(2 it) -- issued after every DMA piece -- and any
-    # since may be outstanding), every wave done with tile it - 1
-    items.append(Item((["s_waitcnt vmcnt(4)"] if KNOBS["vmwait"] else []) + (["s_barrier"] if KNOBS["bar"] else []),
+    # dS stores of E(2 it) -- issued after every DMA piece, two 16-B or four
+    # 8-B ones -- and any since may be outstanding), every wave done with tile it - 1
+    vm = 2 if KNOBS["dswide"] else 4
+    items.append(Item(([f"s_waitcnt vmcnt({vm})"] if KNOBS["vmwait"] else []) + (["s_barrier"] if KNOBS["bar"] else []),
                       8, G_BAR, G_BAR, "bar", split=False))
     # SD reads (tile it + 1): SD(2 it + 2) after the barrier; SD(2 it + 3)'s
     # -lse / -delta rows after E(2 it + 1) let go of the parity-1 registers
@@ -730,7 +761,9 @@ def prologue(a: Asm):
     a(f"v_mov_b32 {vr(V_C2 + 1)}, {sr(S_C)}")
     # dS store: key 16 + hh 8; mask base r - 4 hh
     a(f"v_lshlrev_b32 {vr(V_DSO)}, 4, {vr(r)}")
-    a(f"v_lshl_add_u32 {vr(V_DSO)}, {vr(hh)}, 3, {vr(V_DSO)}")
+    # lane half hh: + 8 B (4 of the group's 8 queries) for the 8-B stores, + 512 B
+    # (the next query group) for the 16-B ones (e_items)
+    a(f"v_lshl_add_u32 {vr(V_DSO)}, {vr(hh)}, {9 if KNOBS['dswide'] else 3}, {vr(V_DSO)}")
     a(f"v_lshlrev_b32 {vr(t)}, 2, {vr(hh)}")
     a(f"v_sub_u32 {vr(V_MD0)}, {vr(r)}, {vr(t)}")
     # --- K / V rows of this wave's keys -> B-operand fragments (AGPRs)

@@ -88,11 +88,35 @@ class Wave:
         self.pc = 0
         self.done = False
         self.wid = wid
+        self.vmq = []          # outstanding VMEM ops, oldest first (Emu.strict_vm)
 
 
 class Emu:
-    def __init__(self, asm_text: str, kernel: str):
+    """strict_vm (default): a VMEM load lands -- in LDS for an LDS-DMA, in
+    its VGPRs otherwise -- only when the issuing wave's s_waitcnt vmcnt(N)
+    retires it (in issue order, stores counted too, as on gfx950) or the wave
+    ends; its global data are read at issue.  A wait that counts too few
+    outstanding ops therefore leaves stale LDS / VGPRs behind and the kernel's
+    output wrong, as it would be on the hardware.  With strict_vm False every
+    load lands at issue (the round-5 model)."""
+
+    def __init__(self, asm_text: str, kernel: str, strict_vm: bool = True):
         self.prog, self.labels = self._parse(asm_text, kernel)
+        self.strict_vm = strict_vm
+
+    def _vm_issue(self, w, effect):
+        """Queue a VMEM op's effect (None for a store: its memory write is
+        made at issue; it only occupies a vmcnt slot)."""
+        if self.strict_vm:
+            w.vmq.append(effect)
+        elif effect is not None:
+            effect()
+
+    def _vm_retire(self, w, keep: int):
+        while len(w.vmq) > keep:
+            eff = w.vmq.pop(0)
+            if eff is not None:
+                eff()
 
     # ------------------------------------------------------------ parsing
     @staticmethod
@@ -346,7 +370,10 @@ class Emu:
         self.sset(w, a[0], (hw_id >> off) & ((1 << size) - 1))
 
     def op_s_waitcnt(self, w, a, m):
-        pass
+        for tok in list(a) + list(m):
+            for part in str(tok).split():
+                if part.startswith("vmcnt("):
+                    self._vm_retire(w, int(part[6:].rstrip(")")))
 
     def op_s_nop(self, w, a, m):
         pass
@@ -358,6 +385,7 @@ class Emu:
         return "barrier"
 
     def op_s_endpgm(self, w, a, m):
+        self._vm_retire(w, 0)
         w.done = True
         return "barrier"
 
@@ -647,7 +675,10 @@ class Emu:
             addr = self._buffer_addr(w, a[1:], mods, 16)
             data = self._gread(addr, 16).view(np.uint32).reshape(64, 4)
             lo, hi = self.vrange(w, a[0])
-            w.v[lo:hi] = data.T
+
+            def land(lo=lo, hi=hi, data=data):
+                w.v[lo:hi] = data.T
+            self._vm_issue(w, land)
             return
         assert "offen" in mods
         addr = self._buffer_addr(w, a, mods, 16)
@@ -655,8 +686,11 @@ class Emu:
         dst = w.m0 + 16 * np.arange(64)
         if dst.max() + 16 > self.lds.size:
             raise IndexError("LDS-DMA past the LDS")
-        for l in range(64):
-            self.lds[dst[l]:dst[l] + 16] = data[l]
+
+        def land(dst=dst, data=data):
+            for l in range(64):
+                self.lds[dst[l]:dst[l] + 16] = data[l]
+        self._vm_issue(w, land)
 
     def op_buffer_load_dword(self, w, a, mods):
         """4-B load into a VGPR.  Lanes past num_records read 0, as on the
@@ -670,8 +704,11 @@ class Emu:
             dst = w.m0 + 4 * np.arange(64)
             if dst.max() + 4 > self.lds.size:
                 raise IndexError("LDS-DMA past the LDS")
-            for l in range(64):
-                self.lds[dst[l]:dst[l] + 4] = data[l]
+
+            def land(dst=dst, data=data):
+                for l in range(64):
+                    self.lds[dst[l]:dst[l] + 4] = data[l]
+            self._vm_issue(w, land)
             return
         voff = self.vget(w, a[1]).astype(np.uint64)
         kind, lo_, hi_ = self._reg(w, a[2])
@@ -690,13 +727,19 @@ class Emu:
             rel = (addr - b0).astype(np.int64)
             out[ok] = np.stack([buf[rel + i] for i in range(4)], axis=1).view(np.uint32).reshape(-1)
         lo, hi = self.vrange(w, a[0])
-        w.v[lo] = out
+
+        def land(lo=lo, out=out):
+            w.v[lo] = out
+        self._vm_issue(w, land)
 
     def op_buffer_load_dwordx2(self, w, a, mods):
         addr = self._buffer_addr(w, a[1:], mods, 8)
         data = self._gread(addr, 8).view(np.uint32).reshape(64, 2)
         lo, hi = self.vrange(w, a[0])
-        w.v[lo:hi] = data.T
+
+        def land(lo=lo, hi=hi, data=data):
+            w.v[lo:hi] = data.T
+        self._vm_issue(w, land)
 
     def _dropped(self, w, a) -> bool:
         """A store through a resource of num_records 0 writes nothing (the
@@ -709,6 +752,7 @@ class Emu:
         return False
 
     def op_buffer_store_dword(self, w, a, mods):
+        self._vm_issue(w, None)
         if self._dropped(w, a):
             return
         addr = self._buffer_addr(w, a[1:], mods, 4)
@@ -716,6 +760,7 @@ class Emu:
         self._gwrite(addr, np.ascontiguousarray(w.v[lo]).view(np.uint8).reshape(64, 4))
 
     def op_buffer_store_dwordx4(self, w, a, mods):
+        self._vm_issue(w, None)
         if self._dropped(w, a):
             return
         addr = self._buffer_addr(w, a[1:], mods, 16)
@@ -723,6 +768,7 @@ class Emu:
         self._gwrite(addr, np.ascontiguousarray(w.v[lo:hi].T).view(np.uint8).reshape(64, 16))
 
     def op_buffer_store_dwordx2(self, w, a, mods):
+        self._vm_issue(w, None)
         if self._dropped(w, a):
             return
         addr = self._buffer_addr(w, a[1:], mods, 8)

@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_N = 50 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_N = 52 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -62,7 +62,7 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // the plain kernel's ninth A/B arm (after the table above was laid out)
                            "toa_gemm_tn_asm_plain_v9",
                            // the dK/dV kernel's arm s7 (attn_bwd_gen.py VARIANTS, appended)
-                           "toa_attn_dkdv_asm_s7"};
+                           "toa_attn_dkdv_asm_s7", "toa_attn_dkdv_asm_d8", "toa_attn_dkdv_asm_s8"};
 
 struct DevModule {
   std::once_flag once;
@@ -639,11 +639,11 @@ extern "C" int toa_attn_dkdv_asm_variant(int v, const bf16_t* q, const bf16_t* k
                                          const bf16_t* dout, const float* nlse2, const float* ndelta, bf16_t* dk,
                                          bf16_t* dv, bf16_t* ds, int B, int H, int Hk, int S, int D, float scale,
                                          int flags, const float* cosv, const float* sinv, int H3, hipStream_t stream) {
-  // arms 1..14 sit at K_DKDV_D1.., arm 15 (s7) was appended at K_DKDV_S7
-  constexpr int kDkdvArms = K_SWIGLU_FWD_R4 - K_DKDV_D1 + 1;
-  if (v < 0 || v > kDkdvArms || (v && v < kDkdvArms && K_DKDV_D1 + v - 1 == K_DKDV_T1))
+  // arms 1..14 sit at K_DKDV_D1.., arms 15.. (s7, d8, s8) were appended from K_DKDV_S7
+  constexpr int kDkdvArms = K_SWIGLU_FWD_R4 - K_DKDV_D1;
+  if (v < 0 || v > kDkdvArms + (K_DKDV_S8 - K_DKDV_S7 + 1) || (v && v <= kDkdvArms && K_DKDV_D1 + v - 1 == K_DKDV_T1))
     return (int)hipErrorInvalidValue;  // the timing arm takes its own entry
-  const int which = v == 0 ? K_ATTN_DKDV : (v < kDkdvArms ? K_DKDV_D1 + v - 1 : K_DKDV_S7);
+  const int which = v == 0 ? K_ATTN_DKDV : (v <= kDkdvArms ? K_DKDV_D1 + v - 1 : K_DKDV_S7 + v - kDkdvArms - 1);
   return attn_dkdv_launch(which, q, k, v_, dout, nlse2, ndelta, dk, dv, ds, B, H, Hk, S, D, scale, flags, cosv, sinv,
                           H3, stream);
 }

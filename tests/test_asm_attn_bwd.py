@@ -142,13 +142,15 @@ def check(r, S):
     assert err < 1e-2 * max(1.0, np.abs(ref).max()), f"dS max err {err}"
 
 
-def expected_drops(B, H, Hk, S):
+def expected_drops(B, H, Hk, S, per_block=None):
     """Stores of blocks wholly above the diagonal: per (kv head, query head,
-    key block kb) step mod < 2, half m, wave w with 2 mod + m < w -- four
-    stores each."""
+    key block kb) step mod < 2, half m, wave w with 2 mod + m < w -- two
+    16-B stores each (four 8-B ones in round 5's form, arm s8)."""
+    if per_block is None:
+        per_block = 2 if attn_bwd_gen.KNOBS["dswide"] else 4
     rep = H // Hk
     per = sum(1 for mod in range(2) for m in range(2) for w in range(4) if 2 * mod + m < w)
-    return 4 * per * B * Hk * rep * (S // 128)
+    return per_block * per * B * Hk * rep * (S // 128)
 
 
 def test_kernel_mfma_count():
@@ -202,4 +204,17 @@ def test_dkdv_packed_valu_arm_matches():
     r = run(rnd((B, H, S, 128), 5), rnd((B, Hk, S, 128), 6), rnd((B, Hk, S, 128), 7), rnd((B, H, S, 128), 8),
             bshd=True, text=text, name=attn_bwd_gen.NAME + "_s7")
     check(r, S)
-    assert r["dropped"] == expected_drops(B, H, Hk, S)
+    assert r["dropped"] == expected_drops(B, H, Hk, S)   # (s7 keeps the 16-B stores)
+
+
+def test_dkdv_wide_store_arm_matches():
+    """Arm s8 (two 16-B dS stores per block built by permlane32 swaps instead
+    of the product's four 8-B ones; the barrier's vmcnt counts two): the same
+    outputs under the strict-VMEM emulator, two drops per block."""
+    knobs = dict(attn_bwd_gen.VARIANTS)["s8"]
+    text = attn_bwd_gen.generate([attn_bwd_gen.variant_kernel("s8", knobs)])
+    B, H, Hk, S = 1, 2, 1, 256
+    r = run(rnd((B, H, S, 128), 5), rnd((B, Hk, S, 128), 6), rnd((B, Hk, S, 128), 7), rnd((B, H, S, 128), 8),
+            bshd=True, text=text, name=attn_bwd_gen.NAME + "_s8")
+    check(r, S)
+    assert r["dropped"] == expected_drops(B, H, Hk, S, per_block=2)
