@@ -463,8 +463,14 @@ def collectives_ab(tr, batches, args, info, rccl_ok) -> dict:
     k = max(1, args.ab_steps)
     times = {"rccl": [], "sdma": []}
     windows = []
+    # TOA_AB_INJECT_SIGNAL=<rank>:<signal number>:<window>: that rank sends
+    # itself the signal as that window starts (rehearses the last-line path)
+    inj = [int(x) for x in os.environ.get("TOA_AB_INJECT_SIGNAL", "-1:0:0").split(":")]
     try:
-        for arm in (default, other, other, default):
+        for w, arm in enumerate((default, other, other, default)):
+            if inj[0] == info.rank and inj[2] == w:
+                sys.stdout.flush()
+                os.kill(os.getpid(), inj[1])
             tr.set_collective_transport(arm)
             tr.step(batches)                      # the first step after a switch is not timed
             tdist.barrier()
@@ -491,10 +497,10 @@ def collectives_ab(tr, batches, args, info, rccl_ok) -> dict:
     return out
 
 
-def _ab_watchdog(budget_s: float, emit):
+def _ab_watchdog(budget_s: float, emit, code: int = 0):
     """A hung A/B window (a stalled copy-engine pull, a collective that never
-    completes) must not cost the headline line: after `budget_s` rank 0
-    emits what it has and every rank leaves."""
+    completes) or teardown must not cost the headline line: after `budget_s`
+    rank 0 emits what it has (once) and every rank leaves with `code`."""
     import threading
 
     def fire():
@@ -502,7 +508,7 @@ def _ab_watchdog(budget_s: float, emit):
             emit()
         finally:
             sys.stdout.flush()
-            os._exit(0)
+            os._exit(code)
 
     t = threading.Timer(budget_s, fire)
     t.daemon = True
@@ -676,26 +682,58 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
         if probe is not None:
             _attach_probe(out, probe)
 
+    from ..utils import lastline
+
+    emitted = []
+
+    def render(ab) -> str:
+        return json.dumps(dict(out, collectives_ab=dict(
+            ab, rccl_transport_ok=None if ok is None else bool(ok and not any_bad))))
+
     def emit(ab):
-        if out is None:
+        if out is None or emitted:
             return
-        out["collectives_ab"] = dict(ab, rccl_transport_ok=None if ok is None else bool(ok and not any_bad))
+        emitted.append(1)
         if args.result_file:
             tmp = args.result_file + ".tmp"
             with open(tmp, "w") as f:
-                json.dump(out, f)
+                f.write(render(ab))
             os.replace(tmp, args.result_file)
         else:
-            print(json.dumps(out), flush=True)
+            print(render(ab), flush=True)
 
     # the two ZeRO-1 collective transports, timed after the headline (which
-    # stays on the configured default); a hung window still emits the line
+    # stays on the configured default).  The headline line survives the A/B:
+    # a hung window -> the watchdog emits it; a fatal signal (a GPU fault in a
+    # copy-engine pull, SIGTERM from the elastic agent when a peer dies) -> the
+    # native handler writes the pre-rendered line (utils/lastline.py).  Either
+    # way the A/B field says what ended it and the process leaves with rc.
     budget = 120.0 + 3.0 * 4 * (max(1, args.ab_steps) + 1) * max(ms, 1.0) / 1e3
-    wd = _ab_watchdog(budget, lambda: emit({"error": f"A/B did not finish within {budget:.0f} s"}))
+
+    def on_timeout():
+        lastline.arm("", rc)
+        emit({"error": f"A/B did not finish within {budget:.0f} s"})
+
+    wd = _ab_watchdog(budget, on_timeout, rc)
+    armed = False
+    runs_ab = args.collectives_ab == "1" or (args.collectives_ab == "auto" and n_gpus > 1)
+    if on_gpu and runs_ab and not args.result_file:
+        err = {"error": f"signal {lastline.SIGNO} ended the process during the A/B"}
+        armed = lastline.arm(render(err) + "\n" if out is not None else "", rc)
     ab = collectives_ab(tr, batches, args, info, False if any_bad else ok)
-    wd.cancel()
     emit(ab)
-    tdist.shutdown()
+    if armed:
+        lastline.arm("", rc)   # the line is out; a fatal signal in the teardown only ends the process
+    if "error" not in ab:
+        tr.close()             # copy-engine transports: drain, barrier, then unmap (no-op without them)
+    finished = tdist.teardown(failed="error" in ab)
+    wd.cancel()
+    if armed:
+        lastline.disarm()
+    if not finished:
+        print("[bench] process group teardown did not finish; leaving", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(rc)
     return rc
 
 

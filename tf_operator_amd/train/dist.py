@@ -165,14 +165,13 @@ def _bounded(fn, timeout: float) -> bool:
     return not t.is_alive()
 
 
-def _shutdown_quietly():
-    """atexit teardown of the process group.  After a clean run: graceful
-    destroy.  After an uncaught exception: abort the group (no waiting on
-    outstanding collectives), and if even that does not return within
-    EXIT_TEARDOWN_S, leave with status 1 right away, so a failed replica
-    always exits non-zero and the operator can restart it."""
+def teardown(failed: bool = False, timeout: float | None = None) -> bool:
+    """Bounded teardown of the process group; False if it did not finish in
+    time (the caller then leaves with os._exit).  failed=False: graceful
+    destroy.  failed=True: abort the group, no waiting on outstanding
+    collectives a dead peer never completes."""
     if not dist.is_initialized():
-        return
+        return True
 
     def graceful():
         try:
@@ -186,13 +185,26 @@ def _shutdown_quietly():
         except Exception:  # noqa: BLE001 - fall back to the graceful path, still bounded
             graceful()
 
+    if timeout is None:
+        timeout = EXIT_TEARDOWN_S if failed else 3 * EXIT_TEARDOWN_S
+    return _bounded(abort if failed else graceful, timeout)
+
+
+def _shutdown_quietly():
+    """atexit teardown of the process group.  After a clean run: graceful
+    destroy.  After an uncaught exception: abort the group (no waiting on
+    outstanding collectives), and if even that does not return within
+    EXIT_TEARDOWN_S, leave with status 1 right away, so a failed replica
+    always exits non-zero and the operator can restart it."""
+    if not dist.is_initialized():
+        return
     if _FAILED or _EXIT_STATUS:
         status = _EXIT_STATUS[-1] if _EXIT_STATUS else 1
-        if not _bounded(abort, EXIT_TEARDOWN_S):
+        if not teardown(failed=True):
             sys.stderr.write(f"[dist] process group teardown did not finish after a failure; exiting {status}\n")
             sys.stderr.flush()
             os._exit(status)
-    elif not _bounded(graceful, 3 * EXIT_TEARDOWN_S):
+    elif not teardown(failed=False):
         sys.stderr.write("[dist] process group teardown hung after a clean run; exiting 0\n")
         sys.stderr.flush()
         os._exit(0)
