@@ -238,3 +238,16 @@ def test_pull_gather_world8_lost_peer_fails_every_rank_in_time():
             continue   # it pulls from live peers; its own failure shows up as theirs
         assert f"rank {lost} never published" in msg, (r, msg)
         assert dt < 10.0, (r, dt)
+
+
+def test_sdma_reduce_scatter_refuses_accumulated_grads():
+    """TOA_ZERO_RS=sdma with TOA_FRESH_GRADS=0: the next step's zeroing pass is
+    not ordered after the owners' pulls of this rank's gradient slices, so the
+    trainer refuses the combination before anything is built (advice r5)."""
+    import types
+
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    stub = types.SimpleNamespace(fresh_grads=False, bucketer=None, flat=None)
+    with pytest.raises(RuntimeError, match="needs fresh gradients"):
+        LlamaTrainer._build_pull_reduce(stub)

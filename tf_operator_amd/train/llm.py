@@ -223,11 +223,6 @@ class LlamaTrainer:
     def _build_pull_reduce(self):
         from ..parallel import pull_gather
 
-        bk = self.bucketer
-        if (self.flat.grad.device.type != "cuda" or self.flat.grad.dtype != torch.bfloat16
-                or int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != bk.world):
-            raise RuntimeError("TOA_ZERO_RS=sdma needs bf16 gradients on a GPU job whose ranks share one node "
-                               "(LOCAL_WORLD_SIZE == world: the operator's node-local layout)")
         if not self.fresh_grads:
             # the zeroing pass at the start of step t+1 runs on the compute
             # stream before any wait, and nothing orders it after the owners'
@@ -236,6 +231,11 @@ class LlamaTrainer:
             # the next backward's first write to a bucket comes after the
             # forward waited for that bucket's updated shard, i.e. after the pull.
             raise RuntimeError("TOA_ZERO_RS=sdma needs fresh gradients (TOA_FRESH_GRADS=1, the default)")
+        bk = self.bucketer
+        if (self.flat.grad.device.type != "cuda" or self.flat.grad.dtype != torch.bfloat16
+                or int(os.environ.get("LOCAL_WORLD_SIZE", "0")) != bk.world):
+            raise RuntimeError("TOA_ZERO_RS=sdma needs bf16 gradients on a GPU job whose ranks share one node "
+                               "(LOCAL_WORLD_SIZE == world: the operator's node-local layout)")
         t = pull_gather.GpuIpcTransport(self.flat.grad, bk.rank, bk.world, len(bk.buckets), group=bk.group,
                                         what="reduce-scatter", timeout_ms=pull_gather.timeout_ms_from_env())
         return pull_gather.PullReduceScatter(t, [(b[0], b[1]) for b in bk.buckets], bk.rank, bk.world)
