@@ -1304,7 +1304,7 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     if epi == "plain" and not trace and not variant:
         stage_exit(a, 1)
     persist = SCHED["persist"]
-    assert not persist or (epi == "plain" and not trace and not SCHED["timing"])
+    assert not persist or (not trace and not SCHED["timing"])
     l_tile = a.fresh("tile")
     if persist:
         a.label(l_tile)
@@ -1435,12 +1435,16 @@ def persistent_next(a: Asm, epi: str, l_tile: str):
     tile_setup(a, epi, sr(S_ITER))                 # SRD_X / SRD_W / (S_TM, S_TN) of the next tile
     prologue_dma(a)
     epi_offsets(a, epi)
-    epilogue_plain(a)
+    n0 = len(a.out)
+    {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
+    n_vm = sum(1 for ins in a.out[n0:] if ins.lstrip().startswith(("buffer_load", "buffer_store")))
     tile_c(a, epi)
     zero_acc(a)
-    # the next tile's k-tile 0 landed: the epilogue's 32 stores and k-tile 1's
-    # 16 pieces are younger
-    a("s_waitcnt vmcnt(48)")
+    # the next tile's k-tile 0 landed: k-tile 1's 16 pieces and the epilogue's
+    # loads / stores are younger (plain: 32 stores -> 48; the SwiGLU epilogues
+    # issue more than the counter holds, and their own waits already retired
+    # everything up to their last load: 63 is then no wait at all)
+    a(f"s_waitcnt vmcnt({min(63, 16 + n_vm)})")
     a("s_barrier")
     a(f"s_branch {l_tile}")
     a.label(l_last)
@@ -1623,6 +1627,13 @@ PLAIN_VARIANTS = (
 # DIAGNOSTIC arms of the fused SwiGLU backward (wrong outputs by design),
 # launched by index through toa_gemm_asm_swiglu_bwd_variant: where the fused
 # epilogue's time goes (scripts/asm_gemm_bench.py --swiglu-variants).
+# Persistent fused SwiGLU GEMMs (one workgroup per CU walks its tiles; the
+# next tile's first two k-tiles are staged before the current tile's
+# epilogue, so its gu loads / dgu stores overlap that DMA instead of a fresh
+# workgroup's prologue): A/B arms with correct outputs, launched by
+# toa_gemm_asm_set_swiglu_persist.
+SWIGLU_PERSIST_VARIANTS = (("swiglu_fwd", "p1", {"persist": True}), ("swiglu_bwd", "p1", {"persist": True}))
+
 SWIGLU_BWD_VARIANTS = (
     ("b1", {"epi_none": True}),          # the main loop alone
     ("b2", {"epi_noload": True}),        # math + stores, no gu loads
@@ -1669,6 +1680,10 @@ def generate() -> str:
         metas.append(meta)
     for vname, knobs in SWIGLU_BWD_VARIANTS:
         body, meta = _with_knobs(knobs, lambda: kernel("swiglu_bwd", variant=vname))
+        parts.append(body)
+        metas.append(meta)
+    for epi, vname, knobs in SWIGLU_PERSIST_VARIANTS:
+        body, meta = _with_knobs(knobs, lambda: kernel(epi, variant=vname))
         parts.append(body)
         metas.append(meta)
     import attn_gen   # the attention forward and the weight-gradient kernel share this code object

@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_N = 52 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_SWFWD_P1 = 52, K_SWBWD_P1 = 53, K_N = 54 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -62,7 +62,9 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // the plain kernel's ninth A/B arm (after the table above was laid out)
                            "toa_gemm_tn_asm_plain_v9",
                            // the dK/dV kernel's arm s7 (attn_bwd_gen.py VARIANTS, appended)
-                           "toa_attn_dkdv_asm_s7", "toa_attn_dkdv_asm_d8", "toa_attn_dkdv_asm_s8"};
+                           "toa_attn_dkdv_asm_s7", "toa_attn_dkdv_asm_d8", "toa_attn_dkdv_asm_s8",
+                           // the persistent fused SwiGLU GEMMs (gemm_gen.py SWIGLU_PERSIST_VARIANTS)
+                           "toa_gemm_tn_asm_swiglu_fwd_p1", "toa_gemm_tn_asm_swiglu_bwd_p1"};
 
 struct DevModule {
   std::once_flag once;
@@ -553,6 +555,32 @@ extern "C" int toa_gemm_asm_set_epi_variant(int v) {
   return 0;
 }
 
+// Persistent fused SwiGLU GEMMs (gemm_gen.py SWIGLU_PERSIST_VARIANTS: a
+// workgroup per CU walks its tiles, the next tile's first k-tiles staged
+// before the current tile's epilogue).  bit 0: the forward, bit 1: the
+// backward.  Set by toa_gemm_asm_set_swiglu_persist or TOA_ASM_SWIGLU_PERSIST.
+static int g_swiglu_persist = -1;
+static int swiglu_persist() {
+  if (g_swiglu_persist < 0) {
+    const char* e = getenv("TOA_ASM_SWIGLU_PERSIST");
+    g_swiglu_persist = (e && *e) ? (atoi(e) & 3) : 0;
+  }
+  return g_swiglu_persist;
+}
+extern "C" int toa_gemm_asm_set_swiglu_persist(int v) {
+  if (v < 0 || v > 3) return (int)hipErrorInvalidValue;
+  g_swiglu_persist = v;
+  return 0;
+}
+static int launch_swiglu(int which, int persist_bit, const Args& a, hipStream_t stream) {
+  if (!g_epi_r4 && (swiglu_persist() & persist_bit)) {
+    const unsigned tiles = a.tiles_m * a.tiles_n;
+    return launch(which == K_SWIGLU_FWD ? K_SWFWD_P1 : K_SWBWD_P1, a, stream,
+                  tiles < kPersistGrid ? tiles : kPersistGrid);
+  }
+  return launch(which, a, stream);
+}
+
 extern "C" int toa_gemm_asm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* Wgu, int64_t ldw, bf16_t* GU,
                                    int64_t ldgu, bf16_t* S, int64_t lds_, int M, int F, int K, hipStream_t stream) {
   if (!common_ok(M, K, ldx, ldw, X, Wgu) || F <= 0 || F % 128 || !ld_ok(ldgu, 2 * F) || !ld_ok(lds_, F) || !al16(GU) ||
@@ -563,7 +591,7 @@ extern "C" int toa_gemm_asm_swiglu(const bf16_t* X, int64_t ldx, const bf16_t* W
   a.lds = (uint32_t)(lds_ * 2);
   a.fw = (uint32_t)((int64_t)F * ldw * 2);
   a.fc = (uint32_t)(F * 2);
-  return launch(g_epi_r4 ? K_SWIGLU_FWD_R4 : K_SWIGLU_FWD, a, stream);
+  return g_epi_r4 ? launch(K_SWIGLU_FWD_R4, a, stream) : launch_swiglu(K_SWIGLU_FWD, 1, a, stream);
 }
 
 extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16_t* WdT, int64_t ldw,
@@ -576,7 +604,7 @@ extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16
   a.S = (uint64_t)GU;
   a.lds = (uint32_t)(ldgu * 2);
   a.fc = (uint32_t)(F * 2);
-  return launch(g_epi_r4 ? K_SWIGLU_BWD_R4 : K_SWIGLU_BWD, a, stream);
+  return g_epi_r4 ? launch(K_SWIGLU_BWD_R4, a, stream) : launch_swiglu(K_SWIGLU_BWD, 2, a, stream);
 }
 
 // DIAGNOSTIC: arm v (1..) of the fused SwiGLU backward (gemm_gen.py
@@ -585,7 +613,7 @@ extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16
 extern "C" int toa_gemm_asm_swiglu_bwd_variant(int v, const bf16_t* dY, int64_t ldy, const bf16_t* WdT, int64_t ldw,
                                                const bf16_t* GU, int64_t ldgu, bf16_t* dGU, int64_t lddgu, int M,
                                                int F, int K, hipStream_t stream) {
-  if (v < 0 || v > K_N - K_SWBWD_V1 || !common_ok(M, K, ldy, ldw, dY, WdT) || F <= 0 || F % 256 ||
+  if (v < 0 || v > K_PLAIN_V9 - K_SWBWD_V1 || !common_ok(M, K, ldy, ldw, dY, WdT) || F <= 0 || F % 256 ||
       !ld_ok(ldgu, 2 * F) || !ld_ok(lddgu, 2 * F) || !al16(GU) || !al16(dGU))
     return (int)hipErrorInvalidValue;
   Args a = base_args(dY, ldy, WdT, ldw, dGU, lddgu, M, F / 256, K);

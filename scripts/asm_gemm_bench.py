@@ -424,6 +424,16 @@ def bench(a):
                      (f"asm_fused_bwd_map{tm_}", lambda tm_=tm_: mapped(tm_, lambda: asm_swiglu_bwd(d2, wdt, gu)))]
         for v in [int(t) for t in a.swiglu_variants.split(",") if t]:
             arms.append((f"asm_fused_bwd_b{v}", lambda v=v: asm_swiglu_bwd_variant(v, d2, wdt, gu, dgu_v)))
+        def persistent(bit, fn):
+            _lib.call("toa_gemm_asm_set_swiglu_persist", bit)
+            try:
+                return fn()
+            finally:
+                _lib.call("toa_gemm_asm_set_swiglu_persist", 0)
+
+        if a.swiglu_persist:
+            arms += [("asm_fused_fwd_p1", lambda: persistent(1, lambda: asm_swiglu(x, wgu))),
+                     ("asm_fused_bwd_p1", lambda: persistent(2, lambda: asm_swiglu_bwd(d2, wdt, gu)))]
         for ph in phases:
             arms += [(f"asm_fused_fwd_ph{ph:#x}", lambda ph=ph: with_phase(1, ph, lambda: asm_swiglu(x, wgu))),
                      (f"asm_fused_bwd_ph{ph:#x}", lambda ph=ph: with_phase(2, ph, lambda: asm_swiglu_bwd(d2, wdt, gu)))]
@@ -439,7 +449,13 @@ def bench(a):
                     with_phase(1, ph, lambda: asm_swiglu(x, wgu)), ref_f))
                     and torch.equal(with_phase(2, ph, lambda: asm_swiglu_bwd(d2, wdt, gu)), ref_b))
                 for ph in phases}
-        print(json.dumps({"mlp_ms": out["mlp_ms"]}), flush=True)
+        if a.swiglu_persist:   # the persistent arms compute what the product kernels compute
+            ref_f, ref_b = asm_swiglu(x, wgu), asm_swiglu_bwd(d2, wdt, gu)
+            pf, pb = persistent(1, lambda: asm_swiglu(x, wgu)), persistent(2, lambda: asm_swiglu_bwd(d2, wdt, gu))
+            out["mlp_persist_bit_identical"] = bool(all(torch.equal(p_, q_) for p_, q_ in zip(pf, ref_f))
+                                                    and torch.equal(pb, ref_b))
+        print(json.dumps({"mlp_ms": out["mlp_ms"], **({"persist_same": out["mlp_persist_bit_identical"]}
+                                                      if a.swiglu_persist else {})}), flush=True)
     print(json.dumps(out))
 
 
@@ -458,6 +474,7 @@ def main():
     ap.add_argument("--maps", default="", help="tile orders to add as arms (kernarg map words, e.g. 2,3,18,20)")
     ap.add_argument("--swiglu-variants", default="", help="fused SwiGLU backward diagnostic arms (1..5) "
                                                           "added to the MLP arms (gemm_gen.SWIGLU_BWD_VARIANTS)")
+    ap.add_argument("--swiglu-persist", action="store_true", help="add the persistent fused SwiGLU arms (p1)")
     ap.add_argument("--phases", default="", help="first-wave start-offset words to add as arms (n | log2 g << 16, "
                                                  "e.g. 0x10028,0x20014): plain forms and the fused MLP")
     ap.add_argument("--timing", action="store_true", help="wait-cycle breakdown of the product kernel (--forms)")

@@ -10,6 +10,7 @@ attnb=N / attnd=N (toa_attn_set_fwd_variant / _bwd_variant / _dkdv_variant forms
 epi=r4|pipe (the fused SwiGLU GEMMs' epilogues, toa_gemm_asm_set_epi_variant),
 wmap=N (the weight-gradient tile order, toa_wgrad_asm_set_map; -1 = the per-shape rule),
 persist=N (the plain TN kernel's persistent form, toa_gemm_asm_set_persist; -1 = the per-shape rule),
+swp=N (the fused SwiGLU GEMMs' persistent forms, toa_gemm_asm_set_swiglu_persist: bit 0 fwd, bit 1 bwd),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -54,6 +55,8 @@ def apply(arm: str):
             _lib.call("toa_attn_dkdv_asm_set_arm", int(val))
         elif key == "persist":   # TN plain kernel: -1 = the per-shape rule, 0 = never persistent, 1 = always
             _lib.call("toa_gemm_asm_set_persist", int(val))
+        elif key == "swp":   # fused SwiGLU GEMMs persistent: bit 0 forward, bit 1 backward
+            _lib.call("toa_gemm_asm_set_swiglu_persist", int(val))
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":

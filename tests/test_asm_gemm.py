@@ -204,6 +204,42 @@ def test_asm_gemm_swiglu_bwd_emulated():
     close(dgu[:, F:], ds * g * sg)
 
 
+@pytest.mark.parametrize("epi,grid", [("swiglu_fwd", 1), ("swiglu_fwd", 4), ("swiglu_bwd", 1), ("swiglu_bwd", 4)])
+def test_asm_gemm_swiglu_persistent_emulated(epi, grid):
+    """The persistent fused SwiGLU arms (SWIGLU_PERSIST_VARIANTS): `grid`
+    workgroups walk the 6 tiles, the next tile's first k-tiles staged before
+    the current tile's epilogue (whose gu loads / dgu stores then sit behind
+    that DMA in the in-order vmcnt); every output equals the product kernel's
+    bit for bit.  K = 320: an odd k-tile count (the stage parity fix-up)."""
+    rng = np.random.default_rng(23)
+    M, K = 512, 320
+    F = 384 if epi == "swiglu_fwd" else 768
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((2 * F if epi == "swiglu_fwd" else F, K)) * 0.1)
+    GU = bf16(rng.standard_normal((M, 2 * F)))
+    tiles_n = F // 128 if epi == "swiglu_fwd" else F // 256
+    outs = []
+    for name, g in ((f"toa_gemm_tn_asm_{epi}", None), (f"toa_gemm_tn_asm_{epi}_p1", grid)):
+        mem = emu.Memory()
+        ax, aw = mem.add(X), mem.add(W)
+        if epi == "swiglu_fwd":
+            ac, as_ = mem.add(np.zeros((M, 2 * F), np.uint16)), mem.add(np.zeros((M, F), np.uint16))
+            karg = host_args.pack(ax, aw, ac, as_, 2 * K, 2 * K, 4 * F, 2 * F, K, M // 256, tiles_n,
+                                  fw_b=F * 2 * K, fc_b=2 * F, grid=g)
+        else:
+            ac, as_ = mem.add(np.zeros((M, 2 * F), np.uint16)), mem.add(GU)
+            karg = host_args.pack(ax, aw, ac, as_, 2 * K, 2 * K, 4 * F, 4 * F, K, M // 256, tiles_n, fc_b=2 * F,
+                                  grid=g)
+        run_all(name, karg, (M // 256) * tiles_n if g is None else g, mem)
+        outs.append([mem.bufs[i][1].copy() for i in (2, 3)])
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    if epi == "swiglu_bwd":
+        ds = tof(bf16(tof(X) @ tof(W).T))
+        dgu = tof(outs[1][0].view(np.uint16).reshape(M, 2 * F))
+        close(dgu[:, F:], ds * tof(GU[:, :F]) / (1 + np.exp(-tof(GU[:, :F]))))
+
+
 @pytest.mark.parametrize("tile_map", [0, 1, 2, 3, 4, 16, 17, 18, 19, 20])
 def test_asm_gemm_tile_order_is_a_bijection(tile_map):
     """The XCD remap + group walk (row groups, or column groups with the walk
@@ -275,7 +311,7 @@ def test_host_kernel_table_matches_generator():
     import attn_gen
     # + the round-4 SwiGLU epilogue arms (2) + the SwiGLU backward's diagnostic arms
     assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
-        len(attn_bwd_gen.VARIANTS) + 2 + len(gemm_gen.SWIGLU_BWD_VARIANTS)
+        len(attn_bwd_gen.VARIANTS) + 2 + len(gemm_gen.SWIGLU_BWD_VARIANTS) + len(gemm_gen.SWIGLU_PERSIST_VARIANTS)
     flags = re.search(r"kVariantPersist\[kNumPlainVariants\] = \{([^}]*)\}", src).group(1)
     assert int(re.search(r"kNumPlainVariants = (\d+)", src).group(1)) == len(gemm_gen.PLAIN_VARIANTS)
     assert [f.strip() == "true" for f in flags.split(",")] == [bool(k.get("persist")) for _, k in gemm_gen.PLAIN_VARIANTS]

@@ -1308,6 +1308,38 @@ def test_gemm_asm_swiglu_epilogues(M, F, K):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("M,F,K", [(1024, 1536, 320), (2048, 3072, 4096)])
+def test_gemm_asm_swiglu_persistent_bit_identical(M, F, K):
+    """The persistent fused SwiGLU GEMMs (toa_gemm_asm_set_swiglu_persist:
+    a workgroup per CU walks its tiles) write the product kernels' gu, s and
+    dgu bit for bit: the grid of 2048 x 3072 has more tiles than CUs, so
+    workgroups walk several (the emulator covers 1-4 workgroups)."""
+    from tf_operator_amd.ops import gemm
+
+    _lib()
+    torch.manual_seed(4)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    wgu = (torch.randn(2 * F, K, device=DEV) / K ** 0.5).to(torch.bfloat16)
+    wd = (torch.randn(K, F, device=DEV) / F ** 0.5).to(torch.bfloat16)
+    wd._toa_wt = wd.t().contiguous()
+    d2 = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    old = gemm.mode()
+    gemm.set_mode("asm")
+    outs = []
+    try:
+        for bits in (0, 3):
+            _lib().call("toa_gemm_asm_set_swiglu_persist", bits)
+            gu, s = gemm.swiglu_gate_up(x, wgu)
+            dgu = gemm.swiglu_down_dgrad(d2, wd, gu)
+            torch.cuda.synchronize()
+            outs.append((gu.clone(), s.clone(), dgu.clone()))
+    finally:
+        _lib().call("toa_gemm_asm_set_swiglu_persist", 0)
+        gemm.set_mode(old)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_llama_layer_fused_mlp_matches_library_path():
     """A llama-tiny128 training step with the assembly GEMMs and the fused
     SwiGLU (TOA_GEMM=asm, the default) follows the hipBLASLt path's loss."""
