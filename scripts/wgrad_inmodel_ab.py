@@ -11,6 +11,7 @@ epi=r4|pipe (the fused SwiGLU GEMMs' epilogues, toa_gemm_asm_set_epi_variant),
 wmap=N (the weight-gradient tile order, toa_wgrad_asm_set_map; -1 = the per-shape rule),
 persist=N (the plain TN kernel's persistent form, toa_gemm_asm_set_persist; -1 = the per-shape rule),
 swp=N (the fused SwiGLU GEMMs' persistent forms, toa_gemm_asm_set_swiglu_persist: bit 0 fwd, bit 1 bwd),
+ovl=0|1 (AdamW per bucket on a side stream under the next forward, FlatAdamW overlap),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -30,6 +31,9 @@ import torch
 sys.path.insert(0, ".")
 from tf_operator_amd.ops import _lib, gemm  # noqa: E402
 from tf_operator_amd.train.llm import LlamaTrainer  # noqa: E402
+
+
+TR = None   # the trainer (arms that switch trainer state: ovl)
 
 
 def apply(arm: str):
@@ -57,6 +61,9 @@ def apply(arm: str):
             _lib.call("toa_gemm_asm_set_persist", int(val))
         elif key == "swp":   # fused SwiGLU GEMMs persistent: bit 0 forward, bit 1 backward
             _lib.call("toa_gemm_asm_set_swiglu_persist", int(val))
+        elif key == "ovl":   # AdamW per bucket on a side stream under the next forward (FlatAdamW overlap)
+            TR.opt.wait_all()
+            TR.opt.overlap = bool(int(val))
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":
@@ -77,7 +84,9 @@ def main():
     arms = a.arms.split(",")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    tr = LlamaTrainer("llama3-8b", dev, micro_batch=a.micro_batch, seq_len=4096)
+    global TR
+    tr = TR = LlamaTrainer("llama3-8b", dev, micro_batch=a.micro_batch, seq_len=4096,
+                           overlap_optimizer=True if "ovl=" in a.arms else None)
     batch = [tr.synthetic_batch()]
     for arm in arms:  # every arm warm (code objects, plans)
         apply(arm)

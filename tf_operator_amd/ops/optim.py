@@ -47,9 +47,9 @@ class FlatAdamW:
     """AdamW over a :class:`tf_operator_amd.parallel.flat.FlatParams`.
 
     overlap=True (GPU): after the global grad norm, the update runs on a side
-    stream bucket by bucket in FORWARD order, zeroing each gradient slice as
-    it reads it (no separate zero_grad pass), and records one event per
-    bucket.  The next step's forward waits per bucket (wait_bucket, called
+    stream bucket by bucket in FORWARD order (zeroing each gradient slice as
+    it reads it when fuse_zero_grad; with fresh gradients nothing needs
+    zeroing), and records one event per bucket.  The next step's forward waits per bucket (wait_bucket, called
     from module pre-hooks), so the memory-bound update of late layers runs
     under the compute-bound GEMMs of early ones; backward waits for all of it
     (wait_all) before writing gradients.  Measured on Llama-3-8B it gains
@@ -100,7 +100,7 @@ class FlatAdamW:
         self.last_norm_sq = self._norm
         self.overlap = bool(overlap) and flat.device.type == "cuda" and _lib.available()
         # zero each gradient slice as the update reads it (the caller then skips zero_grad)
-        self.fuse_zero_grad = bool(fuse_zero_grad) or self.overlap
+        self.fuse_zero_grad = bool(fuse_zero_grad)
         self.grads_zeroed = False  # the last step() zeroed the gradients itself
         if self.overlap:
             self.side = torch.cuda.Stream(device=flat.device)
@@ -197,7 +197,7 @@ class FlatAdamW:
                 for (a, b, decay) in self.runs:
                     a2, b2 = max(a, lo), min(b, hi)
                     if a2 < b2:
-                        self._launch(a2, b2, decay, lr, grad_scale, clip, True, s)
+                        self._launch(a2, b2, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
                 if self.post_update is not None:
                     with torch.cuda.stream(self.side):
                         self.post_update(lo, hi)
@@ -210,7 +210,7 @@ class FlatAdamW:
             # tensors used on the side stream must not be recycled by the main stream's allocator
             for t in (f.grad, f.param, f.master, f.exp_avg, f.exp_avg_sq, self._norm):
                 t.record_stream(self.side)
-            self.grads_zeroed = True
+            self.grads_zeroed = self.fuse_zero_grad
             return
         self.grads_zeroed = False
         if _lib.use_hip(f.grad):

@@ -154,7 +154,7 @@ class LlamaTrainer:
             return self._step(batches)
 
     def _step(self, batches):
-        if self.fresh_grads and not self.opt.overlap:
+        if self.fresh_grads:
             self.flat.mark_fresh()
         elif not self.opt.grads_zeroed:
             self.flat.zero_grad()
@@ -169,7 +169,7 @@ class LlamaTrainer:
             (loss / len(batches)).backward()
             self._phase("first_bwd_issued")
             loss_sum = loss.detach() if loss_sum is None else loss_sum + loss.detach()
-        if self.fresh_grads and not self.opt.overlap:
+        if self.fresh_grads:
             self.flat.zero_stale()  # parameters no producer wrote this step
         self.bucketer.armed = True
         self.bucketer.finish()
