@@ -290,3 +290,36 @@ extern "C" int toa_cast_f32_to_bf16(const float* x, bf16_t* y, int64_t n, hipStr
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid), dim3(256), 0, stream, x, y, n / 8);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// A stream whose kernels may only use some of the CUs
+// (hipExtStreamCreateWithCUMask): the overlapped AdamW (FlatAdamW overlap,
+// TOA_OPT_CUS) runs its memory-bound update on a few CUs beside the
+// compute-bound GEMMs instead of taking every CU a finished GEMM workgroup
+// frees.  mode 0: CUs 0 .. n-1 of the mask; mode 1: n CUs spread evenly over
+// the mask (which bit is which XCD is the driver's mapping: the probe
+// scripts/cu_mask_probe.py measures both).
+// ---------------------------------------------------------------------------
+extern "C" int toa_stream_create_cu_mask(int mode, int n, void** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  int total = 0;
+  e = hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return (int)e;
+  if (out == nullptr || n <= 0 || n > total || total > 1024 || (mode != 0 && mode != 1))
+    return (int)hipErrorInvalidValue;
+  uint32_t mask[32] = {};
+  const int words = (total + 31) / 32;
+  for (int i = 0; i < n; ++i) {
+    const int cu = mode == 0 ? i : (int)((int64_t)i * total / n);
+    mask[cu / 32] |= 1u << (cu % 32);
+  }
+  hipStream_t s = nullptr;
+  e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+  if (e != hipSuccess) return (int)e;
+  *out = (void*)s;
+  return 0;
+}
+
+extern "C" int toa_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }

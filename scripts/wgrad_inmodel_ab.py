@@ -12,6 +12,7 @@ wmap=N (the weight-gradient tile order, toa_wgrad_asm_set_map; -1 = the per-shap
 persist=N (the plain TN kernel's persistent form, toa_gemm_asm_set_persist; -1 = the per-shape rule),
 swp=N (the fused SwiGLU GEMMs' persistent forms, toa_gemm_asm_set_swiglu_persist: bit 0 fwd, bit 1 bwd),
 ovl=0|1 (AdamW per bucket on a side stream under the next forward, FlatAdamW overlap),
+ovlcu=n[:mode] (that side stream limited to n CUs, toa_stream_create_cu_mask; 0 = unmasked),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -64,6 +65,13 @@ def apply(arm: str):
         elif key == "ovl":   # AdamW per bucket on a side stream under the next forward (FlatAdamW overlap)
             TR.opt.wait_all()
             TR.opt.overlap = bool(int(val))
+        elif key == "ovlcu":   # the overlapped update's stream: n CUs (mode 1: spread; n:mode), 0 = unmasked
+            from tf_operator_amd.ops.optim import masked_stream
+            TR.opt.wait_all()
+            torch.cuda.synchronize()
+            n, _, mode = val.partition(":")
+            TR.opt.side = (masked_stream(int(n), int(mode or 1), TR.device) if int(n)
+                           else torch.cuda.Stream(device=TR.device))
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":

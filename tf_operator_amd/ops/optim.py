@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -41,6 +42,20 @@ def adamw_reference(master, grad, m, v, *, lr, beta1, beta2, eps, weight_decay, 
     bc2 = 1 - beta2 ** step
     denom = v.sqrt() / math.sqrt(bc2) + eps
     master.add_(-lr * (m / bc1) / denom - lr * weight_decay * master)
+
+
+_MASKED = []   # (ExternalStream, handle): kept for the process's life
+
+
+def masked_stream(n: int, mode: int = 1, device=None):
+    """A torch stream over a HIP stream whose kernels may use only `n` CUs
+    (csrc/hip/optim.hip toa_stream_create_cu_mask; mode 1 spreads them over
+    the mask, mode 0 takes the first n)."""
+    h = ctypes.c_void_p()
+    _lib.call("toa_stream_create_cu_mask", int(mode), int(n), ctypes.byref(h))
+    st = torch.cuda.ExternalStream(h.value, device=device)
+    _MASKED.append((st, h))
+    return st
 
 
 class FlatAdamW:
@@ -103,7 +118,12 @@ class FlatAdamW:
         self.fuse_zero_grad = bool(fuse_zero_grad)
         self.grads_zeroed = False  # the last step() zeroed the gradients itself
         if self.overlap:
-            self.side = torch.cuda.Stream(device=flat.device)
+            # TOA_OPT_CUS=n[:mode]: the update's stream may use only n CUs
+            # (masked_stream), so it runs beside the GEMMs instead of taking
+            # every CU a finished GEMM workgroup frees
+            cus = os.environ.get("TOA_OPT_CUS", "")
+            self.side = (masked_stream(*[int(x) for x in cus.split(":")], device=flat.device) if cus
+                         else torch.cuda.Stream(device=flat.device))
             ranges = [(b[0], b[1]) for b in buckets] if buckets else [(0, flat.numel)]
             # flat order is backward order: the forward needs the last bucket first
             self.order = list(range(len(ranges)))[::-1]
