@@ -68,7 +68,9 @@ class FlatAdamW:
     from module pre-hooks), so the memory-bound update of late layers runs
     under the compute-bound GEMMs of early ones; backward waits for all of it
     (wait_all) before writing gradients.  Measured on Llama-3-8B it gains
-    nothing (1100 vs 1098 ms/step): the GEMMs already hold every CU, so the
+    nothing (round 2: 1100 vs 1098 ms/step; round 6 with the assembly GEMMs:
+    -1.6 +- 0.6 and +5.2 +- 4.5 ms in two A/Bs, and slower on a CU-masked
+    stream, TOA_OPT_CUS; docs/kernels.md): the GEMMs hold every CU, so the
     update only slots in between them; it stays opt-in (TOA_OPT_OVERLAP=1).
 
     fuse_zero_grad=True: the update zeroes the gradient as it reads it
