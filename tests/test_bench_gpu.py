@@ -47,12 +47,15 @@ def _run(n, extra_env=None, timeout=240):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-def test_bench_collectives_ab_four_ranks_one_gpu():
-    p, lines = _run(4)
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_collectives_ab_ranks_on_one_gpu(n):
+    """n = 8: the driver's N = 8 command shape (torchrun, 8 ranks, ZeRO-1
+    over 8 shards, the A/B's copy-engine pulls at world 8)."""
+    p, lines = _run(n)
     assert p.returncode == 0, p.stderr[-4000:]
     assert len(lines) == 1, p.stdout[-3000:]
     r = json.loads(lines[0])
-    assert r["n_gpus"] == 4 and r["value"] > 0 and r["replicas_identical"] is True
+    assert r["n_gpus"] == n and r["value"] > 0 and r["replicas_identical"] is True
     ab = r["collectives_ab"]
     print(json.dumps(ab))
     assert "rccl_transport_ok" in ab
