@@ -179,85 +179,9 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
   }
 }
 
-// Two 8-element chunks per thread (i and i + the grid's thread count), all
-// 14 loads issued before either update: twice the bytes in flight per wave at
-// half the waves.  A/B arm (variant bit 2); bit-identical to the one-chunk
-// kernel (each element's arithmetic is the same).
-template <bool GRAD_BF16>
-__global__ __launch_bounds__(256) void adamw_flat2_kernel(float* __restrict__ master, bf16_t* __restrict__ param,
-                                                          void* __restrict__ grad, int zero_grad,
-                                                          float* __restrict__ m, float* __restrict__ v, int64_t n8,
-                                                          float lr, float b1, float b2, float eps, float wd,
-                                                          float inv_bc1, float inv_sqrt_bc2, float grad_scale,
-                                                          const float* __restrict__ norm_sq, float max_norm,
-                                                          const int* __restrict__ step_dev) {
-  const float scale = adam_prologue(b1, b2, grad_scale, norm_sq, max_norm, step_dev, inv_bc1, inv_sqrt_bc2);
-  const float omb1 = 1.f - b1, omb2 = 1.f - b2, lrwd = lr * wd;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n8; i0 += 2 * stride) {
-    const int64_t idx[2] = {i0, i0 + stride};
-    const bool two = idx[1] < n8;
-    f32x4 gv[2][2], pv[2][2], mv[2][2], vv[2][2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      if (c == 1 && !two) break;
-      const int64_t i = idx[c];
-      if (GRAD_BF16) {
-        const u32x4 gb = ld_s((const u32x4*)grad + i, true);
-        float g8[8];
-        unpack8(gb, g8);
-        gv[c][0] = f32x4{g8[0], g8[1], g8[2], g8[3]};
-        gv[c][1] = f32x4{g8[4], g8[5], g8[6], g8[7]};
-      } else {
-        gv[c][0] = ld_s((const f32x4*)grad + 2 * i, true);
-        gv[c][1] = ld_s((const f32x4*)grad + 2 * i + 1, true);
-      }
-      pv[c][0] = ld_s((const f32x4*)master + 2 * i, true);
-      pv[c][1] = ld_s((const f32x4*)master + 2 * i + 1, true);
-      mv[c][0] = ld_s((const f32x4*)m + 2 * i, true);
-      mv[c][1] = ld_s((const f32x4*)m + 2 * i + 1, true);
-      vv[c][0] = ld_s((const f32x4*)v + 2 * i, true);
-      vv[c][1] = ld_s((const f32x4*)v + 2 * i + 1, true);
-    }
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      if (c == 1 && !two) break;
-      const int64_t i = idx[c];
-      if (zero_grad) {
-        if (GRAD_BF16) {
-          st16((bf16_t*)grad + i * 8, u32x4{0, 0, 0, 0});
-        } else {
-          *((f32x4*)grad + 2 * i) = f32x4{0.f, 0.f, 0.f, 0.f};
-          *((f32x4*)grad + 2 * i + 1) = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      float p[8];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float pp = pv[c][h][j], mm = mv[c][h][j], vq = vv[c][h][j];
-          adam_elem(gv[c][h][j], pp, mm, vq, scale, b1, b2, omb1, omb2, lr, lrwd, eps, inv_bc1, inv_sqrt_bc2);
-          pv[c][h][j] = pp;
-          mv[c][h][j] = mm;
-          vv[c][h][j] = vq;
-          p[4 * h + j] = pp;
-        }
-      st_s((f32x4*)master + 2 * i, pv[c][0], true);
-      st_s((f32x4*)master + 2 * i + 1, pv[c][1], true);
-      st_s((f32x4*)m + 2 * i, mv[c][0], true);
-      st_s((f32x4*)m + 2 * i + 1, mv[c][1], true);
-      st_s((f32x4*)v + 2 * i, vv[c][0], true);
-      st_s((f32x4*)v + 2 * i + 1, vv[c][1], true);
-      if (param != nullptr) st_s((u32x4*)param + i, pack8(p), true);
-    }
-  }
-}
-
 // Variant switch for in-process A/B (scripts/stream_ab.py,
 // scripts/adamw_grid_bench.py): bit 0 = the non-temporal AdamW, bit 1 = the
-// row-structured non-temporal SwiGLU, bit 2 = AdamW two chunks per thread
-// (adamw_flat2_kernel), bits 8.. = AdamW grid cap / 1024 (0:
+// row-structured non-temporal SwiGLU, bits 8.. = AdamW grid cap / 1024 (0:
 // toa_stream_grid's 2048).  Defaults from A/Bs on MI355X: AdamW NT
 // (profiles/r2_stream_ab/), SwiGLU rows+NT fwd 0.404 -> 0.373 ms and bwd
 // 0.723 -> 0.653 ms at T = 24576, F = 14336; and the AdamW grid at one
@@ -291,10 +215,6 @@ static int adamw_launch(float* master, bf16_t* param, void* grad, int grad_flags
   const bool nt = (g_stream_variant & 1) && n8 >= (int64_t)(1 << 20);
   auto k = (grad_flags & 1) ? (nt ? adamw_flat_kernel<true, true> : adamw_flat_kernel<true, false>)
                             : (nt ? adamw_flat_kernel<false, true> : adamw_flat_kernel<false, false>);
-  if (nt && (g_stream_variant & 4)) {  // A/B arm: two chunks per thread, half the grid
-    k = (grad_flags & 1) ? adamw_flat2_kernel<true> : adamw_flat2_kernel<false>;
-    grid = (int)std::max<int64_t>((grid + 1) / 2, 1);
-  }
   hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, n8, lr, beta1, beta2,
                      eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq, max_norm, step_dev);
   return (int)hipGetLastError();

@@ -23,10 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--caps", default="2,16,64,255", help="grid caps / 1024")
-    ap.add_argument("--two", action="store_true", help="add the two-chunks-per-thread arms (variant bit 2)")
     a = ap.parse_args()
-    a.caps = [int(c) for c in a.caps.split(",")]
     torch.manual_seed(0)
     shapes = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
     ps = [torch.nn.Parameter(torch.randn(*s, device="cuda").to(torch.bfloat16) * 0.02) for s in shapes]
@@ -36,25 +33,13 @@ def main():
     plain = FlatAdamW(flat, lr=1e-4, max_grad_norm=0.0)
     flat.grad.copy_(torch.randn(flat.grad.numel(), device="cuda").to(flat.grad.dtype) * 1e-3)
     nparam = sum(p.numel() for p in ps)
-    # arm -> (variant word, optimizer): bits 8.. grid cap / 1024, bit 2 two chunks per thread
-    arms = {f"cap{c}" + ("x2" if two else "") + ("+refresh" if o is with_wt else ""): (1 | 2 | (4 if two else 0) | (c << 8), o)
-            for c in a.caps for two in ((False, True) if a.two else (False,)) for o in (plain, with_wt)}
+    arms = {f"cap{c}" + ("+refresh" if o is with_wt else ""): (c, o)
+            for c in (2, 16, 64, 255) for o in (plain, with_wt)}
     times = {k: [] for k in arms}
-    if a.two:   # the two-chunk kernel updates every element as the one-chunk kernel does
-        state = [t.clone() for t in (flat.master, flat.exp_avg, flat.exp_avg_sq, flat.param)]
-        outs = []
-        for word in (1 | 2 | (255 << 8), 1 | 2 | 4 | (255 << 8)):
-            for t, s0 in zip((flat.master, flat.exp_avg, flat.exp_avg_sq, flat.param), state):
-                t.data.copy_(s0)
-            _lib.call_ret("toa_set_stream_variant", word)
-            plain.step()
-            torch.cuda.synchronize()
-            outs.append([t.clone() for t in (flat.master, flat.exp_avg, flat.exp_avg_sq, flat.param)])
-        print(json.dumps({"two_chunk_bit_identical": all(torch.equal(x, y) for x, y in zip(*outs))}), flush=True)
 
     def run(arm):
-        word, o = arms[arm]
-        _lib.call_ret("toa_set_stream_variant", word)
+        cap, o = arms[arm]
+        _lib.call_ret("toa_set_stream_variant", 1 | 2 | (cap << 8))
         o.step()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

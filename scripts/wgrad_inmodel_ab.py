@@ -74,8 +74,6 @@ def apply(arm: str):
                            else torch.cuda.Stream(device=TR.device))
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
-        elif key == "adam2":   # flat AdamW with two chunks per thread (variant bit 2)
-            _lib.call_ret("toa_set_stream_variant", 1 | 2 | (4 if int(val) else 0) | (255 << 8))
         elif key == "adamcap":
             _lib.call_ret("toa_set_stream_variant", 1 | 2 | (int(val) << 8))
         else:
