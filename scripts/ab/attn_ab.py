@@ -2,7 +2,7 @@
 same inputs, interleaved rounds, median ms per kernel family; each variant's
 outputs are checked against the first's.
 
-    python scripts/ab/attn_ab.py base noslp prio [--B 6]
+    python scripts/ab/attn_ab.py base noslp [--B 6]
 """
 import argparse
 import ctypes

@@ -1,7 +1,7 @@
 """Build variants of one HIP source into separate .so files for in-process
 A/B timing (guide §5.4 rule 24: compare arms in one process, interleaved).
 
-    python scripts/ab/build_variants.py csrc/hip/attention.hip base: noslp:-fno-slp-vectorize prio:-DATTN_STATIC_PRIO
+    python scripts/ab/build_variants.py csrc/hip/attention.hip base: noslp:-fno-slp-vectorize
 """
 import os
 import subprocess
