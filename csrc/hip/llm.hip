@@ -355,7 +355,10 @@ __global__ __launch_bounds__(512) void xent_fwd_kernel(const T* __restrict__ log
   }
 }
 
-template <typename T>
+// U chunks of 8 per thread per round, all U loads issued before the first
+// store: one 16-B load in flight per thread (U = 1, the round-5 loop) left
+// the sweep at 5.1 TB/s.  toa_xent_set_unroll picks U (A/B; bit-identical).
+template <typename T, int U>
 __global__ __launch_bounds__(512) void xent_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                        const float* __restrict__ lse_in,
                                                        const float* __restrict__ grad_out,
@@ -369,25 +372,50 @@ __global__ __launch_bounds__(512) void xent_bwd_kernel(const T* __restrict__ log
   const float scale = ign ? 0.f : grad_out[0] / fmaxf(n_valid[0], 1.f);
   const float lse = lse_in[row];
   const int v8 = (V % 8 == 0 && ldx % 8 == 0) ? V / 8 : 0;
-  for (int i = threadIdx.x; i < v8; i += blockDim.x) {
+  const int nb = blockDim.x;
+  int i = threadIdx.x;
+  for (; i + (U - 1) * nb < v8; i += U * nb) {
+    float f[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ld8<T>(x + (int64_t)(i + u * nb) * 8, f[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = i + u * nb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float p = __expf(f[u][j] - lse);
+        if (c * 8 + j == target) p -= 1.f;
+        f[u][j] = p * scale;
+      }
+      st8<T>(d + (int64_t)c * 8, f[u]);
+    }
+  }
+  for (; i < v8; i += nb) {
     float f[8];
-    ld8<T>(x + i * 8, f);
+    ld8<T>(x + (int64_t)i * 8, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float p = __expf(f[j] - lse);
       if (i * 8 + j == target) p -= 1.f;
       f[j] = p * scale;
     }
-    st8<T>(d + i * 8, f);
+    st8<T>(d + (int64_t)i * 8, f);
   }
-  for (int i = v8 * 8 + threadIdx.x; i < V; i += blockDim.x) {
-    float p = __expf(ld1<T>(x + i) - lse);
-    if (i == target) p -= 1.f;
+  for (int k = v8 * 8 + threadIdx.x; k < V; k += nb) {
+    float p = __expf(ld1<T>(x + k) - lse);
+    if (k == target) p -= 1.f;
     if (sizeof(T) == 2)
-      ((bf16_t*)d)[i] = f2bf(p * scale);
+      ((bf16_t*)d)[k] = f2bf(p * scale);
     else
-      ((float*)d)[i] = p * scale;
+      ((float*)d)[k] = p * scale;
   }
+}
+
+static int g_xent_unroll = 4;
+extern "C" int toa_xent_set_unroll(int u) {
+  if (u != 1 && u != 2 && u != 4) return (int)hipErrorInvalidValue;
+  g_xent_unroll = u;
+  return 0;
 }
 
 extern "C" int toa_xent_fwd(int dtype, const void* logits, const int64_t* tgt, float* loss, float* lse, int64_t rows,
@@ -404,12 +432,15 @@ extern "C" int toa_xent_fwd(int dtype, const void* logits, const int64_t* tgt, f
 extern "C" int toa_xent_bwd(int dtype, const void* logits, const int64_t* tgt, const float* lse,
                             const float* grad_out, const float* n_valid, void* dx, int64_t rows, int V, int64_t ldx,
                             int ignore_index, hipStream_t stream) {
-  if (dtype == 0)
-    hipLaunchKernelGGL(xent_bwd_kernel<bf16_t>, dim3(rows), dim3(512), 0, stream, (const bf16_t*)logits, tgt, lse,
-                       grad_out, n_valid, (bf16_t*)dx, V, ldx, ignore_index);
-  else
-    hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(rows), dim3(512), 0, stream, (const float*)logits, tgt, lse,
+  if (dtype == 0) {
+    auto k = g_xent_unroll == 4 ? xent_bwd_kernel<bf16_t, 4>
+                                : (g_xent_unroll == 2 ? xent_bwd_kernel<bf16_t, 2> : xent_bwd_kernel<bf16_t, 1>);
+    hipLaunchKernelGGL(k, dim3(rows), dim3(512), 0, stream, (const bf16_t*)logits, tgt, lse, grad_out, n_valid,
+                       (bf16_t*)dx, V, ldx, ignore_index);
+  } else {
+    hipLaunchKernelGGL((xent_bwd_kernel<float, 1>), dim3(rows), dim3(512), 0, stream, (const float*)logits, tgt, lse,
                        grad_out, n_valid, (float*)dx, V, ldx, ignore_index);
+  }
   return (int)hipGetLastError();
 }
 

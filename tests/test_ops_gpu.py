@@ -381,7 +381,8 @@ def test_wgrad_routing_matches_hipblaslt():
     assert (w.main_grad.float() - ref.float()).abs().max() <= 2e-2 * ref.float().abs().max()
 
 
-@pytest.mark.parametrize("R,C,pad", [(64, 64, 0), (128, 320, 0), (6144, 4096, 0), (192, 256, 64)])
+@pytest.mark.parametrize("R,C,pad", [(64, 64, 0), (128, 320, 0), (6144, 4096, 0), (192, 256, 64), (256, 384, 64),
+                                     (4096, 14336, 0)])
 def test_transpose_bf16_kernel(R, C, pad):
     """csrc/hip/transpose.hip is an exact transpose, incl. strided source /
     destination rows."""

@@ -42,6 +42,8 @@ _SIGS = {
     "toa_lastline_arm": [ctypes.c_char_p, c_i64, c_i64, c_int],
     "toa_lastline_disarm": [],
     "toa_gemm_asm_set_swiglu_persist": [c_int],
+    "toa_xent_set_unroll": [c_int],
+    "toa_transpose_set_variant": [c_int],
     "toa_stream_create_cu_mask": [c_int, c_int, ctypes.POINTER(ctypes.c_void_p)],
     "toa_stream_destroy": [c_p],
     "toa_step_inc": [c_p, c_p],
