@@ -50,7 +50,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[u].append(e0.elapsed_time(e1) / a.reps)
-    _lib.call("toa_xent_set_unroll", 4)
+    _lib.call("toa_xent_set_unroll", 2)
     nbytes = 2 * R * V * 2
     out = {f"u{u}": {"ms": round(statistics.median(t), 4), "TBps": round(nbytes / statistics.median(t) / 1e9, 2)}
            for u, t in times.items()}
