@@ -1417,3 +1417,26 @@ def test_attn_dkdv_asm_vs_hip(B, H, Hk, S, bshd, rope):
         assert torch.isfinite(a.float()).all(), name
         assert rel(a, h) < 1e-2, (name, rel(a, h))
         assert torch.equal(a, a2), name
+
+
+def test_cu_masked_stream_runs_kernels():
+    """toa_stream_create_cu_mask (the overlapped AdamW's TOA_OPT_CUS stream):
+    a kernel on a stream limited to 32 CUs computes what it computes on the
+    default stream; bad arguments are refused."""
+    import ctypes
+
+    from tf_operator_amd.ops.optim import masked_stream
+
+    lib = _lib()
+    st = masked_stream(32, 1, torch.device(DEV))
+    x = torch.randn(1 << 20, device=DEV)
+    ref = (x * 2).sum()
+    with torch.cuda.stream(st):
+        got = (x * 2).sum()
+    st.synchronize()
+    assert torch.equal(got, ref)
+    h = ctypes.c_void_p()
+    with pytest.raises(RuntimeError):
+        lib.call("toa_stream_create_cu_mask", 2, 32, ctypes.byref(h))
+    with pytest.raises(RuntimeError):
+        lib.call("toa_stream_create_cu_mask", 1, 0, ctypes.byref(h))
