@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <mutex>
 
 namespace {
 
@@ -31,6 +32,7 @@ int g_code = 0;
 std::atomic<int> g_fired{0};
 bool g_armed = false;
 struct sigaction g_prev[kNumSignals];
+std::mutex g_mu;  // arm / disarm from several threads (the bench's watchdog and main thread)
 
 void write_all(int fd, const char* p, long n) {
   while (n > 0) {
@@ -71,6 +73,7 @@ extern "C" {
 // signo_at >= 0: offset of two placeholder characters that receive the
 // signal number.  Returns 0, or -1 if a handler could not be installed.
 int toa_lastline_arm(const char* text, long len, long signo_at, int code) {
+  std::lock_guard<std::mutex> lock(g_mu);
   restore();  // never swap the buffer under an installed handler
   free(g_text);
   g_text = nullptr;
@@ -100,6 +103,7 @@ int toa_lastline_arm(const char* text, long len, long signo_at, int code) {
 
 // Put back the handlers that were installed before toa_lastline_arm.
 int toa_lastline_disarm() {
+  std::lock_guard<std::mutex> lock(g_mu);
   restore();
   return 0;
 }
