@@ -13,6 +13,7 @@ persist=N (the plain TN kernel's persistent form, toa_gemm_asm_set_persist; -1 =
 swp=N (the fused SwiGLU GEMMs' persistent forms, toa_gemm_asm_set_swiglu_persist: bit 0 fwd, bit 1 bwd),
 ovl=0|1 (AdamW per bucket on a side stream under the next forward, FlatAdamW overlap),
 ovlcu=n[:mode] (that side stream limited to n CUs, toa_stream_create_cu_mask; 0 = unmasked),
+xent=N (cross-entropy backward chunks per thread), tpose=0|1 (the W^T refresh's transpose kernel),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -72,6 +73,10 @@ def apply(arm: str):
             n, _, mode = val.partition(":")
             TR.opt.side = (masked_stream(int(n), int(mode or 1), TR.device) if int(n)
                            else torch.cuda.Stream(device=TR.device))
+        elif key == "xent":   # cross-entropy backward chunks per thread (1, 2, 4)
+            _lib.call("toa_xent_set_unroll", int(val))
+        elif key == "tpose":   # W^T refresh: 1 LDS-staged 128 x 128 tiles, 0 the register kernel
+            _lib.call("toa_transpose_set_variant", int(val))
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":
