@@ -725,7 +725,11 @@ def run_replica(args, t_proc_start: float, probe: dict | None = None, launched_b
     if armed:
         lastline.arm("", rc)   # the line is out; a fatal signal in the teardown only ends the process
     if "error" not in ab:
-        tr.close()             # copy-engine transports: drain, barrier, then unmap (no-op without them)
+        try:
+            tr.close()         # copy-engine transports: drain, barrier, then unmap (no-op without them)
+        except Exception as e:  # noqa: BLE001 - the line is out; report, then the bounded teardown
+            print(f"[bench] closing the copy-engine transports failed: {type(e).__name__}: {e}", file=sys.stderr,
+                  flush=True)
     finished = tdist.teardown(failed="error" in ab)
     wd.cancel()
     if armed:
