@@ -63,7 +63,7 @@ def wgrad_plan(M: int, N: int, K: int) -> tuple[int, int]:
     return (tiles, 1) if best == 1 else (tiles - rem, best)
 
 
-def pack_nt(A, B, C, WS, lda_b, ldb_b, ldc_b, beta, K, tiles_m, tiles_n, full, split, tile_map=3) -> bytes:
+def pack_nt(A, B, C, WS, lda_b, ldb_b, ldc_b, beta, K, tiles_m, tiles_n, full, split, tile_map=3, sq=0) -> bytes:
     """The weight-gradient kernel's block (csrc/asm/wgrad_gen.py KARG): the
     same bytes, with beta / full / rem / split in the forward kernels'
     lds / xq / xr / per_group slots and the tile order in the map slot
@@ -74,4 +74,5 @@ def pack_nt(A, B, C, WS, lda_b, ldb_b, ldc_b, beta, K, tiles_m, tiles_n, full, s
     struct.pack_into("<IIII", buf, 32, lda_b, ldb_b, ldc_b, beta)
     struct.pack_into("<IIIIII", buf, 48, K // 64, tiles_m, tiles_n, full, rem, split)
     struct.pack_into("<I", buf, KARG["map"], tile_map)
+    struct.pack_into("<Q", buf, 88, sq)     # wgrad_gen.KARG "sq": the sum-of-squares partials (0 = off)
     return bytes(buf)

@@ -69,7 +69,7 @@ def pos(r: int, c: int) -> int:
 
 # kernarg block (byte offsets)
 KARG = {"A": 0, "B": 8, "C": 16, "WS": 24, "lda": 32, "ldb": 36, "ldc": 40, "beta": 44, "ktiles": 48,
-        "tiles_m": 52, "tiles_n": 56, "full": 60, "rem": 64, "split": 68, "map": 80}
+        "tiles_m": 52, "tiles_n": 56, "full": 60, "rem": 64, "split": 68, "map": 80, "sq": 88}
 MAP_DEFAULT = 3     # groups of 8 row tiles (dW rows) walk the column tiles: the round-4/5 order
 
 # SGPRs
@@ -88,7 +88,8 @@ S_Q, S_R = 69, 70
 S_S, S_J, S_PIECE = 71, 72, 73   # k-piece index, tail tile index, 1 for a k-piece workgroup
 S_ADVA, S_ADVB, S_KTP = 74, 75, 76   # 64 lda, 64 ldb, k-tiles of this workgroup
 S_MAPW, S_LG, S_WALK = 77, 78, 79    # kernarg tile order (gemm_gen.KARG "map"): word, log2 group, walk flag
-N_SGPR = 80
+SRD_SQ = 80         # s80..s83: the sum-of-squares partials (kernarg "sq" in s[80:81]; 0 = off)
+N_SGPR = 84
 
 # VGPRs
 V_DA, V_RALO, V_RAHI = 1, 2, 3
@@ -97,6 +98,7 @@ V_TID, V_DB, V_RBLO, V_RBHI = 132, 133, 134, 135
 V_T = 136                                        # 136..139 scratch
 V_TGALO, V_TGAHI, V_TGBLO, V_TGBHI = 140, 141, 142, 143
 V_E = 144                                        # 144..255 epilogue scratch
+V_SQ = V_E + 100                                 # 244..247: sum-of-squares accumulators (whole-K tiles)
 
 # slot map: the forward kernel's product placement (gemm_gen.SLOT_MAPS
 # "lib0": barriers one MFMA after their waits, M0 / resource advances one
@@ -108,6 +110,7 @@ def prologue(a: Asm):
     a(f"s_load_dwordx16 {sr(4, 16)}, s[0:1], 0x0")
     a(f"s_load_dwordx4 {sr(20, 4)}, s[0:1], 0x40")
     a(f"s_load_dword {sr(S_MAPW)}, s[0:1], {KARG['map']:#x}")
+    a(f"s_load_dwordx2 {sr(SRD_SQ, 2)}, s[0:1], {KARG['sq']:#x}")
     a("s_mov_b32 m0, 0")
     a(f"v_mov_b32 {vr(V_TID)}, v0")
     a("s_waitcnt lgkmcnt(0)")
@@ -412,6 +415,8 @@ def epilogue(a: Asm):
     l_nobeta = a.fresh("nobeta")
     a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")             # 16 rows
     a(f"s_mov_b32 {sr(S_E0)}, 0")
+    for r in range(4):
+        a(f"v_mov_b32 {vr(V_SQ + r)}, 0")
     for i in range(8):
         # pk alternates between two register sets and nothing waits for the
         # stores (the TN epilogue re-uses its store registers at once: the
@@ -429,11 +434,17 @@ def epilogue(a: Asm):
             for r in range(4):
                 a(f"v_add_f32 {vr(f + 4 * j + r)}, {vr(f + 4 * j + r)}, {vr(V_E + 88 + r)}")
         a.label(f"{l_nobeta}_{i}")
+        # the gradient-norm partials: squares of the tile's final fp32 values
+        # (four chains; the clipping norm of train/llm.py, ops/gemm.SumsqSession)
+        for j in range(8):
+            for r in range(4):
+                a(f"v_fma_f32 {vr(V_SQ + r)}, {vr(f + 4 * j + r)}, {vr(f + 4 * j + r)}, {vr(V_SQ + r)}")
         for j in range(8):
             G.cvt_pack(a, pk + 2 * j, f + 4 * j)
         for j in range(8):
             a(f"buffer_store_dwordx2 {vr(pk + 2 * j, 2)}, {vr(V_E)}, {sr(SRD_C, 4)}, {sr(S_E0)} offen offset:{32 * j}")
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+    sumsq_store(a)
     a(f"s_branch {l_end}")
     # --- fp32 partials into the workspace tile (256 x 256 x 4 B, row-major)
     a.label(l_piece)
@@ -446,6 +457,32 @@ def epilogue(a: Asm):
             a(f"buffer_store_dwordx4 {vr(f + 4 * j, 4)}, {vr(V_E + 1)}, {sr(SRD_WS, 4)}, {sr(S_E0)} offen offset:{64 * j}")
         a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {16 * 1024}")
     a.label(l_end)
+
+
+def sumsq_store(a: Asm):
+    """Whole-K tiles with a partials buffer (kernarg "sq" != 0): lane l of wave
+    w stores its sum of squares at float (tm tiles_n + tn) 256 + 64 w + l --
+    a slot per tile independent of the tile order, so the host's sum over the
+    buffer is deterministic.  The k-piece tiles' slots are written by
+    wgrad_tile_reduce_kernel (csrc/hip/wgrad.hip)."""
+    l_do, l_skip = a.fresh("sq_do"), a.fresh("sq_skip")
+    a(f"s_cmp_lg_u32 {sr(SRD_SQ)}, 0")
+    a(f"s_cbranch_scc1 {l_do}")
+    a(f"s_cmp_lg_u32 {sr(SRD_SQ + 1)}, 0")
+    a(f"s_cbranch_scc0 {l_skip}")
+    a.label(l_do)
+    a(f"v_add_f32 {vr(V_SQ)}, {vr(V_SQ)}, {vr(V_SQ + 1)}")
+    a(f"v_add_f32 {vr(V_SQ + 2)}, {vr(V_SQ + 2)}, {vr(V_SQ + 3)}")
+    a(f"v_add_f32 {vr(V_SQ)}, {vr(V_SQ)}, {vr(V_SQ + 2)}")
+    a(f"s_mul_i32 {sr(S_T0)}, {sr(S_TM)}, {sr(S_TN_N)}")
+    a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_TN)}")
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_T0)}, 10")          # 256 floats per tile
+    a(f"s_mul_i32 {sr(SRD_SQ + 2)}, {sr(S_TM_N)}, {sr(S_TN_N)}")
+    a(f"s_lshl_b32 {sr(SRD_SQ + 2)}, {sr(SRD_SQ + 2)}, 10")   # num_records: the whole buffer
+    a(f"s_mov_b32 {sr(SRD_SQ + 3)}, 0x20000")
+    a(f"v_lshlrev_b32 {vr(V_SQ + 1)}, 2, {vr(V_TID)}")
+    a(f"buffer_store_dword {vr(V_SQ)}, {vr(V_SQ + 1)}, {sr(SRD_SQ, 4)}, {sr(S_T0)} offen")
+    a.label(l_skip)
 
 
 def kernel(variant: str = "") -> tuple[str, str]:

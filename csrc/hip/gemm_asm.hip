@@ -368,6 +368,18 @@ extern "C" int toa_gemm_asm_probe(void* out, const bf16_t* X, int64_t ldx, const
 extern "C" int toa_wgrad_split(int M, int N, int K);
 extern "C" int toa_wgrad_reduce_map(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem,
                                     int split, int beta, unsigned map, hipStream_t stream);
+extern "C" int toa_wgrad_reduce_map_sq(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem,
+                                       int split, int beta, unsigned map, float* sq, hipStream_t stream);
+
+// Gradient-norm partials of the NEXT weight-gradient launch (one-shot; the
+// launch consumes it): per tile 256 floats at (tm tiles_n + tn) 256 -- the
+// whole-K tiles from the assembly kernel's epilogue (wgrad_gen.py KARG "sq"),
+// the k-piece tiles from the reduce kernel.  ops/gemm.py SumsqSession.
+static float* g_wgrad_sq = nullptr;
+extern "C" int toa_wgrad_asm_set_sumsq(float* sq) {
+  g_wgrad_sq = sq;
+  return 0;
+}
 
 static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C,
                             int64_t ldc, float* W, int M, int N, int K, int split, int beta, hipStream_t stream);
@@ -451,6 +463,9 @@ static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_
   a.xr = (uint32_t)rem;
   a.per_group = (uint32_t)split;
   a.map = wgrad_tile_map(M / 256, N / 256);
+  float* sq = g_wgrad_sq;
+  g_wgrad_sq = nullptr;
+  memcpy(&a.phase, &sq, sizeof(sq));   // bytes 88..95: wgrad_gen.py KARG "sq"
   hipError_t err;
   hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
@@ -459,7 +474,7 @@ static int wgrad_asm_launch(int which, const bf16_t* A, int64_t lda, const bf16_
   const unsigned nwg = (unsigned)(full + (split > 1 ? rem * split : 0));
   err = hipModuleLaunchKernel(fn, nwg, 1, 1, 256, 1, 1, 0, stream, nullptr, cfg);
   if (err != hipSuccess) return (int)err;
-  if (split > 1 && rem > 0) return toa_wgrad_reduce_map(W, C, ldc, M, N, full, rem, split, beta, a.map, stream);
+  if (split > 1 && rem > 0) return toa_wgrad_reduce_map_sq(W, C, ldc, M, N, full, rem, split, beta, a.map, sq, stream);
   return 0;
 }
 

@@ -57,6 +57,33 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
   if (threadIdx.x == 0) out[0] = accumulate ? out[0] + t : t;
 }
 
+// Plain sum of an fp32 vector, the same two passes (the gradient-norm
+// partials that the weight-gradient kernels write, ops/gemm.py SumsqSession).
+__global__ __launch_bounds__(256) void sum_partial_kernel(const float* __restrict__ x, int64_t n,
+                                                          float* __restrict__ partial) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const int64_t n4 = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const f32x4 a = *((const f32x4*)x + i);
+    acc += (a[0] + a[1]) + (a[2] + a[3]);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) acc += x[i];
+  float t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+extern "C" int toa_sum_f32(const float* x, int64_t n, float* workspace, float* out, int accumulate,
+                           hipStream_t stream) {
+  if (n <= 0 || ((uintptr_t)x & 15)) return (int)hipErrorInvalidValue;
+  const int64_t n4 = n / 4 > 0 ? n / 4 : 1;
+  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 32768);
+  hipLaunchKernelGGL(sum_partial_kernel, dim3(grid), dim3(256), 0, stream, x, n, workspace);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, stream, workspace, grid, out, accumulate);
+  return (int)hipGetLastError();
+}
+
 // workspace must hold >= TOA_SUMSQ_WS (32768) floats.  Grid: one 8-element
 // chunk per thread up to 32768 blocks (the flat AdamW's measurement: a grid
 // capped at 2048 blocks left each thread looping, 5-6 % slower per byte).

@@ -258,12 +258,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_nt_kernel(const bf16_t* __restri
 }
 
 // Tail tile j of `rem`: C = (beta ? C : 0) + sum_s W[s][j], summed in split order.
+// sq != nullptr: each thread also stores the sum of squares of its fp32
+// results at sq[(tm tiles_n + tn) 256 + thread] -- the tile's slots in the
+// gradient-norm partials the assembly kernel writes for whole-K tiles.
 __global__ __launch_bounds__(256) void wgrad_tile_reduce_kernel(const float* __restrict__ W, bf16_t* __restrict__ C,
                                                                 int64_t ldc, int M, int N, int full, int rem,
-                                                                int split, int beta, unsigned map) {
+                                                                int split, int beta, unsigned map,
+                                                                float* __restrict__ sq) {
   const int j = blockIdx.x;
   int tm, tn;
   wg_tile_coords_map(full + j, M / WG_BM, N / WG_BN, map, &tm, &tn);
+  float ss = 0.f;
   for (int e = threadIdx.x; e < WG_BM * WG_BN / 8; e += 256) {
     const int row = e / (WG_BN / 8), col = (e % (WG_BN / 8)) * 8;
     bf16_t* p = C + (int64_t)(tm * WG_BM + row) * ldc + tn * WG_BN + col;
@@ -283,8 +288,11 @@ __global__ __launch_bounds__(256) void wgrad_tile_reduce_kernel(const float* __r
         acc[4 + q] += b[q];
       }
     }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ss = fmaf(acc[q], acc[q], ss);
     st16(p, pack8(acc));
   }
+  if (sq != nullptr) sq[((int64_t)tm * (N / WG_BN) + tn) * 256 + threadIdx.x] = ss;
 }
 
 static bool wg_split_ok(int K, int s) { return K % (4 * WG_BK * s) == 0 && K / s >= 16 * WG_BK; }
@@ -312,12 +320,17 @@ static void wg_plan(int M, int N, int K, int* full, int* split) {
 // (csrc/hip/gemm_asm.hip toa_wgrad_asm), which writes the same tile-major
 // fp32 partials.
 // map: the tile order the pieces were computed in (wg_tile_coords_map).
-extern "C" int toa_wgrad_reduce_map(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem,
-                                    int split, int beta, unsigned map, hipStream_t stream) {
+extern "C" int toa_wgrad_reduce_map_sq(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem,
+                                       int split, int beta, unsigned map, float* sq, hipStream_t stream) {
   if (rem <= 0 || split < 2 || W == nullptr || map >= 32u || (map & 15u) > 6u) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split, beta,
-                     map);
+                     map, sq);
   return (int)hipGetLastError();
+}
+
+extern "C" int toa_wgrad_reduce_map(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem,
+                                    int split, int beta, unsigned map, hipStream_t stream) {
+  return toa_wgrad_reduce_map_sq(W, C, ldc, M, N, full, rem, split, beta, map, nullptr, stream);
 }
 
 extern "C" int toa_wgrad_reduce(const float* W, bf16_t* C, int64_t ldc, int M, int N, int full, int rem, int split,
@@ -365,6 +378,6 @@ extern "C" int toa_wgrad(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t 
                      beta);
   if (split > 1 && rem > 0)
     hipLaunchKernelGGL(wgrad_tile_reduce_kernel, dim3(rem), dim3(256), 0, stream, W, C, ldc, M, N, full, rem, split,
-                       beta, 3u);
+                       beta, 3u, (float*)nullptr);
   return (int)hipGetLastError();
 }

@@ -76,6 +76,41 @@ def run(M, N, T, beta, split=None, seed=0):
     return C, ws, ref, full, rem, sp
 
 
+@pytest.mark.parametrize("beta,tile_map", [(0, 3), (1, 18)])
+def test_wgrad_asm_sumsq_partials_emulated(beta, tile_map):
+    """Kernarg "sq": each whole-K tile writes 256 per-lane sums of squares of
+    its final fp32 values at slot (tm tiles_n + tn) 256 + tid, whatever the
+    tile order; C is the same bit for bit as without the partials; the tile
+    slots sum to the squared norm of the tile (fp32 values, before the bf16
+    rounding of C)."""
+    M, N, T = 512, 768, 256
+    rng = np.random.default_rng(9)
+    A = bf16(rng.standard_normal((T, M)))
+    B = bf16(rng.standard_normal((T, N)))
+    C0 = bf16(rng.standard_normal((M, N)))
+    tm_n, tn_n = M // 256, N // 256
+    outs = []
+    for with_sq in (False, True):
+        mem = emu.Memory()
+        aa, ab, ac = mem.add(A), mem.add(B), mem.add(C0.copy())
+        aw = mem.add(np.zeros(65536, np.float32))
+        asq = mem.add(np.full(tm_n * tn_n * 256, np.nan, np.float32))
+        karg = host_args.pack_nt(aa, ab, ac, aw, 2 * M, 2 * N, 2 * N, beta, T, tm_n, tn_n, tm_n * tn_n, 1,
+                                 tile_map=tile_map, sq=asq if with_sq else 0)
+        e = emu.Emu(TEXT, "toa_wgrad_nt_asm")
+        for wg in range(tm_n * tn_n):
+            e.run(karg, wg, mem)
+        outs.append((mem.bufs[2][1].copy(), mem.bufs[4][1].view(np.float32).copy()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.isnan(outs[0][1]).all()                     # "sq" = 0: nothing written
+    sq = outs[1][1].reshape(tm_n, tn_n, 256).astype(np.float64)
+    ref = tof(A).T @ tof(B) + (tof(C0) if beta else 0)
+    for tm in range(tm_n):
+        for tn in range(tn_n):
+            want = (ref[256 * tm:256 * (tm + 1), 256 * tn:256 * (tn + 1)] ** 2).sum()
+            assert abs(sq[tm, tn].sum() - want) <= 1e-4 * want, (tm, tn)
+
+
 @pytest.mark.parametrize("beta", [0, 1])
 def test_wgrad_asm_full_tiles_emulated(beta):
     C, _, ref, full, rem, sp = run(256, 512, 256, beta, seed=beta)

@@ -1440,3 +1440,66 @@ def test_cu_masked_stream_runs_kernels():
         lib.call("toa_stream_create_cu_mask", 2, 32, ctypes.byref(h))
     with pytest.raises(RuntimeError):
         lib.call("toa_stream_create_cu_mask", 1, 0, ctypes.byref(h))
+
+
+def test_fused_clipping_norm_matches_full_pass(monkeypatch):
+    """World 1: the clipping norm from the weight-gradient kernels' partials
+    (ops/gemm.SumsqSession, TOA_FUSED_NORM default) equals the full pass over
+    the gradient to fp32 summation order, every step is served from the
+    partials, and the training trajectory follows the full-pass trainer."""
+    from tf_operator_amd.models.llama import PRESETS
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    _lib()
+    runs = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TOA_FUSED_NORM", fused)
+        tr = LlamaTrainer(PRESETS["llama-tiny128"], torch.device(DEV), micro_batch=2, seq_len=512, seed=0)
+        assert (tr.opt.sumsq is not None) == (fused == "1")
+        b = tr.synthetic_batch()
+        norms, losses = [], []
+        for _ in range(3):
+            losses.append(float(tr.step([b])))
+            norms.append(float(tr.opt.last_norm_sq))
+        if fused == "1":
+            assert tr.opt.sumsq.hits == 3, "a step fell back to the full pass"
+            # the partials' region layout covers every linear weight; the rest is embeddings / norms
+            assert len(tr.opt.sumsq.regions) == 2 * 4 + 1   # wqkv, wo, wgu, wd per layer + lm_head
+        runs[fused] = (norms, losses)
+    for a, b in zip(runs["1"][0], runs["0"][0]):
+        assert abs(a - b) <= 1e-3 * b, (runs["1"][0], runs["0"][0])
+    for a, b in zip(runs["1"][1], runs["0"][1]):
+        assert abs(a - b) <= 2e-2, (runs["1"][1], runs["0"][1])
+
+
+def test_wgrad_sumsq_partials_whole_and_split_tiles():
+    """The weight-gradient GEMM with a partials region: 384 tiles = 256
+    whole-K tiles (assembly epilogue) + 128 tail tiles in 2 k-pieces (the
+    reduce kernel) -- the region sums to the squared norm of the result."""
+    import types
+
+    from tf_operator_amd.ops import gemm
+
+    _lib()
+    torch.manual_seed(6)
+    T, N, K = 2048, 6144, 4096
+    dy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    w = torch.nn.Parameter(torch.zeros(N, K, device=DEV, dtype=torch.bfloat16))
+    w.main_grad = torch.zeros(N, K, device=DEV, dtype=torch.bfloat16)
+    seg = types.SimpleNamespace(param=w, offset=0, numel=N * K)
+    flat = types.SimpleNamespace(segments=[seg], device=torch.device(DEV), numel=N * K, grad=w.main_grad.view(-1))
+    sess = gemm.SumsqSession(flat, [w])
+    gemm._SESSIONS.add(sess)
+    try:
+        gemm.wgrad_hip_(w.main_grad, dy, x, 0.0)
+        torch.cuda.synchronize()
+    finally:
+        gemm._SESSIONS.discard(sess)
+    assert sess.written == {w.main_grad.data_ptr()}
+    got = float(sess.buf.double().sum())
+    want = float(w.main_grad.double().pow(2).sum())
+    assert abs(got - want) <= 1e-3 * want, (got, want)
+    out, ws = torch.zeros(1, device=DEV), torch.empty(32768, device=DEV)
+    sess.norm_sq(out, ws)
+    assert abs(float(out) - want) <= 1e-3 * want

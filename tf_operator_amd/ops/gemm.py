@@ -43,6 +43,7 @@ import ctypes
 import json
 import os
 import threading
+import weakref
 
 import torch
 
@@ -413,6 +414,87 @@ def wgrad_hip_ok(g, dy2, x2) -> bool:
             and g.data_ptr() % 16 == 0 and tuple(g.shape) == (N, K))
 
 
+class SumsqSession:
+    """The clipping norm from partials the weight-gradient kernels write as
+    they produce the gradients (no separate pass over the 16 GB of bf16
+    gradients at Llama-3-8B): every 2-D weight in `params` whose gradient
+    the assembly kernel produces gets a fixed region of `buf`, 256 floats per
+    256 x 256 output tile (wgrad_gen.py KARG "sq"; the split-K tail tiles via
+    the reduce kernel).  norm_sq() sums the whole buffer in one fixed-order
+    pass when every region was written this step and adds the squares of the
+    flat ranges outside the regions (embeddings, norm weights); otherwise it
+    falls back to the full pass over the gradient.  Only for an unsharded,
+    unreduced world-1 update: the partials are of this rank's gradient.
+    Differs from the full pass only in summation order and in squaring the
+    fp32 tile values before their bf16 rounding."""
+
+    def __init__(self, flat, params):
+        self.flat = flat
+        want = {id(p) for p in params}
+        self.regions = {}      # grad view data_ptr -> (offset in buf, floats, [N, K])
+        off = 0
+        covered = []
+        for sgm in flat.segments:
+            p = sgm.param
+            if id(p) not in want or p.dim() != 2 or p.shape[0] % 256 or p.shape[1] % 256:
+                continue
+            n = (p.shape[0] // 256) * (p.shape[1] // 256) * 256
+            self.regions[p.main_grad.data_ptr()] = (off, n, tuple(p.shape))
+            covered.append((sgm.offset, sgm.offset + sgm.numel))
+            off += n
+        self.buf = torch.zeros(max(off, 4), device=flat.device, dtype=torch.float32)
+        # the flat ranges no region covers, as contiguous runs
+        covered.sort()
+        self.rest, pos = [], 0
+        for a, b in covered:
+            if a > pos:
+                self.rest.append((pos, a))
+            pos = max(pos, b)
+        if pos < flat.numel:
+            self.rest.append((pos, flat.numel))
+        self.written = set()
+        self.hits = 0           # steps served from the partials (tests, diagnostics)
+
+    def owns(self, g) -> bool:
+        return g.data_ptr() in self.regions
+
+    def arm(self, g) -> bool:
+        """Point the next weight-gradient launch at g's region."""
+        off, n, shape = self.regions[g.data_ptr()]
+        if tuple(g.shape) != shape:
+            return False
+        _lib.call("toa_wgrad_asm_set_sumsq", self.buf.data_ptr() + 4 * off)
+        return True
+
+    def norm_sq(self, out, ws):
+        """out[0] = the squared gradient norm; the written set is cleared."""
+        f = self.flat
+        s = _lib.stream(f.grad)
+        full = len(self.written) == len(self.regions)
+        self.written = set()
+        if not full:
+            _lib.call("toa_sumsq", _lib.ptr(f.grad), f.grad.numel(), int(f.grad.dtype == torch.bfloat16),
+                      _lib.ptr(ws), _lib.ptr(out), 0, s)
+            return out
+        self.hits += 1
+        _lib.call("toa_sum_f32", _lib.ptr(self.buf), self.buf.numel(), _lib.ptr(ws), _lib.ptr(out), 0, s)
+        esz = f.grad.element_size()
+        for a, b in self.rest:
+            _lib.call("toa_sumsq", f.grad.data_ptr() + esz * a, b - a, int(f.grad.dtype == torch.bfloat16),
+                      _lib.ptr(ws), _lib.ptr(out), 1, s)
+        return out
+
+
+_SESSIONS = weakref.WeakSet()   # live SumsqSession objects (each held by its trainer's optimizer)
+
+
+def _session_for(g):
+    for sess in _SESSIONS:
+        if sess.owns(g):
+            return sess
+    return None
+
+
 def wgrad_hip_(g, dy2, x2, beta=1.0, split=None):
     """g[N,K] (+)= dy2[T,N]^T x2[T,K] on the hand-written MFMA kernel.
     split=None: the kernel's auto plan (whole-K waves, only the tail tiles
@@ -427,8 +509,17 @@ def wgrad_hip_(g, dy2, x2, beta=1.0, split=None):
             N, K, T, int(split), int(beta != 0.0), _lib.stream(dy2))
     kern = wgrad_kernel()
     if kern in ("asm", "asm_v1"):
-        rc = _lib.call_ret("toa_wgrad_asm", *args) if kern == "asm" else _lib.call_ret("toa_wgrad_asm_variant", 1, *args)
+        sess = _session_for(g) if _SESSIONS else None
+        armed = sess is not None and sess.arm(g)
+        try:
+            rc = (_lib.call_ret("toa_wgrad_asm", *args) if kern == "asm"
+                  else _lib.call_ret("toa_wgrad_asm_variant", 1, *args))
+        finally:
+            if armed:
+                _lib.call("toa_wgrad_asm_set_sumsq", None)   # one-shot: never left for another launch
         if rc == 0:
+            if armed:
+                sess.written.add(g.data_ptr())
             return g
         if rc != HIP_ERROR_INVALID_VALUE:
             raise RuntimeError(f"toa_wgrad_asm failed: hipError {rc}")

@@ -90,6 +90,7 @@ class FlatAdamW:
                  overlap=False, buckets=None, fuse_zero_grad=False, post_update=None, owned=None, group=None,
                  device_step=False):
         self.post_update = post_update
+        self.sumsq = None   # an ops.gemm.SumsqSession (set by the trainer): the clipping norm from kernel partials
         # device_step: the step count lives in device memory and is advanced
         # by a kernel, so a captured HIP graph of the whole training step
         # replays with fresh bias corrections (train/simple.py graph mode)
@@ -163,6 +164,9 @@ class FlatAdamW:
     def _norm_sq(self):
         f = self.flat
         if self.owned is None:
+            if self.sumsq is not None:   # partials from the weight-gradient kernels (ops/gemm.SumsqSession)
+                self.sumsq.norm_sq(self._norm, self._ws)
+                return
             grad_norm_sq(f.grad, self._ws, self._norm)
             return
         import torch.distributed as dist

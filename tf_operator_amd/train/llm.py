@@ -88,6 +88,7 @@ class LlamaTrainer:
             self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
                                  fuse_zero_grad=not self.fresh_grads,
                                  post_update=self.wt.refresh if self.wt else None)
+        self._fused_norm(model)
         if self.opt.overlap or self.gather is not None:
             self._hooks = self._install_param_waits()
         self._closed = False
@@ -103,6 +104,27 @@ class LlamaTrainer:
         # step's forward / backward / update are issued (host side; the
         # replica runtime's mark, examples/llama_train.py)
         self.on_phase = None
+
+    def _fused_norm(self, model):
+        """World 1, unsharded, clipping on, the assembly weight gradients:
+        the clipping norm from the partials the weight-gradient kernels write
+        (ops/gemm.SumsqSession) instead of a pass over the whole gradient.
+        TOA_FUSED_NORM=0 turns it off."""
+        from ..ops import _lib
+        from ..ops import gemm as _g
+
+        if (os.environ.get("TOA_FUSED_NORM", "1") == "0" or self.flat.device.type != "cuda"
+                or not _lib.has("toa_wgrad_asm_set_sumsq") or self.gather is not None
+                or self.bucketer.world != 1 or not self.opt.max_grad_norm):
+            return
+        head = model.head_weight()
+        lin = [p for n, p in model.named_parameters() if p.dim() == 2 and not n.startswith("embed.")]
+        if not any(head is p for p in lin) and not any(head is p for n, p in model.named_parameters()
+                                                        if n.startswith("embed.")):
+            lin.append(head)   # an untied head: its gradient has one producer, the weight-gradient GEMM
+        sess = _g.SumsqSession(self.flat, lin)
+        self.opt.sumsq = sess
+        _g._SESSIONS.add(sess)
 
     def _phase(self, name):
         if self.on_phase is not None and self.step_idx == 0:
