@@ -14,6 +14,7 @@ swp=N (the fused SwiGLU GEMMs' persistent forms, toa_gemm_asm_set_swiglu_persist
 ovl=0|1 (AdamW per bucket on a side stream under the next forward, FlatAdamW overlap),
 ovlcu=n[:mode] (that side stream limited to n CUs, toa_stream_create_cu_mask; 0 = unmasked),
 xent=N (cross-entropy backward chunks per thread), tpose=0|1 (the W^T refresh's transpose kernel),
+fnorm=0|1 (the clipping norm from the weight-gradient kernels' partials, or the full pass),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -77,6 +78,16 @@ def apply(arm: str):
             _lib.call("toa_xent_set_unroll", int(val))
         elif key == "tpose":   # W^T refresh: 1 LDS-staged 128 x 128 tiles, 0 the register kernel
             _lib.call("toa_transpose_set_variant", int(val))
+        elif key == "fnorm":   # clipping norm from the weight-gradient partials (1) or the full pass (0)
+            sess = getattr(TR, "_sumsq", None)
+            if sess is None:
+                raise SystemExit("fnorm: the trainer has no SumsqSession (TOA_FUSED_NORM=0?)")
+            if int(val):
+                gemm._SESSIONS.add(sess)
+                TR.opt.sumsq = sess
+            else:
+                gemm._SESSIONS.discard(sess)
+                TR.opt.sumsq = None
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":

@@ -122,7 +122,7 @@ class LlamaTrainer:
         if not any(head is p for p in lin) and not any(head is p for n, p in model.named_parameters()
                                                         if n.startswith("embed.")):
             lin.append(head)   # an untied head: its gradient has one producer, the weight-gradient GEMM
-        sess = _g.SumsqSession(self.flat, lin)
+        sess = self._sumsq = _g.SumsqSession(self.flat, lin)
         self.opt.sumsq = sess
         _g._SESSIONS.add(sess)
 
