@@ -51,43 +51,6 @@ def main():
             torch.cuda.synchronize()
             times[u].append(e0.elapsed_time(e1) / a.reps)
     _lib.call("toa_xent_set_unroll", 2)
-    # the fused forward + gradient (toa_xent_fused, in place) against the two kernels
-    loss = torch.empty(R, device=dev)
-    buf = logits.clone()
-
-    def two():
-        _lib.call("toa_xent_fwd", 0, _lib.ptr(logits), _lib.ptr(tgt), _lib.ptr(loss), _lib.ptr(lse), R, V, V, -100,
-                  _lib.stream(logits))
-        _lib.call("toa_xent_bwd", 0, _lib.ptr(logits), _lib.ptr(tgt), _lib.ptr(lse), _lib.ptr(gout), _lib.ptr(nval),
-                  _lib.ptr(outs[2]), R, V, V, -100, _lib.stream(logits))
-
-    def fused():
-        buf.copy_(logits)   # timed separately below and subtracted
-        _lib.call("toa_xent_fused", _lib.ptr(buf), _lib.ptr(tgt), _lib.ptr(loss), _lib.ptr(nval), 1.0, R, V, V, -100,
-                  _lib.stream(logits))
-
-    def copy_only():
-        buf.copy_(logits)
-
-    tf = {"two_kernels": [], "fused_plus_copy": [], "copy": []}
-    for r in range(a.rounds):
-        for name, fn in (("two_kernels", two), ("fused_plus_copy", fused), ("copy", copy_only)):
-            fn()
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.reps):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            tf[name].append(e0.elapsed_time(e1) / a.reps)
-    med = {k: statistics.median(v) for k, v in tf.items()}
-    fused_ms = med["fused_plus_copy"] - med["copy"]
-    fused()
-    torch.cuda.synchronize()
-    ferr = float((buf.float() - outs[2].float()).abs().max() / outs[2].float().abs().max())
-    print(json.dumps({"two_kernels_ms": round(med["two_kernels"], 4), "fused_ms": round(fused_ms, 4),
-                      "fused_vs_two_rel_err": ferr}), flush=True)
     nbytes = 2 * R * V * 2
     out = {f"u{u}": {"ms": round(statistics.median(t), 4), "TBps": round(nbytes / statistics.median(t) / 1e9, 2)}
            for u, t in times.items()}
