@@ -418,141 +418,6 @@ extern "C" int toa_xent_set_unroll(int u) {
   return 0;
 }
 
-// ---------------------------------------------------------------------------
-// Cross entropy forward AND the logits gradient in one pass, in place (bf16
-// logits, V % 8 == 0): one workgroup of 1024 threads per row holds the row
-// in registers (CH 16-byte chunks per thread, chunk c = i * 1024 + tid), so
-// the row is read from HBM once: the separate forward + backward read it
-// twice (12.6 + 6.3 GB at 24576 x 128256).  The gradient is written with the
-// scale gscale / n_valid -- the backward's incoming gradient the caller
-// expects (1 for loss.backward()); toa_xent_rescale fixes the rare other
-// value on the device.  lse is not needed afterwards.
-// ---------------------------------------------------------------------------
-template <int CH>
-__global__ __launch_bounds__(1024) void xent_fused_kernel(bf16_t* __restrict__ x_io, const int64_t* __restrict__ tgt,
-                                                          float* __restrict__ loss, const float* __restrict__ n_valid,
-                                                          float gscale, int V, int64_t ldx, int ignore_index) {
-  __shared__ float sm[16], ss[16];
-  __shared__ float s_lse, s_tv;
-  const int64_t row = blockIdx.x;
-  bf16_t* x = x_io + row * ldx;
-  const int64_t target = tgt[row];
-  const bool ign = target == ignore_index || target < 0 || target >= V;
-  const int v8 = V / 8;
-  const int tid = threadIdx.x;
-  u32x4 r[CH];
-#pragma unroll
-  for (int i = 0; i < CH; ++i) {
-    const int c = i * 1024 + tid;
-    r[i] = c < v8 ? __builtin_nontemporal_load((const u32x4*)(x + (int64_t)c * 8)) : u32x4{0, 0, 0, 0};
-  }
-  float m = -INFINITY, s = 0.f;
-#pragma unroll
-  for (int i = 0; i < CH; ++i) {
-    const int c = i * 1024 + tid;
-    if (c < v8) {
-      float f[8];
-      unpack8(r[i], f);
-      float mx = f[0];
-#pragma unroll
-      for (int j = 1; j < 8; ++j) mx = fmaxf(mx, f[j]);
-      const float mn = fmaxf(m, mx);
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc += __expf(f[j] - mn);
-      s = s * __expf(m - mn) + acc;
-      m = mn;
-      if (!ign && target / 8 == c) s_tv = f[target % 8];
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
-    lse_merge(m, s, m2, s2);
-  }
-  const int lane = tid & 63, wid = tid >> 6;
-  if (lane == 0) {
-    sm[wid] = m;
-    ss[wid] = s;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float M = sm[0], S = ss[0];
-    for (int i = 1; i < 16; ++i) lse_merge(M, S, sm[i], ss[i]);
-    const float lse = M + __logf(S);
-    s_lse = lse;
-    loss[row] = ign ? 0.f : lse - s_tv;
-  }
-  __syncthreads();
-  const float lse = s_lse;
-  const float scale = ign ? 0.f : gscale / fmaxf(n_valid[0], 1.f);
-#pragma unroll
-  for (int i = 0; i < CH; ++i) {
-    const int c = i * 1024 + tid;
-    if (c < v8) {
-      float f[8];
-      unpack8(r[i], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float p = __expf(f[j] - lse);
-        if (c * 8 + j == target) p -= 1.f;
-        f[j] = p * scale;
-      }
-      st16(x + (int64_t)c * 8, pack8(f));
-    }
-  }
-}
-
-extern "C" int toa_xent_fused(bf16_t* logits, const int64_t* tgt, float* loss, const float* n_valid, float gscale,
-                              int64_t rows, int V, int64_t ldx, int ignore_index, hipStream_t stream) {
-  if (rows <= 0 || V <= 0 || V % 8 || ldx % 8 || ldx < V || ((uintptr_t)logits & 15)) return (int)hipErrorInvalidValue;
-  const int chunks = (V / 8 + 1023) / 1024;
-  switch (chunks) {
-    case 1: hipLaunchKernelGGL(xent_fused_kernel<1>, dim3(rows), dim3(1024), 0, stream, logits, tgt, loss, n_valid,
-                               gscale, V, ldx, ignore_index); break;
-    case 2: hipLaunchKernelGGL(xent_fused_kernel<2>, dim3(rows), dim3(1024), 0, stream, logits, tgt, loss, n_valid,
-                               gscale, V, ldx, ignore_index); break;
-    case 3: case 4: hipLaunchKernelGGL(xent_fused_kernel<4>, dim3(rows), dim3(1024), 0, stream, logits, tgt, loss,
-                                       n_valid, gscale, V, ldx, ignore_index); break;
-    case 5: case 6: case 7: case 8:
-      hipLaunchKernelGGL(xent_fused_kernel<8>, dim3(rows), dim3(1024), 0, stream, logits, tgt, loss, n_valid, gscale, V,
-                         ldx, ignore_index); break;
-    default:
-      if (chunks > 16) return (int)hipErrorInvalidValue;
-      hipLaunchKernelGGL(xent_fused_kernel<16>, dim3(rows), dim3(1024), 0, stream, logits, tgt, loss, n_valid, gscale,
-                         V, ldx, ignore_index);
-  }
-  return (int)hipGetLastError();
-}
-
-// dx *= g[0] / expected when the backward's incoming gradient is not the one
-// the fused forward assumed (every workgroup reads g and leaves at once when
-// it is): the common case costs one launch of idle workgroups.
-__global__ __launch_bounds__(256) void xent_rescale_kernel(bf16_t* __restrict__ dx, const float* __restrict__ g,
-                                                           float expected, int64_t rows, int V, int64_t ldx) {
-  const float gv = g[0];
-  if (gv == expected) return;
-  const float k = gv / expected;
-  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
-    bf16_t* d = dx + row * ldx;
-    for (int c = threadIdx.x; c < V / 8; c += blockDim.x) {
-      float f[8];
-      unpack8(ld16(d + (int64_t)c * 8), f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= k;
-      st16(d + (int64_t)c * 8, pack8(f));
-    }
-  }
-}
-
-extern "C" int toa_xent_rescale(bf16_t* dx, const float* g, float expected, int64_t rows, int V, int64_t ldx,
-                                hipStream_t stream) {
-  if (rows <= 0 || V % 8 || expected == 0.f) return (int)hipErrorInvalidValue;
-  const int grid = (int)(rows < 2048 ? rows : 2048);
-  hipLaunchKernelGGL(xent_rescale_kernel, dim3(grid), dim3(256), 0, stream, dx, g, expected, rows, V, ldx);
-  return (int)hipGetLastError();
-}
-
 extern "C" int toa_xent_fwd(int dtype, const void* logits, const int64_t* tgt, float* loss, float* lse, int64_t rows,
                             int V, int64_t ldx, int ignore_index, hipStream_t stream) {
   if (dtype == 0)

@@ -15,7 +15,6 @@ ovl=0|1 (AdamW per bucket on a side stream under the next forward, FlatAdamW ove
 ovlcu=n[:mode] (that side stream limited to n CUs, toa_stream_create_cu_mask; 0 = unmasked),
 xent=N (cross-entropy backward chunks per thread), tpose=0|1 (the W^T refresh's transpose kernel),
 fnorm=0|1 (the clipping norm from the weight-gradient kernels' partials, or the full pass),
-xfused=0|1 (cross entropy and its logits gradient in one pass over the logits, or two kernels),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -89,9 +88,6 @@ def apply(arm: str):
             else:
                 gemm._SESSIONS.discard(sess)
                 TR.opt.sumsq = None
-        elif key == "xfused":   # cross entropy + logits gradient in one pass (1) or the two kernels (0)
-            import os
-            os.environ["TOA_XENT_FUSED"] = val
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":

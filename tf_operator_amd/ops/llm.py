@@ -208,19 +208,6 @@ def swiglu_mlp(x, wgu, wd):
 # ---------------------------------------------------------------------------
 # Cross entropy (mean over non-ignored tokens)
 # ---------------------------------------------------------------------------
-# The incoming gradient the fused cross entropy writes its logits gradient
-# for (toa_xent_fused): 1 for loss.backward(); a trainer that backpropagates
-# loss / n (gradient accumulation) sets 1 / n here.  Any other value is fixed
-# on the device by toa_xent_rescale (a pass over the gradient).
-XENT_GRAD_HINT = 1.0
-
-
-def _xent_fused_ok(x, inplace_grad) -> bool:
-    return (inplace_grad and x.dtype == torch.bfloat16 and x.stride(-1) == 1 and x.shape[-1] % 8 == 0
-            and x.stride(0) % 8 == 0 and x.shape[-1] // 8 <= 16 * 1024 and x.data_ptr() % 16 == 0
-            and os.environ.get("TOA_XENT_FUSED", "1") != "0" and _lib.has("toa_xent_fused"))
-
-
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, ignore_index, inplace_grad):
@@ -228,18 +215,6 @@ class _CrossEntropy(torch.autograd.Function):
         x = logits.reshape(-1, V)
         t = target.reshape(-1).to(torch.int64).contiguous()
         rows = x.shape[0]
-        ctx.fused = None
-        if _lib.use_hip(x) and _xent_fused_ok(x, inplace_grad):
-            # loss and the logits gradient in one read of the logits, written over them
-            n_valid = (t != ignore_index).sum().float().reshape(1)
-            loss = torch.empty(rows, device=x.device, dtype=torch.float32)
-            hint = float(XENT_GRAD_HINT)
-            _lib.call("toa_xent_fused", _lib.ptr(x), _lib.ptr(t), _lib.ptr(loss), _lib.ptr(n_valid), hint, rows, V,
-                      x.stride(0), int(ignore_index), _lib.stream(x))
-            ctx.save_for_backward(x)
-            ctx.fused = hint
-            ctx.shape = logits.shape
-            return loss.sum() / n_valid.clamp(min=1.0).reshape(())
         if _lib.use_hip(x):
             if x.stride(-1) != 1:
                 x = x.contiguous()
@@ -262,12 +237,6 @@ class _CrossEntropy(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        if ctx.fused is not None:   # the gradient is already in the logits buffer, for g == the hint
-            (dx,) = ctx.saved_tensors
-            go = g.reshape(1).float().contiguous()
-            _lib.call("toa_xent_rescale", _lib.ptr(dx), _lib.ptr(go), ctx.fused, dx.shape[0], dx.shape[-1],
-                      dx.stride(0), _lib.stream(dx))
-            return dx.view(ctx.shape), None, None, None
         x, t, lse, n_valid = ctx.saved_tensors
         V = x.shape[-1]
         if _lib.use_hip(x):

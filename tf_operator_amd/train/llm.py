@@ -181,9 +181,6 @@ class LlamaTrainer:
         elif not self.opt.grads_zeroed:
             self.flat.zero_grad()
         loss_sum = None
-        from ..ops import llm as _llm_ops
-
-        _llm_ops.XENT_GRAD_HINT = 1.0 / len(batches)   # backward() of loss / len(batches): the fused xent's scale
         for i, (tok, tgt) in enumerate(batches):
             loss = self.model(tok, tgt)
             self._phase("first_fwd_issued")
