@@ -419,10 +419,7 @@ static int norm_fwd_launch(const void* x, const void* res, void* h_out, const vo
 // only after every wave has passed row k + 1's barrier, i.e. read row k's).
 // Each wave's dW partials cover its own columns: written straight to
 // partial[blockIdx.x][cols] for col_reduce_kernel, no LDS reduction.
-// HOIST: the residual-gradient (dadd) loads issued with the row's h / dy
-// loads, before the row-sum barrier, instead of after it (one memory round
-// trip per row fewer on the critical path; +8 VGPRs at CPL 2).
-template <int CPL, bool HOIST = true>
+template <int CPL>
 __global__ __launch_bounds__(256) void rms_bwd_row_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
                                                           const bf16_t* __restrict__ w,
                                                           const float* __restrict__ rstd_in,
@@ -444,12 +441,6 @@ __global__ __launch_bounds__(256) void rms_bwd_row_kernel(const bf16_t* __restri
     const float rstd = rstd_in[row];
     const int64_t base = (int64_t)row * cols + col0;
     float xh[CPL][8], g[CPL][8];
-    u32x4 ad[CPL];
-    if (HOIST && dadd != nullptr) {
-#pragma unroll
-      for (int c = 0; c < CPL; ++c)
-        ad[c] = __builtin_nontemporal_load((const u32x4*)(dadd + base + (c * 64 + lane) * 8));
-    }
     float s1 = 0.f;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
@@ -476,7 +467,7 @@ __global__ __launch_bounds__(256) void rms_bwd_row_kernel(const bf16_t* __restri
       for (int j = 0; j < 8; ++j) o[j] = (g[c][j] - xh[c][j] * s1) * rstd;
       if (dadd != nullptr) {
         float a[8];
-        unpack8(HOIST ? ad[c] : __builtin_nontemporal_load((const u32x4*)(dadd + off)), a);
+        unpack8(__builtin_nontemporal_load((const u32x4*)(dadd + off)), a);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] += a[j];
       }
@@ -500,13 +491,6 @@ extern "C" int toa_norm_bwd_blocks(int rows, int cols) {
   return nb < cap ? nb : cap;
 }
 
-static int g_rms_bwd_hoist = 1;
-extern "C" int toa_norm_set_bwd_hoist(int v) {
-  if (v < 0 || v > 1) return (int)hipErrorInvalidValue;
-  g_rms_bwd_hoist = v;
-  return 0;
-}
-
 template <typename T, bool RMS>
 static int norm_bwd_launch(const void* dy, const void* h, const void* w, const float* mean, const float* rstd,
                            const void* dadd, void* dx, float* partial, void* dw, int dw_bf16, void* db,
@@ -519,11 +503,6 @@ static int norm_bwd_launch(const void* dy, const void* h, const void* w, const f
     const bf16_t *dy16 = (const bf16_t*)dy, *h16 = (const bf16_t*)h, *w16 = (const bf16_t*)w,
                  *a16 = (const bf16_t*)dadd;
     bf16_t* dx16 = (bf16_t*)dx;
-    if (!g_rms_bwd_hoist && cols / 2048 == 2) {   // A/B arm: the dadd loads after the barrier
-      hipLaunchKernelGGL((rms_bwd_row_kernel<2, false>), dim3(nb), dim3(256), 0, s, dy16, h16, w16, rstd, a16, dx16,
-                         partial, rows, cols);
-      return (int)hipGetLastError();
-    }
     switch (cols / 2048) {
       case 1: hipLaunchKernelGGL(rms_bwd_row_kernel<1>, dim3(nb), dim3(256), 0, s, dy16, h16, w16, rstd, a16, dx16,
                                  partial, rows, cols); break;
