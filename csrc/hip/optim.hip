@@ -206,6 +206,110 @@ __global__ __launch_bounds__(256) void adamw_flat_kernel(float* __restrict__ mas
   }
 }
 
+// ---------------------------------------------------------------------------
+// AdamW over one 2-D weight [R][C] of the flat buffers (R, C multiples of
+// 128, bf16 gradient) that also writes the weight's transposed bf16 copy
+// W^T [C][R] (row stride ldt) in the same pass -- the copy the data-gradient
+// GEMMs read (ops/wt.py).  The separate refresh re-read the bf16 weight the
+// update had just written (2 B / parameter); here the fresh bf16 values go
+// through a 128 x 128 LDS tile (the XOR-swizzled image of transpose.hip's
+// LDS kernel) and out as 256-byte runs of W^T.  Per element the arithmetic is
+// adam_elem, as in adamw_flat_kernel: bit-identical master / m / v / weight.
+// A workgroup walks 128 x 128 tiles; each pass of its 256 threads updates
+// 16 rows x 128 columns (16 lanes per 256-byte row).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adamw_wt_kernel(float* __restrict__ master, bf16_t* __restrict__ param,
+                                                       bf16_t* __restrict__ grad, int zero_grad,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       bf16_t* __restrict__ wt, int64_t ldt, int R, int C, float lr,
+                                                       float b1, float b2, float eps, float wd, float inv_bc1,
+                                                       float inv_sqrt_bc2, float grad_scale,
+                                                       const float* __restrict__ norm_sq, float max_norm) {
+  __shared__ u32x4 tile[128 * 16];
+  const float scale = adam_prologue(b1, b2, grad_scale, norm_sq, max_norm, nullptr, inv_bc1, inv_sqrt_bc2);
+  const float omb1 = 1.f - b1, omb2 = 1.f - b2, lrwd = lr * wd;
+  const int tid = threadIdx.x;
+  const int lr_ = tid >> 4, lc = tid & 15;   // update: row lr_ + 16 p, chunk lc
+  const int a = tid & 15, bq = tid >> 4;     // transposed store: rows 8a.., chunk bq
+  const int tiles_c = C >> 7;
+  const int64_t ntiles = (int64_t)(R >> 7) * tiles_c;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int tr = (int)(t / tiles_c), tc = (int)(t - (int64_t)tr * tiles_c);
+    const int64_t r0 = (int64_t)tr * 128, c0 = (int64_t)tc * 128;
+    __syncthreads();   // the previous tile's transposed reads are done
+#pragma unroll 1
+    for (int pp = 0; pp < 8; pp += 2) {
+      u32x4 gb[2];
+      f32x4 pv[2][2], mv[2][2], vv[2][2];
+      int64_t e8[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int r = lr_ + 16 * (pp + q);
+        e8[q] = ((r0 + r) * C + c0) / 8 + lc;   // 8-element chunk index in the weight
+        gb[q] = ld_s((const u32x4*)grad + e8[q], true);
+        pv[q][0] = ld_s((const f32x4*)master + 2 * e8[q], true);
+        pv[q][1] = ld_s((const f32x4*)master + 2 * e8[q] + 1, true);
+        mv[q][0] = ld_s((const f32x4*)m + 2 * e8[q], true);
+        mv[q][1] = ld_s((const f32x4*)m + 2 * e8[q] + 1, true);
+        vv[q][0] = ld_s((const f32x4*)v + 2 * e8[q], true);
+        vv[q][1] = ld_s((const f32x4*)v + 2 * e8[q] + 1, true);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int r = lr_ + 16 * (pp + q);
+        float g[8], p[8];
+        unpack8(gb[q], g);
+        if (zero_grad) st16(grad + e8[q] * 8, u32x4{0, 0, 0, 0});
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float pp_ = pv[q][h][j], mm = mv[q][h][j], vq = vv[q][h][j];
+            adam_elem(g[4 * h + j], pp_, mm, vq, scale, b1, b2, omb1, omb2, lr, lrwd, eps, inv_bc1, inv_sqrt_bc2);
+            pv[q][h][j] = pp_;
+            mv[q][h][j] = mm;
+            vv[q][h][j] = vq;
+            p[4 * h + j] = pp_;
+          }
+        st_s((f32x4*)master + 2 * e8[q], pv[q][0], true);
+        st_s((f32x4*)master + 2 * e8[q] + 1, pv[q][1], true);
+        st_s((f32x4*)m + 2 * e8[q], mv[q][0], true);
+        st_s((f32x4*)m + 2 * e8[q] + 1, mv[q][1], true);
+        st_s((f32x4*)v + 2 * e8[q], vv[q][0], true);
+        st_s((f32x4*)v + 2 * e8[q] + 1, vv[q][1], true);
+        const u32x4 pk = pack8(p);
+        st_s((u32x4*)param + e8[q], pk, true);
+        tile[r * 16 + (lc ^ ((r >> 3) & 15))] = pk;
+      }
+    }
+    __syncthreads();
+    u32x4 in[8], out[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) in[i] = tile[(8 * a + i) * 16 + (bq ^ a)];
+    tr8x8(in, out);
+    bf16_t* d = wt + (c0 + 8 * bq) * ldt + r0 + 8 * a;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) __builtin_nontemporal_store(out[j], (u32x4*)(d + j * ldt));
+  }
+}
+
+extern "C" int toa_adamw_wt(float* master, bf16_t* param, bf16_t* grad, int zero_grad, float* m, float* v,
+                            bf16_t* wt, int64_t ldt, int R, int C, float lr, float beta1, float beta2, float eps,
+                            float weight_decay, int step, float grad_scale, const float* norm_sq, float max_norm,
+                            hipStream_t stream) {
+  if (R <= 0 || C <= 0 || R % 128 || C % 128 || ldt < R || ldt % 8 || ((uintptr_t)master & 15) ||
+      ((uintptr_t)m & 15) || ((uintptr_t)v & 15) || ((uintptr_t)grad & 15) || ((uintptr_t)param & 15) ||
+      ((uintptr_t)wt & 15) || step < 1)
+    return (int)hipErrorInvalidValue;
+  const float inv_bc1 = 1.f / (1.f - powf(beta1, (float)step));
+  const float inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(beta2, (float)step));
+  const int64_t tiles = (int64_t)(R / 128) * (C / 128);
+  const int grid = (int)(tiles < 16384 ? tiles : 16384);
+  hipLaunchKernelGGL(adamw_wt_kernel, dim3(grid), dim3(256), 0, stream, master, param, grad, zero_grad, m, v, wt, ldt,
+                     R, C, lr, beta1, beta2, eps, weight_decay, inv_bc1, inv_sqrt_bc2, grad_scale, norm_sq, max_norm);
+  return (int)hipGetLastError();
+}
+
 // Variant switch for in-process A/B (scripts/stream_ab.py,
 // scripts/adamw_grid_bench.py): bit 0 = the non-temporal AdamW, bit 1 = the
 // row-structured non-temporal SwiGLU, bits 8.. = AdamW grid cap / 1024 (0:

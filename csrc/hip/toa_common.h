@@ -109,3 +109,22 @@ static inline int toa_stream_grid(int64_t work_items, int block) {
   if (g < 1) g = 1;
   return (int)g;
 }
+
+// 8 x 8 block of 16-bit values: row i = 4 dwords, element (i, j) in dword
+// j/2, half j&1.  Returns the transposed block in the same format.
+__device__ __forceinline__ void tr8x8(const u32x4* in, u32x4* out) {
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    // out row j   = in[0..7] element j
+    // out row j+1 = in[0..7] element j+1
+    const int d = j >> 1;
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const uint32_t a = in[i][d], b = in[i + 1][d];
+      // low halves of a, b -> (a.lo | b.lo << 16); high halves -> (a.hi | b.hi << 16)
+      out[j][i >> 1] = __builtin_amdgcn_perm(b, a, 0x05040100u);
+      out[j + 1][i >> 1] = __builtin_amdgcn_perm(b, a, 0x07060302u);
+    }
+  }
+}
+

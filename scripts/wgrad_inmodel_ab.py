@@ -15,6 +15,7 @@ ovl=0|1 (AdamW per bucket on a side stream under the next forward, FlatAdamW ove
 ovlcu=n[:mode] (that side stream limited to n CUs, toa_stream_create_cu_mask; 0 = unmasked),
 xent=N (cross-entropy backward chunks per thread), tpose=0|1 (the W^T refresh's transpose kernel),
 fnorm=0|1 (the clipping norm from the weight-gradient kernels' partials, or the full pass),
+adamwt=0|1 (AdamW writes the W^T copies itself, or the refresh transposes after it),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -88,6 +89,10 @@ def apply(arm: str):
             else:
                 gemm._SESSIONS.discard(sess)
                 TR.opt.sumsq = None
+        elif key == "adamwt":   # the update writes the W^T copies itself (1) or they are refreshed after it (0)
+            if not hasattr(TR, "_fused_wt_saved"):
+                TR._fused_wt_saved = TR.opt.fused_wt
+            TR.opt.fused_wt = TR._fused_wt_saved if int(val) else None
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":

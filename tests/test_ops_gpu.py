@@ -1503,3 +1503,30 @@ def test_wgrad_sumsq_partials_whole_and_split_tiles():
     out, ws = torch.zeros(1, device=DEV), torch.empty(32768, device=DEV)
     sess.norm_sq(out, ws)
     assert abs(float(out) - want) <= 1e-3 * want
+
+
+def test_adamw_writes_transposed_copies_bit_identical(monkeypatch):
+    """TOA_ADAM_WT (default): the update writes each weight's W^T copy in the
+    same pass (toa_adamw_wt) -- master, moments and bf16 weights bit for bit
+    as the flat update + separate refresh, and every copy equals W^T."""
+    from tf_operator_amd.models.llama import PRESETS
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    _lib()
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("TOA_ADAM_WT", mode)
+        tr = LlamaTrainer(PRESETS["llama-tiny128"], torch.device(DEV), micro_batch=2, seq_len=512, seed=0)
+        assert (tr.opt.fused_wt is not None) == (mode == "1")
+        if mode == "1":
+            assert len(tr.opt._fused_items()) == 2 * 4 + 1
+        b = tr.synthetic_batch()
+        losses = [float(tr.step([b])) for _ in range(3)]
+        torch.cuda.synchronize()
+        for _, _, p, view in tr.wt.items:
+            assert torch.equal(view, p.data.t())
+        f = tr.flat
+        out[mode] = (losses, f.master.clone(), f.exp_avg.clone(), f.exp_avg_sq.clone(), f.param.detach().clone())
+    assert out["1"][0] == out["0"][0]
+    for a, b in zip(out["1"][1:], out["0"][1:]):
+        assert torch.equal(a, b)

@@ -13,6 +13,7 @@ import os
 import torch
 
 from . import _lib
+from .wt import transpose_into
 
 
 SUMSQ_WS = 32768  # floats of toa_sumsq's partials workspace (its grid cap)
@@ -91,6 +92,10 @@ class FlatAdamW:
                  device_step=False):
         self.post_update = post_update
         self.sumsq = None   # an ops.gemm.SumsqSession (set by the trainer): the clipping norm from kernel partials
+        # fused_wt: an ops.wt.TransposedWeights whose 2-D weights (R, C multiples of 128) the update writes
+        # together with their W^T copies (toa_adamw_wt) instead of refreshing them afterwards (set by the
+        # trainer for an unsharded update; post_update then refreshes only the others)
+        self.fused_wt = None
         # device_step: the step count lives in device memory and is advanced
         # by a kernel, so a captured HIP graph of the whole training step
         # replays with fresh bias corrections (train/simple.py graph mode)
@@ -149,6 +154,34 @@ class FlatAdamW:
                   float(self.beta1), float(self.beta2), float(self.eps),
                   float(self.weight_decay if decay else 0.0), step, float(grad_scale),
                   _lib.ptr(self._norm) if clip else None, float(self.max_grad_norm or 0.0), stream)
+
+    def _fused_items(self) -> dict:
+        """{(lo, hi): (lo, hi, param, view)} of the W^T copies the update can
+        write itself: unsharded, HIP, bf16 gradient, no device step count, R
+        and C multiples of 128, the weight in one state range."""
+        wt = self.fused_wt
+        f = self.flat
+        if (wt is None or self.owned is not None or self.device_step or f.grad.dtype != torch.bfloat16
+                or not _lib.has("toa_adamw_wt")):
+            return {}
+        out = {}
+        for a, b, p, view in wt.items:
+            R, C = p.shape
+            if R % 128 == 0 and C % 128 == 0 and f.state_index(b - 1) == f.state_index(a) + (b - a - 1):
+                out[(a, b)] = (a, b, p, view)
+        return out
+
+    def _launch_wt(self, item, decay, lr, grad_scale, clip, stream):
+        a, b, p, view = item
+        f = self.flat
+        si = f.state_index(a)
+        R, C = p.shape
+        _lib.call("toa_adamw_wt", f.master.data_ptr() + 4 * si, f.param.data_ptr() + 2 * a,
+                  f.grad.data_ptr() + 2 * a, int(bool(self.fuse_zero_grad)), f.exp_avg.data_ptr() + 4 * si,
+                  f.exp_avg_sq.data_ptr() + 4 * si, _lib.ptr(view), view.stride(0), R, C, float(lr),
+                  float(self.beta1), float(self.beta2), float(self.eps), float(self.weight_decay if decay else 0.0),
+                  self.step_count, float(grad_scale), _lib.ptr(self._norm) if clip else None,
+                  float(self.max_grad_norm or 0.0), stream)
 
     def _work_runs(self):
         """(a, b, decay) runs this rank updates."""
@@ -244,12 +277,25 @@ class FlatAdamW:
             pbf = f.param.dtype == torch.bfloat16
             if self.device_step:
                 _lib.call("toa_step_inc", _lib.ptr(self._dstep), s)
+            fused = self._fused_items() if pbf else {}
             for (a, b, decay) in self._work_runs():
-                self._launch(a, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
+                pos = a
+                for ia, ib in sorted(k for k in fused if a <= k[0] and k[1] <= b):
+                    if pos < ia:
+                        self._launch(pos, ia, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
+                    self._launch_wt(fused[(ia, ib)], decay, lr, grad_scale, clip, s)
+                    pos = ib
+                if pos < b:
+                    self._launch(pos, b, decay, lr, grad_scale, clip, self.fuse_zero_grad, s)
             self.grads_zeroed = self.fuse_zero_grad and self.owned is None
             if not pbf:
                 f.param_from_master()
-            if self.post_update is not None:
+            if fused:
+                done = {id(it[2]) for it in fused.values()}
+                for _, _, p, view in self.fused_wt.items:   # the copies the fused update did not write
+                    if id(p) not in done:
+                        transpose_into(view, p.data)
+            elif self.post_update is not None:
                 self.post_update(0, f.numel)
         else:
             for (a, b, decay) in self._work_runs():

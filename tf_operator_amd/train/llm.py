@@ -88,6 +88,9 @@ class LlamaTrainer:
             self.opt = FlatAdamW(self.flat, lr=lr, overlap=overlap_optimizer, buckets=self.bucketer.buckets,
                                  fuse_zero_grad=not self.fresh_grads,
                                  post_update=self.wt.refresh if self.wt else None)
+            if self.wt is not None and os.environ.get("TOA_ADAM_WT", "1") != "0":
+                # the update writes the W^T copies itself (ops/optim.py toa_adamw_wt)
+                self.opt.fused_wt = self.wt
         self._fused_norm(model)
         if self.opt.overlap or self.gather is not None:
             self._hooks = self._install_param_waits()
