@@ -91,7 +91,7 @@ KARG = {
 MAP_WALK_COLS = 16
 MAP_DEFAULT = 2          # groups of 4 row tiles walk the column tiles
 
-EPIS = ("plain", "swiglu_fwd", "swiglu_bwd")
+EPIS = ("plain", "swiglu_fwd", "swiglu_bwd", "rope")
 
 # ---------------------------------------------------------------- registers
 # SGPRs: s[0:1] kernarg pointer, s2 workgroup id (the descriptor's order)
@@ -357,7 +357,7 @@ def tile_c(a: Asm, epi: str):
     a(f"s_addc_u32 {sr(S_T3)}, {sr(S_T3)}, 0")
     a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDC)}, 8")
     srd(a, SRD_C, S_C, S_T2, S_T3, S_T1)
-    if epi != "plain":
+    if epi in ("swiglu_fwd", "swiglu_bwd"):
         a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
         mul64(a, S_T2, S_T3, S_T0, S_LDS)
         a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TN)}, {8 if epi == 'swiglu_fwd' else 9}")
@@ -888,6 +888,150 @@ def acc_index(i: int, j: int) -> int:
     return 4 * (8 * i + j)
 
 
+ROPE_DEPTH = 2   # cos / sin row blocks loaded this many blocks ahead (staging in the fragment VGPRs)
+
+
+def epilogue_rope(a: Asm):
+    """The fused-QKV projection's epilogue with RoPE and the head-major
+    relayout (replaces toa_rope_fwd): C is never written as [T, (Hq + 2 Hkv)
+    128]; wave (wm, wn) owns head h = 2 tn + wn for 128 tokens and stores
+    them rotated (q, k heads; rotate-half pairs (d, d + 64), both in the
+    lane: fragment pairs p and p + 2) or as they are (v heads) into out =
+    [q: B Hq S 128 | k: B Hkv S 128 | v: B Hkv S 128] bf16 (kernarg C).
+    Rotation on the fp32 accumulators (the unfused path rotated the bf16-
+    rounded GEMM output).  Kernarg S: cos | sin [2][S][64] fp32; fw = S (a
+    multiple of 256, so a tile's 256 tokens are one sequence's), fc = Hq |
+    Hkv << 16.  cos / sin rows for row block j + ROPE_DEPTH load while j is
+    rotated (counted vmcnt, as epilogue_swiglu_bwd_pipe)."""
+    v = V_T
+    # ---- wave-uniform: w, wm, wn, head, batch, s0 (SGPRs S_E0.. / S_T*)
+    a(f"v_lshrrev_b32 {vr(v)}, 6, {vr(V_TID)}")
+    a("s_nop 4")
+    a(f"v_readfirstlane_b32 {sr(S_Q)}, {vr(v)}")              # w
+    a(f"s_and_b32 {sr(S_R)}, {sr(S_Q)}, 1")                   # wm
+    a(f"s_lshr_b32 {sr(S_Q)}, {sr(S_Q)}, 1")                  # wn
+    a(f"s_lshl_b32 {sr(S_E0)}, {sr(S_TN)}, 1")
+    a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_Q)}")         # head h
+    a(f"s_lshl_b32 {sr(S_T3)}, {sr(S_TM)}, 8")                # first token of the tile
+    udiv(a, S_T0, S_T1, S_T3, S_FW)                           # b = t0 / S, s_tile = t0 % S
+    a(f"s_lshl_b32 {sr(S_R)}, {sr(S_R)}, 7")
+    a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_R)}")         # s0 = s_tile + 128 wm
+    a(f"s_and_b32 {sr(S_T2)}, {sr(S_FC)}, 0xffff")            # Hq
+    a(f"s_lshr_b32 {sr(S_T3)}, {sr(S_FC)}, 16")               # Hkv
+    # Btot = tiles_m 256 / S (whole sequences): S_E1
+    a(f"s_lshl_b32 {sr(S_Q)}, {sr(S_TM_N)}, 8")
+    udiv(a, S_E1, S_R, S_Q, S_FW)
+    # head row index (in units of S rows of 128 elements) into out, by section:
+    #   q: (b Hq + h) ; k: Btot Hq + b Hkv + (h - Hq) ; v: Btot (Hq + Hkv) + b Hkv + (h - Hq - Hkv)
+    l_k, l_v, l_base = a.fresh("rope_k"), a.fresh("rope_v"), a.fresh("rope_base")
+    a(f"s_mov_b32 {sr(S_LOOP)}, 1")                           # rotate flag (q and k heads)
+    a(f"s_cmp_ge_u32 {sr(S_E0)}, {sr(S_T2)}")
+    a(f"s_cbranch_scc1 {l_k}")
+    a(f"s_mul_i32 {sr(S_Q)}, {sr(S_T0)}, {sr(S_T2)}")
+    a(f"s_add_u32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_E0)}")
+    a(f"s_branch {l_base}")
+    a.label(l_k)
+    a(f"s_sub_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_T2)}")        # h - Hq
+    a(f"s_mul_i32 {sr(S_Q)}, {sr(S_E1)}, {sr(S_T2)}")         # Btot Hq
+    a(f"s_cmp_ge_u32 {sr(S_E0)}, {sr(S_T3)}")
+    a(f"s_cbranch_scc1 {l_v}")
+    a(f"s_mul_i32 {sr(S_R)}, {sr(S_T0)}, {sr(S_T3)}")
+    a(f"s_add_u32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_R)}")
+    a(f"s_add_u32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_E0)}")
+    a(f"s_branch {l_base}")
+    a.label(l_v)
+    a(f"s_mov_b32 {sr(S_LOOP)}, 0")
+    a(f"s_sub_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_T3)}")        # h - Hq - Hkv
+    a(f"s_mul_i32 {sr(S_R)}, {sr(S_E1)}, {sr(S_T3)}")
+    a(f"s_add_u32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_R)}")           # Btot (Hq + Hkv)
+    a(f"s_mul_i32 {sr(S_R)}, {sr(S_T0)}, {sr(S_T3)}")
+    a(f"s_add_u32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_R)}")
+    a(f"s_add_u32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_E0)}")
+    a.label(l_base)
+    # byte offset of (head row, s0): (S_Q S + s0) 256 -> SRD_C over this wave's 128 rows
+    a(f"s_mul_i32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_FW)}")
+    a(f"s_add_u32 {sr(S_Q)}, {sr(S_Q)}, {sr(S_T1)}")
+    a(f"s_mov_b32 {sr(S_R)}, 256")
+    mul64(a, S_T2, S_T3, S_Q, S_R)
+    a(f"s_mov_b32 {sr(S_R)}, {128 * 256}")
+    srd(a, SRD_C, S_C, S_T2, S_T3, S_R)
+    # cos / sin rows s0 .. s0 + 127: SRD_S at cos + s0 256, sin + S 256 (soffset S_E1 = S 256)
+    a(f"s_mov_b32 {sr(S_R)}, 256")
+    mul64(a, S_T2, S_T3, S_T1, S_R)
+    a(f"s_mul_i32 {sr(S_E1)}, {sr(S_FW)}, 256")
+    a(f"s_add_u32 {sr(S_R)}, {sr(S_E1)}, {128 * 256}")
+    srd(a, SRD_S, S_S, S_T2, S_T3, S_R)
+    # ---- per lane: C offset (row l & 15, group g = l >> 4: 16 g bytes), cos offset 32 g bytes
+    a(f"v_and_b32 {vr(v + 1)}, 63, {vr(V_TID)}")
+    a(f"v_and_b32 {vr(v + 2)}, 15, {vr(v + 1)}")
+    a(f"v_lshlrev_b32 {vr(v + 2)}, 8, {vr(v + 2)}")           # row * 256
+    a(f"v_lshrrev_b32 {vr(v + 3)}, 4, {vr(v + 1)}")           # g
+    a(f"v_lshl_add_u32 {vr(V_E)}, {vr(v + 3)}, 4, {vr(v + 2)}")      # out: 16 g
+    a(f"v_lshl_add_u32 {vr(V_E + 1)}, {vr(v + 3)}, 5, {vr(v + 2)}")  # cos: 32 g
+    a(f"s_mov_b32 {sr(S_T0)}, 0")                             # row block soffset (out and cos: 16 rows x 256 B)
+    a(f"s_mov_b32 {sr(S_T1)}, 0")                             # cos prefetch soffset
+    a(f"s_add_u32 {sr(S_T2)}, {sr(S_E1)}, 0")                 # sin prefetch soffset (S 256 + row block)
+    l_plain, l_end = a.fresh("rope_plain"), a.fresh("rope_end")
+    a(f"s_cmp_eq_u32 {sr(S_LOOP)}, 0")
+    a(f"s_cbranch_scc1 {l_plain}")
+    D = ROPE_DEPTH
+    seq: list = []
+
+    def slot(j):
+        return V_FX0 + 32 * (j % D)             # cos 16 regs, sin 16 regs
+
+    def issue(j):
+        st = slot(j)
+        for p in range(2):
+            for h in range(2):
+                a(f"buffer_load_dwordx4 {vr(st + 8 * p + 4 * h, 4)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T1)} offen offset:{128 * p + 16 * h}")
+                a(f"buffer_load_dwordx4 {vr(st + 16 + 8 * p + 4 * h, 4)}, {vr(V_E + 1)}, {sr(SRD_S, 4)}, {sr(S_T2)} offen offset:{128 * p + 16 * h}")
+                seq.extend([("L", j), ("L", j)])
+        a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, 4096")
+        a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, 4096")
+
+    for j in range(min(D, 8)):
+        issue(j)
+    f, pk, t = V_E + 8, V_E + 40, V_E + 56
+    for j in range(8):
+        for p in range(4):
+            read_pair(a, f + 8 * p, p, j)
+        last = max(i for i, x in enumerate(seq) if x == ("L", j))
+        a(f"s_waitcnt vmcnt({min(63, len(seq) - last - 1)})")
+        cs, sn = slot(j), slot(j) + 16
+        for p in range(2):
+            for e in range(8):
+                x1, x2 = f + 8 * p + e, f + 8 * (p + 2) + e
+                c_, s_ = cs + 8 * p + e, sn + 8 * p + e
+                a(f"v_mul_f32 {vr(t)}, {vr(x2)}, {vr(s_)}")
+                a(f"v_mul_f32 {vr(t + 1)}, {vr(x1)}, {vr(s_)}")
+                a(f"v_mul_f32 {vr(t + 2)}, {vr(x1)}, {vr(c_)}")
+                a(f"v_fma_f32 {vr(x2)}, {vr(x2)}, {vr(c_)}, {vr(t + 1)}")   # x2 c + x1 s
+                a(f"v_sub_f32 {vr(x1)}, {vr(t + 2)}, {vr(t)}")              # x1 c - x2 s
+        if j + D < 8:
+            issue(j + D)                          # into the slot just consumed
+        for p in range(4):
+            cvt_pack8(a, pk + 4 * p, f + 8 * p)
+        for p in range(4):
+            store16(a, pk + 4 * p, V_E, SRD_C, S_T0, p)
+        seq.extend([("S", j)] * 4)
+        a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, 4096")
+        a("s_nop 1")
+    a(f"s_branch {l_end}")
+    # ---- v heads: the relayout alone
+    a.label(l_plain)
+    for j in range(8):
+        for p in range(4):
+            read_pair(a, f + 8 * p, p, j)
+        for p in range(4):
+            cvt_pack8(a, pk + 4 * p, f + 8 * p)
+        for p in range(4):
+            store16(a, pk + 4 * p, V_E, SRD_C, S_T0, p)
+        a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, 4096")
+        a("s_nop 1")
+    a.label(l_end)
+
+
 def epi_offsets(a: Asm, epi: str):
     """Per-lane output byte offsets.  Lane l of wave (wm, wn) holds, for
     fragments (2p, j) and (2p+1, j): row m = wm*128 + 16 j + (l & 15) and the
@@ -1361,8 +1505,10 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
     if persist:
         persistent_next(a, epi, l_tile)
     if not SCHED["epi_none"]:   # (the "none" arm: DIAGNOSTIC, the main loop alone)
-        epi_offsets(a, epi)
-        {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd}[epi](a)
+        if epi != "rope":
+            epi_offsets(a, epi)
+        {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd,
+         "rope": epilogue_rope}[epi](a)
     if trace or timing or SCHED["drain_end"]:
         a("s_waitcnt vmcnt(0)")
     # else: end with the epilogue's stores still in flight -- the wave's end

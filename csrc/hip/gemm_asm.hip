@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_SWFWD_P1 = 52, K_SWBWD_P1 = 53, K_N = 54 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_SWFWD_P1 = 52, K_SWBWD_P1 = 53, K_ROPE = 54, K_N = 55 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -64,7 +64,9 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // the dK/dV kernel's arm s7 (attn_bwd_gen.py VARIANTS, appended)
                            "toa_attn_dkdv_asm_s7", "toa_attn_dkdv_asm_d8", "toa_attn_dkdv_asm_s8",
                            // the persistent fused SwiGLU GEMMs (gemm_gen.py SWIGLU_PERSIST_VARIANTS)
-                           "toa_gemm_tn_asm_swiglu_fwd_p1", "toa_gemm_tn_asm_swiglu_bwd_p1"};
+                           "toa_gemm_tn_asm_swiglu_fwd_p1", "toa_gemm_tn_asm_swiglu_bwd_p1",
+                           // the fused-QKV projection with RoPE + head-major relayout (gemm_gen.py epilogue_rope)
+                           "toa_gemm_tn_asm_rope"};
 
 struct DevModule {
   std::once_flag once;
@@ -620,6 +622,24 @@ extern "C" int toa_gemm_asm_swiglu_bwd(const bf16_t* dY, int64_t ldy, const bf16
   a.lds = (uint32_t)(ldgu * 2);
   a.fc = (uint32_t)(F * 2);
   return g_epi_r4 ? launch(K_SWIGLU_BWD_R4, a, stream) : launch_swiglu(K_SWIGLU_BWD, 2, a, stream);
+}
+
+// The fused-QKV projection x Wqkv^T written as RoPE-rotated, head-major
+// q | k | v (gemm_gen.py epilogue_rope; replaces toa_rope_fwd): out =
+// [B Hq S 128 | B Hkv S 128 | B Hkv S 128] bf16, cossin = cos | sin [2][S][64]
+// fp32.  N = (Hq + 2 Hkv) 128 must be a multiple of 256, S of 256, M of S.
+extern "C" int toa_gemm_asm_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* out,
+                                 const float* cossin, int M, int K, int S, int Hq, int Hkv, hipStream_t stream) {
+  const int64_t N = (int64_t)(Hq + 2 * Hkv) * 128;
+  if (!common_ok(M, K, ldx, ldw, X, W) || Hq <= 0 || Hkv <= 0 || Hq > 4096 || Hkv > 4096 || N % 256 || S <= 0 ||
+      S % 256 || M % S || !al16(out) || !al16(cossin) || (int64_t)M * N * 2 >= (1ll << 32) ||
+      (int64_t)S * 512 + 128 * 256 >= (1ll << 32))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, W, ldw, out, 0, M, (int)(N / 256), K);
+  a.S = (uint64_t)cossin;
+  a.fw = (uint32_t)S;
+  a.fc = (uint32_t)(Hq | (Hkv << 16));
+  return launch(K_ROPE, a, stream);
 }
 
 // DIAGNOSTIC: arm v (1..) of the fused SwiGLU backward (gemm_gen.py

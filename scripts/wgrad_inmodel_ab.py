@@ -16,6 +16,7 @@ ovlcu=n[:mode] (that side stream limited to n CUs, toa_stream_create_cu_mask; 0 
 xent=N (cross-entropy backward chunks per thread), tpose=0|1 (the W^T refresh's transpose kernel),
 fnorm=0|1 (the clipping norm from the weight-gradient kernels' partials, or the full pass),
 adamwt=0|1 (AdamW writes the W^T copies itself, or the refresh transposes after it),
+qkvrope=0|1 (the QKV projection's GEMM applies RoPE and the head-major relayout, or the RoPE pass does),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -93,6 +94,9 @@ def apply(arm: str):
             if not hasattr(TR, "_fused_wt_saved"):
                 TR._fused_wt_saved = TR.opt.fused_wt
             TR.opt.fused_wt = TR._fused_wt_saved if int(val) else None
+        elif key == "qkvrope":   # the QKV GEMM writes rotated head-major q | k | v (1) or qkv + the RoPE pass (0)
+            import os
+            os.environ["TOA_QKV_ROPE"] = val
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":

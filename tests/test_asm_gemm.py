@@ -240,6 +240,46 @@ def test_asm_gemm_swiglu_persistent_emulated(epi, grid):
         close(dgu[:, F:], ds * tof(GU[:, :F]) / (1 + np.exp(-tof(GU[:, :F]))))
 
 
+def _rope_ref(X, W, cs, B, S, Hq, Hkv):
+    D = 128
+    qkv = tof(X) @ tof(W).T                                   # [B S, H3 D]
+    x = qkv.reshape(B, S, Hq + 2 * Hkv, D)
+    c = cs[0].astype(np.float64)[None, :, None, :]             # [1, S, 1, 64]
+    sn = cs[1].astype(np.float64)[None, :, None, :]
+    rot = x.copy()
+    r = slice(0, Hq + Hkv)
+    x1, x2 = x[:, :, r, :64], x[:, :, r, 64:]
+    rot[:, :, r, :64] = x1 * c - x2 * sn
+    rot[:, :, r, 64:] = x2 * c + x1 * sn
+    q = rot[:, :, :Hq].transpose(0, 2, 1, 3)
+    k = rot[:, :, Hq:Hq + Hkv].transpose(0, 2, 1, 3)
+    v = rot[:, :, Hq + Hkv:].transpose(0, 2, 1, 3)
+    return np.concatenate([q.reshape(-1), k.reshape(-1), v.reshape(-1)])
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 256, 2, 1), (1, 512, 4, 2)])
+def test_asm_gemm_rope_epilogue_emulated(B, S, Hq, Hkv):
+    """The fused-QKV projection with the RoPE + head-major epilogue: out =
+    [q B Hq S 128 | k B Hkv S 128 | v B Hkv S 128], q / k rotated
+    (rotate-half, cos / sin [S, 64] fp32 from the fp32 accumulators), v as is."""
+    rng = np.random.default_rng(B * S + Hq)
+    K = 192
+    M, N = B * S, (Hq + 2 * Hkv) * 128
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)) * 0.2)
+    ang = np.arange(S)[:, None] * (10000.0 ** (-np.arange(64) / 64))[None, :]
+    cs = np.stack([np.cos(ang), np.sin(ang)]).astype(np.float32)   # [2, S, 64]
+    mem = emu.Memory()
+    ax, aw = mem.add(X), mem.add(W)
+    ao = mem.add(np.zeros(M * N, np.uint16))
+    acs = mem.add(cs)
+    karg = host_args.pack(ax, aw, ao, acs, 2 * K, 2 * K, 0, 0, K, M // 256, N // 256, fw_b=S, fc_b=Hq | (Hkv << 16))
+    run_all("toa_gemm_tn_asm_rope", karg, (M // 256) * (N // 256), mem)
+    out = tof(mem.bufs[2][1].view(np.uint16))
+    ref = _rope_ref(X, W, cs, B, S, Hq, Hkv)
+    close(out, ref)
+
+
 @pytest.mark.parametrize("tile_map", [0, 1, 2, 3, 4, 16, 17, 18, 19, 20])
 def test_asm_gemm_tile_order_is_a_bijection(tile_map):
     """The XCD remap + group walk (row groups, or column groups with the walk
@@ -310,7 +350,8 @@ def test_host_kernel_table_matches_generator():
     import attn_bwd_gen
     import attn_gen
     # + the round-4 SwiGLU epilogue arms (2) + the SwiGLU backward's diagnostic arms
-    assert n == len(wanted) == 8 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
+    # 9: the four product epilogues (plain, swiglu_fwd, swiglu_bwd, rope), probe, trace, timing, timing2, wgrad
+    assert n == len(wanted) == 9 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
         len(attn_bwd_gen.VARIANTS) + 2 + len(gemm_gen.SWIGLU_BWD_VARIANTS) + len(gemm_gen.SWIGLU_PERSIST_VARIANTS)
     flags = re.search(r"kVariantPersist\[kNumPlainVariants\] = \{([^}]*)\}", src).group(1)
     assert int(re.search(r"kNumPlainVariants = (\d+)", src).group(1)) == len(gemm_gen.PLAIN_VARIANTS)

@@ -1530,3 +1530,40 @@ def test_adamw_writes_transposed_copies_bit_identical(monkeypatch):
     assert out["1"][0] == out["0"][0]
     for a, b in zip(out["1"][1:], out["0"][1:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 4, 2), (1, 1024, 8, 4)])
+def test_qkv_rope_attention_fused_matches_two_nodes(B, S, Hq, Hkv):
+    """toa_gemm_asm_rope (the QKV projection writing rotated head-major
+    q | k | v) + attention against linear + rope_attention: the output and
+    the input / weight gradients, to bf16 rounding (the fused path rotates
+    the fp32 accumulators, the other the bf16 GEMM output)."""
+    from tf_operator_amd.ops import gemm, llm
+    from tf_operator_amd.ops.linear import linear
+
+    _lib()
+    rope_tables = llm.rope_tables
+    old = gemm.mode()
+    gemm.set_mode("asm")
+    try:
+        torch.manual_seed(S + Hq)
+        D, Hd = 128, 512
+        x0 = torch.randn(B * S, Hd, device=DEV).to(torch.bfloat16)
+        w0 = (torch.randn((Hq + 2 * Hkv) * D, Hd, device=DEV) / Hd ** 0.5).to(torch.bfloat16)
+        cos, sin = rope_tables(S, D, device=DEV)
+        dout = torch.randn(B, S, Hq, D, device=DEV).to(torch.bfloat16)
+        res = []
+        for fused in (True, False):
+            x = x0.clone().requires_grad_()
+            w = torch.nn.Parameter(w0.clone())
+            w.main_grad = torch.zeros_like(w)
+            assert llm.qkv_rope_attention_ok(x, w, S, Hq, Hkv, D)
+            o = (llm.qkv_rope_attention(x, w, cos, sin, B, S, Hq, Hkv, D) if fused
+                 else llm.rope_attention(linear(x, w), cos, sin, B, S, Hq, Hkv, D))
+            o.backward(dout)
+            torch.cuda.synchronize()
+            res.append((o.detach().float(), x.grad.float(), w.main_grad.float()))
+    finally:
+        gemm.set_mode(old)
+    for a, b in zip(*res):
+        assert rel(a, b) < 2e-2, rel(a, b)

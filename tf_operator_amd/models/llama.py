@@ -26,7 +26,8 @@ import torch
 
 from ..ops.embedding import Embedding
 from ..ops.linear import linear
-from ..ops.llm import causal_attention, cross_entropy, rope_attention, rope_qkv, rope_tables, swiglu_mlp
+from ..ops.llm import (causal_attention, cross_entropy, qkv_rope_attention, qkv_rope_attention_ok, rope_attention,
+                       rope_qkv, rope_tables, swiglu_mlp)
 from ..ops.norm import RMSNorm, add_rms_norm
 
 
@@ -97,12 +98,17 @@ class LlamaBlock(torch.nn.Module):
             x = self.attn_norm(h)
         else:
             h, x = self.attn_norm(h, delta)
-        qkv = linear(x, self.wqkv)
-        if cfg.kv_layout in ("packed", "auto"):
+        if cfg.kv_layout in ("packed", "auto") and qkv_rope_attention_ok(x, self.wqkv, S, cfg.heads, cfg.kv_heads,
+                                                                         cfg.head_dim):
+            # the projection's GEMM writes rotated head-major q | k | v (no qkv tensor, no RoPE pass)
+            o = qkv_rope_attention(x, self.wqkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim)
+        elif cfg.kv_layout in ("packed", "auto"):
             # the attention kernel reads packed GQA K/V natively; RoPE and
             # attention are one autograd node whose backward writes d(qkv)
+            qkv = linear(x, self.wqkv)
             o = rope_attention(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim)  # [B, S, H, D]
         else:
+            qkv = linear(x, self.wqkv)
             rep = cfg.heads // cfg.kv_heads
             q, k, v = rope_qkv(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim, rep)
             o = causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]: no transpose copy

@@ -346,26 +346,101 @@ class _RopeAttn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse, cos, sin = ctx.saved_tensors
-        B, Hq, S, D = q.shape
-        Hkv = k.shape[1]
-        do = do.contiguous()
-        dqkv = torch.empty(B * S, (Hq + 2 * Hkv) * D, device=q.device, dtype=q.dtype)
-        flags = 1 | (2 if ctx.bshd else 0)
-        ws = _attn_ws(B, Hq, S, D, q.device)
-        if ws is not None and _ROPE_FUSED_BWD and _lib.has("toa_attn_bwd_rope"):
-            delta = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
-            rc = _lib.call_ret("toa_attn_bwd_rope", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do),
-                               _lib.ptr(lse), _lib.ptr(delta), _lib.ptr(ws), _lib.ptr(cos), _lib.ptr(sin),
-                               _lib.ptr(dqkv), B, Hq, Hkv, S, D, flags, float(ctx.scale), _lib.stream(q))
-            if rc == 0:
-                return dqkv, None, None, None, None, None, None, None, None, None
-            if rc != 801:  # hipErrorNotSupported: take the two-pass path below
-                raise RuntimeError(f"toa_attn_bwd_rope failed with hipError {rc}")
-        del ws
-        dq, dk, dv = _attn_bwd(q, k, v, o, lse, do, ctx.scale, ctx.bshd)
-        _lib.call("toa_rope_bwd", _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), _lib.ptr(cos), _lib.ptr(sin),
-                  _lib.ptr(dqkv), B, S, Hq, Hkv, D, 1, _lib.stream(q))
+        dqkv = _rope_attn_dqkv(q, k, v, o, lse, cos, sin, do, ctx.scale, ctx.bshd)
         return dqkv, None, None, None, None, None, None, None, None, None
+
+
+def _rope_attn_dqkv(q, k, v, o, lse, cos, sin, do, scale, bshd):
+    """d(qkv) [B S, (Hq + 2 Hkv) D] of RoPE + causal attention from dO."""
+    B, Hq, S, D = q.shape
+    Hkv = k.shape[1]
+    do = do.contiguous()
+    dqkv = torch.empty(B * S, (Hq + 2 * Hkv) * D, device=q.device, dtype=q.dtype)
+    flags = 1 | (2 if bshd else 0)
+    ws = _attn_ws(B, Hq, S, D, q.device)
+    if ws is not None and _ROPE_FUSED_BWD and _lib.has("toa_attn_bwd_rope"):
+        delta = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
+        rc = _lib.call_ret("toa_attn_bwd_rope", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do),
+                           _lib.ptr(lse), _lib.ptr(delta), _lib.ptr(ws), _lib.ptr(cos), _lib.ptr(sin),
+                           _lib.ptr(dqkv), B, Hq, Hkv, S, D, flags, float(scale), _lib.stream(q))
+        if rc == 0:
+            return dqkv
+        if rc != 801:  # hipErrorNotSupported: take the two-pass path below
+            raise RuntimeError(f"toa_attn_bwd_rope failed with hipError {rc}")
+    del ws
+    dq, dk, dv = _attn_bwd(q, k, v, o, lse, do, scale, bshd)
+    _lib.call("toa_rope_bwd", _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), _lib.ptr(cos), _lib.ptr(sin),
+              _lib.ptr(dqkv), B, S, Hq, Hkv, D, 1, _lib.stream(q))
+    return dqkv
+
+
+_COSSIN: dict = {}   # (cos ptr, sin ptr, S) -> cos | sin [2][S][64] fp32 (toa_gemm_asm_rope's table)
+
+
+def _cossin(cos, sin):
+    key = (cos.data_ptr(), sin.data_ptr(), cos.shape[0])
+    t = _COSSIN.get(key)
+    if t is None:
+        if len(_COSSIN) > 16:
+            _COSSIN.clear()
+        t = _COSSIN[key] = torch.stack([cos.float(), sin.float()]).contiguous()
+    return t
+
+
+class _QKVRopeAttn(torch.autograd.Function):
+    """The fused-QKV projection, RoPE and causal attention as one node: the
+    projection's assembly GEMM writes rotated, head-major q | k | v straight
+    from its accumulators (toa_gemm_asm_rope: no [T, (Hq + 2 Hkv) D] qkv
+    tensor, no toa_rope_fwd pass); backward: d(qkv) from the attention
+    backward (rotated back there), then the projection's data and weight
+    gradients (ops/linear.py)."""
+
+    @staticmethod
+    def forward(ctx, x, wqkv, cos, sin, B, S, Hq, Hkv, D, scale, bshd):
+        x2 = x.reshape(-1, x.shape[-1])
+        T, K = x2.shape
+        out = torch.empty(T * (Hq + 2 * Hkv) * D, device=x.device, dtype=x.dtype)
+        cs = _cossin(cos, sin)
+        _lib.call("toa_gemm_asm_rope", _lib.ptr(x2), x2.stride(0), _lib.ptr(wqkv), wqkv.stride(0), _lib.ptr(out),
+                  _lib.ptr(cs), T, K, S, Hq, Hkv, _lib.stream(x2))
+        nq, nk = B * Hq * S * D, B * Hkv * S * D
+        q = out[:nq].view(B, Hq, S, D)
+        k = out[nq:nq + nk].view(B, Hkv, S, D)
+        v = out[nq + nk:].view(B, Hkv, S, D)
+        o = torch.empty(B, S, Hq, D, device=x.device, dtype=x.dtype) if bshd else torch.empty_like(q)
+        lse = torch.empty(B, Hq, S, device=x.device, dtype=torch.float32)
+        _lib.call("toa_attn_fwd", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(lse), B, Hq, Hkv, S, D,
+                  1 | (2 if bshd else 0), float(scale), _lib.stream(q))
+        ctx.save_for_backward(x, wqkv, q, k, v, o, lse, cos, sin)
+        ctx.scale, ctx.bshd = scale, bshd
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        from .grad import accumulate_mm
+
+        x, wqkv, q, k, v, o, lse, cos, sin = ctx.saved_tensors
+        dqkv = _rope_attn_dqkv(q, k, v, o, lse, cos, sin, do, ctx.scale, ctx.bshd)
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = gemm.linear_dgrad(dqkv, wqkv).view_as(x) if ctx.needs_input_grad[0] else None
+        dw = accumulate_mm(wqkv, dqkv.t(), x2)
+        return dx, dw, None, None, None, None, None, None, None, None, None
+
+
+def qkv_rope_attention_ok(x, wqkv, S, Hq, Hkv, D) -> bool:
+    """The fused projection + RoPE path applies: the assembly GEMM policy,
+    bf16, head dim 128, S and the projection width multiples of 256."""
+    return (x.is_cuda and x.dtype == wqkv.dtype == torch.bfloat16 and D == 128 and S % 256 == 0
+            and ((Hq + 2 * Hkv) * D) % 256 == 0 and Hq % Hkv == 0 and gemm.mode() == "asm"
+            and os.environ.get("TOA_QKV_ROPE", "1") != "0" and _lib.has("toa_gemm_asm_rope")
+            and x.reshape(-1, x.shape[-1]).stride(-1) == 1 and wqkv.stride(-1) == 1
+            and (x.reshape(-1, x.shape[-1]).shape[0]) % S == 0 and x.shape[-1] % 64 == 0)
+
+
+def qkv_rope_attention(x, wqkv, cos, sin, B, S, Hq, Hkv, D, scale=None, out_layout="bshd"):
+    """linear(x, wqkv) -> rope_attention, fused where qkv_rope_attention_ok."""
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    return _QKVRopeAttn.apply(x, wqkv, cos, sin, B, S, Hq, Hkv, D, scale, out_layout == "bshd")
 
 
 def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, scale=None, out_layout="bshd"):
