@@ -791,6 +791,26 @@ class Emu:
         lo, hi = self.vrange(w, a[0])
         w.v[lo:hi] = out.view(np.uint32).reshape(64, 2).T
 
+    def _ds_addr(self, w, tok, mods, nbytes):
+        addr = self.vget(w, tok).astype(np.int64)
+        for md in mods:
+            if md.startswith("offset:"):
+                addr = addr + int(md.split(":")[1])
+        if addr.min() < 0 or addr.max() + nbytes > self.lds.size:
+            raise IndexError("ds access past the LDS")
+        return addr
+
+    def op_ds_write_b32(self, w, a, mods):
+        addr = self._ds_addr(w, a[0], mods, 4)
+        data = self.vget(w, a[1]).astype(np.uint32)
+        for l in range(64):
+            self.lds[addr[l]:addr[l] + 4] = np.frombuffer(np.uint32(data[l]).tobytes(), np.uint8)
+
+    def op_ds_read_b32(self, w, a, mods):
+        addr = self._ds_addr(w, a[1], mods, 4)
+        lo, hi = self.vrange(w, a[0])
+        w.v[lo] = np.array([self.lds[x:x + 4].view(np.uint32)[0] for x in addr], dtype=np.uint32)
+
     def op_ds_read_b128(self, w, a, mods):
         addr = self.vget(w, a[1]).astype(np.int64)
         for md in mods:

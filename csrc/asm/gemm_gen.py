@@ -91,7 +91,7 @@ KARG = {
 MAP_WALK_COLS = 16
 MAP_DEFAULT = 2          # groups of 4 row tiles walk the column tiles
 
-EPIS = ("plain", "swiglu_fwd", "swiglu_bwd", "rope")
+EPIS = ("plain", "swiglu_fwd", "swiglu_bwd", "rope", "delta")
 
 # ---------------------------------------------------------------- registers
 # SGPRs: s[0:1] kernarg pointer, s2 workgroup id (the descriptor's order)
@@ -221,7 +221,7 @@ def mul64(a: Asm, lo: int, hi: int, x: int, y: int):
 
 
 # ---------------------------------------------------------------- prologue
-def prologue_args(a: Asm):
+def prologue_args(a: Asm, epi: str = "plain"):
     a(f"s_load_dwordx16 {sr(S_ARGS, 16)}, s[0:1], 0x0")
     a(f"s_load_dwordx4 {sr(S_ARGS + 16, 4)}, s[0:1], 0x40")
     a(f"s_load_dwordx2 {sr(S_MAP, 2)}, s[0:1], 0x50")
@@ -249,7 +249,8 @@ def prologue_args(a: Asm):
     a(f"s_cmp_ge_u32 {sr(S_MAP)}, {2 * MAP_WALK_COLS}")
     a(f"s_cbranch_scc1 {a.abort}")
     a(f"s_lshr_b32 {sr(S_WALK)}, {sr(S_MAP)}, 4")
-    phase_delay(a)
+    if epi != "delta":      # (its kernarg bytes 88..95 are the delta pointer, not a phase word)
+        phase_delay(a)
     if SCHED["persist"]:
         # persistent: the grid size; 0 would walk one tile forever
         a(f"s_cmp_eq_u32 {sr(S_KGRID)}, 0")
@@ -357,6 +358,14 @@ def tile_c(a: Asm, epi: str):
     a(f"s_addc_u32 {sr(S_T3)}, {sr(S_T3)}, 0")
     a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDC)}, 8")
     srd(a, SRD_C, S_C, S_T2, S_T3, S_T1)
+    if epi == "delta":      # O: the same tile of a tensor laid out like C
+        a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
+        mul64(a, S_T2, S_T3, S_T0, S_LDC)
+        a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TN)}, 9")
+        a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_T0)}")
+        a(f"s_addc_u32 {sr(S_T3)}, {sr(S_T3)}, 0")
+        a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDC)}, 8")
+        srd(a, SRD_S, S_S, S_T2, S_T3, S_T1)
     if epi in ("swiglu_fwd", "swiglu_bwd"):
         a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
         mul64(a, S_T2, S_T3, S_T0, S_LDS)
@@ -369,7 +378,7 @@ def tile_c(a: Asm, epi: str):
 
 
 def prologue(a: Asm, epi: str):
-    prologue_args(a)
+    prologue_args(a, epi)
     tile_setup(a, epi, sr(S_ITER) if SCHED["persist"] else "s2")
     tile_c(a, epi)
     prologue_lanes(a, epi)
@@ -1032,6 +1041,109 @@ def epilogue_rope(a: Asm):
     a.label(l_end)
 
 
+DELTA_DEPTH = 2      # O row blocks loaded this many blocks ahead
+SRD_DL = 72          # s72..s75: the delta rows of this wave (kernarg bytes 88..95)
+
+
+def epilogue_delta(a: Asm):
+    """The attention output projection's data gradient dO = dY Wo (plain C
+    stores) with the attention backward's delta fused in: ndelta[(b H + h) S
+    + s] = -sum_d dO[t][128 h + d] O[t][128 h + d] over the wave's head h =
+    2 tn + wn (kernarg S = O, laid out like C; fw = S, fc = H; bytes 88..95
+    = ndelta fp32 [B, H, S]).  dO enters as the bf16 values stored (what the
+    attention backward's dP reads).  A row's 128 columns sit in 4 lanes
+    (l & 15 fixed); their partial sums meet in 1 KiB of LDS past the
+    pipeline's stages; O row blocks load DELTA_DEPTH blocks ahead.  Replaces
+    attn_delta_kernel's pass over dO and O (csrc/hip/attention.hip)."""
+    v = V_T
+    a(f"s_load_dwordx2 {sr(SRD_DL, 2)}, s[0:1], 0x58")
+    a(f"v_lshrrev_b32 {vr(v)}, 6, {vr(V_TID)}")
+    a("s_nop 4")
+    a(f"v_readfirstlane_b32 {sr(S_Q)}, {vr(v)}")              # w
+    a(f"s_and_b32 {sr(S_R)}, {sr(S_Q)}, 1")                   # wm
+    a(f"s_lshr_b32 {sr(S_T2)}, {sr(S_Q)}, 1")                 # wn
+    a(f"s_lshl_b32 {sr(S_T3)}, {sr(S_TN)}, 1")
+    a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_T3)}")        # head h
+    a(f"s_lshl_b32 {sr(S_T3)}, {sr(S_TM)}, 8")
+    udiv(a, S_T0, S_T1, S_T3, S_FW)                           # b, s_tile
+    a(f"s_lshl_b32 {sr(S_R)}, {sr(S_R)}, 7")
+    a(f"s_add_u32 {sr(S_T1)}, {sr(S_T1)}, {sr(S_R)}")         # s0
+    a(f"s_mul_i32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_FC)}")
+    a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T2)}")        # b H + h
+    a(f"s_mul_i32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_FW)}")
+    a(f"s_add_u32 {sr(S_T0)}, {sr(S_T0)}, {sr(S_T1)}")        # row of s0
+    a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_T0)}, 2")
+    a("s_waitcnt lgkmcnt(0)")
+    a(f"s_add_u32 {sr(SRD_DL)}, {sr(SRD_DL)}, {sr(S_T0)}")
+    a(f"s_addc_u32 {sr(SRD_DL + 1)}, {sr(SRD_DL + 1)}, 0")
+    a(f"s_mov_b32 {sr(SRD_DL + 2)}, {128 * 4}")
+    a(f"s_mov_b32 {sr(SRD_DL + 3)}, 0x20000")
+    # lanes: LDS scratch (wave w: 256 B at LDS_BYTES + 256 w), the delta row (l & 15)
+    a(f"v_and_b32 {vr(v + 1)}, 63, {vr(V_TID)}")
+    a(f"v_lshlrev_b32 {vr(v + 2)}, 2, {vr(V_TID)}")            # 4 (64 w + l)
+    a(f"v_add_u32 {vr(v + 2)}, {LDS_BYTES}, {vr(v + 2)}")       # write address
+    a(f"v_and_b32 {vr(v + 3)}, 15, {vr(v + 1)}")
+    a(f"v_lshlrev_b32 {vr(v + 3)}, 2, {vr(v + 3)}")             # 4 (l & 15): delta offset
+    a(f"v_sub_u32 {vr(V_E + 2)}, {vr(v + 2)}, {vr(v + 1)}")    # ... 4 l ...
+    a(f"v_sub_u32 {vr(V_E + 2)}, {vr(V_E + 2)}, {vr(v + 1)}")
+    a(f"v_sub_u32 {vr(V_E + 2)}, {vr(V_E + 2)}, {vr(v + 1)}")
+    a(f"v_sub_u32 {vr(V_E + 2)}, {vr(V_E + 2)}, {vr(v + 1)}")  # wave base: LDS_BYTES + 256 w
+    a(f"v_add_u32 {vr(V_E + 2)}, {vr(V_E + 2)}, {vr(v + 3)}")  # + 4 (l & 15): the row's 4 partials at +0/64/128/192
+    a(f"s_mov_b32 {sr(S_E0)}, 0")                             # row block offset (C and O)
+    a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")
+    a(f"s_mov_b32 {sr(S_T2)}, 0")                             # O prefetch row block offset
+    D = DELTA_DEPTH
+    seq: list = []
+
+    def slot(j):
+        return V_FX0 + 16 * (j % D)
+
+    def issue(j):
+        for p in range(4):
+            a(f"buffer_load_dwordx4 {vr(slot(j) + 4 * p, 4)}, {vr(V_E)}, {sr(SRD_S, 4)}, {sr(S_T2)} offen offset:{64 * p}")
+            seq.append(("L", j))
+        a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_E1)}")
+
+    for j in range(min(D, 8)):
+        issue(j)
+    f, pk, ob, acc = V_E + 8, V_E + 40, V_E + 56, V_E + 72
+    for j in range(8):
+        for p in range(4):
+            read_pair(a, f + 8 * p, p, j)
+        for p in range(4):
+            cvt_pack8(a, pk + 4 * p, f + 8 * p)
+        for p in range(4):
+            store16(a, pk + 4 * p, V_E, SRD_C, S_E0, p)
+        seq.extend([("S", j)] * 4)
+        for p in range(4):
+            unpack8(a, f + 8 * p, pk + 4 * p)                  # dO as stored (bf16)
+        last = max(i for i, x in enumerate(seq) if x == ("L", j))
+        a(f"s_waitcnt vmcnt({min(63, len(seq) - last - 1)})")
+        for p in range(4):
+            unpack8(a, ob + 8 * (p % 2), slot(j) + 4 * p)
+            for e in range(8):
+                if p == 0 and e == 0:
+                    a(f"v_mul_f32 {vr(acc)}, {vr(f)}, {vr(ob)}")
+                else:
+                    a(f"v_fma_f32 {vr(acc)}, {vr(f + 8 * p + e)}, {vr(ob + 8 * (p % 2) + e)}, {vr(acc)}")
+        if j + D < 8:
+            issue(j + D)
+        a(f"ds_write_b32 {vr(v + 2)}, {vr(acc)}")
+        a("s_waitcnt lgkmcnt(0)")
+        for q in range(4):
+            a(f"ds_read_b32 {vr(acc + 1 + q)}, {vr(V_E + 2)} offset:{64 * q}")
+        a("s_waitcnt lgkmcnt(0)")
+        a(f"v_add_f32 {vr(acc + 1)}, {vr(acc + 1)}, {vr(acc + 2)}")
+        a(f"v_add_f32 {vr(acc + 3)}, {vr(acc + 3)}, {vr(acc + 4)}")
+        a(f"v_add_f32 {vr(acc + 1)}, {vr(acc + 1)}, {vr(acc + 3)}")
+        a(f"v_sub_f32 {vr(acc + 1)}, 0, {vr(acc + 1)}")        # -delta
+        a(f"s_mov_b32 {sr(S_T3)}, {64 * j}")
+        a(f"buffer_store_dword {vr(acc + 1)}, {vr(v + 3)}, {sr(SRD_DL, 4)}, {sr(S_T3)} offen")
+        seq.append(("S", j))
+        a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+        a("s_nop 1")
+
+
 def epi_offsets(a: Asm, epi: str):
     """Per-lane output byte offsets.  Lane l of wave (wm, wn) holds, for
     fragments (2p, j) and (2p+1, j): row m = wm*128 + 16 j + (l & 15) and the
@@ -1508,7 +1620,7 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
         if epi != "rope":
             epi_offsets(a, epi)
         {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd,
-         "rope": epilogue_rope}[epi](a)
+         "rope": epilogue_rope, "delta": epilogue_delta}[epi](a)
     if trace or timing or SCHED["drain_end"]:
         a("s_waitcnt vmcnt(0)")
     # else: end with the epilogue's stores still in flight -- the wave's end
@@ -1539,7 +1651,8 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
         a("s_endpgm")
     a.raw(f".size {name}, .-{name}")
     body = "\n".join(a.out)
-    desc, meta = _descriptor(name)
+    # the delta epilogue's partial sums: 4 waves x 256 B of LDS past the stages
+    desc, meta = _descriptor(name, lds_bytes=LDS_BYTES + 1024 if epi == "delta" else None)
     return body + "\n" + desc, meta
 
 

@@ -1913,6 +1913,15 @@ extern "C" int toa_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
 // inverse of toa_rope_fwd).  hipErrorNotSupported when the dS form is off or
 // the shape is not one it takes; the caller then runs toa_attn_bwd +
 // toa_rope_bwd.  ws: toa_attn_bwd_ws_bytes(B, H, S, D) bytes.
+// -lse log2(e) rows alone: the delta pass's other output, when the delta rows
+// came from the output projection's data-gradient GEMM (toa_gemm_asm_delta).
+__global__ __launch_bounds__(256) void attn_nlse2_kernel(const float* __restrict__ LSE, float* __restrict__ NLSE2,
+                                                         int rows) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < rows) NLSE2[i] = -(LSE[i] * LOG2E);
+}
+
+// flags bit 2: `delta` already holds the -delta rows (toa_gemm_asm_delta).
 extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o,
                                  const bf16_t* dout, const float* lse, float* delta, void* ws, const float* cosv,
                                  const float* sinv, bf16_t* dqkv, int B, int H, int Hk, int S, int D, int flags,
@@ -1927,8 +1936,11 @@ extern "C" int toa_attn_bwd_rope(const bf16_t* q, const bf16_t* k, const bf16_t*
   const int rows = B * H * S;
 #define TOA_ATTN_BWD_ROPE(DD)                                                                                    \
   do {                                                                                                           \
-    hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 256 / (DD / 8) - 1) / (256 / (DD / 8))), dim3(256), \
-                       0, stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);                               \
+    if (flags & 4)                                                                                               \
+      hipLaunchKernelGGL(attn_nlse2_kernel, dim3((rows + 255) / 256), dim3(256), 0, stream, lse, nlse2, rows);   \
+    else                                                                                                         \
+      hipLaunchKernelGGL((attn_delta_kernel<DD>), dim3((rows + 256 / (DD / 8) - 1) / (256 / (DD / 8))),          \
+                         dim3(256), 0, stream, o, dout, lse, delta, nlse2, rows, H, S, o_bshd);                  \
     dkdv_ds_launch<DD, true>(stream, q, k, v, dout, nlse2, delta, dqkv, dqkv, ds, B, H, Hk, S, scale, o_bshd,  \
                              cosv, sinv, H3);                                                                   \
     hipLaunchKernelGGL((attn_bwd_dqg_kernel<DD, true>), dim3((S / FWD_QB) * H * B), dim3(512), 0, stream, k, ds, \

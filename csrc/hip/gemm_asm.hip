@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_SWFWD_P1 = 52, K_SWBWD_P1 = 53, K_ROPE = 54, K_N = 55 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_SWFWD_P1 = 52, K_SWBWD_P1 = 53, K_ROPE = 54, K_DELTA = 55, K_N = 56 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -66,7 +66,9 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // the persistent fused SwiGLU GEMMs (gemm_gen.py SWIGLU_PERSIST_VARIANTS)
                            "toa_gemm_tn_asm_swiglu_fwd_p1", "toa_gemm_tn_asm_swiglu_bwd_p1",
                            // the fused-QKV projection with RoPE + head-major relayout (gemm_gen.py epilogue_rope)
-                           "toa_gemm_tn_asm_rope"};
+                           "toa_gemm_tn_asm_rope",
+                           // the output projection's data gradient with the attention delta (epilogue_delta)
+                           "toa_gemm_tn_asm_delta"};
 
 struct DevModule {
   std::once_flag once;
@@ -144,7 +146,7 @@ int launch(int which, const Args& a, hipStream_t stream, unsigned grid = 0) {
   hipFunction_t fn = get_fn(which, &err);
   if (!fn) return (int)err;
   Args k = a;
-  k.phase = phase_word(which);
+  if (which != K_DELTA) k.phase = phase_word(which);   // (the delta kernel's bytes 88..95 are a pointer)
   size_t sz = sizeof(k);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &k, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned nwg = grid ? grid : a.tiles_m * a.tiles_n;
@@ -640,6 +642,24 @@ extern "C" int toa_gemm_asm_rope(const bf16_t* X, int64_t ldx, const bf16_t* W, 
   a.fw = (uint32_t)S;
   a.fc = (uint32_t)(Hq | (Hkv << 16));
   return launch(K_ROPE, a, stream);
+}
+
+// dX = dY Wt^T (the plain TN kernel's C) with the attention backward's
+// delta fused (gemm_gen.py epilogue_delta): ndelta[(b H + h) S + s] =
+// -sum_d bf16(dX)[t][128 h + d] O[t][128 h + d]; O laid out like dX (row
+// stride ldc), N = H 128.  toa_attn_bwd_rope then skips its delta pass.
+extern "C" int toa_gemm_asm_delta(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C, int64_t ldc,
+                                  const bf16_t* O, float* ndelta, int M, int N, int K, int S, int H,
+                                  hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C) || !al16(O) ||
+      ndelta == nullptr || ((uintptr_t)ndelta & 3) || H <= 0 || (int64_t)H * 128 != N || S <= 0 || S % 256 || M % S)
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  a.S = (uint64_t)O;
+  a.fw = (uint32_t)S;
+  a.fc = (uint32_t)H;
+  memcpy(&a.phase, &ndelta, sizeof(ndelta));   // bytes 88..95
+  return launch(K_DELTA, a, stream);
 }
 
 // DIAGNOSTIC: arm v (1..) of the fused SwiGLU backward (gemm_gen.py

@@ -350,8 +350,9 @@ def test_host_kernel_table_matches_generator():
     import attn_bwd_gen
     import attn_gen
     # + the round-4 SwiGLU epilogue arms (2) + the SwiGLU backward's diagnostic arms
-    # 9: the four product epilogues (plain, swiglu_fwd, swiglu_bwd, rope), probe, trace, timing, timing2, wgrad
-    assert n == len(wanted) == 9 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
+    # 10: the five product epilogues (plain, swiglu_fwd, swiglu_bwd, rope, delta), probe, trace, timing,
+    # timing2, wgrad
+    assert n == len(wanted) == 10 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
         len(attn_bwd_gen.VARIANTS) + 2 + len(gemm_gen.SWIGLU_BWD_VARIANTS) + len(gemm_gen.SWIGLU_PERSIST_VARIANTS)
     flags = re.search(r"kVariantPersist\[kNumPlainVariants\] = \{([^}]*)\}", src).group(1)
     assert int(re.search(r"kNumPlainVariants = (\d+)", src).group(1)) == len(gemm_gen.PLAIN_VARIANTS)
@@ -366,3 +367,35 @@ def test_asm_gemm_assembles(tmp_path):
     subprocess.run(["/opt/rocm/lib/llvm/bin/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
                     "-mcpu=gfx950", "-c", str(s), "-o", str(o)], check=True)
     assert o.stat().st_size > 0
+
+
+@pytest.mark.parametrize("B,S,H", [(2, 256, 4), (1, 512, 2)])
+def test_asm_gemm_delta_epilogue_emulated(B, S, H):
+    """The output projection's data gradient with the attention backward's
+    delta fused: C = dY W^T as the plain kernel writes it (bit for bit), and
+    ndelta[b, h, s] = -sum_d bf16(C)[t][128 h + d] O[t][128 h + d]."""
+    rng = np.random.default_rng(B * S + H)
+    K = 128
+    M, N = B * S, H * 128
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)) * 0.3)
+    O = bf16(rng.standard_normal((M, N)))
+    outs = []
+    for name in ("toa_gemm_tn_asm_plain", "toa_gemm_tn_asm_delta"):
+        mem = emu.Memory()
+        ax, aw, ac = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16))
+        ao = mem.add(O)
+        ad = mem.add(np.full(B * H * S, np.nan, np.float32))
+        delta = name.endswith("delta")
+        # (the plain kernel reads fc as its diagnostic stage-exit word: 0 there)
+        karg = bytearray(host_args.pack(ax, aw, ac, ao, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256,
+                                        fw_b=S if delta else 0, fc_b=H if delta else 0))
+        if delta:
+            karg[88:96] = int(ad).to_bytes(8, "little")
+        run_all(name, bytes(karg), (M // 256) * (N // 256), mem)
+        outs.append((mem.bufs[2][1].copy(), mem.bufs[4][1].view(np.float32).copy()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    C = tof(outs[1][0].view(np.uint16).reshape(M, N))
+    ref = -(C * tof(O)).reshape(B, S, H, 128).sum(-1).transpose(0, 2, 1).reshape(-1)
+    got = outs[1][1].astype(np.float64)
+    assert np.abs(got - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6, np.abs(got - ref).max()

@@ -1567,3 +1567,45 @@ def test_qkv_rope_attention_fused_matches_two_nodes(B, S, Hq, Hkv):
         gemm.set_mode(old)
     for a, b in zip(*res):
         assert rel(a, b) < 2e-2, rel(a, b)
+
+
+def test_attn_out_proj_delta_rows(monkeypatch):
+    """_AttnOutProj: the output projection's data gradient through
+    toa_gemm_asm_delta equals the plain data gradient bit for bit, the -delta
+    rows it leaves equal -rowsum(dO * O) per head, and a llama-tiny128
+    trainer with the rows handed to the attention backward follows the one
+    with the attention's own delta pass."""
+    from tf_operator_amd.models.llama import PRESETS
+    from tf_operator_amd.ops import gemm, llm
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    _lib()
+    old = gemm.mode()
+    gemm.set_mode("asm")
+    try:
+        torch.manual_seed(8)
+        B, S, H, D = 2, 512, 4, 128
+        o = torch.randn(B * S, H * D, device=DEV).to(torch.bfloat16).requires_grad_()
+        wo = torch.nn.Parameter((torch.randn(H * D, H * D, device=DEV) / (H * D) ** 0.5).to(torch.bfloat16))
+        wo.main_grad = torch.zeros_like(wo)
+        wo._toa_wt = wo.data.t().contiguous()
+        dy = torch.randn(B * S, H * D, device=DEV).to(torch.bfloat16)
+        llm.attn_out_proj(o, wo, B, S, H).backward(dy)
+        torch.cuda.synchronize()
+        pend = llm._PENDING_DELTA
+        llm._PENDING_DELTA = None
+        assert pend is not None and pend[0] == o.grad.data_ptr()
+        assert torch.equal(o.grad, gemm.linear_dgrad(dy, wo))
+        ref = -(o.grad.float() * o.detach().float()).view(B, S, H, D).sum(-1).permute(0, 2, 1).reshape(-1)
+        assert rel(pend[2], ref) < 1e-4
+    finally:
+        gemm.set_mode(old)
+    losses = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TOA_ATTN_DELTA_FUSED", fused)
+        tr = LlamaTrainer(PRESETS["llama-tiny128"], torch.device(DEV), micro_batch=2, seq_len=512, seed=0)
+        b = tr.synthetic_batch()
+        losses[fused] = [float(tr.step([b])) for _ in range(3)]
+        assert llm._PENDING_DELTA is None
+    for a, c in zip(losses["1"], losses["0"]):
+        assert abs(a - c) <= 1e-3 * abs(c), losses

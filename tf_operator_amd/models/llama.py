@@ -26,8 +26,8 @@ import torch
 
 from ..ops.embedding import Embedding
 from ..ops.linear import linear
-from ..ops.llm import (causal_attention, cross_entropy, qkv_rope_attention, qkv_rope_attention_ok, rope_attention,
-                       rope_qkv, rope_tables, swiglu_mlp)
+from ..ops.llm import (attn_out_proj, causal_attention, cross_entropy, qkv_rope_attention, qkv_rope_attention_ok,
+                       rope_attention, rope_qkv, rope_tables, swiglu_mlp)
 from ..ops.norm import RMSNorm, add_rms_norm
 
 
@@ -113,7 +113,7 @@ class LlamaBlock(torch.nn.Module):
             q, k, v = rope_qkv(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim, rep)
             o = causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]: no transpose copy
         o = o.reshape(B * S, cfg.heads * cfg.head_dim)
-        a = linear(o, self.wo)
+        a = attn_out_proj(o, self.wo, B, S, cfg.heads) if o.is_cuda else linear(o, self.wo)
         h, x = self.mlp_norm(h, a)
         delta = swiglu_mlp(x, self.wgu, self.wd)  # SwiGLU fused into the GEMMs under TOA_GEMM=hip
         return h, delta

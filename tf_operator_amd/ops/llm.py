@@ -350,16 +350,27 @@ class _RopeAttn(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, None, None, None
 
 
+# (dO data_ptr, numel, -delta rows) left by the output projection's backward
+# (_AttnOutProj: toa_gemm_asm_delta) for the attention backward that follows
+_PENDING_DELTA = None
+
+
 def _rope_attn_dqkv(q, k, v, o, lse, cos, sin, do, scale, bshd):
     """d(qkv) [B S, (Hq + 2 Hkv) D] of RoPE + causal attention from dO."""
+    global _PENDING_DELTA
     B, Hq, S, D = q.shape
     Hkv = k.shape[1]
     do = do.contiguous()
+    pend, _PENDING_DELTA = _PENDING_DELTA, None
     dqkv = torch.empty(B * S, (Hq + 2 * Hkv) * D, device=q.device, dtype=q.dtype)
     flags = 1 | (2 if bshd else 0)
     ws = _attn_ws(B, Hq, S, D, q.device)
     if ws is not None and _ROPE_FUSED_BWD and _lib.has("toa_attn_bwd_rope"):
-        delta = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
+        if pend is not None and bshd and pend[0] == do.data_ptr() and pend[1] == do.numel():
+            delta = pend[2].view(B, Hq, S)   # the -delta rows from the projection's GEMM: no delta pass
+            flags |= 4
+        else:
+            delta = torch.empty(B, Hq, S, device=q.device, dtype=torch.float32)
         rc = _lib.call_ret("toa_attn_bwd_rope", _lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(o), _lib.ptr(do),
                            _lib.ptr(lse), _lib.ptr(delta), _lib.ptr(ws), _lib.ptr(cos), _lib.ptr(sin),
                            _lib.ptr(dqkv), B, Hq, Hkv, S, D, flags, float(scale), _lib.stream(q))
@@ -372,6 +383,56 @@ def _rope_attn_dqkv(q, k, v, o, lse, cos, sin, do, scale, bshd):
     _lib.call("toa_rope_bwd", _lib.ptr(dq), _lib.ptr(dk), _lib.ptr(dv), _lib.ptr(cos), _lib.ptr(sin),
               _lib.ptr(dqkv), B, S, Hq, Hkv, D, 1, _lib.stream(q))
     return dqkv
+
+
+class _AttnOutProj(torch.autograd.Function):
+    """The attention output projection linear(o, wo) whose backward also
+    writes the attention backward's -delta rows: its data-gradient GEMM
+    (toa_gemm_asm_delta) dots each stored dO row with O per head in its
+    epilogue, so the attention backward (_rope_attn_dqkv) skips its pass over
+    dO and O.  Elsewhere (no W^T copy, other shapes) the plain linear."""
+
+    @staticmethod
+    def forward(ctx, o2, wo, B, S, H):
+        ctx.save_for_backward(o2, wo)
+        ctx.dims = (B, S, H)
+        return gemm.linear_fwd(o2, wo)
+
+    @staticmethod
+    def backward(ctx, dy):
+        global _PENDING_DELTA
+        from .grad import accumulate_mm
+
+        o2, wo = ctx.saved_tensors
+        B, S, H = ctx.dims
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = None
+        wt = getattr(wo, "_toa_wt", None)
+        if (ctx.needs_input_grad[0] and wt is not None and dy2.stride(-1) == 1 and wt.stride(-1) == 1
+                and o2.is_contiguous() and os.environ.get("TOA_ATTN_DELTA_FUSED", "1") != "0"
+                and _lib.has("toa_gemm_asm_delta") and gemm.mode() == "asm"):
+            T, N = o2.shape
+            dx = torch.empty_like(o2)
+            nd = torch.empty(B * H * S, device=o2.device, dtype=torch.float32)
+            rc = _lib.call_ret("toa_gemm_asm_delta", _lib.ptr(dy2), dy2.stride(0), _lib.ptr(wt), wt.stride(0),
+                               _lib.ptr(dx), dx.stride(0), _lib.ptr(o2), _lib.ptr(nd), T, N, dy2.shape[1], S, H,
+                               _lib.stream(dy2))
+            if rc == 0:
+                _PENDING_DELTA = (dx.data_ptr(), dx.numel(), nd)
+            elif rc == 1:   # hipErrorInvalidValue: a shape it does not take
+                dx = None
+            else:
+                raise RuntimeError(f"toa_gemm_asm_delta failed with hipError {rc}")
+        if dx is None and ctx.needs_input_grad[0]:
+            dx = gemm.linear_dgrad(dy2, wo)
+        dw = accumulate_mm(wo, dy2.t(), o2)
+        return dx, dw, None, None, None
+
+
+def attn_out_proj(o2, wo, B, S, H):
+    """linear(o2, wo) for the attention output o2 [B S, H 128] (its backward
+    hands the attention backward its delta rows)."""
+    return _AttnOutProj.apply(o2, wo, B, S, H)
 
 
 _COSSIN: dict = {}   # (cos ptr, sin ptr, S) -> cos | sin [2][S][64] fp32 (toa_gemm_asm_rope's table)
