@@ -17,6 +17,7 @@ xent=N (cross-entropy backward chunks per thread), tpose=0|1 (the W^T refresh's 
 fnorm=0|1 (the clipping norm from the weight-gradient kernels' partials, or the full pass),
 adamwt=0|1 (AdamW writes the W^T copies itself, or the refresh transposes after it),
 qkvrope=0|1 (the QKV projection's GEMM applies RoPE and the head-major relayout, or the RoPE pass does),
+dfused=0|1 (the attention delta rows from the output projection's GEMM, or the attention's own pass),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -97,6 +98,9 @@ def apply(arm: str):
         elif key == "qkvrope":   # the QKV GEMM writes rotated head-major q | k | v (1) or qkv + the RoPE pass (0)
             import os
             os.environ["TOA_QKV_ROPE"] = val
+        elif key == "dfused":   # attention delta rows from the output projection's GEMM (1) or its own pass (0)
+            import os
+            os.environ["TOA_ATTN_DELTA_FUSED"] = val
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":
