@@ -84,6 +84,34 @@ extern "C" int toa_sum_f32(const float* x, int64_t n, float* workspace, float* o
   return (int)hipGetLastError();
 }
 
+// Sum of squares over many small ranges of one bf16 vector in one launch
+// (the clipping norm's rest after the weight-gradient partials: the norm
+// weights between the linear weights, ops/gemm.SumsqSession): workgroup b
+// sums range b (offs[b], lens[b]) into partial[b], then one sum, added to
+// out.  Deterministic: fixed ranges, fixed order.
+__global__ __launch_bounds__(256) void sumsq_ranges_kernel(const bf16_t* __restrict__ x,
+                                                           const int64_t* __restrict__ offs,
+                                                           const int64_t* __restrict__ lens,
+                                                           float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int64_t o = offs[blockIdx.x], n = lens[blockIdx.x];
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float f = bf2f(x[o + i]);
+    acc = fmaf(f, f, acc);
+  }
+  float t = block_sum(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+extern "C" int toa_sumsq_ranges(const bf16_t* x, const int64_t* offs, const int64_t* lens, int n, float* workspace,
+                                float* out, int accumulate, hipStream_t stream) {
+  if (n <= 0 || n > 32768) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sumsq_ranges_kernel, dim3(n), dim3(256), 0, stream, x, offs, lens, workspace);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, stream, workspace, n, out, accumulate);
+  return (int)hipGetLastError();
+}
+
 // workspace must hold >= TOA_SUMSQ_WS (32768) floats.  Grid: one 8-element
 // chunk per thread up to 32768 blocks (the flat AdamW's measurement: a grid
 // capped at 2048 blocks left each thread looping, 5-6 % slower per byte).

@@ -46,6 +46,7 @@ _SIGS = {
     "toa_transpose_set_variant": [c_int],
     "toa_wgrad_asm_set_sumsq": [c_p],
     "toa_sum_f32": [c_p, c_i64, c_p, c_p, c_int, c_p],
+    "toa_sumsq_ranges": [c_p, c_p, c_p, c_int, c_p, c_p, c_int, c_p],
     "toa_gemm_asm_rope": [c_p, c_i64, c_p, c_i64, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_delta": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
     "toa_adamw_wt": [c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_f, c_f, c_f, c_f, c_int, c_f,

@@ -452,6 +452,15 @@ class SumsqSession:
             pos = max(pos, b)
         if pos < flat.numel:
             self.rest.append((pos, flat.numel))
+        # the small rest ranges (norm weights) in one launch: offsets / lengths on the device
+        small = [(a, b - a) for a, b in self.rest if b - a < (1 << 20)]
+        self.rest = [(a, b) for a, b in self.rest if b - a >= (1 << 20)]
+        self.small = None
+        if small and flat.grad.dtype == torch.bfloat16 and len(small) <= 32768:
+            t = torch.tensor(small, dtype=torch.int64).t().contiguous().to(flat.device)
+            self.small = (t[0], t[1], len(small))
+        elif small:
+            self.rest = sorted(self.rest + [(a, a + n) for a, n in small])
         self.written = set()
         self.hits = 0           # steps served from the partials (tests, diagnostics)
 
@@ -482,6 +491,10 @@ class SumsqSession:
         for a, b in self.rest:
             _lib.call("toa_sumsq", f.grad.data_ptr() + esz * a, b - a, int(f.grad.dtype == torch.bfloat16),
                       _lib.ptr(ws), _lib.ptr(out), 1, s)
+        if self.small is not None:
+            offs, lens, n = self.small
+            _lib.call("toa_sumsq_ranges", _lib.ptr(f.grad), _lib.ptr(offs), _lib.ptr(lens), n, _lib.ptr(ws),
+                      _lib.ptr(out), 1, s)
         return out
 
 
