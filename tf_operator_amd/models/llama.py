@@ -113,7 +113,10 @@ class LlamaBlock(torch.nn.Module):
             q, k, v = rope_qkv(qkv, cos, sin, B, S, cfg.heads, cfg.kv_heads, cfg.head_dim, rep)
             o = causal_attention(q, k, v, out_layout="bshd")  # [B, S, H, D]: no transpose copy
         o = o.reshape(B * S, cfg.heads * cfg.head_dim)
-        a = attn_out_proj(o, self.wo, B, S, cfg.heads) if o.is_cuda else linear(o, self.wo)
+        # the RoPE-attention nodes consume the delta rows the projection's backward leaves; the other
+        # attention path does not, so it keeps the plain linear
+        packed = cfg.kv_layout in ("packed", "auto")
+        a = attn_out_proj(o, self.wo, B, S, cfg.heads) if (o.is_cuda and packed) else linear(o, self.wo)
         h, x = self.mlp_norm(h, a)
         delta = swiglu_mlp(x, self.wgu, self.wd)  # SwiGLU fused into the GEMMs under TOA_GEMM=hip
         return h, delta
