@@ -461,7 +461,7 @@ def test_zero_trainer_both_collectives_by_copy_engine(tmp_path):
         assert float(d) <= 2e-2 * float(r1["param"].abs().max()), float(d)
 
 
-def _zero8_worker(rank, world, port, out, lost):
+def _zero8_worker(rank, world, port, out, lost, preset="llama-tiny", seq=128):
     """llama-tiny ZeRO-1 on `world` processes sharing the one GPU, both
     collectives by copy-engine pulls (gloo carries nothing else: clipping is
     off, so no norm all-reduce either), every rank on the same batch.
@@ -483,7 +483,7 @@ def _zero8_worker(rank, world, port, out, lost):
         from tf_operator_amd.models.llama import PRESETS
         from tf_operator_amd.train.llm import LlamaTrainer
 
-        tr = LlamaTrainer(PRESETS["llama-tiny"], torch.device("cuda", 0), micro_batch=2, seq_len=128, lr=1e-3,
+        tr = LlamaTrainer(PRESETS[preset], torch.device("cuda", 0), micro_batch=2, seq_len=seq, lr=1e-3,
                           bucket_mb=0.25, shard_optimizer=world > 1)
         tr.opt.max_grad_norm = 0.0   # no clipping: the sharded run must match the unsharded one bit for bit
         if world > 1:
@@ -507,11 +507,11 @@ def _zero8_worker(rank, world, port, out, lost):
     os._exit(code)
 
 
-def _run_zero8(tmp_path, world, lost):
+def _run_zero8(tmp_path, world, lost, preset="llama-tiny", seq=128):
     ctx = mp.get_context("spawn")
-    out = str(tmp_path / f"z{lost}")
+    out = str(tmp_path / f"z{lost}_{preset}_{seq}")
     port = _port()
-    procs = [ctx.Process(target=_zero8_worker, args=(r, world, port, out, lost)) for r in range(world)]
+    procs = [ctx.Process(target=_zero8_worker, args=(r, world, port, out, lost, preset, seq)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -549,3 +549,19 @@ def test_zero1_eight_processes_lost_peer_every_rank_exits_nonzero(tmp_path):
     assert all(c != 0 for c in codes), (codes, [r.get("err") for r in res])
     assert any("rank" in (r.get("err") or "") and "5" in (r.get("err") or "") for r in res), res
     assert max(r["s"] for r in res) < 120, [r["s"] for r in res]
+
+
+@pytest.mark.timeout(600)
+def test_zero1_four_processes_fused_epilogues_bit_exact(tmp_path):
+    """The fused paths of the flagship step under ZeRO-1 (llama-tiny128 at
+    seq 512: the QKV GEMM's RoPE epilogue, the output projection's delta
+    epilogue, the weight-gradient kernels) with both collectives by
+    copy-engine pulls: four ranks train bit for bit like one unsharded rank
+    (whose update also writes the W^T copies, toa_adamw_wt)."""
+    codes, ref = _run_zero8(tmp_path, 1, -1, "llama-tiny128", 512)
+    assert codes == [0], ref
+    codes, res = _run_zero8(tmp_path, 4, -1, "llama-tiny128", 512)
+    assert codes == [0] * 4, [r.get("err") for r in res]
+    for r in range(4):
+        assert res[r]["losses"] == ref[0]["losses"], (r, res[r]["losses"], ref[0]["losses"])
+        assert torch.equal(res[r]["param"], ref[0]["param"]), r
