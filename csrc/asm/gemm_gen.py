@@ -91,7 +91,7 @@ KARG = {
 MAP_WALK_COLS = 16
 MAP_DEFAULT = 2          # groups of 4 row tiles walk the column tiles
 
-EPIS = ("plain", "swiglu_fwd", "swiglu_bwd", "rope", "delta")
+EPIS = ("plain", "swiglu_fwd", "swiglu_bwd", "rope", "delta", "resadd")
 
 # ---------------------------------------------------------------- registers
 # SGPRs: s[0:1] kernarg pointer, s2 workgroup id (the descriptor's order)
@@ -358,7 +358,7 @@ def tile_c(a: Asm, epi: str):
     a(f"s_addc_u32 {sr(S_T3)}, {sr(S_T3)}, 0")
     a(f"s_lshl_b32 {sr(S_T1)}, {sr(S_LDC)}, 8")
     srd(a, SRD_C, S_C, S_T2, S_T3, S_T1)
-    if epi == "delta":      # O: the same tile of a tensor laid out like C
+    if epi in ("delta", "resadd"):   # O / the residual: the same tile of a tensor laid out like C
         a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TM)}, 8")
         mul64(a, S_T2, S_T3, S_T0, S_LDC)
         a(f"s_lshl_b32 {sr(S_T0)}, {sr(S_TN)}, 9")
@@ -1144,6 +1144,51 @@ def epilogue_delta(a: Asm):
         a("s_nop 1")
 
 
+def epilogue_resadd(a: Asm):
+    """C = X W^T + R (bf16 R laid out like C, kernarg S): the residual add of
+    the attention output projection in its epilogue, so the RMSNorm after it
+    reads one tensor and writes one (ops/llm._AttnOutProj).  R row blocks
+    load DELTA_DEPTH blocks ahead (counted vmcnt); the sum is rounded to bf16
+    once, as the unfused add of the bf16 GEMM output and R is not (the fused
+    path adds in fp32 before the one rounding)."""
+    a(f"s_mov_b32 {sr(S_E0)}, 0")
+    a(f"s_lshl_b32 {sr(S_E1)}, {sr(S_LDC)}, 4")
+    a(f"s_mov_b32 {sr(S_T2)}, 0")
+    D = DELTA_DEPTH
+    seq: list = []
+
+    def slot(j):
+        return V_FX0 + 16 * (j % D)
+
+    def issue(j):
+        for p in range(4):
+            a(f"buffer_load_dwordx4 {vr(slot(j) + 4 * p, 4)}, {vr(V_E)}, {sr(SRD_S, 4)}, {sr(S_T2)} offen offset:{64 * p}")
+            seq.append(("L", j))
+        a(f"s_add_u32 {sr(S_T2)}, {sr(S_T2)}, {sr(S_E1)}")
+
+    for j in range(min(D, 8)):
+        issue(j)
+    f, pk, rb = V_E + 8, V_E + 40, V_E + 56
+    for j in range(8):
+        for p in range(4):
+            read_pair(a, f + 8 * p, p, j)
+        last = max(i for i, x in enumerate(seq) if x == ("L", j))
+        a(f"s_waitcnt vmcnt({min(63, len(seq) - last - 1)})")
+        for p in range(4):
+            unpack8(a, rb, slot(j) + 4 * p)
+            for e in range(8):
+                a(f"v_add_f32 {vr(f + 8 * p + e)}, {vr(f + 8 * p + e)}, {vr(rb + e)}")
+        if j + D < 8:
+            issue(j + D)
+        for p in range(4):
+            cvt_pack8(a, pk + 4 * p, f + 8 * p)
+        for p in range(4):
+            store16(a, pk + 4 * p, V_E, SRD_C, S_E0, p)
+        seq.extend([("S", j)] * 4)
+        a(f"s_add_u32 {sr(S_E0)}, {sr(S_E0)}, {sr(S_E1)}")
+        a("s_nop 1")
+
+
 def epi_offsets(a: Asm, epi: str):
     """Per-lane output byte offsets.  Lane l of wave (wm, wn) holds, for
     fragments (2p, j) and (2p+1, j): row m = wm*128 + 16 j + (l & 15) and the
@@ -1620,7 +1665,7 @@ def kernel(epi: str, trace: bool = False, variant: str = "") -> tuple[str, str]:
         if epi != "rope":
             epi_offsets(a, epi)
         {"plain": epilogue_plain, "swiglu_fwd": epilogue_swiglu_fwd, "swiglu_bwd": epilogue_swiglu_bwd,
-         "rope": epilogue_rope, "delta": epilogue_delta}[epi](a)
+         "rope": epilogue_rope, "delta": epilogue_delta, "resadd": epilogue_resadd}[epi](a)
     if trace or timing or SCHED["drain_end"]:
         a("s_waitcnt vmcnt(0)")
     # else: end with the epilogue's stores still in flight -- the wave's end

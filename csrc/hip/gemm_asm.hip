@@ -34,7 +34,7 @@ namespace {
 constexpr int kMaxDev = 64;
 enum { K_PLAIN = 0, K_SWIGLU_FWD = 1, K_SWIGLU_BWD = 2, K_PROBE = 3, K_TRACE = 4, K_TIMING = 5, K_TIMING2 = 6,
        K_WGRAD = 7, K_V1 = 8, K_WGRAD_V1 = 16, K_ATTN_FWD = 17, K_ATTN_D1 = 18, K_ATTN_T1 = 23,
-       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_SWFWD_P1 = 52, K_SWBWD_P1 = 53, K_ROPE = 54, K_DELTA = 55, K_N = 56 };
+       K_ATTN_DKDV = 26, K_DKDV_D1 = 27, K_DKDV_T1 = 34, K_SWIGLU_FWD_R4 = 41, K_SWIGLU_BWD_R4 = 42, K_SWBWD_V1 = 43, K_PLAIN_V9 = 48, K_DKDV_S7 = 49, K_DKDV_D8 = 50, K_DKDV_S8 = 51, K_SWFWD_P1 = 52, K_SWBWD_P1 = 53, K_ROPE = 54, K_DELTA = 55, K_RESADD = 56, K_N = 57 };
 // K_V1 .. K_N - 1: the A/B arms of the plain kernel (gemm_gen.py PLAIN_VARIANTS)
 const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_fwd", "toa_gemm_tn_asm_swiglu_bwd",
                            "toa_gemm_tn_asm_probe",    "toa_gemm_tn_asm_trace",      "toa_gemm_tn_asm_timing",
@@ -68,7 +68,9 @@ const char* kNames[K_N] = {"toa_gemm_tn_asm_plain",    "toa_gemm_tn_asm_swiglu_f
                            // the fused-QKV projection with RoPE + head-major relayout (gemm_gen.py epilogue_rope)
                            "toa_gemm_tn_asm_rope",
                            // the output projection's data gradient with the attention delta (epilogue_delta)
-                           "toa_gemm_tn_asm_delta"};
+                           "toa_gemm_tn_asm_delta",
+                           // C = X W^T + R (epilogue_resadd: the output projection's residual add)
+                           "toa_gemm_tn_asm_resadd"};
 
 struct DevModule {
   std::once_flag once;
@@ -660,6 +662,16 @@ extern "C" int toa_gemm_asm_delta(const bf16_t* X, int64_t ldx, const bf16_t* W,
   a.fc = (uint32_t)H;
   memcpy(&a.phase, &ndelta, sizeof(ndelta));   // bytes 88..95
   return launch(K_DELTA, a, stream);
+}
+
+// C = X W^T + R, R bf16 laid out like C (gemm_gen.py epilogue_resadd).
+extern "C" int toa_gemm_asm_resadd(const bf16_t* X, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* C, int64_t ldc,
+                                   const bf16_t* R, int M, int N, int K, hipStream_t stream) {
+  if (!common_ok(M, K, ldx, ldw, X, W) || N <= 0 || N % 256 || !ld_ok(ldc, N) || !al16(C) || !al16(R))
+    return (int)hipErrorInvalidValue;
+  Args a = base_args(X, ldx, W, ldw, C, ldc, M, N / 256, K);
+  a.S = (uint64_t)R;
+  return launch(K_RESADD, a, stream);
 }
 
 // DIAGNOSTIC: arm v (1..) of the fused SwiGLU backward (gemm_gen.py

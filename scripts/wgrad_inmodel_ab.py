@@ -18,6 +18,7 @@ fnorm=0|1 (the clipping norm from the weight-gradient kernels' partials, or the 
 adamwt=0|1 (AdamW writes the W^T copies itself, or the refresh transposes after it),
 qkvrope=0|1 (the QKV projection's GEMM applies RoPE and the head-major relayout, or the RoPE pass does),
 dfused=0|1 (the attention delta rows from the output projection's GEMM, or the attention's own pass),
+resadd=0|1 (the residual add in the output projection's epilogue, or in the RMSNorm),
 adamcap=N (the flat AdamW grid cap / 1024, toa_set_stream_variant),
 or the presets r4 (every round-4 default kernel: nosk GEMMs, the round-4
 weight-gradient schedule, the HIP attention forward and dK/dV) and head
@@ -101,6 +102,9 @@ def apply(arm: str):
         elif key == "dfused":   # attention delta rows from the output projection's GEMM (1) or its own pass (0)
             import os
             os.environ["TOA_ATTN_DELTA_FUSED"] = val
+        elif key == "resadd":   # the residual add in the output projection's epilogue (1) or in the RMSNorm (0)
+            import os
+            os.environ["TOA_RESADD_FUSED"] = val
         elif key == "wmap":   # weight-gradient tile order: -1 = the per-shape rule, else a map word
             _lib.call("toa_wgrad_asm_set_map", int(val))
         elif key == "adamcap":

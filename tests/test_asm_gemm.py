@@ -350,9 +350,9 @@ def test_host_kernel_table_matches_generator():
     import attn_bwd_gen
     import attn_gen
     # + the round-4 SwiGLU epilogue arms (2) + the SwiGLU backward's diagnostic arms
-    # 10: the five product epilogues (plain, swiglu_fwd, swiglu_bwd, rope, delta), probe, trace, timing,
+    # 11: the six product epilogues (plain, swiglu_fwd, swiglu_bwd, rope, delta, resadd), probe, trace, timing,
     # timing2, wgrad
-    assert n == len(wanted) == 10 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
+    assert n == len(wanted) == 11 + len(gemm_gen.PLAIN_VARIANTS) + 2 + len(attn_gen.VARIANTS) + 1 + \
         len(attn_bwd_gen.VARIANTS) + 2 + len(gemm_gen.SWIGLU_BWD_VARIANTS) + len(gemm_gen.SWIGLU_PERSIST_VARIANTS)
     flags = re.search(r"kVariantPersist\[kNumPlainVariants\] = \{([^}]*)\}", src).group(1)
     assert int(re.search(r"kNumPlainVariants = (\d+)", src).group(1)) == len(gemm_gen.PLAIN_VARIANTS)
@@ -399,3 +399,21 @@ def test_asm_gemm_delta_epilogue_emulated(B, S, H):
     ref = -(C * tof(O)).reshape(B, S, H, 128).sum(-1).transpose(0, 2, 1).reshape(-1)
     got = outs[1][1].astype(np.float64)
     assert np.abs(got - ref).max() <= 1e-4 * np.abs(ref).max() + 1e-6, np.abs(got - ref).max()
+
+
+def test_asm_gemm_resadd_epilogue_emulated():
+    """C = X W^T + R with R laid out like C (the output projection's residual
+    add in its epilogue): one bf16 rounding of the fp32 sum."""
+    rng = np.random.default_rng(31)
+    M, N, K = 512, 512, 192
+    X = bf16(rng.standard_normal((M, K)))
+    W = bf16(rng.standard_normal((N, K)) * 0.2)
+    R = bf16(rng.standard_normal((M, N)))
+    mem = emu.Memory()
+    ax, aw, ac, ar_ = mem.add(X), mem.add(W), mem.add(np.zeros((M, N), np.uint16)), mem.add(R)
+    karg = host_args.pack(ax, aw, ac, ar_, 2 * K, 2 * K, 2 * N, 0, K, M // 256, N // 256)
+    run_all("toa_gemm_tn_asm_resadd", karg, (M // 256) * (N // 256), mem)
+    C = tof(mem.bufs[2][1].view(np.uint16).reshape(M, N))
+    ref = tof(X) @ tof(W).T + tof(R)
+    close(C, ref)
+    assert np.mean(np.abs(C - tof(bf16(ref))) <= np.abs(ref) * 2 ** -7) > 0.999

@@ -1609,3 +1609,37 @@ def test_attn_out_proj_delta_rows(monkeypatch):
         assert llm._PENDING_DELTA is None
     for a, c in zip(losses["1"], losses["0"]):
         assert abs(a - c) <= 1e-3 * abs(c), losses
+
+
+def test_resadd_epilogue_and_presummed_norm(monkeypatch):
+    """The residual add in the output projection's epilogue
+    (toa_gemm_asm_resadd) + the presummed RMSNorm: out = o wo^T + h to one
+    bf16 rounding, and a llama-tiny128 trainer with it follows the one that
+    adds in the norm kernel."""
+    from tf_operator_amd.models.llama import PRESETS
+    from tf_operator_amd.ops import gemm, llm
+    from tf_operator_amd.train.llm import LlamaTrainer
+
+    _lib()
+    old = gemm.mode()
+    gemm.set_mode("asm")
+    try:
+        torch.manual_seed(12)
+        T, Hd = 1024, 512
+        o = torch.randn(T, Hd, device=DEV).to(torch.bfloat16)
+        wo = (torch.randn(Hd, Hd, device=DEV) / Hd ** 0.5).to(torch.bfloat16)
+        h = torch.randn(T, Hd, device=DEV).to(torch.bfloat16)
+        assert llm.attn_out_proj_resadd_ok(o, wo, h)
+        out = llm._AttnOutProj.apply(o, wo, 2, 512, 4, h)
+        ref = o.float() @ wo.float().t() + h.float()
+        assert rel(out, ref) < 1e-2
+    finally:
+        gemm.set_mode(old)
+    losses = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TOA_RESADD_FUSED", fused)
+        tr = LlamaTrainer(PRESETS["llama-tiny128"], torch.device(DEV), micro_batch=2, seq_len=512, seed=0)
+        b = tr.synthetic_batch()
+        losses[fused] = [float(tr.step([b])) for _ in range(3)]
+    for a, c in zip(losses["1"], losses["0"]):
+        assert abs(a - c) <= 2e-3 * abs(c), losses

@@ -26,8 +26,8 @@ import torch
 
 from ..ops.embedding import Embedding
 from ..ops.linear import linear
-from ..ops.llm import (attn_out_proj, causal_attention, cross_entropy, qkv_rope_attention, qkv_rope_attention_ok,
-                       rope_attention, rope_qkv, rope_tables, swiglu_mlp)
+from ..ops.llm import (attn_out_proj, attn_out_proj_resadd_ok, causal_attention, cross_entropy, qkv_rope_attention,
+                       qkv_rope_attention_ok, rope_attention, rope_qkv, rope_tables, swiglu_mlp)
 from ..ops.norm import RMSNorm, add_rms_norm
 
 
@@ -116,8 +116,12 @@ class LlamaBlock(torch.nn.Module):
         # the RoPE-attention nodes consume the delta rows the projection's backward leaves; the other
         # attention path does not, so it keeps the plain linear
         packed = cfg.kv_layout in ("packed", "auto")
-        a = attn_out_proj(o, self.wo, B, S, cfg.heads) if (o.is_cuda and packed) else linear(o, self.wo)
-        h, x = self.mlp_norm(h, a)
+        if o.is_cuda and packed and attn_out_proj_resadd_ok(o, self.wo, h):
+            # the residual add in the projection's epilogue; the norm then reads the sum once
+            h, x = self.mlp_norm.presummed(attn_out_proj(o, self.wo, B, S, cfg.heads, residual=h))
+        else:
+            a = attn_out_proj(o, self.wo, B, S, cfg.heads) if (o.is_cuda and packed) else linear(o, self.wo)
+            h, x = self.mlp_norm(h, a)
         delta = swiglu_mlp(x, self.wgu, self.wd)  # SwiGLU fused into the GEMMs under TOA_GEMM=hip
         return h, delta
 

@@ -49,6 +49,7 @@ _SIGS = {
     "toa_sumsq_ranges": [c_p, c_p, c_p, c_int, c_p, c_p, c_int, c_p],
     "toa_gemm_asm_rope": [c_p, c_i64, c_p, c_i64, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
     "toa_gemm_asm_delta": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
+    "toa_gemm_asm_resadd": [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_int, c_int, c_int, c_p],
     "toa_adamw_wt": [c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_i64, c_int, c_int, c_f, c_f, c_f, c_f, c_f, c_int, c_f,
                      c_p, c_f, c_p],
     "toa_stream_create_cu_mask": [c_int, c_int, ctypes.POINTER(ctypes.c_void_p)],

@@ -393,10 +393,18 @@ class _AttnOutProj(torch.autograd.Function):
     dO and O.  Elsewhere (no W^T copy, other shapes) the plain linear."""
 
     @staticmethod
-    def forward(ctx, o2, wo, B, S, H):
+    def forward(ctx, o2, wo, B, S, H, residual=None):
         ctx.save_for_backward(o2, wo)
         ctx.dims = (B, S, H)
-        return gemm.linear_fwd(o2, wo)
+        ctx.has_res = residual is not None
+        if residual is None:
+            return gemm.linear_fwd(o2, wo)
+        # the residual add in the GEMM's epilogue (toa_gemm_asm_resadd): out = o2 wo^T + residual
+        r2 = residual.reshape(o2.shape[0], -1)
+        out = torch.empty_like(r2)
+        _lib.call("toa_gemm_asm_resadd", _lib.ptr(o2), o2.stride(0), _lib.ptr(wo), wo.stride(0), _lib.ptr(out),
+                  out.stride(0), _lib.ptr(r2), o2.shape[0], wo.shape[0], o2.shape[1], _lib.stream(o2))
+        return out.view_as(residual)
 
     @staticmethod
     def backward(ctx, dy):
@@ -426,13 +434,23 @@ class _AttnOutProj(torch.autograd.Function):
         if dx is None and ctx.needs_input_grad[0]:
             dx = gemm.linear_dgrad(dy2, wo)
         dw = accumulate_mm(wo, dy2.t(), o2)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, (dy if ctx.has_res else None)
 
 
-def attn_out_proj(o2, wo, B, S, H):
-    """linear(o2, wo) for the attention output o2 [B S, H 128] (its backward
-    hands the attention backward its delta rows)."""
-    return _AttnOutProj.apply(o2, wo, B, S, H)
+def attn_out_proj(o2, wo, B, S, H, residual=None):
+    """linear(o2, wo) (+ residual, added in the GEMM's epilogue) for the
+    attention output o2 [B S, H 128]; its backward hands the attention
+    backward its delta rows."""
+    return _AttnOutProj.apply(o2, wo, B, S, H, residual)
+
+
+def attn_out_proj_resadd_ok(o2, wo, residual) -> bool:
+    """The residual add fits the output projection's epilogue (TOA_RESADD_FUSED)."""
+    return (o2.is_cuda and o2.dtype == wo.dtype == residual.dtype == torch.bfloat16 and gemm.mode() == "asm"
+            and o2.is_contiguous() and wo.is_contiguous() and residual.is_contiguous()
+            and o2.shape[0] % 256 == 0 and wo.shape[0] % 256 == 0 and o2.shape[1] % 64 == 0
+            and residual.numel() == o2.shape[0] * wo.shape[0] and _lib.has("toa_gemm_asm_resadd")
+            and os.environ.get("TOA_RESADD_FUSED", "1") != "0")
 
 
 _COSSIN: dict = {}   # (cos ptr, sin ptr, S) -> cos | sin [2][S][64] fp32 (toa_gemm_asm_rope's table)

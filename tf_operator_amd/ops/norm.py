@@ -53,7 +53,10 @@ class _NormFn(torch.autograd.Function):
         rows = x2.shape[0]
         if not x2.is_contiguous():
             x2 = x2.contiguous()
-        r2 = residual.reshape(-1, cols).contiguous() if residual is not None else None
+        # residual == "presummed": x already holds the residual sum (the output
+        # projection's GEMM added it, ops/llm._AttnOutProj): no add, h is x
+        presum = isinstance(residual, str)
+        r2 = residual.reshape(-1, cols).contiguous() if residual is not None and not presum else None
         if _lib.use_hip(x2):
             y = torch.empty_like(x2)
             h = torch.empty_like(x2) if r2 is not None else x2
@@ -74,6 +77,7 @@ class _NormFn(torch.autograd.Function):
         ctx.save_for_backward(h, weight, mean, rstd)
         ctx.rms = rms
         ctx.has_res = residual is not None
+        ctx.presum = presum
         ctx.has_bias = bias is not None
         ctx.bias = bias
         ctx.shape = shape
@@ -145,7 +149,7 @@ class _NormFn(torch.autograd.Function):
             if ctx.has_bias:
                 db = deliver_weight_grad(bias, dbf)
         dx = dx.view(ctx.shape)
-        return dx, (dx if ctx.has_res else None), dw, db, None, None
+        return dx, (dx if ctx.has_res and not ctx.presum else None), dw, db, None, None
 
 
 def rms_norm(x, weight, eps=1e-5):
@@ -175,6 +179,12 @@ class RMSNorm(torch.nn.Module):
         if residual is None:
             return rms_norm(x, self.weight, self.eps)
         return add_rms_norm(x, residual, self.weight, self.eps)
+
+    def presummed(self, h):
+        """(h, rmsnorm(h)) for an h that already holds the residual sum: one
+        read of h, and the backward returns dh + the norm's gradient fused,
+        as the residual form does."""
+        return _NormFn.apply(h, "presummed", self.weight, None, self.eps, True)
 
 
 class LayerNorm(torch.nn.Module):
