@@ -27,7 +27,8 @@ import torch
 from ..ops.embedding import Embedding
 from ..ops.linear import linear
 from ..ops.llm import (attn_out_proj, attn_out_proj_resadd_ok, causal_attention, cross_entropy, qkv_rope_attention,
-                       qkv_rope_attention_ok, rope_attention, rope_qkv, rope_tables, swiglu_mlp)
+                       qkv_rope_attention_ok, rope_attention, rope_qkv, rope_tables, swiglu_mlp,
+                       swiglu_mlp_resadd_ok)
 from ..ops.norm import RMSNorm, add_rms_norm
 
 
@@ -76,6 +77,10 @@ PRESETS = {
 }
 
 
+# a block's second output when its down projection already added the residual (the next norm is presummed)
+PRESUMMED = object()
+
+
 class LlamaBlock(torch.nn.Module):
     def __init__(self, cfg: LlamaConfig, device=None, dtype=torch.bfloat16):
         super().__init__()
@@ -96,6 +101,8 @@ class LlamaBlock(torch.nn.Module):
         cfg = self.cfg
         if delta is None:
             x = self.attn_norm(h)
+        elif delta is PRESUMMED:   # the previous block's down projection added the residual already
+            h, x = self.attn_norm.presummed(h)
         else:
             h, x = self.attn_norm(h, delta)
         if cfg.kv_layout in ("packed", "auto") and qkv_rope_attention_ok(x, self.wqkv, S, cfg.heads, cfg.kv_heads,
@@ -122,6 +129,9 @@ class LlamaBlock(torch.nn.Module):
         else:
             a = attn_out_proj(o, self.wo, B, S, cfg.heads) if (o.is_cuda and packed) else linear(o, self.wo)
             h, x = self.mlp_norm(h, a)
+        if swiglu_mlp_resadd_ok(x, self.wd, h):
+            # + the residual in the down projection's epilogue: the next norm reads the sum once
+            return swiglu_mlp(x, self.wgu, self.wd, residual=h), PRESUMMED
         delta = swiglu_mlp(x, self.wgu, self.wd)  # SwiGLU fused into the GEMMs under TOA_GEMM=hip
         return h, delta
 
@@ -180,7 +190,7 @@ class Llama(torch.nn.Module):
         delta = None
         for blk in self.blocks:
             h, delta = blk(h, delta, cos, sin, B, S)
-        _, x = self.norm(h, delta)
+        _, x = self.norm.presummed(h) if delta is PRESUMMED else self.norm(h, delta)
         logits = linear(x, self.head_weight())
         if targets is None:
             return logits.view(B, S, -1)

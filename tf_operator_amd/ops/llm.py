@@ -168,7 +168,7 @@ class _SwiGLUMLP(torch.autograd.Function):
     Weight gradients land in the flat buffer as in ``ops.linear``."""
 
     @staticmethod
-    def forward(ctx, x, wgu, wd):
+    def forward(ctx, x, wgu, wd, residual=None):
         x2 = x.reshape(-1, x.shape[-1])
         r = gemm.swiglu_gate_up(x2, wgu)
         gu, s = r if r is not None else (None, None)
@@ -176,6 +176,13 @@ class _SwiGLUMLP(torch.autograd.Function):
             gu = gemm.linear_fwd(x2, wgu)
             s = swiglu(gu)
         ctx.save_for_backward(x, wgu, wd, gu, s)
+        ctx.has_res = residual is not None
+        if residual is not None:   # + residual in the down projection's epilogue (toa_gemm_asm_resadd)
+            r2 = residual.reshape(s.shape[0], -1)
+            out = torch.empty_like(r2)
+            _lib.call("toa_gemm_asm_resadd", _lib.ptr(s), s.stride(0), _lib.ptr(wd), wd.stride(0), _lib.ptr(out),
+                      out.stride(0), _lib.ptr(r2), s.shape[0], wd.shape[0], s.shape[1], _lib.stream(s))
+            return out.view_as(residual)
         return gemm.linear_fwd(s, wd).view(*x.shape[:-1], wd.shape[0])
 
     @staticmethod
@@ -191,18 +198,29 @@ class _SwiGLUMLP(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         dx = gemm.linear_dgrad(dgu, wgu).view_as(x) if ctx.needs_input_grad[0] else None
         dwgu = accumulate_mm(wgu, dgu.t(), x2)
-        return dx, dwgu, dwd
+        return dx, dwgu, dwd, (dout if ctx.has_res else None)
 
 
-def swiglu_mlp(x, wgu, wd):
-    """The Llama MLP, x -> swiglu(x Wgu^T) Wd^T, fused where the assembly
-    GEMM takes the shapes (policy ``asm``: the default since round 5, see
-    ops.gemm.resolve_auto), else the two-GEMM + SwiGLU path (``nosk``)."""
+def swiglu_mlp(x, wgu, wd, residual=None):
+    """The Llama MLP, x -> swiglu(x Wgu^T) Wd^T (+ residual, added in the
+    down projection's epilogue: see swiglu_mlp_resadd_ok), fused where the
+    assembly GEMM takes the shapes (policy ``asm``: the default since round
+    5, see ops.gemm.resolve_auto), else the two-GEMM + SwiGLU path (``nosk``)."""
     if gemm.mode() == "asm":
-        return _SwiGLUMLP.apply(x, wgu, wd)
+        return _SwiGLUMLP.apply(x, wgu, wd, residual)
     from .linear import linear
 
-    return swiglu_down(linear(x, wgu), wd)
+    out = swiglu_down(linear(x, wgu), wd)
+    return out if residual is None else out + residual
+
+
+def swiglu_mlp_resadd_ok(x, wd, residual) -> bool:
+    """The residual add fits the fused MLP's down-projection epilogue."""
+    T = x.reshape(-1, x.shape[-1]).shape[0]
+    return (x.is_cuda and residual.dtype == wd.dtype == torch.bfloat16 and gemm.mode() == "asm"
+            and wd.is_contiguous() and residual.is_contiguous() and T % 256 == 0 and wd.shape[0] % 256 == 0
+            and wd.shape[1] % 64 == 0 and residual.numel() == T * wd.shape[0]
+            and _lib.has("toa_gemm_asm_resadd") and os.environ.get("TOA_RESADD_FUSED", "1") != "0")
 
 
 # ---------------------------------------------------------------------------
