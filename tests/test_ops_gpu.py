@@ -1629,7 +1629,6 @@ def test_resadd_epilogue_and_presummed_norm(monkeypatch):
         o = torch.randn(T, Hd, device=DEV).to(torch.bfloat16)
         wo = (torch.randn(Hd, Hd, device=DEV) / Hd ** 0.5).to(torch.bfloat16)
         h = torch.randn(T, Hd, device=DEV).to(torch.bfloat16)
-        monkeypatch.setenv("TOA_RESADD_FUSED", "1")
         assert llm.attn_out_proj_resadd_ok(o, wo, h)
         out = llm._AttnOutProj.apply(o, wo, 2, 512, 4, h)
         ref = o.float() @ wo.float().t() + h.float()

@@ -215,12 +215,10 @@ def swiglu_mlp(x, wgu, wd, residual=None):
 
 
 def resadd_fused_enabled() -> bool:
-    """Residual add in the GEMM epilogues: opt-in (TOA_RESADD_FUSED=1).  It
-    measured -1.7 ms/step on one GPU, but the 4-process ZeRO-1 rehearsal
-    (tests/test_comm_gpu.py test_zero1_four_processes_fused_epilogues_bit_exact)
-    lost bit-exactness with it at step 5 (profiles/r6_ra2); off until that is
-    understood (docs/kernels.md)."""
-    return os.environ.get("TOA_RESADD_FUSED", "0") == "1"
+    """Residual add in the GEMM epilogues (TOA_RESADD_FUSED=0 turns it off):
+    -2.75 +- 0.49 ms/step (profiles/r6_ra3).  The next norm runs presummed,
+    through its module call so ZeRO-1's gather waits still fire (ops/norm)."""
+    return os.environ.get("TOA_RESADD_FUSED", "1") != "0"
 
 
 def swiglu_mlp_resadd_ok(x, wd, residual) -> bool:

@@ -183,8 +183,11 @@ class RMSNorm(torch.nn.Module):
     def presummed(self, h):
         """(h, rmsnorm(h)) for an h that already holds the residual sum: one
         read of h, and the backward returns dh + the norm's gradient fused,
-        as the residual form does."""
-        return _NormFn.apply(h, "presummed", self.weight, None, self.eps, True)
+        as the residual form does.  Goes through the module call so its
+        forward pre-hooks run: ZeRO-1's per-bucket all-gather wait
+        (train/llm._install_param_waits) hangs on this module -- calling
+        _NormFn directly read the weight before its gather had landed."""
+        return self(h, "presummed")
 
 
 class LayerNorm(torch.nn.Module):
