@@ -555,7 +555,9 @@ def test_zero1_eight_processes_lost_peer_every_rank_exits_nonzero(tmp_path):
 def test_zero1_four_processes_fused_epilogues_bit_exact(tmp_path):
     """The fused paths of the flagship step under ZeRO-1 (llama-tiny128 at
     seq 512: the QKV GEMM's RoPE epilogue, the output projection's delta
-    epilogue, the weight-gradient kernels) with both collectives by
+    epilogue, the residual adds in the output / down projections' epilogues
+    with their presummed norms -- whose module hooks carry the gather waits --,
+    the weight-gradient kernels) with both collectives by
     copy-engine pulls: four ranks train bit for bit like one unsharded rank
     (whose update also writes the W^T copies, toa_adamw_wt)."""
     codes, ref = _run_zero8(tmp_path, 1, -1, "llama-tiny128", 512)
